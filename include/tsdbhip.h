@@ -1,0 +1,246 @@
+/*
+ * tsdbhip.h — C-ABI of libtsdbhip.so, the MI355X (gfx950) query-time
+ * aggregation path of OpenTSDB 1.1 (reference: anonthing/opentsdb).
+ *
+ * Plain pointers and sizes only; no HIP, torch or C++ types cross this
+ * boundary, so the Java host binds it through a thin JNI shim (see
+ * INTEGRATION.md) and Python through ctypes (opentsdb_amd/_lib.py).
+ *
+ * What each entry point replaces in the reference (paths relative to the
+ * reference root):
+ *
+ *   tsdbhip_spangroup_run  — the whole lazy iteration of a SpanGroup as the
+ *       consumers drive it (GraphHandler.java:791-808, Plot.java:190-204,
+ *       CliQuery.java:161-170): SpanGroup ctor/add (SpanGroup.java:104-142),
+ *       SGIterator (SpanGroup.java:370-796), Span.Iterator /
+ *       Span.DownsamplingIterator (Span.java:248-530), RowSeq.Iterator
+ *       (RowSeq.java:360-497) and the five Aggregators (Aggregators.java:76-243).
+ *       Row assembly follows Span.addRow / RowSeq.addRow (Span.java:87-132,
+ *       RowSeq.java:92-172), i.e. what TsdbQuery.findSpans does with each
+ *       compacted KeyValue (TsdbQuery.java:240-285).
+ *   tsdbhip_compact_rows   — CompactionQueue.compact(row, compacted[])
+ *       (CompactionQueue.java:243-435, 450-743) for a batch of rows.
+ *   tsdbhip_host_register / unregister — pinning of the JNI DirectByteBuffers
+ *       the bridge packs at TsdbQuery.java:264-266.
+ *
+ * Errors map to the reference's exceptions (the JNI shim rethrows them):
+ *   TSDBHIP_E_ILLEGAL_DATA -> IllegalDataException   (RowSeq.java:203,223;
+ *                             CompactionQueue.java:324,538,640,717,736)
+ *   TSDBHIP_E_NAN_INF      -> IllegalStateException  (SpanGroup.java:660-663)
+ *   TSDBHIP_E_EMPTY_SPAN   -> AssertionError         (SpanGroup.java:452-455)
+ *   others                 -> RuntimeException
+ * The reference is lazy (exceptions surface while iterating); this library
+ * is eager. out->err_index carries the index of the first output point the
+ * reference would NOT have delivered (-1 when unknown), so a host adapter can
+ * replay the lazy behaviour.
+ */
+#ifndef TSDBHIP_H
+#define TSDBHIP_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define TSDBHIP_ABI_VERSION 1
+
+/* ---- return codes ---------------------------------------------------- */
+#define TSDBHIP_OK               0
+#define TSDBHIP_E_ILLEGAL_DATA  -1
+#define TSDBHIP_E_NAN_INF       -2
+#define TSDBHIP_E_EMPTY_SPAN    -3
+#define TSDBHIP_E_CAPACITY      -4
+#define TSDBHIP_E_HIP           -5
+#define TSDBHIP_E_RCCL          -6
+#define TSDBHIP_E_INVALID_ARG   -7
+#define TSDBHIP_E_UNSORTED      -8  /* cells of a span not strictly increasing
+                                       after row assembly: input the reference
+                                       never produces from compacted rows */
+#define TSDBHIP_E_OUT_OF_BOUNDS -9  /* reference would throw
+                                       ArrayIndexOutOfBoundsException */
+#define TSDBHIP_E_NO_DEVICE    -10
+
+/* ---- aggregator op codes (Aggregators.java:44-48 names) --------------- */
+#define TSDBHIP_AGG_SUM 0
+#define TSDBHIP_AGG_MIN 1
+#define TSDBHIP_AGG_MAX 2
+#define TSDBHIP_AGG_AVG 3
+#define TSDBHIP_AGG_DEV 4
+
+/* ---- desc flags ------------------------------------------------------- */
+#define TSDBHIP_DESC_DEVICE   0x1u /* every array pointer in the desc is a
+                                      device pointer (data already in HBM) */
+#define TSDBHIP_EXACT_ORDER   0x2u /* reduce over spans strictly in span order
+                                      (bit-exact double sums / dev; slower) */
+#define TSDBHIP_SHARDED       0x4u /* desc holds this rank's shard of the
+                                      group; exchange with the other ranks of
+                                      the communicator set by tsdbhip_comm_init */
+
+typedef struct tsdbhip_ctx tsdbhip_ctx;
+
+/*
+ * One SpanGroup: the spans (in TreeMap order, TsdbQuery.java:242-243) and
+ * the compacted KeyValues of each span, rows sorted by time within a span.
+ * qual_bytes / val_bytes hold exactly the KeyValue qualifier()/value() bytes
+ * (big-endian, as stored in HBase); a row's qualifier offset must be even.
+ */
+typedef struct tsdbhip_sg_desc {
+  int64_t  start_time;      /* SpanGroup start (u32 held in int64)        */
+  int64_t  end_time;        /* SpanGroup end   (u32 held in int64)        */
+  uint8_t  rate;            /* SpanGroup.rate                              */
+  uint8_t  agg;             /* TSDBHIP_AGG_*  cross-series aggregator      */
+  uint8_t  ds_agg;          /* TSDBHIP_AGG_*  downsampler (ds_interval>0)  */
+  uint8_t  reserved0;
+  uint32_t flags;           /* TSDBHIP_DESC_DEVICE | TSDBHIP_EXACT_ORDER.. */
+  int32_t  ds_interval;     /* seconds, 0 = no downsampling                */
+  uint32_t n_spans;
+  uint64_t n_rows;
+  const uint64_t* span_row_start; /* [n_spans+1] rows of span s are
+                                     [span_row_start[s], span_row_start[s+1]) */
+  const uint32_t* row_base;       /* [n_rows] base_time from the row key      */
+  const uint32_t* row_ncells;     /* [n_rows] qualifier().length / 2          */
+  const uint64_t* row_qual_off;   /* [n_rows] byte offset into qual_bytes     */
+  const uint64_t* row_val_off;    /* [n_rows] byte offset into val_bytes      */
+  const uint32_t* row_val_len;    /* [n_rows] value().length                  */
+  const uint8_t*  qual_bytes;
+  uint64_t        qual_nbytes;
+  const uint8_t*  val_bytes;
+  uint64_t        val_nbytes;
+} tsdbhip_sg_desc;
+
+/* Result of one SpanGroup, in emission order (SGIterator order). */
+typedef struct tsdbhip_sg_out {
+  uint64_t capacity;        /* in:  size of ts/is_int/bits                 */
+  int64_t* ts;              /* out: DataPoint.timestamp()                  */
+  uint8_t* is_int;          /* out: DataPoint.isInteger()                  */
+  int64_t* bits;            /* out: longValue() or doubleToRawLongBits()   */
+  uint64_t n_out;           /* out: SpanGroup.size()                       */
+  uint64_t n_input_points;  /* out: SpanGroup.aggregatedSize()             */
+  int32_t  err_code;        /* out: same as the return code                */
+  int32_t  reserved0;
+  int64_t  err_index;       /* out: first output index not delivered by the
+                               lazy reference, or -1 if unknown / no error  */
+} tsdbhip_sg_out;
+
+/* Per-call device timings of the last tsdbhip_spangroup_run on a ctx,
+ * measured with HIP events on the ctx stream (milliseconds). */
+typedef struct tsdbhip_timing {
+  float    total_ms;        /* first kernel start .. last kernel end        */
+  float    decode_ms;       /* decode(+downsample) kernel — dominant, HBM   */
+  float    grid_ms;         /* union-grid construction                      */
+  float    reduce_ms;       /* cross-span reduction + combine               */
+  float    exchange_ms;     /* RCCL exchange (sharded runs)                 */
+  float    reserved[3];
+  uint64_t decode_bytes;    /* algorithmic bytes read+written by decode      */
+  uint64_t alg_bytes;       /* SURVEY §8(d) algorithmic bytes of the call   */
+  uint64_t n_grid;          /* |G|                                           */
+  uint64_t n_emitted;       /* Σ|E_s| (points after downsampling)           */
+} tsdbhip_timing;
+
+/* ---- row compaction (CompactionQueue.compact) -------------------------- */
+/*
+ * A batch of HBase rows, each a list of KeyValues (qualifier, value) in the
+ * order HBase returns them (sorted by qualifier bytes). For every row the
+ * library computes compacted[0] of CompactionQueue.compact(row, compacted).
+ */
+typedef struct tsdbhip_rows_desc {
+  uint32_t flags;            /* TSDBHIP_DESC_DEVICE                          */
+  uint32_t reserved0;
+  uint64_t n_rows;
+  uint64_t n_kvs;
+  const uint64_t* row_kv_start; /* [n_rows+1]                                */
+  const uint64_t* kv_qual_off;  /* [n_kvs] byte offset into qual_bytes       */
+  const uint32_t* kv_qual_len;  /* [n_kvs]                                   */
+  const uint64_t* kv_val_off;   /* [n_kvs] byte offset into val_bytes        */
+  const uint32_t* kv_val_len;   /* [n_kvs]                                   */
+  const uint8_t*  qual_bytes;
+  uint64_t        qual_nbytes;
+  const uint8_t*  val_bytes;
+  uint64_t        val_nbytes;
+} tsdbhip_rows_desc;
+
+/* Row status codes for tsdbhip_rows_out.row_status */
+#define TSDBHIP_ROW_NONE     0  /* compacted[0] stays null (empty / junk)     */
+#define TSDBHIP_ROW_SINGLE   1  /* the single KV, possibly float-fixed        */
+#define TSDBHIP_ROW_TRIVIAL  2  /* trivialCompact                             */
+#define TSDBHIP_ROW_COMPLEX  3  /* complexCompact                             */
+#define TSDBHIP_ROW_ERROR    4  /* IllegalDataException                       */
+
+typedef struct tsdbhip_rows_out {
+  uint64_t qual_capacity;    /* in: bytes available in qual_bytes           */
+  uint64_t val_capacity;     /* in: bytes available in val_bytes            */
+  uint8_t*  row_status;      /* [n_rows]                                     */
+  uint64_t* row_qual_off;    /* [n_rows] offset of the compacted qualifier   */
+  uint32_t* row_qual_len;    /* [n_rows]                                     */
+  uint64_t* row_val_off;     /* [n_rows]                                     */
+  uint32_t* row_val_len;     /* [n_rows]                                     */
+  uint8_t*  qual_bytes;      /* out                                          */
+  uint8_t*  val_bytes;       /* out                                          */
+  uint64_t  qual_used;
+  uint64_t  val_used;
+} tsdbhip_rows_out;
+
+/* ---- synthetic, HBM-resident inputs (bench / tests) -------------------- */
+#define TSDBHIP_SYN_INT64_COUNTER 0 /* 8-byte longs (flags 0x7), monotone
+                                       counter, increments in (0,1000)       */
+#define TSDBHIP_SYN_FLOAT32       1 /* 4-byte floats (flags 0xB), ~100+N(0,1) */
+#define TSDBHIP_SYN_FLOAT64       2 /* 8-byte doubles (flags 0xF)             */
+
+typedef struct tsdbhip_synth_params {
+  uint64_t seed;
+  uint32_t n_spans;
+  uint32_t n_points;        /* points per span                              */
+  uint32_t t0;              /* first timestamp (divisible by 3600)          */
+  uint32_t step;            /* cadence in seconds (divides 3600)            */
+  uint32_t kind;            /* TSDBHIP_SYN_*                                */
+  uint32_t reserved0;
+} tsdbhip_synth_params;
+
+/* ---- context ----------------------------------------------------------- */
+int         tsdbhip_open(int32_t device, tsdbhip_ctx** out);
+void        tsdbhip_close(tsdbhip_ctx* ctx);
+const char* tsdbhip_last_error(tsdbhip_ctx* ctx);
+int         tsdbhip_abi_version(void);
+
+int tsdbhip_host_register(tsdbhip_ctx* ctx, void* p, size_t n);
+int tsdbhip_host_unregister(tsdbhip_ctx* ctx, void* p);
+
+/* ---- the hot path ------------------------------------------------------ */
+int tsdbhip_spangroup_run(tsdbhip_ctx* ctx, const tsdbhip_sg_desc* desc,
+                          tsdbhip_sg_out* out);
+int tsdbhip_last_timing(tsdbhip_ctx* ctx, tsdbhip_timing* t);
+
+/* ---- secondary path ---------------------------------------------------- */
+int tsdbhip_compact_rows(tsdbhip_ctx* ctx, const tsdbhip_rows_desc* desc,
+                         tsdbhip_rows_out* out);
+
+/* ---- multi-GPU: one process per GPU, RCCL over xGMI -------------------- */
+#define TSDBHIP_UNIQUE_ID_BYTES 128
+int tsdbhip_comm_unique_id(uint8_t out[TSDBHIP_UNIQUE_ID_BYTES]);
+int tsdbhip_comm_init(tsdbhip_ctx* ctx, int32_t nranks, int32_t rank,
+                      const uint8_t id[TSDBHIP_UNIQUE_ID_BYTES]);
+
+/* ---- device-resident synthetic SpanGroup ------------------------------- */
+/* Generates the KeyValue bytes of a synthetic SpanGroup directly in HBM
+ * (same bytes as opentsdb_amd.synth on the host) and fills *desc with device
+ * pointers owned by ctx (flags |= TSDBHIP_DESC_DEVICE). Free with
+ * tsdbhip_synth_free. Only n_spans/n_points/... of params are used; the
+ * query fields of *desc (start/end/agg/...) are left for the caller. */
+int tsdbhip_synth_generate(tsdbhip_ctx* ctx, const tsdbhip_synth_params* p,
+                           tsdbhip_sg_desc* desc);
+int tsdbhip_synth_free(tsdbhip_ctx* ctx, tsdbhip_sg_desc* desc);
+
+/* Copies the device-resident desc's arrays back to host buffers sized by the
+ * desc (for parity checks of the generator). */
+int tsdbhip_desc_download(tsdbhip_ctx* ctx, const tsdbhip_sg_desc* ddesc,
+                          uint64_t* span_row_start, uint32_t* row_base,
+                          uint32_t* row_ncells, uint64_t* row_qual_off,
+                          uint64_t* row_val_off, uint32_t* row_val_len,
+                          uint8_t* qual_bytes, uint8_t* val_bytes);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* TSDBHIP_H */

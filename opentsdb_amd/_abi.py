@@ -1,0 +1,150 @@
+"""ctypes mirror of include/tsdbhip.h (the C-ABI of libtsdbhip.so).
+
+Only plain pointers and sizes cross the boundary; this module holds the
+struct layouts and constants shared by the host adapter (opentsdb_amd.core)
+and the test harness.
+"""
+import ctypes as C
+
+ABI_VERSION = 1
+
+OK = 0
+E_ILLEGAL_DATA = -1
+E_NAN_INF = -2
+E_EMPTY_SPAN = -3
+E_CAPACITY = -4
+E_HIP = -5
+E_RCCL = -6
+E_INVALID_ARG = -7
+E_UNSORTED = -8
+E_OUT_OF_BOUNDS = -9
+E_NO_DEVICE = -10
+
+ERR_NAMES = {
+    OK: "OK", E_ILLEGAL_DATA: "E_ILLEGAL_DATA", E_NAN_INF: "E_NAN_INF",
+    E_EMPTY_SPAN: "E_EMPTY_SPAN", E_CAPACITY: "E_CAPACITY", E_HIP: "E_HIP",
+    E_RCCL: "E_RCCL", E_INVALID_ARG: "E_INVALID_ARG", E_UNSORTED: "E_UNSORTED",
+    E_OUT_OF_BOUNDS: "E_OUT_OF_BOUNDS", E_NO_DEVICE: "E_NO_DEVICE",
+}
+
+AGG_SUM, AGG_MIN, AGG_MAX, AGG_AVG, AGG_DEV = 0, 1, 2, 3, 4
+
+DESC_DEVICE = 0x1
+EXACT_ORDER = 0x2
+SHARDED = 0x4
+
+ROW_NONE, ROW_SINGLE, ROW_TRIVIAL, ROW_COMPLEX, ROW_ERROR = 0, 1, 2, 3, 4
+
+SYN_INT64_COUNTER, SYN_FLOAT32, SYN_FLOAT64 = 0, 1, 2
+
+UNIQUE_ID_BYTES = 128
+
+P8 = C.POINTER(C.c_uint8)
+P32 = C.POINTER(C.c_uint32)
+P64 = C.POINTER(C.c_uint64)
+PI64 = C.POINTER(C.c_int64)
+
+
+class SgDesc(C.Structure):
+    _fields_ = [
+        ("start_time", C.c_int64),
+        ("end_time", C.c_int64),
+        ("rate", C.c_uint8),
+        ("agg", C.c_uint8),
+        ("ds_agg", C.c_uint8),
+        ("reserved0", C.c_uint8),
+        ("flags", C.c_uint32),
+        ("ds_interval", C.c_int32),
+        ("n_spans", C.c_uint32),
+        ("n_rows", C.c_uint64),
+        ("span_row_start", P64),
+        ("row_base", P32),
+        ("row_ncells", P32),
+        ("row_qual_off", P64),
+        ("row_val_off", P64),
+        ("row_val_len", P32),
+        ("qual_bytes", P8),
+        ("qual_nbytes", C.c_uint64),
+        ("val_bytes", P8),
+        ("val_nbytes", C.c_uint64),
+    ]
+
+
+class SgOut(C.Structure):
+    _fields_ = [
+        ("capacity", C.c_uint64),
+        ("ts", PI64),
+        ("is_int", P8),
+        ("bits", PI64),
+        ("n_out", C.c_uint64),
+        ("n_input_points", C.c_uint64),
+        ("err_code", C.c_int32),
+        ("reserved0", C.c_int32),
+        ("err_index", C.c_int64),
+    ]
+
+
+class Timing(C.Structure):
+    _fields_ = [
+        ("total_ms", C.c_float),
+        ("decode_ms", C.c_float),
+        ("grid_ms", C.c_float),
+        ("reduce_ms", C.c_float),
+        ("exchange_ms", C.c_float),
+        ("reserved", C.c_float * 3),
+        ("decode_bytes", C.c_uint64),
+        ("alg_bytes", C.c_uint64),
+        ("n_grid", C.c_uint64),
+        ("n_emitted", C.c_uint64),
+    ]
+
+
+class RowsDesc(C.Structure):
+    _fields_ = [
+        ("flags", C.c_uint32),
+        ("reserved0", C.c_uint32),
+        ("n_rows", C.c_uint64),
+        ("n_kvs", C.c_uint64),
+        ("row_kv_start", P64),
+        ("kv_qual_off", P64),
+        ("kv_qual_len", P32),
+        ("kv_val_off", P64),
+        ("kv_val_len", P32),
+        ("qual_bytes", P8),
+        ("qual_nbytes", C.c_uint64),
+        ("val_bytes", P8),
+        ("val_nbytes", C.c_uint64),
+    ]
+
+
+class RowsOut(C.Structure):
+    _fields_ = [
+        ("qual_capacity", C.c_uint64),
+        ("val_capacity", C.c_uint64),
+        ("row_status", P8),
+        ("row_qual_off", P64),
+        ("row_qual_len", P32),
+        ("row_val_off", P64),
+        ("row_val_len", P32),
+        ("qual_bytes", P8),
+        ("val_bytes", P8),
+        ("qual_used", C.c_uint64),
+        ("val_used", C.c_uint64),
+    ]
+
+
+class SynthParams(C.Structure):
+    _fields_ = [
+        ("seed", C.c_uint64),
+        ("n_spans", C.c_uint32),
+        ("n_points", C.c_uint32),
+        ("t0", C.c_uint32),
+        ("step", C.c_uint32),
+        ("kind", C.c_uint32),
+        ("reserved0", C.c_uint32),
+    ]
+
+
+def ptr(arr, ctype):
+    """numpy array -> ctypes pointer (array must stay alive)."""
+    return arr.ctypes.data_as(C.POINTER(ctype))

@@ -1,0 +1,127 @@
+"""ctypes wrapper of oracle/liboracle.so — TEST INFRASTRUCTURE ONLY.
+
+The CPU restatement of the reference path (see oracle.cc header). Only
+tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg use it, as
+the checker or the timed CPU baseline; the product package never does.
+"""
+import ctypes as C
+import os
+import subprocess
+
+import numpy as np
+
+from opentsdb_amd import _abi
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+_LIB = None
+
+
+def build():
+    subprocess.run(["make", "-s", "-C", _HERE], check=True)
+
+
+def lib():
+    global _LIB
+    if _LIB is None:
+        path = os.path.join(_HERE, "liboracle.so")
+        if not os.path.exists(path):
+            build()
+        L = C.CDLL(path)
+        L.oracle_spangroup_run.argtypes = [C.POINTER(_abi.SgDesc), C.POINTER(_abi.SgOut)]
+        L.oracle_spangroup_run.restype = C.c_int
+        L.oracle_agg_long.argtypes = [C.c_int, C.POINTER(C.c_int64), C.c_size_t, C.POINTER(C.c_int64)]
+        L.oracle_agg_double.argtypes = [C.c_int, C.POINTER(C.c_double), C.c_size_t, C.POINTER(C.c_double)]
+        L.oracle_compact_rows.argtypes = [C.POINTER(_abi.RowsDesc), C.POINTER(_abi.RowsOut)]
+        L.oracle_compact_rows.restype = C.c_int
+        _LIB = L
+    return _LIB
+
+
+class Result:
+    def __init__(self, code, ts, is_int, bits, n_input, err_index):
+        self.code = code
+        self.ts = ts
+        self.is_int = is_int
+        self.bits = bits
+        self.n_input_points = n_input
+        self.err_index = err_index
+
+    def values(self):
+        """Python values: int for integer points, float otherwise."""
+        d = self.bits.view(np.float64)
+        return [int(self.bits[i]) if self.is_int[i] else float(d[i]) for i in range(len(self.ts))]
+
+    def __repr__(self):
+        return f"Result(code={self.code}, n={len(self.ts)}, n_input={self.n_input_points})"
+
+
+def spangroup(spanset, start, end, agg, rate=False, ds_interval=0, ds_agg=0, capacity=None):
+    desc = _abi.SgDesc()
+    spanset.fill_desc(desc)
+    desc.start_time, desc.end_time = int(start), int(end)
+    desc.rate, desc.agg, desc.ds_agg = int(bool(rate)), int(agg), int(ds_agg)
+    desc.ds_interval = int(ds_interval)
+    desc.flags = 0
+    cap = int(capacity if capacity is not None else max(1, spanset.n_cells()))
+    ts = np.zeros(cap, np.int64)
+    isi = np.zeros(cap, np.uint8)
+    bits = np.zeros(cap, np.int64)
+    out = _abi.SgOut()
+    out.capacity = cap
+    out.ts = _abi.ptr(ts, C.c_int64)
+    out.is_int = _abi.ptr(isi, C.c_uint8)
+    out.bits = _abi.ptr(bits, C.c_int64)
+    code = lib().oracle_spangroup_run(C.byref(desc), C.byref(out))
+    n = int(out.n_out)
+    return Result(code, ts[:n].copy(), isi[:n].copy(), bits[:n].copy(),
+                  int(out.n_input_points), int(out.err_index))
+
+
+def agg_long(agg, values):
+    a = np.ascontiguousarray(values, np.int64)
+    r = C.c_int64()
+    rc = lib().oracle_agg_long(agg, _abi.ptr(a, C.c_int64), len(a), C.byref(r))
+    if rc:
+        raise RuntimeError(rc)
+    return r.value
+
+
+def agg_double(agg, values):
+    a = np.ascontiguousarray(values, np.float64)
+    r = C.c_double()
+    rc = lib().oracle_agg_double(agg, _abi.ptr(a, C.c_double), len(a), C.byref(r))
+    if rc:
+        raise RuntimeError(rc)
+    return r.value
+
+
+def compact_rows(rowbatch):
+    """rowbatch: opentsdb_amd.compaction.RowBatch -> list of (status, qual, val)."""
+    desc = rowbatch.fill_desc(_abi.RowsDesc())
+    n = rowbatch.n_rows
+    qcap = max(16, 2 * len(rowbatch.qual_bytes) + 16)
+    vcap = max(16, 2 * len(rowbatch.val_bytes) + 16 + n)
+    st = np.zeros(n, np.uint8)
+    qo = np.zeros(n, np.uint64)
+    ql = np.zeros(n, np.uint32)
+    vo = np.zeros(n, np.uint64)
+    vl = np.zeros(n, np.uint32)
+    qb = np.zeros(qcap, np.uint8)
+    vb = np.zeros(vcap, np.uint8)
+    out = _abi.RowsOut()
+    out.qual_capacity, out.val_capacity = qcap, vcap
+    out.row_status = _abi.ptr(st, C.c_uint8)
+    out.row_qual_off = _abi.ptr(qo, C.c_uint64)
+    out.row_qual_len = _abi.ptr(ql, C.c_uint32)
+    out.row_val_off = _abi.ptr(vo, C.c_uint64)
+    out.row_val_len = _abi.ptr(vl, C.c_uint32)
+    out.qual_bytes = _abi.ptr(qb, C.c_uint8)
+    out.val_bytes = _abi.ptr(vb, C.c_uint8)
+    rc = lib().oracle_compact_rows(C.byref(desc), C.byref(out))
+    if rc:
+        raise RuntimeError(rc)
+    res = []
+    for r in range(n):
+        res.append((int(st[r]), bytes(qb[int(qo[r]):int(qo[r]) + int(ql[r])]),
+                    bytes(vb[int(vo[r]):int(vo[r]) + int(vl[r])])))
+    return res
