@@ -1,0 +1,240 @@
+#!/usr/bin/env python3
+"""Benchmark of the query-time aggregation hot path on MI355X.
+
+Metric (BASELINE.json): input data points/sec aggregated (node) + % HBM
+roofline. A step is one tsdbhip_spangroup_run over one HBM-resident SpanGroup
+(the row bytes of TsdbQuery.findSpans, generated on the device): span
+assembly, RowSeq decode, greedy downsampling, union grid, lerp/rate merge,
+aggregation, and the RCCL exchange when sharded.
+
+Default workload (N=1..8, strong scaling): C3* — 1M series x 3600 points
+@1s, 8-byte long counters (IncomingDataPoints encoding), sum aggregator with
+1m-avg downsampling (the north-star target configuration); series sharded
+over the ranks by contiguous span ranges. `--config c2` runs configs[1]
+(10k float series x 1 day @10s, avg + 1m-avg).
+
+Usage: python bench.py [--gpus N] [--steps K] [--warmup W] [--config c3s|c2|c1]
+       (N>1: python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N)
+"""
+import argparse
+import ctypes as C
+import json
+import os
+import sys
+import threading
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+from opentsdb_amd import _abi, synth  # noqa: E402
+from opentsdb_amd._lib import Context, lib  # noqa: E402
+
+METRIC = "input data points/sec aggregated (node) + % HBM roofline, 1/2/4/8 MI355X"
+HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: 8.0 TB/s spec
+
+CONFIGS = {
+    # name: (n_series, points/series, step s, kind, agg, ds_interval, ds_agg, description)
+    "c3s": (1_000_000, 3600, 1, _abi.SYN_INT64_COUNTER, _abi.AGG_SUM, 60, _abi.AGG_AVG,
+            "C3*: 1M series x 3600 pts @1s (3.6G pts), int64 counters, sum + 1m-avg downsample"),
+    "c2": (10_000, 8640, 10, _abi.SYN_FLOAT32, _abi.AGG_AVG, 60, _abi.AGG_AVG,
+           "C2: 10k float32 series x 1 day @10s (86.4M pts), avg + 1m-avg downsample"),
+    "c1": (100, 3600, 1, _abi.SYN_INT64_COUNTER, _abi.AGG_SUM, 0, 0,
+           "C1: 100 int series x 3600 pts @1s, sum, no downsample"),
+    "c3": (1_000_000, 3600, 1, _abi.SYN_INT64_COUNTER, _abi.AGG_SUM, 0, 0,
+           "C3 (sum, no rate): 1M series x 3600 pts @1s, int64 counters"),
+}
+
+
+def ref_row_bytes(n_series, n_points, step, kind):
+    """per row 4 B base_time + 2 B/cell + value bytes + meta byte."""
+    k = 3600 // step
+    w = 4 if kind == _abi.SYN_FLOAT32 else 8
+    full, rem = divmod(n_points, k)
+    per_span = full * (4 + 2 * k + k * w + (1 if k > 1 else 0))
+    if rem:
+        per_span += 4 + 2 * rem + rem * w + (1 if rem > 1 else 0)
+    return n_series * per_span
+
+
+def dist_setup(n_gpus):
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    if world == 1:
+        return None, 0, 1, int(os.environ.get("LOCAL_RANK", "0"))
+    import torch.distributed as dist
+    dist.init_process_group("gloo")
+    return dist, dist.get_rank(), dist.get_world_size(), int(os.environ.get("LOCAL_RANK", "0"))
+
+
+def cpu_baseline(cfg, seconds=10.0):
+    """The oracle (C++ restatement of the reference's Java iterators) on the
+    host cores, independent SpanGroups per thread (group-by style,
+    TsdbQuery.java:322-362); a bounded sample of the same workload shape."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle
+    n_series, n_points, step, kind, agg, dsi, dsa, _ = CONFIGS[cfg]
+    sample_series = max(1, min(n_series, 200_000 // max(1, n_points // 100)))
+    ss = synth.regular(sample_series, n_points, kind, seed=1, step=step)
+    oracle.lib()
+    # probe one run, then size the sample to ~`seconds` of CPU work
+    t = time.perf_counter()
+    r = oracle.spangroup(ss, 0, (1 << 32) - 1, agg, False, dsi, dsa, capacity=ss.n_cells())
+    probe = time.perf_counter() - t
+    threads = max(1, min(16, os.cpu_count() or 1))
+    reps_per_thread = max(1, int(seconds / max(probe, 1e-3)))
+    total = [0]
+    lock = threading.Lock()
+
+    def work():
+        n = 0
+        for _ in range(reps_per_thread):
+            rr = oracle.spangroup(ss, 0, (1 << 32) - 1, agg, False, dsi, dsa, capacity=ss.n_cells())
+            n += rr.n_input_points
+        with lock:
+            total[0] += n
+
+    ths = [threading.Thread(target=work) for _ in range(threads)]
+    t = time.perf_counter()
+    for th in ths:
+        th.start()
+    for th in ths:
+        th.join()
+    wall = time.perf_counter() - t
+    one_core = r.n_input_points / probe
+    return {
+        "value": total[0] / wall, "unit": "input points/s", "cores": threads, "kind": "port",
+        "value_1core": one_core,
+        "sample": f"{sample_series} series x {n_points} pts of the same workload, "
+                  f"{threads} threads x {reps_per_thread} SpanGroups, {wall:.1f} s wall "
+                  f"(oracle/oracle.cc: C++ restatement of SpanGroup/Span/RowSeq/Aggregators; "
+                  f"no JVM in the image)",
+    }
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--config", default="c3s", choices=sorted(CONFIGS))
+    ap.add_argument("--series", type=int, default=0, help="override the number of series")
+    ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--cpu-seconds", type=float, default=10.0)
+    ap.add_argument("--exact", action="store_true", help="TSDBHIP_EXACT_ORDER")
+    args = ap.parse_args()
+
+    dist, rank, world, local_rank = dist_setup(args.gpus)
+    n_series, n_points, step, kind, agg, dsi, dsa, desc_txt = CONFIGS[args.config]
+    if args.series:
+        n_series = args.series
+    lo = n_series * rank // world
+    hi = n_series * (rank + 1) // world
+
+    ctx = Context(local_rank)
+    L = lib()
+    if world > 1:
+        uid = [Context.unique_id() if rank == 0 else None]
+        dist.broadcast_object_list(uid, src=0)
+        ctx.comm_init(world, rank, uid[0])
+
+    p = _abi.SynthParams(seed=3, n_spans=hi - lo, n_points=n_points, t0=synth.T0, step=step,
+                         kind=kind, span0=lo)
+    d = _abi.SgDesc()
+    ctx.check(L.tsdbhip_synth_generate(ctx.handle, C.byref(p), C.byref(d)))
+    d.start_time = 0
+    d.end_time = (1 << 32) - 1
+    d.agg, d.rate, d.ds_interval, d.ds_agg = agg, 0, dsi, dsa
+    if world > 1:
+        d.flags |= _abi.SHARDED
+    if args.exact:
+        d.flags |= _abi.EXACT_ORDER
+    cap = max(1, n_points if dsi == 0 else (n_points * step) // dsi + 2)
+    ts = np.zeros(cap, np.int64)
+    isi = np.zeros(cap, np.uint8)
+    bits = np.zeros(cap, np.int64)
+    out = _abi.SgOut(capacity=cap, ts=_abi.ptr(ts, C.c_int64), is_int=_abi.ptr(isi, C.c_uint8),
+                     bits=_abi.ptr(bits, C.c_int64))
+
+    def step_once():
+        ctx.check(L.tsdbhip_spangroup_run(ctx.handle, C.byref(d), C.byref(out)))
+
+    def barrier():
+        if dist is not None:
+            dist.barrier()
+
+    for _ in range(args.warmup):
+        step_once()
+    import torch
+    barrier()
+    torch.cuda.synchronize()
+    decode_ms, total_ms = [], []
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step_once()
+        tm = ctx.timing()
+        decode_ms.append(tm.decode_ms)
+        total_ms.append(tm.total_ms)
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    barrier()
+    if dist is not None:
+        import torch as _t
+        x = _t.tensor([elapsed], dtype=_t.float64)
+        dist.all_reduce(x, op=dist.ReduceOp.MAX)
+        elapsed = float(x.item())
+    n_input = int(out.n_input_points)  # global (allreduced when sharded)
+    ms_step = elapsed / args.steps * 1e3
+    value = n_input / (elapsed / args.steps)
+
+    local_bytes = ref_row_bytes(hi - lo, n_points, step, kind)
+    dec = float(np.mean(decode_ms))
+    achieved = local_bytes / (dec * 1e-3) / 1e9
+    if rank == 0:
+        res = {
+            "metric": METRIC,
+            "value": value,
+            "unit": "input points/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": ms_step,
+            "higher_is_better": True,
+            "scaling": "strong",
+            "vs_baseline": None,
+            "dtype": "int64" if kind == _abi.SYN_INT64_COUNTER else "f64",
+            "data": "synthetic (device-generated KeyValue bytes in the reference encoding)",
+            "config": {
+                "workload": desc_txt,
+                "n_series": n_series,
+                "points_per_series": n_points,
+                "aggregator": ["sum", "min", "max", "avg", "dev"][agg],
+                "downsample": f"{dsi}s-{['sum', 'min', 'max', 'avg', 'dev'][dsa]}" if dsi else "none",
+                "parallelism": f"series-sharded x{world} (RCCL exchange of per-t partials)" if world > 1
+                               else "single GPU",
+            },
+            "roofline": {
+                "bound": "hbm",
+                "kernel": "k_decode_ds (RowSeq decode + greedy downsample)" if dsi else "k_decode_nods",
+                "achieved": achieved,
+                "peak": HBM_PEAK_GBS,
+                "unit": "GB/s",
+                "frac": achieved / HBM_PEAK_GBS,
+                "traffic": None,
+                "alg_bytes_per_launch": local_bytes,
+                "kernel_ms": dec,
+                "step_device_ms": float(np.mean(total_ms)),
+            },
+        }
+        if not args.no_cpu and world == 1:
+            res["cpu_baseline"] = cpu_baseline(args.config, args.cpu_seconds)
+        print(json.dumps(res), flush=True)
+    L.tsdbhip_synth_free(ctx.handle, C.byref(d))
+    ctx.close()
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

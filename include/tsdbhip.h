@@ -61,6 +61,9 @@ extern "C" {
 #define TSDBHIP_E_OUT_OF_BOUNDS -9  /* reference would throw
                                        ArrayIndexOutOfBoundsException */
 #define TSDBHIP_E_NO_DEVICE    -10
+#define TSDBHIP_E_UNSUPPORTED  -11 /* Q1 stale-qualifier seek whose shifted
+                                       reads cross merged rows (never on the
+                                       TsdbQuery path)      */
 
 /* ---- aggregator op codes (Aggregators.java:44-48 names) --------------- */
 #define TSDBHIP_AGG_SUM 0
@@ -195,7 +198,7 @@ typedef struct tsdbhip_synth_params {
   uint32_t t0;              /* first timestamp (divisible by 3600)          */
   uint32_t step;            /* cadence in seconds (divides 3600)            */
   uint32_t kind;            /* TSDBHIP_SYN_*                                */
-  uint32_t reserved0;
+  uint32_t span0;           /* global index of the first span (shards)      */
 } tsdbhip_synth_params;
 
 /* ---- context ----------------------------------------------------------- */

@@ -19,6 +19,7 @@ E_INVALID_ARG = -7
 E_UNSORTED = -8
 E_OUT_OF_BOUNDS = -9
 E_NO_DEVICE = -10
+E_UNSUPPORTED = -11
 
 ERR_NAMES = {
     OK: "OK", E_ILLEGAL_DATA: "E_ILLEGAL_DATA", E_NAN_INF: "E_NAN_INF",
@@ -141,7 +142,7 @@ class SynthParams(C.Structure):
         ("t0", C.c_uint32),
         ("step", C.c_uint32),
         ("kind", C.c_uint32),
-        ("reserved0", C.c_uint32),
+        ("span0", C.c_uint32),
     ]
 
 

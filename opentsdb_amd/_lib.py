@@ -1,0 +1,127 @@
+"""Loader for libtsdbhip.so (built in-tree by opentsdb_amd/csrc/Makefile).
+
+There is no fallback: if the library or a GPU is missing, the product path
+raises. `import torch` comes first so that the HIP runtime torch ships with
+is the one libtsdbhip binds to (both use soname libamdhip64.so.7; loading
+ours first would pull a second copy of the runtime into the process).
+"""
+import ctypes as C
+import os
+import subprocess
+
+from . import _abi
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "libtsdbhip.so")
+CSRC = os.path.join(HERE, "csrc")
+
+_LIB = None
+
+EXPORTS = [
+    "tsdbhip_open", "tsdbhip_close", "tsdbhip_last_error", "tsdbhip_abi_version",
+    "tsdbhip_host_register", "tsdbhip_host_unregister", "tsdbhip_spangroup_run",
+    "tsdbhip_last_timing", "tsdbhip_compact_rows", "tsdbhip_comm_unique_id",
+    "tsdbhip_comm_init", "tsdbhip_synth_generate", "tsdbhip_synth_free",
+    "tsdbhip_desc_download",
+]
+
+
+class TsdbHipError(RuntimeError):
+    def __init__(self, code, msg=""):
+        self.code = code
+        super().__init__(f"{_abi.ERR_NAMES.get(code, code)}: {msg}")
+
+
+def build(force=False):
+    """Compile libtsdbhip.so for gfx950 (hipcc cross-compiles without a GPU)."""
+    args = ["make", "-s", "-C", CSRC]
+    if force:
+        args.append("-B")
+    subprocess.run(args, check=True)
+
+
+def lib():
+    global _LIB
+    if _LIB is not None:
+        return _LIB
+    if not os.path.exists(LIB_PATH):
+        raise TsdbHipError(_abi.E_NO_DEVICE, f"{LIB_PATH} not built; run opentsdb_amd._lib.build()")
+    try:
+        import torch  # noqa: F401  (pins the HIP runtime, see module doc)
+    except Exception:  # pragma: no cover - torch is part of the image
+        pass
+    L = C.CDLL(LIB_PATH)
+    P = C.POINTER
+    L.tsdbhip_open.argtypes = [C.c_int32, P(C.c_void_p)]
+    L.tsdbhip_open.restype = C.c_int
+    L.tsdbhip_close.argtypes = [C.c_void_p]
+    L.tsdbhip_close.restype = None
+    L.tsdbhip_last_error.argtypes = [C.c_void_p]
+    L.tsdbhip_last_error.restype = C.c_char_p
+    L.tsdbhip_abi_version.restype = C.c_int
+    L.tsdbhip_host_register.argtypes = [C.c_void_p, C.c_void_p, C.c_size_t]
+    L.tsdbhip_host_unregister.argtypes = [C.c_void_p, C.c_void_p]
+    L.tsdbhip_spangroup_run.argtypes = [C.c_void_p, P(_abi.SgDesc), P(_abi.SgOut)]
+    L.tsdbhip_spangroup_run.restype = C.c_int
+    L.tsdbhip_last_timing.argtypes = [C.c_void_p, P(_abi.Timing)]
+    L.tsdbhip_compact_rows.argtypes = [C.c_void_p, P(_abi.RowsDesc), P(_abi.RowsOut)]
+    L.tsdbhip_compact_rows.restype = C.c_int
+    L.tsdbhip_comm_unique_id.argtypes = [C.c_char_p]
+    L.tsdbhip_comm_init.argtypes = [C.c_void_p, C.c_int32, C.c_int32, C.c_char_p]
+    L.tsdbhip_synth_generate.argtypes = [C.c_void_p, P(_abi.SynthParams), P(_abi.SgDesc)]
+    L.tsdbhip_synth_free.argtypes = [C.c_void_p, P(_abi.SgDesc)]
+    L.tsdbhip_desc_download.argtypes = [C.c_void_p, P(_abi.SgDesc)] + [C.c_void_p] * 8
+    if L.tsdbhip_abi_version() != _abi.ABI_VERSION:
+        raise TsdbHipError(_abi.E_INVALID_ARG, "ABI version mismatch")
+    _LIB = L
+    return L
+
+
+class Context:
+    """One tsdbhip_ctx: a GPU, its stream and its HBM scratch."""
+
+    def __init__(self, device=0):
+        self._lib = lib()
+        self._h = C.c_void_p()
+        rc = self._lib.tsdbhip_open(int(device), C.byref(self._h))
+        if rc:
+            raise TsdbHipError(rc, self._lib.tsdbhip_last_error(None).decode())
+        self.device = device
+
+    @property
+    def handle(self):
+        return self._h
+
+    def last_error(self):
+        return self._lib.tsdbhip_last_error(self._h).decode()
+
+    def check(self, rc):
+        if rc:
+            raise TsdbHipError(rc, self.last_error())
+
+    def timing(self):
+        t = _abi.Timing()
+        self._lib.tsdbhip_last_timing(self._h, C.byref(t))
+        return t
+
+    def comm_init(self, nranks, rank, uid):
+        self.check(self._lib.tsdbhip_comm_init(self._h, nranks, rank, uid))
+
+    @staticmethod
+    def unique_id():
+        buf = C.create_string_buffer(_abi.UNIQUE_ID_BYTES)
+        rc = lib().tsdbhip_comm_unique_id(buf)
+        if rc:
+            raise TsdbHipError(rc, lib().tsdbhip_last_error(None).decode())
+        return buf.raw
+
+    def close(self):
+        if self._h:
+            self._lib.tsdbhip_close(self._h)
+            self._h = C.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass

@@ -1,0 +1,240 @@
+"""Host-side mirror of the reference call surface for the aggregation path.
+
+Mirrors (names, argument meaning, error behaviour):
+  Aggregators / Aggregator        src/core/Aggregators.java:22-245, Aggregator.java:24-86
+  Span (addRow)                   src/core/Span.java:33-132
+  SpanGroup (ctor, add, size,
+    aggregatedSize, iterator,
+    timestamp/isInteger/
+    longValue/doubleValue(i))     src/core/SpanGroup.java:46-254
+  DataPoint                       src/core/DataPoint.java:20-56
+  IllegalDataException            src/core/IllegalDataException.java
+
+The whole SpanGroup is evaluated by libtsdbhip on the GPU on first access
+(tsdbhip_spangroup_run); iteration then replays the reference's lazy
+exception behaviour: points before the failing one are delivered, then the
+mapped exception is raised.
+"""
+import ctypes as C
+import numpy as np
+
+from . import _abi
+from ._lib import Context, TsdbHipError
+from .packing import KeyValue, SpanSet, pack_spans
+
+
+class IllegalDataException(Exception):
+    """net.opentsdb.core.IllegalDataException"""
+
+
+class IllegalStateException(Exception):
+    """java.lang.IllegalStateException ("Got NaN or Infinity")"""
+
+
+class ArrayIndexOutOfBoundsException(IndexError):
+    """java.lang.ArrayIndexOutOfBoundsException"""
+
+
+def _exception_for(code, msg):
+    if code == _abi.E_ILLEGAL_DATA:
+        return IllegalDataException(msg)
+    if code == _abi.E_NAN_INF:
+        return IllegalStateException(msg)
+    if code == _abi.E_EMPTY_SPAN:
+        return AssertionError(msg)
+    if code == _abi.E_OUT_OF_BOUNDS:
+        return ArrayIndexOutOfBoundsException(msg)
+    return TsdbHipError(code, msg)
+
+
+class Aggregator:
+    """One of the five stateless aggregators; identity = op code."""
+
+    def __init__(self, name, code):
+        self._name = name
+        self.code = code
+
+    def toString(self):
+        return self._name
+
+    __str__ = toString
+
+    def __repr__(self):
+        return f"Aggregator({self._name})"
+
+
+class Aggregators:
+    SUM = Aggregator("sum", _abi.AGG_SUM)
+    MIN = Aggregator("min", _abi.AGG_MIN)
+    MAX = Aggregator("max", _abi.AGG_MAX)
+    AVG = Aggregator("avg", _abi.AGG_AVG)
+    DEV = Aggregator("dev", _abi.AGG_DEV)
+    _BY_NAME = {"sum": SUM, "min": MIN, "max": MAX, "avg": AVG, "dev": DEV}
+
+    @classmethod
+    def get(cls, name):
+        try:
+            return cls._BY_NAME[name]
+        except KeyError:
+            raise LookupError("No such aggregator: " + name) from None
+
+    @classmethod
+    def set(cls):
+        return set(cls._BY_NAME)
+
+
+class DataPoint:
+    __slots__ = ("_ts", "_isint", "_bits")
+
+    def __init__(self, ts, isint, bits):
+        self._ts, self._isint, self._bits = int(ts), bool(isint), int(bits)
+
+    def timestamp(self):
+        return self._ts
+
+    def isInteger(self):
+        return self._isint
+
+    def longValue(self):
+        if not self._isint:
+            raise TypeError("ClassCastException: value is a double")
+        return self._bits
+
+    def doubleValue(self):
+        if self._isint:
+            raise TypeError("ClassCastException: value is a long")
+        return float(np.int64(self._bits).view(np.float64))
+
+    def toDouble(self):
+        return float(self._bits) if self._isint else self.doubleValue()
+
+    def __repr__(self):
+        v = self._bits if self._isint else self.doubleValue()
+        return f"DataPoint({self._ts}, {v!r})"
+
+
+class Span:
+    """The compacted rows of one time series, in scan order. The row
+    acceptance rules of Span.addRow are applied by the library."""
+
+    def __init__(self, rows=None):
+        self.rows = list(rows or [])
+
+    def addRow(self, row: KeyValue):
+        self.rows.append(row)
+
+
+def run_spanset(ctx, spanset: SpanSet, start, end, agg, rate=False, ds_interval=0, ds_agg=0,
+                exact=False, capacity=None, device_desc=None):
+    """Low-level: one tsdbhip_spangroup_run. Returns (code, ts, is_int, bits,
+    n_input_points, err_index)."""
+    desc = _abi.SgDesc()
+    if device_desc is not None:
+        C.pointer(desc)[0] = device_desc
+    else:
+        spanset.fill_desc(desc)
+        desc.flags = 0
+    desc.start_time, desc.end_time = int(start), int(end)
+    desc.rate, desc.agg, desc.ds_agg = int(bool(rate)), int(agg), int(ds_agg)
+    desc.ds_interval = int(ds_interval)
+    if exact:
+        desc.flags |= _abi.EXACT_ORDER
+    cap = capacity
+    if cap is None:
+        cap = max(1, spanset.n_cells()) if spanset is not None else 1 << 20
+    ts = np.zeros(cap, np.int64)
+    isi = np.zeros(cap, np.uint8)
+    bits = np.zeros(cap, np.int64)
+    out = _abi.SgOut()
+    out.capacity = cap
+    out.ts = _abi.ptr(ts, C.c_int64)
+    out.is_int = _abi.ptr(isi, C.c_uint8)
+    out.bits = _abi.ptr(bits, C.c_int64)
+    rc = ctx._lib.tsdbhip_spangroup_run(ctx.handle, C.byref(desc), C.byref(out))
+    n = int(out.n_out)
+    return rc, ts[:n], isi[:n], bits[:n], int(out.n_input_points), int(out.err_index)
+
+
+class SpanGroup:
+    """net.opentsdb.core.SpanGroup over libtsdbhip (SpanGroup.java:104-254)."""
+
+    _default_ctx = None
+
+    def __init__(self, tsdb, start_time, end_time, spans, rate, aggregator, interval=0,
+                 downsampler=None, ctx=None):
+        self.start_time = int(start_time)
+        self.end_time = int(end_time)
+        self.spans = []
+        self.rate = bool(rate)
+        self.aggregator = aggregator
+        self.sample_interval = int(interval)
+        self.downsampler = downsampler
+        self._ctx = ctx
+        self._result = None
+        if spans is not None:
+            for s in spans:
+                self.add(s)
+
+    def add(self, span):
+        # SpanGroup.add's time filter (SpanGroup.java:135-139) needs the
+        # assembled span; the library applies it, so every span is handed over.
+        self.spans.append(span)
+        self._result = None
+
+    def _context(self):
+        if self._ctx is None:
+            if SpanGroup._default_ctx is None:
+                SpanGroup._default_ctx = Context(0)
+            self._ctx = SpanGroup._default_ctx
+        return self._ctx
+
+    def _run(self):
+        if self._result is None:
+            ss = pack_spans([s.rows for s in self.spans])
+            ds = self.downsampler is not None and self.sample_interval > 0
+            self._result = run_spanset(self._context(), ss, self.start_time, self.end_time,
+                                       self.aggregator.code, self.rate,
+                                       self.sample_interval if ds else 0,
+                                       self.downsampler.code if ds else 0)
+        return self._result
+
+    def _points(self):
+        rc, ts, isi, bits, _, _ = self._run()
+        for i in range(len(ts)):
+            yield DataPoint(ts[i], isi[i], bits[i])
+        if rc:
+            raise _exception_for(rc, self._context().last_error())
+
+    def aggregatedSize(self):
+        return self._run()[4]
+
+    def size(self):
+        n = 0
+        for _ in self._points():
+            n += 1
+        return n
+
+    def iterator(self):
+        return self._points()
+
+    __iter__ = iterator
+
+    def _get(self, i):
+        if i < 0:
+            raise IndexError("negative index: %d" % i)
+        for j, dp in enumerate(self._points()):
+            if j == i:
+                return dp
+        raise IndexError("index %d too large" % i)
+
+    def timestamp(self, i):
+        return self._get(i).timestamp()
+
+    def isInteger(self, i):
+        return self._get(i).isInteger()
+
+    def longValue(self, i):
+        return self._get(i).longValue()
+
+    def doubleValue(self, i):
+        return self._get(i).doubleValue()

@@ -1,0 +1,837 @@
+// api.hip — libtsdbhip.so: the C-ABI declared in include/tsdbhip.h and the
+// host orchestration of the gfx950 kernels. One unity translation unit.
+//
+// Pipeline of tsdbhip_spangroup_run (all on the ctx stream):
+//   k_assemble        Span.addRow / RowSeq.addRow rules, S7 keep rule, E caps
+//   scans             kept-span list, E offsets                     [sync 1]
+//   k_decode_*        RowSeq decode (+ greedy downsampling) -> E_s   (HBM-bound)
+//   k_span_summary    grid range, F*                                [sync 2]
+//   k_grid_*          union grid G as bitmap + ranks                 [sync 3]
+//   k_reduce          per (tile, span chunk) lerp/rate + aggregation
+//   k_finalize_*      chunk combine, int/double select, NaN check   [sync 4]
+// With TSDBHIP_SHARDED the grid bitmap and the per-t partials are exchanged
+// over RCCL (allgather, then a rank-ordered combine on every rank).
+#include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
+
+#include <algorithm>
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+#include <map>
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "../../include/tsdbhip.h"
+#include "dev_common.h"
+#include "k_assemble.hip"
+#include "k_decode.hip"
+#include "k_grid.hip"
+#include "k_reduce.hip"
+#include "k_util.hip"
+
+using namespace tsdb;
+
+namespace {
+
+struct Buf {
+  void* p = nullptr;
+  size_t n = 0;
+};
+
+struct Fail {
+  int code;
+};
+
+}  // namespace
+
+struct tsdbhip_ctx {
+  int device = 0;
+  hipStream_t stream = nullptr;
+  std::mutex mu;
+  std::string err;
+  std::map<std::string, Buf> bufs;
+  void* host_small = nullptr;  // pinned readback area
+  hipEvent_t ev[8] = {};
+  tsdbhip_timing timing = {};
+  ncclComm_t comm = nullptr;
+  int nranks = 1, rank = 0;
+};
+
+static thread_local std::string g_thread_err;
+
+static void set_error(tsdbhip_ctx* c, const char* fmt, ...) {
+  char buf[512];
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(buf, sizeof buf, fmt, ap);
+  va_end(ap);
+  g_thread_err = buf;
+  if (c) c->err = buf;
+}
+
+#define HIPCHK(x)                                                                  \
+  do {                                                                             \
+    hipError_t e_ = (x);                                                           \
+    if (e_ != hipSuccess) {                                                        \
+      set_error(ctx, "%s failed: %s (%s:%d)", #x, hipGetErrorString(e_), __FILE__, \
+                __LINE__);                                                         \
+      throw Fail{TSDBHIP_E_HIP};                                                   \
+    }                                                                              \
+  } while (0)
+
+#define NCCLCHK(x)                                                              \
+  do {                                                                          \
+    ncclResult_t r_ = (x);                                                      \
+    if (r_ != ncclSuccess) {                                                    \
+      set_error(ctx, "%s failed: %s (%s:%d)", #x, ncclGetErrorString(r_),       \
+                __FILE__, __LINE__);                                            \
+      throw Fail{TSDBHIP_E_RCCL};                                               \
+    }                                                                           \
+  } while (0)
+
+// grow-only named scratch
+template <typename T>
+static T* scratch(tsdbhip_ctx* ctx, const char* name, size_t count, bool zero = false) {
+  size_t bytes = std::max<size_t>(count * sizeof(T), 16) + 64;
+  Buf& b = ctx->bufs[name];
+  if (b.n < bytes) {
+    if (b.p) HIPCHK(hipFree(b.p));
+    b.p = nullptr;
+    size_t alloc = std::max(bytes, b.n + b.n / 4);
+    HIPCHK(hipMalloc(&b.p, alloc));
+    b.n = alloc;
+  }
+  if (zero) HIPCHK(hipMemsetAsync(b.p, 0, bytes, ctx->stream));
+  return (T*)b.p;
+}
+
+static unsigned grid_for(uint64_t work, unsigned per_block, unsigned cap = 1u << 20) {
+  uint64_t g = (work + per_block - 1) / per_block;
+  if (g < 1) g = 1;
+  if (g > cap) g = cap;
+  return (unsigned)g;
+}
+
+static void dscan_u64(tsdbhip_ctx* ctx, const uint64_t* in, uint64_t* out, uint64_t n, uint64_t* d_total,
+                      const char* tag) {
+  const uint64_t nb = (n + 1023) / 1024;
+  std::string key = std::string("scan_blocks_") + tag;
+  uint64_t* bs = scratch<uint64_t>(ctx, key.c_str(), nb + 1);
+  if (n == 0) {
+    HIPCHK(hipMemsetAsync(d_total, 0, 8, ctx->stream));
+    return;
+  }
+  hipLaunchKernelGGL(k_scan_block_u64, dim3((unsigned)nb), dim3(256), 0, ctx->stream, in, out, n, bs);
+  hipLaunchKernelGGL(k_scan_blocks_u64, dim3(1), dim3(256), 0, ctx->stream, bs, nb, d_total);
+  hipLaunchKernelGGL(k_scan_add_u64, dim3(grid_for(n, 256)), dim3(256), 0, ctx->stream, out, n, bs);
+}
+
+// ----------------------------------------------------------------------------
+extern "C" int tsdbhip_abi_version(void) { return TSDBHIP_ABI_VERSION; }
+
+extern "C" const char* tsdbhip_last_error(tsdbhip_ctx* ctx) {
+  return ctx ? ctx->err.c_str() : g_thread_err.c_str();
+}
+
+extern "C" int tsdbhip_open(int32_t device, tsdbhip_ctx** out) {
+  tsdbhip_ctx* ctx = nullptr;
+  if (!out) return TSDBHIP_E_INVALID_ARG;
+  *out = nullptr;
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess || n <= 0) {
+    set_error(nullptr, "no HIP device available");
+    return TSDBHIP_E_NO_DEVICE;
+  }
+  if (device < 0 || device >= n) {
+    set_error(nullptr, "device %d out of range (%d devices)", device, n);
+    return TSDBHIP_E_INVALID_ARG;
+  }
+  ctx = new tsdbhip_ctx();
+  ctx->device = device;
+  try {
+    HIPCHK(hipSetDevice(device));
+    HIPCHK(hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking));
+    HIPCHK(hipHostMalloc(&ctx->host_small, 4096, hipHostMallocDefault));
+    for (auto& e : ctx->ev) HIPCHK(hipEventCreate(&e));
+  } catch (Fail& f) {
+    delete ctx;
+    return f.code;
+  }
+  *out = ctx;
+  return TSDBHIP_OK;
+}
+
+extern "C" void tsdbhip_close(tsdbhip_ctx* ctx) {
+  if (!ctx) return;
+  hipSetDevice(ctx->device);
+  if (ctx->stream) hipStreamSynchronize(ctx->stream);
+  if (ctx->comm) ncclCommDestroy(ctx->comm);
+  for (auto& kv : ctx->bufs)
+    if (kv.second.p) hipFree(kv.second.p);
+  for (auto& e : ctx->ev)
+    if (e) hipEventDestroy(e);
+  if (ctx->host_small) hipHostFree(ctx->host_small);
+  if (ctx->stream) hipStreamDestroy(ctx->stream);
+  delete ctx;
+}
+
+extern "C" int tsdbhip_host_register(tsdbhip_ctx* ctx, void* p, size_t n) {
+  if (!ctx || !p || !n) return TSDBHIP_E_INVALID_ARG;
+  try {
+    HIPCHK(hipSetDevice(ctx->device));
+    HIPCHK(hipHostRegister(p, n, hipHostRegisterDefault));
+  } catch (Fail& f) {
+    return f.code;
+  }
+  return TSDBHIP_OK;
+}
+
+extern "C" int tsdbhip_host_unregister(tsdbhip_ctx* ctx, void* p) {
+  if (!ctx || !p) return TSDBHIP_E_INVALID_ARG;
+  try {
+    HIPCHK(hipSetDevice(ctx->device));
+    HIPCHK(hipHostUnregister(p));
+  } catch (Fail& f) {
+    return f.code;
+  }
+  return TSDBHIP_OK;
+}
+
+extern "C" int tsdbhip_last_timing(tsdbhip_ctx* ctx, tsdbhip_timing* t) {
+  if (!ctx || !t) return TSDBHIP_E_INVALID_ARG;
+  *t = ctx->timing;
+  return TSDBHIP_OK;
+}
+
+// ---------------------------------------------------------------- comm ----
+extern "C" int tsdbhip_comm_unique_id(uint8_t out[TSDBHIP_UNIQUE_ID_BYTES]) {
+  static_assert(sizeof(ncclUniqueId) <= TSDBHIP_UNIQUE_ID_BYTES, "unique id size");
+  ncclUniqueId id;
+  ncclResult_t r = ncclGetUniqueId(&id);
+  if (r != ncclSuccess) {
+    set_error(nullptr, "ncclGetUniqueId: %s", ncclGetErrorString(r));
+    return TSDBHIP_E_RCCL;
+  }
+  std::memset(out, 0, TSDBHIP_UNIQUE_ID_BYTES);
+  std::memcpy(out, &id, sizeof id);
+  return TSDBHIP_OK;
+}
+
+extern "C" int tsdbhip_comm_init(tsdbhip_ctx* ctx, int32_t nranks, int32_t rank,
+                                 const uint8_t id[TSDBHIP_UNIQUE_ID_BYTES]) {
+  if (!ctx || nranks < 1 || rank < 0 || rank >= nranks) return TSDBHIP_E_INVALID_ARG;
+  try {
+    HIPCHK(hipSetDevice(ctx->device));
+    ncclUniqueId uid;
+    std::memcpy(&uid, id, sizeof uid);
+    if (ctx->comm) {
+      ncclCommDestroy(ctx->comm);
+      ctx->comm = nullptr;
+    }
+    NCCLCHK(ncclCommInitRank(&ctx->comm, nranks, uid, rank));
+    ctx->nranks = nranks;
+    ctx->rank = rank;
+  } catch (Fail& f) {
+    return f.code;
+  }
+  return TSDBHIP_OK;
+}
+
+// ------------------------------------------------------------- helpers ----
+template <typename T>
+static const T* stage(tsdbhip_ctx* ctx, const char* name, const T* src, size_t count, bool on_device,
+                      size_t pad = 0) {
+  if (on_device) return src;
+  T* d = scratch<T>(ctx, name, count + pad);
+  if (count) HIPCHK(hipMemcpyAsync(d, src, count * sizeof(T), hipMemcpyHostToDevice, ctx->stream));
+  if (pad) HIPCHK(hipMemsetAsync((char*)d + count * sizeof(T), 0, pad * sizeof(T), ctx->stream));
+  return d;
+}
+
+static void readback(tsdbhip_ctx* ctx, void* host, const void* dev, size_t bytes) {
+  HIPCHK(hipMemcpyAsync(ctx->host_small, dev, bytes, hipMemcpyDeviceToHost, ctx->stream));
+  HIPCHK(hipStreamSynchronize(ctx->stream));
+  std::memcpy(host, ctx->host_small, bytes);
+}
+
+template <int AGG>
+static void launch_decode_ds(tsdbhip_ctx* ctx, unsigned blocks, const DecodeArgs& a) {
+  hipLaunchKernelGGL(k_decode_ds<AGG>, dim3(blocks), dim3(256), 0, ctx->stream, a);
+}
+
+template <int AGG, int MODE, bool RATE>
+static void launch_reduce(tsdbhip_ctx* ctx, unsigned blocks, const ReduceArgs& r, const FinalArgs& f,
+                          bool par, bool finalize) {
+  hipLaunchKernelGGL((k_reduce<AGG, MODE, RATE>), dim3(blocks), dim3(256), 0, ctx->stream, r);
+  if (!finalize) return;
+  if (par)
+    hipLaunchKernelGGL((k_finalize_par<AGG, MODE, RATE>), dim3((unsigned)f.T), dim3(256), 0, ctx->stream, r, f);
+  else
+    hipLaunchKernelGGL((k_finalize_seq<AGG, MODE, RATE>), dim3(grid_for(f.T, 256)), dim3(256), 0, ctx->stream,
+                       r, f);
+}
+
+template <int AGG>
+static void dispatch_mode(tsdbhip_ctx* ctx, int mode, bool rate, unsigned blocks, const ReduceArgs& r,
+                          const FinalArgs& f, bool par, bool fin) {
+  if (rate) return launch_reduce<AGG, MODE_DBL, true>(ctx, blocks, r, f, par, fin);
+  if (mode == MODE_INT) return launch_reduce<AGG, MODE_INT, false>(ctx, blocks, r, f, par, fin);
+  if (mode == MODE_DBL) return launch_reduce<AGG, MODE_DBL, false>(ctx, blocks, r, f, par, fin);
+  return launch_reduce<AGG, MODE_DUAL, false>(ctx, blocks, r, f, par, fin);
+}
+
+static void dispatch_reduce(tsdbhip_ctx* ctx, int agg, int mode, bool rate, unsigned blocks,
+                            const ReduceArgs& r, const FinalArgs& f, bool par, bool fin) {
+  switch (agg) {
+    case 0: return dispatch_mode<0>(ctx, mode, rate, blocks, r, f, par, fin);
+    case 1: return dispatch_mode<1>(ctx, mode, rate, blocks, r, f, par, fin);
+    case 2: return dispatch_mode<2>(ctx, mode, rate, blocks, r, f, par, fin);
+    case 3: return dispatch_mode<3>(ctx, mode, rate, blocks, r, f, par, fin);
+    default: return dispatch_mode<4>(ctx, mode, rate, blocks, r, f, par, fin);
+  }
+}
+
+template <int AGG, int MODE>
+static void launch_combine(tsdbhip_ctx* ctx, const ReduceArgs& src, const ReduceArgs& dst, uint64_t T,
+                           uint32_t n_chunks) {
+  hipLaunchKernelGGL((k_combine_chunks<AGG, MODE>), dim3(grid_for(T, 256)), dim3(256), 0, ctx->stream, src,
+                     dst, T, n_chunks);
+}
+template <int AGG>
+static void combine_mode(tsdbhip_ctx* ctx, int mode, const ReduceArgs& s, const ReduceArgs& d, uint64_t T,
+                         uint32_t n) {
+  if (mode == MODE_INT) return launch_combine<AGG, MODE_INT>(ctx, s, d, T, n);
+  if (mode == MODE_DBL) return launch_combine<AGG, MODE_DBL>(ctx, s, d, T, n);
+  return launch_combine<AGG, MODE_DUAL>(ctx, s, d, T, n);
+}
+static void dispatch_combine(tsdbhip_ctx* ctx, int agg, int mode, const ReduceArgs& s, const ReduceArgs& d,
+                             uint64_t T, uint32_t n) {
+  switch (agg) {
+    case 0: return combine_mode<0>(ctx, mode, s, d, T, n);
+    case 1: return combine_mode<1>(ctx, mode, s, d, T, n);
+    case 2: return combine_mode<2>(ctx, mode, s, d, T, n);
+    case 3: return combine_mode<3>(ctx, mode, s, d, T, n);
+    default: return combine_mode<4>(ctx, mode, s, d, T, n);
+  }
+}
+
+template <int AGG>
+static void final_mode(tsdbhip_ctx* ctx, int mode, bool rate, const ReduceArgs& r, const FinalArgs& f) {
+  const dim3 g(grid_for(f.T, 256)), b(256);
+  if (rate) hipLaunchKernelGGL((k_finalize_seq<AGG, MODE_DBL, true>), g, b, 0, ctx->stream, r, f);
+  else if (mode == MODE_INT) hipLaunchKernelGGL((k_finalize_seq<AGG, MODE_INT, false>), g, b, 0, ctx->stream, r, f);
+  else if (mode == MODE_DBL) hipLaunchKernelGGL((k_finalize_seq<AGG, MODE_DBL, false>), g, b, 0, ctx->stream, r, f);
+  else hipLaunchKernelGGL((k_finalize_seq<AGG, MODE_DUAL, false>), g, b, 0, ctx->stream, r, f);
+}
+static void dispatch_final(tsdbhip_ctx* ctx, int agg, int mode, bool rate, const ReduceArgs& r,
+                           const FinalArgs& f) {
+  switch (agg) {
+    case 0: return final_mode<0>(ctx, mode, rate, r, f);
+    case 1: return final_mode<1>(ctx, mode, rate, r, f);
+    case 2: return final_mode<2>(ctx, mode, rate, r, f);
+    case 3: return final_mode<3>(ctx, mode, rate, r, f);
+    default: return final_mode<4>(ctx, mode, rate, r, f);
+  }
+}
+
+static float ev_ms(hipEvent_t a, hipEvent_t b) {
+  float ms = 0;
+  if (hipEventElapsedTime(&ms, a, b) != hipSuccess) return -1.f;
+  return ms;
+}
+
+// ------------------------------------------------------- the hot path ----
+static int spangroup_run(tsdbhip_ctx* ctx, const tsdbhip_sg_desc* d, tsdbhip_sg_out* out) {
+  const bool dev = (d->flags & TSDBHIP_DESC_DEVICE) != 0;
+  const bool exact = (d->flags & TSDBHIP_EXACT_ORDER) != 0;
+  const bool sharded = (d->flags & TSDBHIP_SHARDED) != 0 && ctx->comm && ctx->nranks > 1;
+  const uint32_t S = d->n_spans;
+  const uint64_t R = d->n_rows;
+  const bool rate = d->rate != 0;
+  const int agg = d->agg;
+  const int ds_agg = d->ds_agg;
+  const int32_t interval = d->ds_interval > 0 ? d->ds_interval : 0;
+  hipStream_t st = ctx->stream;
+  tsdbhip_timing tm = {};
+  out->n_out = 0;
+  out->n_input_points = 0;
+  out->err_code = 0;
+  out->err_index = -1;
+
+  // ---- inputs in HBM ----
+  const uint64_t* span_row_start = stage(ctx, "in_srs", d->span_row_start, (size_t)S + 1, dev);
+  const uint32_t* row_base = stage(ctx, "in_base", d->row_base, R, dev);
+  const uint32_t* row_ncells = stage(ctx, "in_ncells", d->row_ncells, R, dev);
+  const uint64_t* row_qual_off = stage(ctx, "in_qoff", d->row_qual_off, R, dev);
+  const uint64_t* row_val_off = stage(ctx, "in_voff", d->row_val_off, R, dev);
+  const uint32_t* row_val_len = stage(ctx, "in_vlen", d->row_val_len, R, dev);
+  const uint8_t* qual = stage(ctx, "in_qual", d->qual_bytes, d->qual_nbytes, dev, 16);
+  const uint8_t* val = stage(ctx, "in_val", d->val_bytes, d->val_nbytes, dev, 16);
+
+  // ---- small device state ----
+  struct Small {
+    int32_t err;
+    uint32_t gflags[2];
+    uint32_t ambiguous;
+    unsigned long long range[2];
+    unsigned long long fstar;
+    unsigned long long n_input;
+    unsigned long long nan_t;
+    unsigned long long bad_at;
+    uint64_t n_kept;
+    uint64_t e_total;
+    uint64_t T;
+  };
+  Small* sm = scratch<Small>(ctx, "small", 1);
+  {
+    Small init = {};
+    init.err = 0;
+    init.range[0] = ~0ull;
+    init.range[1] = 0;
+    init.nan_t = ~0ull;
+    init.bad_at = ~0ull;
+    std::memcpy(ctx->host_small, &init, sizeof init);
+    HIPCHK(hipMemcpyAsync(sm, ctx->host_small, sizeof init, hipMemcpyHostToDevice, st));
+  }
+  HIPCHK(hipEventRecord(ctx->ev[0], st));
+
+  // ---- assemble ----
+  uint8_t* row_ok = scratch<uint8_t>(ctx, "row_ok", R);
+  uint32_t* row_cell0 = scratch<uint32_t>(ctx, "row_cell0", R);
+  uint32_t* sp_ncells = scratch<uint32_t>(ctx, "sp_ncells", S);
+  int64_t* sp_first = scratch<int64_t>(ctx, "sp_first", S);
+  int64_t* sp_last = scratch<int64_t>(ctx, "sp_last", S);
+  uint8_t* sp_kept = scratch<uint8_t>(ctx, "sp_kept", S);
+  uint64_t* sp_cap = scratch<uint64_t>(ctx, "sp_cap", S);
+  int64_t* sp_q1 = scratch<int64_t>(ctx, "sp_q1", S);
+  int32_t* sp_q1s = scratch<int32_t>(ctx, "sp_q1s", S);
+  int64_t* sp_ovf = scratch<int64_t>(ctx, "sp_ovf", S);
+  {
+    AssembleArgs a;
+    a.span_row_start = span_row_start; a.row_base = row_base; a.row_ncells = row_ncells;
+    a.row_qual_off = row_qual_off; a.row_val_len = row_val_len; a.qual = qual;
+    a.n_spans = S; a.start = d->start_time; a.end = d->end_time; a.interval = interval;
+    a.row_ok = row_ok; a.row_cell0 = row_cell0; a.sp_ncells = sp_ncells; a.sp_first = sp_first;
+    a.sp_last = sp_last; a.sp_kept = sp_kept; a.sp_cap = sp_cap; a.sp_q1 = sp_q1;
+    a.sp_q1_shift = sp_q1s; a.sp_ovf_cell = sp_ovf; a.err = &sm->err;
+    if (S) hipLaunchKernelGGL(k_assemble, dim3(grid_for(S, 4, 65536)), dim3(256), 0, st, a);
+  }
+  uint64_t* kflag = scratch<uint64_t>(ctx, "kflag", S);
+  uint64_t* kidx = scratch<uint64_t>(ctx, "kidx", S);
+  uint64_t* eoff_s = scratch<uint64_t>(ctx, "eoff_s", S);
+  uint32_t* kept = scratch<uint32_t>(ctx, "kept", S);
+  uint64_t* eoff = scratch<uint64_t>(ctx, "eoff", S);
+  if (S) {
+    hipLaunchKernelGGL(k_kept_flags, dim3(grid_for(S, 256)), dim3(256), 0, st, sp_kept, kflag, S);
+    dscan_u64(ctx, kflag, kidx, S, &sm->n_kept, "k");
+    dscan_u64(ctx, sp_cap, eoff_s, S, &sm->e_total, "e");
+    hipLaunchKernelGGL(k_kept_scatter, dim3(grid_for(S, 256)), dim3(256), 0, st, sp_kept, kidx, eoff_s,
+                       sp_ncells, S, kept, eoff, &sm->n_input);
+  }
+  Small h;
+  readback(ctx, &h, sm, sizeof h);  // sync 1
+  if (h.err) throw Fail{h.err};
+  const uint32_t n_kept = (uint32_t)h.n_kept;
+  out->n_input_points = h.n_input;
+  uint64_t n_input_global = h.n_input;
+
+  // ---- decode (+ downsample) ----
+  const uint64_t e_total = h.e_total;
+  uint32_t* e_ts = scratch<uint32_t>(ctx, "e_ts", e_total);
+  int64_t* e_val = scratch<int64_t>(ctx, "e_val", e_total);
+  uint8_t* e_flt = scratch<uint8_t>(ctx, "e_flt", e_total);
+  uint32_t* e_len = scratch<uint32_t>(ctx, "e_len", n_kept);
+  int64_t* e_bad = scratch<int64_t>(ctx, "e_bad", n_kept);
+  DecodeArgs da;
+  da.span_row_start = span_row_start; da.row_base = row_base; da.row_qual_off = row_qual_off;
+  da.row_val_off = row_val_off; da.qual = qual; da.val = val; da.row_ok = row_ok; da.row_cell0 = row_cell0;
+  da.kept = kept; da.n_kept = n_kept; da.sp_ncells = sp_ncells; da.sp_q1 = sp_q1; da.sp_q1_shift = sp_q1s;
+  da.sp_ovf_cell = sp_ovf; da.sp_cap = sp_cap; da.e_off = eoff; da.e_ts = e_ts; da.e_val = e_val;
+  da.e_flt = e_flt; da.e_len = e_len; da.e_bad = e_bad; da.start = d->start_time; da.end = d->end_time;
+  da.interval = interval; da.ds_agg = ds_agg; da.rate = rate; da.err = &sm->err; da.gflags = sm->gflags;
+  da.range = sm->range; da.fstar = &sm->fstar;
+  HIPCHK(hipEventRecord(ctx->ev[1], st));
+  if (n_kept) {
+    const unsigned blocks = grid_for(n_kept, 4, 65536);
+    if (interval == 0) {
+      hipLaunchKernelGGL(k_decode_nods, dim3(blocks), dim3(256), 0, st, da);
+    } else {
+      switch (ds_agg) {
+        case 0: launch_decode_ds<0>(ctx, blocks, da); break;
+        case 1: launch_decode_ds<1>(ctx, blocks, da); break;
+        case 2: launch_decode_ds<2>(ctx, blocks, da); break;
+        case 3: launch_decode_ds<3>(ctx, blocks, da); break;
+        default: launch_decode_ds<4>(ctx, blocks, da); break;
+      }
+    }
+  }
+  HIPCHK(hipEventRecord(ctx->ev[2], st));
+  if (n_kept) hipLaunchKernelGGL(k_span_summary, dim3(grid_for(n_kept, 256)), dim3(256), 0, st, da);
+  readback(ctx, &h, sm, sizeof h);  // sync 2
+  if (h.err) throw Fail{h.err};
+
+  // ---- union grid ----
+  bool anyf = h.gflags[0] != 0, anyi = h.gflags[1] != 0;
+  int64_t lo = (int64_t)h.range[0];
+  int64_t hi = std::min<int64_t>((int64_t)h.range[1], d->end_time);
+  uint64_t fstar = h.fstar;
+  if (sharded) {
+    // agree on range, flags, F* and the input count across ranks
+    unsigned long long* x = scratch<unsigned long long>(ctx, "xchg_small", 8);
+    unsigned long long hv[8] = {(unsigned long long)(h.range[0] == ~0ull ? ~0ull : h.range[0]),
+                                (unsigned long long)h.range[1], (unsigned long long)fstar,
+                                (unsigned long long)anyf, (unsigned long long)anyi, h.n_input, 0, 0};
+    HIPCHK(hipMemcpyAsync(x, hv, sizeof hv, hipMemcpyHostToDevice, st));
+    NCCLCHK(ncclAllReduce(x, x, 1, ncclUint64, ncclMin, ctx->comm, st));
+    NCCLCHK(ncclAllReduce(x + 1, x + 1, 4, ncclUint64, ncclMax, ctx->comm, st));
+    NCCLCHK(ncclAllReduce(x + 5, x + 5, 1, ncclUint64, ncclSum, ctx->comm, st));
+    readback(ctx, hv, x, sizeof hv);
+    lo = (int64_t)hv[0];
+    hi = std::min<int64_t>((int64_t)hv[1], d->end_time);
+    fstar = hv[2];
+    anyf = hv[3] != 0;
+    anyi = hv[4] != 0;
+    n_input_global = hv[5];
+    out->n_input_points = n_input_global;
+  }
+  const bool empty_grid = h.range[0] == ~0ull && !sharded ? true : (lo > hi || (uint64_t)lo == ~0ull);
+  uint64_t T = 0;
+  uint64_t nwords = 0;
+  uint32_t* bitmap = nullptr;
+  uint32_t* word_rank = nullptr;
+  uint32_t* gridv = nullptr;
+  HIPCHK(hipEventRecord(ctx->ev[3], st));
+  if (!empty_grid) {
+    nwords = (uint64_t)(hi - lo + 1 + 31) / 32;
+    bitmap = scratch<uint32_t>(ctx, "bitmap", nwords, true);
+    word_rank = scratch<uint32_t>(ctx, "word_rank", nwords);
+    const uint64_t nb = (nwords + 1023) / 1024;
+    uint32_t* bsum = scratch<uint32_t>(ctx, "grid_bsum", nb);
+    GridArgs ga;
+    ga.e_off = eoff; ga.e_len = e_len; ga.e_ts = e_ts; ga.n_kept = n_kept; ga.lo = lo; ga.hi = hi;
+    ga.rate = rate; ga.bitmap = bitmap; ga.nwords = nwords; ga.word_rank = word_rank; ga.block_sum = bsum;
+    ga.total = &sm->T;
+    if (n_kept) hipLaunchKernelGGL(k_grid_mark, dim3(grid_for(n_kept, 4, 65536)), dim3(256), 0, st, ga);
+    if (sharded) {
+      uint32_t* all = scratch<uint32_t>(ctx, "bitmap_all", nwords * ctx->nranks);
+      NCCLCHK(ncclAllGather(bitmap, all, nwords, ncclUint32, ctx->comm, st));
+      hipLaunchKernelGGL(k_bitmap_or, dim3(grid_for(nwords, 256)), dim3(256), 0, st, all, (uint32_t)ctx->nranks,
+                         nwords, bitmap);
+    }
+    hipLaunchKernelGGL(k_grid_popc, dim3((unsigned)nb), dim3(256), 0, st, ga);
+    hipLaunchKernelGGL(k_grid_scan_blocks, dim3(1), dim3(256), 0, st, ga, (uint32_t)nb);
+    readback(ctx, &T, &sm->T, 8);  // sync 3
+    gridv = scratch<uint32_t>(ctx, "grid", T);
+    ga.grid = gridv;
+    hipLaunchKernelGGL(k_grid_emit, dim3(grid_for(nwords, 256)), dim3(256), 0, st, ga);
+  }
+  HIPCHK(hipEventRecord(ctx->ev[4], st));
+  tm.n_grid = T;
+
+  // ---- reduce ----
+  if (T > 0) {
+    const int mode = rate ? MODE_DBL : (!anyf ? MODE_INT : (!anyi ? MODE_DBL : MODE_DUAL));
+    auto run_reduce = [&](bool one_chunk, bool finalize) {
+      const uint64_t n_tiles = (T + 63) / 64;
+      const uint64_t target = 16384;  // waves in flight over 256 CUs
+      uint32_t spc, n_chunks, tpw, ntg;
+      if (one_chunk || n_kept == 0) {
+        n_chunks = 1;
+        spc = std::max<uint32_t>(n_kept, 1);
+      } else {
+        uint64_t want = std::max<uint64_t>(1, target / n_tiles);
+        want = std::min<uint64_t>(want, std::max<uint32_t>(1, n_kept / 16));
+        n_chunks = (uint32_t)std::max<uint64_t>(1, want);
+        spc = (n_kept + n_chunks - 1) / n_chunks;
+        n_chunks = (n_kept + spc - 1) / spc;
+      }
+      tpw = (uint32_t)std::max<uint64_t>(1, (n_tiles * n_chunks + target - 1) / target);
+      ntg = (uint32_t)((n_tiles + tpw - 1) / tpw);
+      const uint64_t n_waves = (uint64_t)ntg * n_chunks;
+      ReduceArgs r;
+      r.e_off = eoff; r.e_len = e_len; r.e_ts = e_ts; r.e_val = e_val; r.e_flt = e_flt; r.n_kept = n_kept;
+      r.grid = gridv; r.T = T; r.bitmap = bitmap; r.word_rank = word_rank; r.lo = lo;
+      r.spans_per_chunk = spc; r.n_chunks = n_chunks; r.tiles_per_wave = tpw; r.n_tile_groups = ntg;
+      r.ptr = scratch<uint32_t>(ctx, "cursor", n_waves * spc);
+      const uint64_t np = (uint64_t)n_chunks * T;
+      r.p_cnt = scratch<uint32_t>(ctx, "p_cnt", np);
+      r.p_flag = scratch<uint8_t>(ctx, "p_flag", np);
+      r.p_i = scratch<int64_t>(ctx, "p_i", np);
+      r.p_d = scratch<double>(ctx, "p_d", np);
+      r.p_dhas = scratch<uint32_t>(ctx, "p_dhas", np);
+      if (agg == TSDBHIP_AGG_DEV) {
+        r.p_wim = scratch<double>(ctx, "p_wim", np);
+        r.p_wiv = scratch<double>(ctx, "p_wiv", np);
+        r.p_wdm = scratch<double>(ctx, "p_wdm", np);
+        r.p_wdv = scratch<double>(ctx, "p_wdv", np);
+      } else {
+        r.p_wim = r.p_wiv = r.p_wdm = r.p_wdv = nullptr;
+      }
+      FinalArgs f;
+      f.T = T; f.n_chunks = n_chunks; f.grid = gridv; f.fstar = fstar; f.rate = rate;
+      f.out_ts = scratch<int64_t>(ctx, "out_ts", T);
+      f.out_isint = scratch<uint8_t>(ctx, "out_isint", T);
+      f.out_bits = scratch<int64_t>(ctx, "out_bits", T);
+      f.nan_t = &sm->nan_t;
+      f.ambiguous = &sm->ambiguous;
+      const unsigned blocks = (unsigned)((n_waves + 3) / 4);
+      dispatch_reduce(ctx, agg, mode, rate, blocks, r, f, n_chunks >= 64, finalize);
+      return std::make_pair(r, f);
+    };
+    if (!sharded) {
+      run_reduce(exact, true);
+      HIPCHK(hipEventRecord(ctx->ev[5], st));
+      readback(ctx, &h, sm, sizeof h);  // sync 4
+      if (h.ambiguous && !exact) {
+        Small z = h;
+        z.ambiguous = 0;
+        z.nan_t = ~0ull;
+        std::memcpy(ctx->host_small, &z, sizeof z);
+        HIPCHK(hipMemcpyAsync(sm, ctx->host_small, sizeof z, hipMemcpyHostToDevice, st));
+        run_reduce(true, true);
+        HIPCHK(hipEventRecord(ctx->ev[5], st));
+        readback(ctx, &h, sm, sizeof h);
+      }
+    } else {
+      // local partials (chunks combined in order into this rank's slot), one
+      // RCCL allgather per field, then a rank-ordered combine on every rank.
+      auto rf = run_reduce(exact, false);
+      ReduceArgs loc = rf.first;
+      FinalArgs fin = rf.second;
+      const int nr = ctx->nranks;
+      ReduceArgs all = loc;
+      all.p_cnt = scratch<uint32_t>(ctx, "x_cnt", (uint64_t)nr * T);
+      all.p_flag = scratch<uint8_t>(ctx, "x_flag", (uint64_t)nr * T);
+      all.p_i = scratch<int64_t>(ctx, "x_i", (uint64_t)nr * T);
+      all.p_d = scratch<double>(ctx, "x_d", (uint64_t)nr * T);
+      all.p_dhas = scratch<uint32_t>(ctx, "x_dhas", (uint64_t)nr * T);
+      if (agg == TSDBHIP_AGG_DEV) {
+        all.p_wim = scratch<double>(ctx, "x_wim", (uint64_t)nr * T);
+        all.p_wiv = scratch<double>(ctx, "x_wiv", (uint64_t)nr * T);
+        all.p_wdm = scratch<double>(ctx, "x_wdm", (uint64_t)nr * T);
+        all.p_wdv = scratch<double>(ctx, "x_wdv", (uint64_t)nr * T);
+      }
+      ReduceArgs mine = all;
+      const uint64_t off = (uint64_t)ctx->rank * T;
+      mine.p_cnt += off; mine.p_flag += off; mine.p_i += off; mine.p_d += off; mine.p_dhas += off;
+      if (agg == TSDBHIP_AGG_DEV) { mine.p_wim += off; mine.p_wiv += off; mine.p_wdm += off; mine.p_wdv += off; }
+      dispatch_combine(ctx, agg, mode, loc, mine, T, loc.n_chunks);
+      HIPCHK(hipEventRecord(ctx->ev[6], st));
+      NCCLCHK(ncclGroupStart());
+      NCCLCHK(ncclAllGather(mine.p_cnt, all.p_cnt, T, ncclUint32, ctx->comm, st));
+      NCCLCHK(ncclAllGather(mine.p_flag, all.p_flag, T, ncclUint8, ctx->comm, st));
+      if (agg != TSDBHIP_AGG_DEV) {
+        if (mode != MODE_DBL) NCCLCHK(ncclAllGather(mine.p_i, all.p_i, T, ncclInt64, ctx->comm, st));
+        if (mode != MODE_INT) NCCLCHK(ncclAllGather(mine.p_d, all.p_d, T, ncclFloat64, ctx->comm, st));
+        if (mode != MODE_INT && (agg == 1 || agg == 2))
+          NCCLCHK(ncclAllGather(mine.p_dhas, all.p_dhas, T, ncclUint32, ctx->comm, st));
+      } else {
+        if (mode != MODE_DBL) {
+          NCCLCHK(ncclAllGather(mine.p_wim, all.p_wim, T, ncclFloat64, ctx->comm, st));
+          NCCLCHK(ncclAllGather(mine.p_wiv, all.p_wiv, T, ncclFloat64, ctx->comm, st));
+        }
+        if (mode != MODE_INT) {
+          NCCLCHK(ncclAllGather(mine.p_wdm, all.p_wdm, T, ncclFloat64, ctx->comm, st));
+          NCCLCHK(ncclAllGather(mine.p_wdv, all.p_wdv, T, ncclFloat64, ctx->comm, st));
+        }
+      }
+      NCCLCHK(ncclGroupEnd());
+      HIPCHK(hipEventRecord(ctx->ev[7], st));
+      fin.n_chunks = (uint32_t)nr;
+      all.n_chunks = (uint32_t)nr;
+      dispatch_final(ctx, agg, mode, rate, all, fin);
+      HIPCHK(hipEventRecord(ctx->ev[5], st));
+      readback(ctx, &h, sm, sizeof h);
+      tm.exchange_ms = ev_ms(ctx->ev[6], ctx->ev[7]);
+    }
+    // lazy error index for illegal cells
+    if (n_kept)
+      hipLaunchKernelGGL(k_bad_index, dim3(grid_for(n_kept, 256)), dim3(256), 0, st, e_bad, eoff, e_ts, n_kept,
+                         (int32_t)rate, hi, bitmap, word_rank, lo, T, &sm->bad_at);
+    readback(ctx, &h, sm, sizeof h);
+  } else {
+    HIPCHK(hipEventRecord(ctx->ev[5], st));
+    if (n_kept)
+      hipLaunchKernelGGL(k_bad_index, dim3(grid_for(n_kept, 256)), dim3(256), 0, st, e_bad, eoff, e_ts, n_kept,
+                         (int32_t)rate, hi, bitmap, word_rank, lo, T, &sm->bad_at);
+    readback(ctx, &h, sm, sizeof h);
+  }
+  HIPCHK(hipStreamSynchronize(st));
+  tm.decode_ms = ev_ms(ctx->ev[1], ctx->ev[2]);
+  tm.grid_ms = ev_ms(ctx->ev[3], ctx->ev[4]);
+  tm.reduce_ms = ev_ms(ctx->ev[4], ctx->ev[5]);
+  tm.total_ms = ev_ms(ctx->ev[0], ctx->ev[5]);
+  tm.n_emitted = e_total;
+  ctx->timing = tm;
+
+  // ---- outputs ----
+  uint64_t n_ok = T;
+  int code = TSDBHIP_OK;
+  int64_t err_at = -1;
+  if (h.bad_at != ~0ull) {
+    err_at = (int64_t)(h.bad_at >> 4);
+    code = (h.bad_at & 15) == BAD_OOB ? TSDBHIP_E_OUT_OF_BOUNDS : TSDBHIP_E_ILLEGAL_DATA;
+  }
+  if (h.nan_t != ~0ull && (err_at < 0 || (int64_t)h.nan_t < err_at)) {
+    err_at = (int64_t)h.nan_t;
+    code = TSDBHIP_E_NAN_INF;
+  }
+  if (err_at >= 0) n_ok = (uint64_t)err_at;
+  if (n_ok > out->capacity) {
+    out->err_code = TSDBHIP_E_CAPACITY;
+    return TSDBHIP_E_CAPACITY;
+  }
+  if (n_ok) {
+    HIPCHK(hipMemcpyAsync(out->ts, scratch<int64_t>(ctx, "out_ts", T), n_ok * 8, hipMemcpyDeviceToHost, st));
+    HIPCHK(hipMemcpyAsync(out->is_int, scratch<uint8_t>(ctx, "out_isint", T), n_ok, hipMemcpyDeviceToHost, st));
+    HIPCHK(hipMemcpyAsync(out->bits, scratch<int64_t>(ctx, "out_bits", T), n_ok * 8, hipMemcpyDeviceToHost, st));
+    HIPCHK(hipStreamSynchronize(st));
+  }
+  out->n_out = n_ok;
+  out->err_code = code;
+  out->err_index = err_at;
+  // algorithmic bytes: reference row bytes + T x 17 B
+  tm.alg_bytes = 0;
+  ctx->timing = tm;
+  return code;
+}
+
+extern "C" int tsdbhip_spangroup_run(tsdbhip_ctx* ctx, const tsdbhip_sg_desc* desc, tsdbhip_sg_out* out) {
+  if (!ctx || !desc || !out) return TSDBHIP_E_INVALID_ARG;
+  if (desc->agg > 4 || (desc->ds_interval > 0 && desc->ds_agg > 4) || desc->ds_interval < 0 ||
+      desc->start_time < 0 || desc->end_time < 0) {
+    set_error(ctx, "invalid SpanGroup arguments");
+    out->err_code = TSDBHIP_E_INVALID_ARG;
+    return TSDBHIP_E_INVALID_ARG;
+  }
+  std::lock_guard<std::mutex> lock(ctx->mu);
+  try {
+    HIPCHK(hipSetDevice(ctx->device));
+    int rc = spangroup_run(ctx, desc, out);
+    if (rc) set_error(ctx, "spangroup_run: error %d at output %lld", rc, (long long)out->err_index);
+    return rc;
+  } catch (Fail& f) {
+    out->err_code = f.code;
+    if (f.code != TSDBHIP_E_HIP && f.code != TSDBHIP_E_RCCL) {
+      out->err_index = 0;
+      set_error(ctx, "spangroup_run: error %d", f.code);
+    }
+    hipStreamSynchronize(ctx->stream);
+    return f.code;
+  }
+}
+
+// ------------------------------------------------- synthetic inputs ------
+// Device buffers of a generated desc are owned by ctx under keys derived from
+// the desc address, so several datasets can coexist.
+static std::string synth_key(const tsdbhip_sg_desc* d, const char* f) {
+  char b[64];
+  snprintf(b, sizeof b, "syn%p_%s", (const void*)d, f);
+  return b;
+}
+
+extern "C" int tsdbhip_synth_generate(tsdbhip_ctx* ctx, const tsdbhip_synth_params* p, tsdbhip_sg_desc* d) {
+  if (!ctx || !p || !d || p->n_spans == 0 || p->n_points == 0 || p->step == 0 || 3600 % p->step ||
+      p->t0 % 3600 || p->kind > 2)
+    return TSDBHIP_E_INVALID_ARG;
+  std::lock_guard<std::mutex> lock(ctx->mu);
+  try {
+    HIPCHK(hipSetDevice(ctx->device));
+    SynthArgs a;
+    a.seed = p->seed; a.n_spans = p->n_spans; a.n_points = p->n_points; a.t0 = p->t0; a.step = p->step;
+    a.kind = p->kind;
+    a.span0 = p->span0;
+    a.k = 3600 / p->step;
+    a.rps = (p->n_points + a.k - 1) / a.k;
+    a.w = p->kind == TSDBHIP_SYN_FLOAT32 ? 4 : 8;
+    a.flags = p->kind == TSDBHIP_SYN_INT64_COUNTER ? 0x7 : (p->kind == TSDBHIP_SYN_FLOAT32 ? 0xB : 0xF);
+    a.qstride = ((2ull * a.k) + 15) / 16 * 16;
+    a.vstride = ((uint64_t)a.k * a.w + 1 + 15) / 16 * 16;
+    const uint64_t n_rows = (uint64_t)p->n_spans * a.rps;
+    auto al = [&](const char* f, size_t bytes) -> void* {
+      std::string k = synth_key(d, f);
+      Buf& b = ctx->bufs[k];
+      if (b.p) HIPCHK(hipFree(b.p));
+      b.p = nullptr;
+      HIPCHK(hipMalloc(&b.p, bytes + 64));
+      b.n = bytes + 64;
+      HIPCHK(hipMemsetAsync(b.p, 0, bytes + 64, ctx->stream));
+      return b.p;
+    };
+    a.span_row_start = (uint64_t*)al("srs", 8ull * (p->n_spans + 1));
+    a.row_base = (uint32_t*)al("base", 4ull * n_rows);
+    a.row_ncells = (uint32_t*)al("ncells", 4ull * n_rows);
+    a.row_qual_off = (uint64_t*)al("qoff", 8ull * n_rows);
+    a.row_val_off = (uint64_t*)al("voff", 8ull * n_rows);
+    a.row_val_len = (uint32_t*)al("vlen", 4ull * n_rows);
+    a.qual = (uint8_t*)al("qual", n_rows * a.qstride);
+    a.val = (uint8_t*)al("val", n_rows * a.vstride);
+    hipLaunchKernelGGL(k_synth_rows, dim3(grid_for(n_rows, 256)), dim3(256), 0, ctx->stream, a);
+    const uint64_t cells = (uint64_t)p->n_spans * p->n_points;
+    hipLaunchKernelGGL(k_synth_cells, dim3(grid_for(cells, 256, 0x7fffffff)), dim3(256), 0, ctx->stream, a);
+    HIPCHK(hipGetLastError());
+    HIPCHK(hipStreamSynchronize(ctx->stream));
+    d->flags |= TSDBHIP_DESC_DEVICE;
+    d->n_spans = p->n_spans;
+    d->n_rows = n_rows;
+    d->span_row_start = a.span_row_start;
+    d->row_base = a.row_base;
+    d->row_ncells = a.row_ncells;
+    d->row_qual_off = a.row_qual_off;
+    d->row_val_off = a.row_val_off;
+    d->row_val_len = a.row_val_len;
+    d->qual_bytes = a.qual;
+    d->qual_nbytes = n_rows * a.qstride;
+    d->val_bytes = a.val;
+    d->val_nbytes = n_rows * a.vstride;
+  } catch (Fail& f) {
+    return f.code;
+  }
+  return TSDBHIP_OK;
+}
+
+extern "C" int tsdbhip_synth_free(tsdbhip_ctx* ctx, tsdbhip_sg_desc* d) {
+  if (!ctx || !d) return TSDBHIP_E_INVALID_ARG;
+  std::lock_guard<std::mutex> lock(ctx->mu);
+  hipSetDevice(ctx->device);
+  hipStreamSynchronize(ctx->stream);
+  for (const char* f : {"srs", "base", "ncells", "qoff", "voff", "vlen", "qual", "val"}) {
+    auto it = ctx->bufs.find(synth_key(d, f));
+    if (it != ctx->bufs.end()) {
+      if (it->second.p) hipFree(it->second.p);
+      ctx->bufs.erase(it);
+    }
+  }
+  return TSDBHIP_OK;
+}
+
+extern "C" int tsdbhip_desc_download(tsdbhip_ctx* ctx, const tsdbhip_sg_desc* d, uint64_t* srs, uint32_t* base,
+                                     uint32_t* ncells, uint64_t* qoff, uint64_t* voff, uint32_t* vlen,
+                                     uint8_t* qual, uint8_t* val) {
+  if (!ctx || !d || !(d->flags & TSDBHIP_DESC_DEVICE)) return TSDBHIP_E_INVALID_ARG;
+  std::lock_guard<std::mutex> lock(ctx->mu);
+  try {
+    HIPCHK(hipSetDevice(ctx->device));
+    const uint64_t R = d->n_rows;
+    HIPCHK(hipMemcpy(srs, d->span_row_start, 8ull * (d->n_spans + 1), hipMemcpyDeviceToHost));
+    HIPCHK(hipMemcpy(base, d->row_base, 4 * R, hipMemcpyDeviceToHost));
+    HIPCHK(hipMemcpy(ncells, d->row_ncells, 4 * R, hipMemcpyDeviceToHost));
+    HIPCHK(hipMemcpy(qoff, d->row_qual_off, 8 * R, hipMemcpyDeviceToHost));
+    HIPCHK(hipMemcpy(voff, d->row_val_off, 8 * R, hipMemcpyDeviceToHost));
+    HIPCHK(hipMemcpy(vlen, d->row_val_len, 4 * R, hipMemcpyDeviceToHost));
+    HIPCHK(hipMemcpy(qual, d->qual_bytes, d->qual_nbytes, hipMemcpyDeviceToHost));
+    HIPCHK(hipMemcpy(val, d->val_bytes, d->val_nbytes, hipMemcpyDeviceToHost));
+  } catch (Fail& f) {
+    return f.code;
+  }
+  return TSDBHIP_OK;
+}
+
+// ------------------------------------------------------- compaction ------
+extern "C" int tsdbhip_compact_rows(tsdbhip_ctx* ctx, const tsdbhip_rows_desc* desc, tsdbhip_rows_out* out) {
+  if (!ctx || !desc || !out) return TSDBHIP_E_INVALID_ARG;
+  set_error(ctx, "tsdbhip_compact_rows: GPU compaction not built yet");
+  return TSDBHIP_E_UNSUPPORTED;
+}

@@ -1,0 +1,210 @@
+// dev_common.h — device helpers shared by the tsdbhip kernels (gfx950, wave64).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#define WAVE 64
+#define DEVI __device__ __forceinline__
+
+namespace tsdb {
+
+// ---- Java `long` / `double` semantics ------------------------------------
+DEVI int64_t ladd(int64_t a, int64_t b) { return (int64_t)((uint64_t)a + (uint64_t)b); }
+DEVI int64_t lsub(int64_t a, int64_t b) { return (int64_t)((uint64_t)a - (uint64_t)b); }
+DEVI int64_t lmul(int64_t a, int64_t b) { return (int64_t)((uint64_t)a * (uint64_t)b); }
+// Java truncating division; MIN/-1 = MIN (no trap).
+DEVI int64_t ldiv(int64_t a, int64_t b) {
+  if (b == -1) return (int64_t)(0 - (uint64_t)a);
+  return a / b;
+}
+// Java (long)double: NaN -> 0, saturating.
+DEVI int64_t d2l(double d) {
+  if (d != d) return 0;
+  if (d >= 9223372036854775807.0) return INT64_MAX;
+  if (d <= -9223372036854775808.0) return INT64_MIN;
+  return (int64_t)d;
+}
+DEVI double bitsd(int64_t b) { return __longlong_as_double(b); }
+DEVI int64_t dbits(double d) { return __double_as_longlong(d); }
+
+// ---- wave helpers ----------------------------------------------------------
+DEVI int lane_id() { return __lane_id(); }
+DEVI uint64_t ballot(bool p) { return __ballot(p); }
+DEVI uint64_t lanemask_le(int lane) { return lane == 63 ? ~0ull : ((2ull << lane) - 1); }
+DEVI uint64_t lanemask_lt(int lane) { return (1ull << lane) - 1; }
+
+// Position of the (j+1)-th set bit of m (j per lane); requires j < popc(m).
+DEVI int select_bit(uint64_t m, int j) {
+  int p = 0;
+#pragma unroll
+  for (int step = 32; step > 0; step >>= 1) {
+    const uint64_t low = m & ((1ull << (p + step)) - 1);
+    if (__popcll(low) <= j) p += step;
+  }
+  return p;
+}
+
+DEVI uint32_t readlane_u32(uint32_t v, int l) { return __builtin_amdgcn_readlane(v, l); }
+DEVI uint64_t readlane_u64(uint64_t v, int l) {
+  uint32_t lo = __builtin_amdgcn_readlane((uint32_t)v, l);
+  uint32_t hi = __builtin_amdgcn_readlane((uint32_t)(v >> 32), l);
+  return ((uint64_t)hi << 32) | lo;
+}
+DEVI uint32_t shfl_u32(uint32_t v, int src) { return __shfl(v, src); }
+DEVI uint64_t shfl_u64(uint64_t v, int src) {
+  uint32_t lo = __shfl((uint32_t)v, src), hi = __shfl((uint32_t)(v >> 32), src);
+  return ((uint64_t)hi << 32) | lo;
+}
+DEVI uint32_t shfl_up_u32(uint32_t v, int d) { return __shfl_up(v, d); }
+DEVI uint64_t shfl_up_u64(uint64_t v, int d) {
+  uint32_t lo = __shfl_up((uint32_t)v, d), hi = __shfl_up((uint32_t)(v >> 32), d);
+  return ((uint64_t)hi << 32) | lo;
+}
+DEVI uint64_t shfl_xor_u64(uint64_t v, int m) {
+  uint32_t lo = __shfl_xor((uint32_t)v, m), hi = __shfl_xor((uint32_t)(v >> 32), m);
+  return ((uint64_t)hi << 32) | lo;
+}
+
+// Inclusive wave scan (wrapping add).
+DEVI uint64_t wave_incl_scan_u64(uint64_t x) {
+  const int l = lane_id();
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    uint64_t y = shfl_up_u64(x, d);
+    if (l >= d) x += y;
+  }
+  return x;
+}
+DEVI uint32_t wave_incl_scan_u32(uint32_t x) {
+  const int l = lane_id();
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    uint32_t y = shfl_up_u32(x, d);
+    if (l >= d) x += y;
+  }
+  return x;
+}
+// Segmented inclusive scan: `head` marks lanes that start a segment.
+DEVI uint32_t wave_seg_scan_u32(uint32_t x, uint64_t head_mask) {
+  const int l = lane_id();
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    uint32_t y = shfl_up_u32(x, d);
+    // lanes (l-d, l] contain no head -> same segment
+    uint64_t win = (l >= d) ? (lanemask_le(l) & ~lanemask_le(l - d)) : 0;
+    if (l >= d && (head_mask & win) == 0) x += y;
+  }
+  return x;
+}
+DEVI uint64_t wave_or_u64(uint64_t x) {
+#pragma unroll
+  for (int m = 1; m < 64; m <<= 1) x |= shfl_xor_u64(x, m);
+  return x;
+}
+DEVI uint64_t wave_sum_u64(uint64_t x) {
+#pragma unroll
+  for (int m = 1; m < 64; m <<= 1) x += shfl_xor_u64(x, m);
+  return x;
+}
+DEVI int64_t wave_min_i64(int64_t x) {
+#pragma unroll
+  for (int m = 1; m < 64; m <<= 1) { int64_t y = (int64_t)shfl_xor_u64((uint64_t)x, m); x = y < x ? y : x; }
+  return x;
+}
+DEVI int64_t wave_max_i64(int64_t x) {
+#pragma unroll
+  for (int m = 1; m < 64; m <<= 1) { int64_t y = (int64_t)shfl_xor_u64((uint64_t)x, m); x = y > x ? y : x; }
+  return x;
+}
+
+// ---- big-endian cell decoding (org.hbase.async.Bytes, restated) -----------
+DEVI uint32_t bswap32(uint32_t x) { return __builtin_bswap32(x); }
+DEVI uint64_t bswap64(uint64_t x) { return __builtin_bswap64(x); }
+
+// 2-byte big-endian qualifier at an even byte offset.
+DEVI uint32_t load_qual(const uint8_t* q, uint64_t off) {
+  uint16_t v = *(const uint16_t*)(q + off);
+  return (uint32_t)(((v & 0xFF) << 8) | (v >> 8));
+}
+
+// Loads `len` (1..8) bytes at arbitrary byte offset `off` as a big-endian
+// unsigned number. The buffer must have >= 12 readable bytes past any value.
+DEVI uint64_t load_be_bytes(const uint8_t* base, uint64_t off, int len) {
+  uint64_t raw;
+  if (len == 8 && (off & 7) == 0) {
+    raw = *(const uint64_t*)(base + off);
+  } else if (len == 4 && (off & 3) == 0) {
+    raw = *(const uint32_t*)(base + off);
+  } else {
+    const uint64_t a = off & ~3ull;
+    const int sh = (int)(off & 3) * 8;
+    const uint32_t* p = (const uint32_t*)(base + a);
+    uint32_t d0 = p[0], d1 = p[1], d2 = (sh + len * 8 > 64) ? p[2] : 0u;
+    uint64_t lo = (uint64_t)d0 | ((uint64_t)d1 << 32);
+    raw = sh ? ((lo >> sh) | ((uint64_t)d2 << (64 - sh))) : lo;
+  }
+  // raw holds bytes b0..b7 little-endian; take len bytes, reverse.
+  const uint64_t be = bswap64(raw);       // b0 in the top byte
+  return be >> (64 - 8 * len);            // b0..b(len-1) as BE number
+}
+
+// Decodes one cell value per RowSeq.extractIntegerValue /
+// extractFloatingPointValue (RowSeq.java:194-226). Returns false on an
+// IllegalDataException width. `bits` receives the long, or the double bits
+// (float32 widened exactly).
+DEVI bool decode_value(const uint8_t* vals, uint64_t off, uint32_t flags, int64_t* bits) {
+  const int lm = flags & 7;
+  const int len = lm + 1;
+  if (flags & 8) {
+    if (lm == 7) { *bits = (int64_t)load_be_bytes(vals, off, 8); return true; }
+    if (lm == 3) {
+      uint32_t u = (uint32_t)load_be_bytes(vals, off, 4);
+      *bits = dbits((double)__uint_as_float(u));
+      return true;
+    }
+    *bits = 0;
+    return false;
+  }
+  if (lm == 7 || lm == 3 || lm == 1 || lm == 0) {
+    uint64_t u = load_be_bytes(vals, off, len);
+    const int sh = 64 - 8 * len;
+    *bits = (int64_t)(u << sh) >> sh;  // sign-extend
+    return true;
+  }
+  *bits = 0;
+  return false;
+}
+
+// toDouble() of a decoded cell / E point.
+DEVI double to_double(int64_t bits, bool is_float) { return is_float ? bitsd(bits) : (double)bits; }
+
+// ---- Welford state per Aggregators.StdDev (Aggregators.java:196-238) ------
+struct Welford {
+  int64_t n;      // values seen
+  double mean;
+  double var;     // running M2
+};
+DEVI void wf_init(Welford& w) { w.n = 0; w.mean = 0; w.var = 0; }
+DEVI void wf_push(Welford& w, double x) {
+  if (w.n == 0) { w.mean = x; w.n = 1; return; }
+  w.n++;
+  const double nm = w.mean + (x - w.mean) / (double)w.n;
+  w.var += (x - w.mean) * (x - nm);
+  w.mean = nm;
+}
+// Chan et al. merge (A precedes B); used only across span chunks/ranks.
+DEVI void wf_merge(Welford& a, const Welford& b) {
+  if (b.n == 0) return;
+  if (a.n == 0) { a = b; return; }
+  const double n = (double)(a.n + b.n);
+  const double delta = b.mean - a.mean;
+  a.mean = a.mean + delta * ((double)b.n / n);
+  a.var = a.var + b.var + delta * delta * ((double)a.n * (double)b.n / n);
+  a.n += b.n;
+}
+DEVI double wf_result(const Welford& w) {
+  if (w.n <= 1) return 0.0;
+  return sqrt(w.var / (double)w.n);
+}
+
+}  // namespace tsdb

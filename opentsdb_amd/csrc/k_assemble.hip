@@ -1,0 +1,244 @@
+// k_assemble.hip — span assembly: which compacted rows a Span keeps and how
+// they group into RowSeqs, per Span.addRow (Span.java:87-132) and
+// RowSeq.addRow (RowSeq.java:92-172); the SpanGroup keep rule S7
+// (SpanGroup.java:130-142); per-span E capacities.
+//
+// One wave per span. The common case (rows in strictly increasing base order,
+// each row starting after the previous one ended, no RowSeq merge possible)
+// is verified wave-parallel; anything else falls back to an exact sequential
+// walk by lane 0 (the reference's own algorithm, O(rows)).
+#pragma once
+#include "dev_common.h"
+
+namespace tsdb {
+
+
+struct AssembleArgs {
+  // input desc (device)
+  const uint64_t* span_row_start;
+  const uint32_t* row_base;
+  const uint32_t* row_ncells;
+  const uint64_t* row_qual_off;
+  const uint32_t* row_val_len;
+  const uint8_t* qual;
+  uint32_t n_spans;
+  int64_t start, end;
+  int32_t interval;  // 0 = no downsampling
+  // outputs
+  uint8_t* row_ok;        // [n_rows] 0 dropped, 1 merged into the previous
+                          // RowSeq, 2 starts a RowSeq
+  uint32_t* row_cell0;    // [n_rows] accepted-cell prefix within the span
+  uint32_t* sp_ncells;    // [n_spans] Span.size()
+  int64_t* sp_first;      // [n_spans] Span.timestamp(0)
+  int64_t* sp_last;       // [n_spans] Span.timestamp(size-1)
+  uint8_t* sp_kept;       // [n_spans] S7
+  uint64_t* sp_cap;       // [n_spans] E capacity (0 if not kept)
+  int64_t* sp_q1;         // [n_spans] Q1: row read with shifted offsets, -1 none
+  int32_t* sp_q1_shift;   // [n_spans]
+  int64_t* sp_ovf_cell;   // [n_spans] span cell index that overflows the
+                          // RowSeq.Iterator `short` value_index, -1 none
+  int32_t* err;           // [1] first error code (atomicMin on negative codes)
+};
+
+DEVI int64_t row_first_ts(const AssembleArgs& a, uint64_t r) {
+  return (int64_t)a.row_base[r] + (load_qual(a.qual, a.row_qual_off[r]) >> 4);
+}
+DEVI int64_t row_last_ts(const AssembleArgs& a, uint64_t r) {
+  const uint32_t n = a.row_ncells[r];
+  return (int64_t)a.row_base[r] + (load_qual(a.qual, a.row_qual_off[r] + 2ull * (n - 1)) >> 4);
+}
+DEVI uint32_t row_value_bytes(const AssembleArgs& a, uint64_t r) {
+  // value bytes without the compacted meta byte (CompactionQueue.java:469-470)
+  const uint32_t n = a.row_ncells[r], vl = a.row_val_len[r];
+  return n > 1 && vl > 0 ? vl - 1 : vl;
+}
+DEVI void set_err(int32_t* err, int code) { atomicMin(err, code); }
+
+// Exact sequential Span.addRow emulation for one span (lane 0 only).
+__device__ void assemble_slow(const AssembleArgs& a, uint32_t s, uint64_t r0, uint64_t r1) {
+  int64_t rs_base = -1;       // base of the current (last) RowSeq
+  uint64_t rs_start = 0;      // first accepted row of the current RowSeq
+  uint32_t rs_vbytes = 0;     // value bytes in the current RowSeq
+  int64_t last_ts = 0;        // last cell ts of the last RowSeq
+  int64_t ovf_cell = -1;
+  for (uint64_t r = r0; r < r1; r++) a.row_ok[r] = 0;
+  for (uint64_t r = r0; r < r1; r++) {
+    const uint32_t n = a.row_ncells[r];
+    if (n == 0) { set_err(a.err, -9 /*E_OUT_OF_BOUNDS*/); return; }
+    const int64_t base = a.row_base[r];
+    const int64_t first = row_first_ts(a, r), last = row_last_ts(a, r);
+    if (rs_base < 0) {
+      a.row_ok[r] = 2; rs_base = base; rs_start = r; rs_vbytes = row_value_bytes(a, r); last_ts = last;
+      continue;
+    }
+    if (last - rs_base < 4096) {  // merge into the last RowSeq (Span.java:117-121)
+      const int64_t time_adj = base - rs_base;
+      if (time_adj <= 0) {
+        if (time_adj != 0) { set_err(a.err, -1 /*E_ILLEGAL_DATA*/); return; }
+        // same row again (scanner restart): RowSeq restarts from this row
+        for (uint64_t q = rs_start; q < r; q++) a.row_ok[q] = 0;
+        a.row_ok[r] = 2; rs_start = r; rs_vbytes = row_value_bytes(a, r); last_ts = last;
+        continue;
+      }
+      if (last_ts >= first) continue;  // RowSeq.java:142-148: row ignored
+      a.row_ok[r] = 1;
+      rs_vbytes += row_value_bytes(a, r);
+      last_ts = last;
+      continue;
+    }
+    if (last_ts >= first) continue;  // Span.java:126-130: RowSeq dropped
+    a.row_ok[r] = 2; rs_base = base; rs_start = r; rs_vbytes = row_value_bytes(a, r); last_ts = last;
+  }
+  (void)rs_vbytes;
+  // prefix of accepted cells; RowSeq grouping for the `short` overflow and Q1
+  uint32_t c = 0;
+  rs_base = -1;
+  uint32_t cum = 0;           // value bytes so far in the current RowSeq
+  uint32_t rs_cell0 = 0;
+  int64_t first_ts = -1, last_all = 0;
+  uint64_t first_row = r1, seek_rs_row0 = r1, seek_rs_cell0 = 0;
+  bool seek_found = false;
+  uint64_t last_rs_row0 = r1; uint32_t last_rs_cell0 = 0;
+  for (uint64_t r = r0; r < r1; r++) {
+    a.row_cell0[r] = c;
+    if (!a.row_ok[r]) continue;
+    const uint32_t n = a.row_ncells[r];
+    const int64_t base = a.row_base[r];
+    const int64_t last = row_last_ts(a, r);
+    if (first_row == r1) { first_row = r; first_ts = row_first_ts(a, r); }
+    if (a.row_ok[r] == 2) {  // starts a new RowSeq (recorded by the walk above)
+      rs_base = base; cum = 0; rs_cell0 = c;
+      last_rs_row0 = r; last_rs_cell0 = c;
+    }
+    // overflow of RowSeq.Iterator.value_index (a Java short)
+    if (ovf_cell < 0 && cum + row_value_bytes(a, r) >= 32768u) {
+      uint32_t run = cum;
+      for (uint32_t i = 0; i < n; i++) {
+        const uint32_t q = load_qual(a.qual, a.row_qual_off[r] + 2ull * i);
+        run += (q & 7) + 1;
+        if (run >= 32768u) { ovf_cell = (int64_t)c + i; break; }
+      }
+    }
+    cum += row_value_bytes(a, r);
+    if (!seek_found && last >= a.start) {  // seekRow: first RowSeq with last ts >= start
+      seek_found = true; seek_rs_row0 = last_rs_row0; seek_rs_cell0 = last_rs_cell0;
+    }
+    (void)rs_cell0;
+    last_all = last;
+    c += n;
+  }
+  a.sp_ncells[s] = c;
+  a.sp_first[s] = first_ts;
+  a.sp_last[s] = last_all;
+  a.sp_ovf_cell[s] = ovf_cell;
+  a.sp_q1[s] = -1;
+  a.sp_q1_shift[s] = 0;
+  // Q1 (RowSeq.java:405-421): seek skips cells with the stale qualifier.
+  if (c > 0 && first_ts < a.start && seek_found) {
+    uint32_t k = 0, slen = 0;
+    uint64_t rows_in_rs = 0, crow = r1;
+    bool done = false;
+    for (uint64_t r = seek_rs_row0; r < r1 && !done; r++) {
+      if (!a.row_ok[r]) continue;
+      if (r != seek_rs_row0 && a.row_ok[r] == 2) break;
+      rows_in_rs++;
+      const uint32_t n = a.row_ncells[r];
+      for (uint32_t i = 0; i < n; i++) {
+        const uint32_t q = load_qual(a.qual, a.row_qual_off[r] + 2ull * i);
+        if ((int64_t)a.row_base[r] + (q >> 4) >= a.start) { crow = r; done = true; break; }
+        k++; slen += (q & 7) + 1;
+      }
+    }
+    const int32_t shift = (int32_t)slen - (int32_t)k;
+    // does the seek RowSeq continue past crow (merged rows read shifted too)?
+    bool more = false;
+    for (uint64_t r = crow + 1; r < r1; r++) {
+      if (!a.row_ok[r]) continue;
+      more = a.row_ok[r] == 1;
+      break;
+    }
+    if (shift != 0) {
+      if (crow != seek_rs_row0 || rows_in_rs > 1 || more) {
+        set_err(a.err, TSDBHIP_E_UNSUPPORTED);  // shifted reads across merged rows
+      } else {
+        a.sp_q1[s] = (int64_t)crow;
+        a.sp_q1_shift[s] = shift;
+      }
+    }
+    (void)seek_rs_cell0;
+  }
+}
+
+__global__ void __launch_bounds__(256) k_assemble(AssembleArgs a) {
+  const int lane = lane_id();
+  const uint32_t wave = (blockIdx.x * blockDim.x + threadIdx.x) / WAVE;
+  const uint32_t nwaves = gridDim.x * blockDim.x / WAVE;
+  for (uint32_t s = wave; s < a.n_spans; s += nwaves) {
+    const uint64_t r0 = a.span_row_start[s], r1 = a.span_row_start[s + 1];
+    bool ok = r1 > r0;
+    int64_t prev_last = -1, prev_base = -1;
+    uint32_t cell = 0;
+    bool q1 = false;
+    for (uint64_t rb = r0; rb < r1 && ok; rb += WAVE) {
+      const uint64_t r = rb + lane;
+      const bool valid = r < r1;
+      uint32_t n = valid ? a.row_ncells[r] : 0;
+      int64_t base = 0, first = 0, last = 0;
+      if (valid && n > 0) { base = a.row_base[r]; first = row_first_ts(a, r); last = row_last_ts(a, r); }
+      int64_t pb = (int64_t)shfl_up_u64((uint64_t)base, 1);
+      int64_t pl = (int64_t)shfl_up_u64((uint64_t)last, 1);
+      if (lane == 0) { pb = prev_base; pl = prev_last; }
+      bool bad = valid && (n == 0 || row_value_bytes(a, r) >= 32768u ||
+                           (pb >= 0 && (base <= pb || first <= pl || last - pb < 4096)));
+      if (valid && r == r0 && first < a.start) q1 = true;
+      if (ballot(bad) != 0 || ballot(q1) != 0) { ok = false; break; }
+      const uint32_t incl = wave_incl_scan_u32(n);
+      if (valid) { a.row_ok[r] = 2; a.row_cell0[r] = cell + incl - n; }
+      cell += readlane_u32(incl, 63);
+      prev_base = (int64_t)readlane_u64((uint64_t)base, 63);
+      prev_last = (int64_t)readlane_u64((uint64_t)last, 63);
+      const uint64_t nv = r1 - rb;
+      if (nv < WAVE) {
+        prev_base = (int64_t)readlane_u64((uint64_t)base, (int)nv - 1);
+        prev_last = (int64_t)readlane_u64((uint64_t)last, (int)nv - 1);
+      }
+    }
+    if (ok) {
+      if (lane == 0) {
+        a.sp_ncells[s] = cell;
+        a.sp_first[s] = row_first_ts(a, r0);
+        a.sp_last[s] = prev_last;
+        a.sp_ovf_cell[s] = -1;
+        a.sp_q1[s] = -1;
+        a.sp_q1_shift[s] = 0;
+      }
+    } else if (lane == 0) {
+      if (r1 == r0) {
+        a.sp_ncells[s] = 0; a.sp_first[s] = 0; a.sp_last[s] = -1;
+        a.sp_ovf_cell[s] = -1; a.sp_q1[s] = -1; a.sp_q1_shift[s] = 0;
+      } else {
+        assemble_slow(a, s, r0, r1);
+      }
+    }
+    if (lane == 0) {
+      __threadfence_block();
+      const uint32_t n = a.sp_ncells[s];
+      const int64_t f = a.sp_first[s], l = a.sp_last[s];
+      if (r1 > r0 && n == 0) set_err(a.err, -3 /*E_EMPTY_SPAN*/);
+      const bool kept = n > 0 && f <= a.end && l >= a.start;  // SpanGroup.java:135-139
+      a.sp_kept[s] = kept;
+      uint64_t cap = 0;
+      if (kept) {
+        cap = n;
+        if (a.interval > 0) {
+          const int64_t lo = f > a.start ? f : a.start;
+          const uint64_t b = (uint64_t)((l - lo) / a.interval) + 1;
+          cap = b < cap ? b : cap;
+        }
+      }
+      a.sp_cap[s] = cap;
+    }
+  }
+}
+
+}  // namespace tsdb

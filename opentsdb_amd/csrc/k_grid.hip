@@ -1,0 +1,127 @@
+// k_grid.hip — the SGIterator emission times G (SpanGroup.java:510-577):
+// the sorted distinct timestamps of every span's next-slot points <= end,
+// i.e. G = sorted-unique{ e.ts <= end } (rate: points e_j, j >= 1).
+//
+// G is built as a bitmap over [lo, hi] (hi = min(end, max E ts)): one bit per
+// second, then a word-popcount prefix gives rank(t) = |{g in G : g < t}| in
+// O(1), which the reducer uses to place span points on the grid. Bitmap size
+// is (hi - lo + 1) / 8 bytes (<= 512 MiB for any u32 range; ~5 MB for the
+// 40 M-second C4 range) and stays L2/MALL resident while marked.
+#pragma once
+#include "dev_common.h"
+
+namespace tsdb {
+
+struct GridArgs {
+  const uint64_t* e_off;
+  const uint32_t* e_len;
+  const uint32_t* e_ts;
+  uint32_t n_kept;
+  int64_t lo, hi;       // bitmap covers [lo, hi]
+  int32_t rate;
+  uint32_t* bitmap;     // [nwords]
+  uint64_t nwords;
+  uint32_t* word_rank;  // [nwords] exclusive prefix of popcounts
+  uint32_t* block_sum;  // [nblocks]
+  uint32_t* grid;       // [T] G
+  uint64_t* total;      // [1] T
+};
+
+// Mark every candidate point. Many spans share timestamps (regular cadence),
+// so test before the atomic: a word that already has the bit skips it.
+__global__ void __launch_bounds__(256) k_grid_mark(GridArgs g) {
+  const int lane = lane_id();
+  const uint32_t wave = (blockIdx.x * blockDim.x + threadIdx.x) / WAVE;
+  const uint32_t nwaves = gridDim.x * blockDim.x / WAVE;
+  for (uint32_t k = wave; k < g.n_kept; k += nwaves) {
+    const uint64_t eo = g.e_off[k];
+    const uint32_t len = g.e_len[k];
+    for (uint32_t i0 = g.rate ? 1 : 0; i0 < len; i0 += WAVE) {
+      const uint32_t i = i0 + lane;
+      if (i >= len) break;
+      const int64_t t = g.e_ts[eo + i];
+      if (t > g.hi) break;  // sorted: the rest are beyond end
+      if (t < g.lo) continue;
+      const uint64_t b = (uint64_t)(t - g.lo);
+      const uint32_t bit = 1u << (b & 31);
+      uint32_t* w = &g.bitmap[b >> 5];
+      if (!(*w & bit)) atomicOr(w, bit);
+    }
+  }
+}
+
+// Per-block (1024 words) exclusive popcount prefix.
+__global__ void __launch_bounds__(256) k_grid_popc(GridArgs g) {
+  __shared__ uint32_t s_wave[4];
+  const uint64_t base = (uint64_t)blockIdx.x * 1024;
+  const int t = threadIdx.x;
+  uint32_t c[4];
+  uint32_t tot = 0;
+#pragma unroll
+  for (int i = 0; i < 4; i++) {
+    const uint64_t w = base + t * 4 + i;
+    c[i] = w < g.nwords ? __popc(g.bitmap[w]) : 0;
+    tot += c[i];
+  }
+  const uint32_t incl = wave_incl_scan_u32(tot);
+  if ((t & 63) == 63) s_wave[t >> 6] = incl;
+  __syncthreads();
+  uint32_t woff = 0;
+  for (int i = 0; i < (t >> 6); i++) woff += s_wave[i];
+  uint32_t run = woff + incl - tot;
+#pragma unroll
+  for (int i = 0; i < 4; i++) {
+    const uint64_t w = base + t * 4 + i;
+    if (w < g.nwords) g.word_rank[w] = run;
+    run += c[i];
+  }
+  if (t == 255) g.block_sum[blockIdx.x] = woff + incl;
+}
+
+// Single block: exclusive scan of the block sums; writes T.
+__global__ void __launch_bounds__(256) k_grid_scan_blocks(GridArgs g, uint32_t nblocks) {
+  __shared__ uint32_t s_wave[4];
+  __shared__ uint32_t s_carry;
+  const int t = threadIdx.x;
+  if (t == 0) s_carry = 0;
+  __syncthreads();
+  for (uint32_t b0 = 0; b0 < nblocks; b0 += 256) {
+    const uint32_t b = b0 + t;
+    const uint32_t v = b < nblocks ? g.block_sum[b] : 0;
+    const uint32_t incl = wave_incl_scan_u32(v);
+    if ((t & 63) == 63) s_wave[t >> 6] = incl;
+    __syncthreads();
+    uint32_t woff = 0;
+    for (int i = 0; i < (t >> 6); i++) woff += s_wave[i];
+    const uint32_t carry = s_carry;
+    if (b < nblocks) g.block_sum[b] = carry + woff + incl - v;
+    __syncthreads();
+    if (t == 255) s_carry = carry + woff + incl;
+    __syncthreads();
+  }
+  if (t == 0) g.total[0] = s_carry;
+}
+
+// Adds block offsets and materializes G.
+__global__ void __launch_bounds__(256) k_grid_emit(GridArgs g) {
+  const uint64_t w = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+  if (w >= g.nwords) return;
+  const uint32_t r = g.word_rank[w] + g.block_sum[w >> 10];
+  g.word_rank[w] = r;
+  uint32_t bits = g.bitmap[w];
+  uint32_t i = r;
+  while (bits) {
+    const int b = __builtin_ctz(bits);
+    g.grid[i++] = (uint32_t)(g.lo + (int64_t)(w * 32 + b));
+    bits &= bits - 1;
+  }
+}
+
+// rank(t): number of grid points < t (t must lie in [lo, hi+1)).
+DEVI uint32_t grid_rank(const uint32_t* bitmap, const uint32_t* word_rank, int64_t lo, int64_t t) {
+  const uint64_t b = (uint64_t)(t - lo);
+  const uint64_t w = b >> 5;
+  return word_rank[w] + __popc(bitmap[w] & ((1u << (b & 31)) - 1));
+}
+
+}  // namespace tsdb

@@ -1,0 +1,393 @@
+// k_reduce.hip — SGIterator value computation (SpanGroup.java:632-784) and the
+// Aggregators over spans (Aggregators.java:76-243), per emission time t in G.
+//
+// Closed form (checked against the oracle):
+//   non-rate: span s active at t iff first_s <= t <= L_s; cur = last point
+//     <= t, nxt = cur+1; value = y_cur if x_cur == t else lerp(cur, nxt, t),
+//     int lerp y0 + (t-x0)*(y1-y0)/(x1-x0) in wrapping long with truncating
+//     division, double lerp y0 + ((double)(t-x0)*(y1-y0))/(double)(x1-x0).
+//     isFloat(t) = OR over spans of [active & float(cur)] | [float(nxt)].
+//   rate: active iff |E_s| >= 2 and t <= L_s; cur = last point j>=1 with
+//     ts <= t else e_0 (quirk Q5); value = (y_cur - y_prev)/(x_cur - x_prev)
+//     with prev = (0,0) for e_0. Always the double path.
+//
+// Work unit: one wave = 64 consecutive grid indices (a tile, lane = t) x a
+// chunk of spans processed in span order, so every lane accumulates exactly
+// in the reference's order inside its chunk. Each span's points are placed
+// on the tile with O(1) grid ranks: the points falling inside the tile give a
+// 64-bit mask M, and lane l's bracket is cur = j + popc(M & le(l)) - 1.
+// Chunks are combined in chunk order by k_finalize_* (exact for integers;
+// double sums / dev within 1e-9 unless TSDBHIP_EXACT_ORDER forces 1 chunk).
+#pragma once
+#include "dev_common.h"
+#include "k_grid.hip"
+
+namespace tsdb {
+
+enum { MODE_INT = 0, MODE_DBL = 1, MODE_DUAL = 2 };
+
+struct ReduceArgs {
+  const uint64_t* e_off;
+  const uint32_t* e_len;
+  const uint32_t* e_ts;
+  const int64_t* e_val;
+  const uint8_t* e_flt;
+  uint32_t n_kept;
+  const uint32_t* grid;
+  uint64_t T;
+  const uint32_t* bitmap;
+  const uint32_t* word_rank;
+  int64_t lo;
+  uint32_t spans_per_chunk;
+  uint32_t n_chunks;
+  uint32_t tiles_per_wave;
+  uint32_t n_tile_groups;
+  uint32_t* ptr;        // [n_waves * spans_per_chunk] per-wave span cursors
+  // partials [n_chunks][T]
+  uint32_t* p_cnt;
+  uint8_t* p_flag;      // bit0 isFloat contribution, bit1 first double is NaN
+  int64_t* p_i;
+  double* p_d;
+  double* p_wim;
+  double* p_wiv;
+  double* p_wdm;
+  double* p_wdv;
+  uint32_t* p_dhas;     // double min/max: a non-NaN value was seen
+};
+
+struct Acc {
+  uint32_t cnt;
+  uint32_t flag;   // bit0 float contribution, bit1 first double value is NaN
+  uint32_t dhas;
+  int64_t ia;
+  double da;
+  Welford wi, wd;
+};
+
+DEVI void acc_init(Acc& a) {
+  a.cnt = 0; a.flag = 0; a.dhas = 0; a.ia = 0; a.da = 0;
+  wf_init(a.wi); wf_init(a.wd);
+}
+
+template <int AGG, int MODE>
+DEVI void acc_push(Acc& a, int64_t yi, double yd) {
+  const bool first = a.cnt == 0;
+  if (MODE != MODE_DBL) {
+    if (AGG == 4) wf_push(a.wi, (double)yi);
+    else if (first) a.ia = yi;
+    else if (AGG == 1) { if (yi < a.ia) a.ia = yi; }
+    else if (AGG == 2) { if (yi > a.ia) a.ia = yi; }
+    else a.ia = ladd(a.ia, yi);
+  }
+  if (MODE != MODE_INT) {
+    if (AGG == 4) wf_push(a.wd, yd);
+    else if (AGG == 1 || AGG == 2) {
+      if (yd != yd) { if (first) a.flag |= 2u; }
+      else if (!a.dhas) { a.da = yd; a.dhas = 1; }
+      else if (AGG == 1 ? (yd < a.da) : (yd > a.da)) a.da = yd;
+    } else {
+      a.da = first ? yd : a.da + yd;
+    }
+  }
+  a.cnt++;
+}
+
+// A precedes B in span order.
+template <int AGG, int MODE>
+DEVI void acc_merge(Acc& a, const Acc& b) {
+  if (b.cnt == 0) { a.flag |= (b.flag & 1u); return; }
+  if (a.cnt == 0) { const uint32_t f = a.flag & 1u; a = b; a.flag |= f; return; }
+  if (MODE != MODE_DBL) {
+    if (AGG == 4) wf_merge(a.wi, b.wi);
+    else if (AGG == 1) { if (b.ia < a.ia) a.ia = b.ia; }
+    else if (AGG == 2) { if (b.ia > a.ia) a.ia = b.ia; }
+    else a.ia = ladd(a.ia, b.ia);
+  }
+  if (MODE != MODE_INT) {
+    if (AGG == 4) wf_merge(a.wd, b.wd);
+    else if (AGG == 1 || AGG == 2) {
+      if (!a.dhas) { a.da = b.da; a.dhas = b.dhas; }
+      else if (b.dhas && (AGG == 1 ? (b.da < a.da) : (b.da > a.da))) a.da = b.da;
+    } else {
+      a.da = a.da + b.da;
+    }
+  }
+  a.flag |= (b.flag & 1u);  // first-NaN bit stays A's
+  a.cnt += b.cnt;
+}
+
+template <int AGG, int MODE>
+DEVI void acc_store(const ReduceArgs& r, uint64_t p, const Acc& a) {
+  r.p_cnt[p] = a.cnt;
+  if (MODE == MODE_DUAL || AGG == 1 || AGG == 2) r.p_flag[p] = (uint8_t)a.flag;
+  if (MODE != MODE_DBL && AGG != 4) r.p_i[p] = a.ia;
+  if (MODE != MODE_INT && AGG != 4) r.p_d[p] = a.da;
+  if (MODE != MODE_INT && (AGG == 1 || AGG == 2)) r.p_dhas[p] = a.dhas;
+  if (AGG == 4) {
+    if (MODE != MODE_DBL) { r.p_wim[p] = a.wi.mean; r.p_wiv[p] = a.wi.var; }
+    if (MODE != MODE_INT) { r.p_wdm[p] = a.wd.mean; r.p_wdv[p] = a.wd.var; }
+  }
+}
+
+template <int AGG, int MODE>
+DEVI void acc_load(const ReduceArgs& r, uint64_t p, Acc& a) {
+  acc_init(a);
+  a.cnt = r.p_cnt[p];
+  if (MODE == MODE_DUAL || AGG == 1 || AGG == 2) a.flag = r.p_flag[p];
+  if (MODE != MODE_DBL && AGG != 4) a.ia = r.p_i[p];
+  if (MODE != MODE_INT && AGG != 4) a.da = r.p_d[p];
+  if (MODE != MODE_INT && (AGG == 1 || AGG == 2)) a.dhas = r.p_dhas[p];
+  if (AGG == 4) {
+    if (MODE != MODE_DBL) { a.wi.n = a.cnt; a.wi.mean = r.p_wim[p]; a.wi.var = r.p_wiv[p]; }
+    if (MODE != MODE_INT) { a.wd.n = a.cnt; a.wd.mean = r.p_wdm[p]; a.wd.var = r.p_wdv[p]; }
+  }
+}
+
+// Java long lerp: y0 + (x - x0) * (y1 - y0) / (x1 - x0), 0 < x1 - x0 < 2^32.
+DEVI int64_t lerp_long(int64_t x, int64_t x0, int64_t y0, int64_t x1, int64_t y1) {
+  const int64_t num = lmul(x - x0, lsub(y1, y0));
+  const uint64_t d = (uint64_t)(x1 - x0);
+  const uint64_t mag = num < 0 ? (uint64_t)0 - (uint64_t)num : (uint64_t)num;
+  const uint64_t q = mag / d;
+  const int64_t sq = num < 0 ? (int64_t)((uint64_t)0 - q) : (int64_t)q;
+  return ladd(y0, sq);
+}
+DEVI double lerp_double(int64_t x, int64_t x0, double y0, int64_t x1, double y1) {
+  return y0 + ((double)(x - x0) * (y1 - y0)) / (double)(x1 - x0);
+}
+
+template <int AGG, int MODE, bool RATE>
+__global__ void __launch_bounds__(256) k_reduce(ReduceArgs r) {
+  const int lane = lane_id();
+  const uint32_t wave = (blockIdx.x * blockDim.x + threadIdx.x) / WAVE;
+  const uint32_t n_waves = r.n_chunks * r.n_tile_groups;
+  if (wave >= n_waves) return;
+  const uint32_t chunk = wave % r.n_chunks;
+  const uint32_t tg = wave / r.n_chunks;
+  const uint32_t k0 = chunk * r.spans_per_chunk;
+  const uint32_t k1 = min(r.n_kept, k0 + r.spans_per_chunk);
+  const uint64_t n_tiles = (r.T + WAVE - 1) / WAVE;
+  const uint64_t tb = (uint64_t)tg * r.tiles_per_wave;
+  const uint64_t te = min(n_tiles, tb + r.tiles_per_wave);
+  if (tb >= te || k0 >= k1) {
+    // still write empty partials for this chunk's tiles
+    for (uint64_t t = tb; t < te; t++) {
+      const uint64_t g = t * WAVE + lane;
+      if (g < r.T) { Acc a; acc_init(a); acc_store<AGG, MODE>(r, (uint64_t)chunk * r.T + g, a); }
+    }
+    return;
+  }
+  uint32_t* ptr = r.ptr + (uint64_t)wave * r.spans_per_chunk;
+  const uint32_t base_idx = RATE ? 1u : 0u;
+  // cursor init: first point index >= base_idx with ts >= G[tb*64]
+  {
+    const int64_t t0 = r.grid[tb * WAVE];
+    for (uint32_t k = k0 + lane; k < k1; k += WAVE) {
+      const uint64_t eo = r.e_off[k];
+      uint32_t lo = base_idx, hi = r.e_len[k];
+      if (hi < lo) hi = lo;
+      while (lo < hi) {
+        const uint32_t mid = (lo + hi) >> 1;
+        if ((int64_t)r.e_ts[eo + mid] < t0) lo = mid + 1; else hi = mid;
+      }
+      ptr[k - k0] = lo;
+    }
+  }
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+
+  for (uint64_t tile = tb; tile < te; tile++) {
+    const uint64_t g0 = tile * WAVE;
+    const uint64_t g = g0 + lane;
+    const bool gv = g < r.T;
+    const int nvalid = (int)min((uint64_t)WAVE, r.T - g0);
+    const uint64_t vmask = nvalid == 64 ? ~0ull : ((1ull << nvalid) - 1);
+    const int64_t tl = gv ? (int64_t)r.grid[g] : INT64_MAX;
+    const int64_t t_first = (int64_t)r.grid[g0];
+    const int64_t t_last = (int64_t)r.grid[g0 + nvalid - 1];
+    Acc acc;
+    acc_init(acc);
+    for (uint32_t k = k0; k < k1; k++) {
+      const uint64_t eo = r.e_off[k];
+      const uint32_t len = r.e_len[k];
+      const int64_t first = r.e_ts[eo], last = r.e_ts[eo + len - 1];
+      if (RATE) {
+        if (len < 2 || last < t_first) continue;
+      } else {
+        if (first > t_last || last < t_first) continue;  // not started (F*) / expired
+      }
+      const uint32_t j = ptr[k - k0];
+      const uint32_t idx = j + lane;
+      const int64_t pts = idx < len ? (int64_t)r.e_ts[eo + idx] : INT64_MAX;
+      const bool in = pts <= t_last;
+      const uint64_t inmask = ballot(in);
+      const int kk = __popcll(inmask);
+      uint64_t M;
+      if (kk == nvalid) {
+        M = vmask;  // every grid point of the tile is a point of this span
+      } else if (kk) {
+        uint64_t bit = 0;
+        if (in) bit = 1ull << (grid_rank(r.bitmap, r.word_rank, r.lo, pts) - g0);
+        M = wave_or_u64(bit);
+      } else {
+        M = 0;
+      }
+      if (lane == 0) ptr[k - k0] = j + kk;
+      const int cl = __popcll(M & lanemask_le(lane));
+      const int64_t cur = (int64_t)j + cl - 1;
+      // bracket timestamps: inside the tile they are this wave's loaded points
+      const int64_t ts_in = (int64_t)shfl_u64((uint64_t)pts, cl > 0 ? cl - 1 : 0);
+      if (!gv) continue;
+      if (RATE) {
+        if (tl > last) continue;
+        const int64_t xc = cl > 0 ? ts_in : (int64_t)r.e_ts[eo + cur];
+        const double yc = to_double(r.e_val[eo + cur], r.e_flt[eo + cur] != 0);
+        double yp = 0.0;
+        int64_t xp = 0;
+        if (cur >= 1) { xp = r.e_ts[eo + cur - 1]; yp = to_double(r.e_val[eo + cur - 1], r.e_flt[eo + cur - 1] != 0); }
+        acc_push<AGG, MODE>(acc, 0, (yc - yp) / (double)(xc - xp));
+        continue;
+      }
+      if (cur < 0) {  // not started: next slot holds e_0
+        if (MODE == MODE_DUAL && r.e_flt[eo]) acc.flag |= 1u;
+        continue;
+      }
+      const int64_t xc = cl > 0 ? ts_in : (int64_t)r.e_ts[eo + cur];
+      const bool active = (uint32_t)cur < len - 1 || xc == tl;
+      if (!active) continue;  // expired: nothing in either slot
+      const int64_t vc = r.e_val[eo + cur];
+      bool fc = false, fn = false;
+      if (MODE == MODE_DUAL) {
+        fc = r.e_flt[eo + cur] != 0;
+        if ((uint32_t)cur + 1 < len) fn = r.e_flt[eo + cur + 1] != 0;
+        if (fc || fn) acc.flag |= 1u;
+      }
+      if (xc == tl) {
+        acc_push<AGG, MODE>(acc, vc, MODE == MODE_INT ? 0.0 : to_double(vc, MODE == MODE_DBL || fc));
+      } else {
+        const int64_t xn = r.e_ts[eo + cur + 1];
+        const int64_t vn = r.e_val[eo + cur + 1];
+        int64_t yi = 0;
+        double yd = 0.0;
+        if (MODE != MODE_DBL) yi = lerp_long(tl, xc, vc, xn, vn);
+        if (MODE != MODE_INT)
+          yd = lerp_double(tl, xc, to_double(vc, MODE == MODE_DBL || fc), xn,
+                           to_double(vn, MODE == MODE_DBL || fn));
+        acc_push<AGG, MODE>(acc, yi, yd);
+      }
+    }
+    if (gv) acc_store<AGG, MODE>(r, (uint64_t)chunk * r.T + g, acc);
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+  }
+}
+
+// ------------------------------------------------------------- finalize ---
+struct FinalArgs {
+  uint64_t T;
+  uint32_t n_chunks;
+  const uint32_t* grid;
+  uint64_t fstar;            // max float-first ts + 1 (0: none)
+  int32_t rate;
+  int64_t* out_ts;
+  uint8_t* out_isint;
+  int64_t* out_bits;
+  unsigned long long* nan_t; // [1] min t index with NaN/Inf double
+  unsigned int* ambiguous;   // [1] int dev near an integer after a Chan merge
+};
+
+template <int AGG, int MODE, bool RATE>
+DEVI void finalize_one(const FinalArgs& f, uint64_t g, const Acc& a) {
+  const int64_t t = f.grid[g];
+  const bool isflt = RATE || MODE == MODE_DBL || (a.flag & 1u) || ((uint64_t)t + 1 < f.fstar);
+  int64_t bits;
+  if (isflt) {
+    double d;
+    if (AGG == 0) d = a.da;
+    else if (AGG == 3) d = a.da / (double)(int32_t)a.cnt;
+    else if (AGG == 4) d = wf_result(a.wd);
+    else d = (a.flag & 2u) ? __longlong_as_double(0x7ff8000000000000LL) : a.da;
+    if (d != d || isinf(d)) atomicMin(f.nan_t, (unsigned long long)g);
+    bits = dbits(d);
+  } else {
+    if (AGG == 3) bits = ldiv(a.ia, (int64_t)(int32_t)a.cnt);
+    else if (AGG == 4) {
+      const double v = wf_result(a.wi);
+      bits = d2l(v);
+      if (f.n_chunks > 1) {
+        const double fr = v - floor(v);
+        const double tol = 1e-7 * (v > 1.0 ? v : 1.0);
+        if (fr < tol || 1.0 - fr < tol) atomicOr(f.ambiguous, 1u);
+      }
+    } else bits = a.ia;
+  }
+  f.out_ts[g] = t;
+  f.out_isint[g] = isflt ? 0 : 1;
+  f.out_bits[g] = bits;
+}
+
+// few chunks: one thread per t, chunks in order
+template <int AGG, int MODE, bool RATE>
+__global__ void __launch_bounds__(256) k_finalize_seq(ReduceArgs r, FinalArgs f) {
+  const uint64_t g = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (g >= f.T) return;
+  Acc a;
+  acc_load<AGG, MODE>(r, g, a);
+  for (uint32_t c = 1; c < f.n_chunks; c++) {
+    Acc b;
+    acc_load<AGG, MODE>(r, (uint64_t)c * f.T + g, b);
+    acc_merge<AGG, MODE>(a, b);
+  }
+  finalize_one<AGG, MODE, RATE>(f, g, a);
+}
+
+// many chunks: one block per t; 256 threads take contiguous chunk ranges,
+// then an order-preserving tree.
+template <int AGG, int MODE, bool RATE>
+__global__ void __launch_bounds__(256) k_finalize_par(ReduceArgs r, FinalArgs f) {
+  __shared__ Acc s_acc[256];
+  const uint64_t g = blockIdx.x;
+  const uint32_t t = threadIdx.x;
+  const uint32_t per = (f.n_chunks + 255) / 256;
+  const uint32_t c0 = t * per, c1 = min(f.n_chunks, c0 + per);
+  Acc a;
+  acc_init(a);
+  for (uint32_t c = c0; c < c1; c++) {
+    Acc b;
+    acc_load<AGG, MODE>(r, (uint64_t)c * f.T + g, b);
+    acc_merge<AGG, MODE>(a, b);
+  }
+  s_acc[t] = a;
+  __syncthreads();
+  for (uint32_t d = 1; d < 256; d <<= 1) {
+    if ((t % (2 * d)) == 0) {
+      Acc x = s_acc[t];
+      acc_merge<AGG, MODE>(x, s_acc[t + d]);
+      s_acc[t] = x;
+    }
+    __syncthreads();
+  }
+  if (t == 0) finalize_one<AGG, MODE, RATE>(f, g, s_acc[0]);
+}
+
+}  // namespace tsdb
+
+namespace tsdb {
+// Combines n_chunks partials per t (in chunk order) into dst slot g.
+template <int AGG, int MODE>
+__global__ void __launch_bounds__(256) k_combine_chunks(ReduceArgs src, ReduceArgs dst, uint64_t T,
+                                                        uint32_t n_chunks) {
+  const uint64_t g = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (g >= T) return;
+  Acc a;
+  acc_load<AGG, MODE>(src, g, a);
+  for (uint32_t c = 1; c < n_chunks; c++) {
+    Acc b;
+    acc_load<AGG, MODE>(src, (uint64_t)c * T + g, b);
+    acc_merge<AGG, MODE>(a, b);
+  }
+  acc_store<AGG, MODE>(dst, g, a);
+}
+}  // namespace tsdb

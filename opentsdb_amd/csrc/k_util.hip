@@ -1,0 +1,189 @@
+// k_util.hip — device-wide exclusive scan (u64), kept-span compaction, the
+// synthetic KeyValue generator, and the lazy-error index.
+#pragma once
+#include "dev_common.h"
+#include "k_grid.hip"
+
+namespace tsdb {
+
+// ---- exclusive scan over u64 (1024 elements per block) --------------------
+__global__ void __launch_bounds__(256) k_scan_block_u64(const uint64_t* in, uint64_t* out, uint64_t n,
+                                                        uint64_t* block_sums) {
+  __shared__ uint64_t s_wave[4];
+  const uint64_t base = (uint64_t)blockIdx.x * 1024;
+  const int t = threadIdx.x;
+  uint64_t v[4];
+  uint64_t tot = 0;
+#pragma unroll
+  for (int i = 0; i < 4; i++) {
+    const uint64_t e = base + t * 4 + i;
+    v[i] = e < n ? in[e] : 0;
+    tot += v[i];
+  }
+  const uint64_t incl = wave_incl_scan_u64(tot);
+  if ((t & 63) == 63) s_wave[t >> 6] = incl;
+  __syncthreads();
+  uint64_t woff = 0;
+  for (int i = 0; i < (t >> 6); i++) woff += s_wave[i];
+  uint64_t run = woff + incl - tot;
+#pragma unroll
+  for (int i = 0; i < 4; i++) {
+    const uint64_t e = base + t * 4 + i;
+    if (e < n) out[e] = run;
+    run += v[i];
+  }
+  if (t == 255) block_sums[blockIdx.x] = woff + incl;
+}
+
+__global__ void __launch_bounds__(256) k_scan_blocks_u64(uint64_t* block_sums, uint64_t nb, uint64_t* total) {
+  __shared__ uint64_t s_wave[4];
+  __shared__ uint64_t s_carry;
+  const int t = threadIdx.x;
+  if (t == 0) s_carry = 0;
+  __syncthreads();
+  for (uint64_t b0 = 0; b0 < nb; b0 += 256) {
+    const uint64_t b = b0 + t;
+    const uint64_t v = b < nb ? block_sums[b] : 0;
+    const uint64_t incl = wave_incl_scan_u64(v);
+    if ((t & 63) == 63) s_wave[t >> 6] = incl;
+    __syncthreads();
+    uint64_t woff = 0;
+    for (int i = 0; i < (t >> 6); i++) woff += s_wave[i];
+    const uint64_t carry = s_carry;
+    if (b < nb) block_sums[b] = carry + woff + incl - v;
+    __syncthreads();
+    if (t == 255) s_carry = carry + woff + incl;
+    __syncthreads();
+  }
+  if (t == 0) *total = s_carry;
+}
+
+__global__ void __launch_bounds__(256) k_scan_add_u64(uint64_t* out, uint64_t n, const uint64_t* block_sums) {
+  const uint64_t e = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+  if (e < n) out[e] += block_sums[e >> 10];
+}
+
+// ---- kept spans ------------------------------------------------------------
+__global__ void k_kept_flags(const uint8_t* kept, uint64_t* kflag, uint32_t n) {
+  const uint32_t s = blockIdx.x * blockDim.x + threadIdx.x;
+  if (s < n) kflag[s] = kept[s];
+}
+__global__ void k_kept_scatter(const uint8_t* kept, const uint64_t* kidx, const uint64_t* eoff_s,
+                               const uint32_t* ncells, uint32_t n, uint32_t* kept_list,
+                               uint64_t* eoff_k, unsigned long long* n_input) {
+  const uint32_t s = blockIdx.x * blockDim.x + threadIdx.x;
+  if (s >= n || !kept[s]) return;
+  const uint64_t k = kidx[s];
+  kept_list[k] = s;
+  eoff_k[k] = eoff_s[s];
+  atomicAdd(n_input, (unsigned long long)ncells[s]);
+}
+
+// ---- lazy error index (where the reference would throw) ----------------------
+// A bad cell in E point k is read when point k-1 moves into the current slot
+// (SpanGroup.java:583-608), i.e. while emitting ts(e_{k-1}); points 0 (and 1
+// for rate) are read by the SGIterator constructor.
+__global__ void k_bad_index(const int64_t* e_bad, const uint64_t* e_off, const uint32_t* e_ts,
+                            uint32_t n_kept, int32_t rate, int64_t hi, const uint32_t* bitmap,
+                            const uint32_t* word_rank, int64_t lo, uint64_t T,
+                            unsigned long long* out) {
+  const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
+  if (k >= n_kept) return;
+  const int64_t b = e_bad[k];
+  if (b < 0) return;
+  const uint64_t idx = (uint64_t)(b >> 4), code = (uint64_t)(b & 15);
+  uint64_t at;
+  if (idx == 0 || (rate && idx == 1)) {
+    at = 0;
+  } else {
+    const int64_t tp = e_ts[e_off[k] + idx - 1];
+    if (tp > hi) return;  // never consumed
+    at = T == 0 ? 0 : grid_rank(bitmap, word_rank, lo, tp);
+  }
+  atomicMin(out, (unsigned long long)((at << 4) | code));
+}
+
+// ---- synthetic KeyValues (bit-identical to opentsdb_amd/synth.py) -----------
+DEVI uint64_t splitmix64(uint64_t x) {
+  uint64_t z = x + 0x9E3779B97F4A7C15ull;
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  return z ^ (z >> 31);
+}
+DEVI uint64_t hash3(uint64_t seed, uint64_t s, uint64_t i) {
+  return splitmix64(splitmix64(seed ^ (s * 0xD1B54A32D192ED03ull)) ^ i);
+}
+
+struct SynthArgs {
+  uint64_t seed;
+  uint32_t n_spans, n_points, t0, step, kind, span0;
+  uint32_t k;            // cells per full row
+  uint32_t rps;          // rows per span
+  uint32_t w;            // value width
+  uint32_t flags;
+  uint64_t qstride, vstride;
+  uint64_t* span_row_start;
+  uint32_t* row_base;
+  uint32_t* row_ncells;
+  uint64_t* row_qual_off;
+  uint64_t* row_val_off;
+  uint32_t* row_val_len;
+  uint8_t* qual;
+  uint8_t* val;
+};
+
+__global__ void k_synth_rows(SynthArgs a) {
+  const uint64_t R = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const uint64_t n_rows = (uint64_t)a.n_spans * a.rps;
+  if (R == 0) a.span_row_start[a.n_spans] = n_rows;
+  if (R >= n_rows) return;
+  const uint64_t r = R % a.rps, s = R / a.rps;
+  if (r == 0) a.span_row_start[s] = R;
+  const int64_t left = (int64_t)a.n_points - (int64_t)r * a.k;
+  const uint32_t nc = (uint32_t)(left < (int64_t)a.k ? left : a.k);
+  a.row_ncells[R] = nc;
+  a.row_base[R] = a.t0 + (uint32_t)r * 3600u;
+  a.row_qual_off[R] = R * a.qstride;
+  a.row_val_off[R] = R * a.vstride;
+  a.row_val_len[R] = nc > 1 ? nc * a.w + 1 : nc * a.w;
+}
+
+__global__ void k_synth_cells(SynthArgs a) {
+  const uint64_t cell = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const uint64_t total = (uint64_t)a.n_spans * a.n_points;
+  if (cell >= total) return;
+  const uint64_t ls = cell / a.n_points, i = cell % a.n_points;
+  const uint64_t row = ls * a.rps + i / a.k, c = i % a.k;
+  const uint64_t s = ls + a.span0;  // global series index keys the hash
+  const uint32_t q = (uint32_t)((c * a.step) << 4) | a.flags;
+  uint8_t* qp = a.qual + row * a.qstride + 2 * c;
+  qp[0] = (uint8_t)(q >> 8);
+  qp[1] = (uint8_t)q;
+  uint64_t be;  // value bytes, big-endian, in the low a.w bytes
+  if (a.kind == 0) {
+    const uint64_t base = hash3(a.seed, s, 0xFFFFFFFFull) >> 24;
+    const uint64_t rr = hash3(a.seed, s, i) % 500ull;
+    be = base + 500ull * i + rr;
+  } else {
+    const uint64_t h = hash3(a.seed, s, i);
+    const int64_t sum = (int64_t)((h & 0xFFFF) + ((h >> 16) & 0xFFFF) + ((h >> 32) & 0xFFFF) + ((h >> 48) & 0xFFFF)) - 131070;
+    const double prod = (double)sum * 0x1.bb685d0b4e463p-16;  // 1/37837
+    const double v = 100.0 + prod;
+    if (a.kind == 1) be = (uint64_t)__float_as_uint((float)v);
+    else be = (uint64_t)__double_as_longlong(v);
+  }
+  uint8_t* vp = a.val + row * a.vstride + (uint64_t)c * a.w;
+  for (uint32_t b = 0; b < a.w; b++) vp[b] = (uint8_t)(be >> (8 * (a.w - 1 - b)));
+}
+
+}  // namespace tsdb
+
+namespace tsdb {
+__global__ void k_bitmap_or(const uint32_t* all, uint32_t nranks, uint64_t nwords, uint32_t* out) {
+  const uint64_t w = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (w >= nwords) return;
+  uint32_t x = 0;
+  for (uint32_t r = 0; r < nranks; r++) x |= all[(uint64_t)r * nwords + w];
+  out[w] = x;
+}
+}  // namespace tsdb

@@ -61,9 +61,10 @@ def counter_value(seed, s, i):
         return (base + _U(500) * np.asarray(i, np.uint64) + r).astype(np.int64)
 
 
-def regular(n_spans, n_points, kind, seed=1, t0=T0, step=1):
+def regular(n_spans, n_points, kind, seed=1, t0=T0, step=1, span0=0):
     """Regular-cadence SpanGroup (C1/C2/C3 shapes), device-generator layout:
-    row R = s * rows_per_span + r, quals at R*qstride, values at R*vstride."""
+    row R = s * rows_per_span + r, quals at R*qstride, values at R*vstride.
+    Series s of this set is global series span0 + s (shards)."""
     if t0 % MAX_TIMESPAN or MAX_TIMESPAN % step:
         raise ValueError("t0 must be hour aligned and step must divide 3600")
     k = MAX_TIMESPAN // step
@@ -84,9 +85,10 @@ def regular(n_spans, n_points, kind, seed=1, t0=T0, step=1):
     qb = np.zeros(n_rows * qstride, np.uint8)
     vb = np.zeros(n_rows * vstride, np.uint8)
     # all cells
-    s_idx = np.repeat(np.arange(n_spans, dtype=np.int64), n_points)
+    l_idx = np.repeat(np.arange(n_spans, dtype=np.int64), n_points)
     i_idx = np.tile(np.arange(n_points, dtype=np.int64), n_spans)
-    row = s_idx * rps + i_idx // k
+    row = l_idx * rps + i_idx // k
+    s_idx = l_idx + span0
     c = i_idx % k
     delta = c * step
     q = ((delta << 4) | flags).astype(np.uint16)

@@ -27,6 +27,7 @@
 #include <string>
 #include <vector>
 #include <algorithm>
+#include <chrono>
 
 #include "../include/tsdbhip.h"
 
@@ -847,6 +848,11 @@ extern "C" {
 
 int oracle_abi_version(void) { return TSDBHIP_ABI_VERSION; }
 
+// Seconds spent in the last oracle_spangroup_run of this thread, split into
+// Span assembly (Span.addRow over the KeyValues) and SpanGroup iteration.
+static thread_local double t_assemble = 0, t_iterate = 0;
+void oracle_last_seconds(double* assemble, double* iterate) { *assemble = t_assemble; *iterate = t_iterate; }
+
 // Runs one SpanGroup exactly as GraphHandler.respondAsciiQuery consumes it
 // (GraphHandler.java:791-808): for each point timestamp(), isInteger(),
 // then longValue() or doubleValue(). Host pointers only.
@@ -856,6 +862,9 @@ int oracle_spangroup_run(const tsdbhip_sg_desc* d, tsdbhip_sg_out* out) {
   out->err_code = 0;
   out->err_index = -1;
   int64_t emitted = 0;
+  auto t0 = std::chrono::steady_clock::now();
+  auto t1 = t0;
+  t_assemble = t_iterate = 0;
   try {
     std::vector<std::unique_ptr<Span>> spans(d->n_spans);
     for (uint32_t s = 0; s < d->n_spans; s++) {
@@ -881,6 +890,8 @@ int oracle_spangroup_run(const tsdbhip_sg_desc* d, tsdbhip_sg_out* out) {
       g.add(sp.get());
     }
     out->n_input_points = (uint64_t)g.aggregatedSize();
+    t1 = std::chrono::steady_clock::now();
+    t_assemble = std::chrono::duration<double>(t1 - t0).count();
     SpanGroup::SGIterator it(&g);
     while (it.hasNext()) {
       it.next();
@@ -897,6 +908,7 @@ int oracle_spangroup_run(const tsdbhip_sg_desc* d, tsdbhip_sg_out* out) {
       emitted++;
       out->n_out = (uint64_t)emitted;
     }
+    t_iterate = std::chrono::duration<double>(std::chrono::steady_clock::now() - t1).count();
   } catch (JavaException& e) {
     out->err_code = e.code;
     out->err_index = emitted;

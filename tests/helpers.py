@@ -1,0 +1,53 @@
+"""Shared test helpers: build SpanGroups, run GPU and oracle, compare."""
+import numpy as np
+
+import oracle
+from opentsdb_amd import _abi, core, synth, packing
+
+T0 = synth.T0
+U32MAX = (1 << 32) - 1
+
+
+def I(pts, minimal=True):
+    """int series rows from [(ts, value)]"""
+    return synth.series_rows(synth.points_int([p[0] for p in pts], [p[1] for p in pts], minimal))
+
+
+def F(pts, double=False):
+    return synth.series_rows(synth.points_float([p[0] for p in pts], [p[1] for p in pts], double))
+
+
+def M(pts):
+    """mixed series rows from [(ts, value)] — python int -> long, float -> float32"""
+    out = []
+    for t, v in pts:
+        if isinstance(v, float):
+            out.append((t,) + synth.encode_float(v))
+        else:
+            out.append((t,) + synth.encode_long(v))
+    return synth.series_rows(out)
+
+
+def run_both(ctx, spanset, start=0, end=U32MAX, agg=0, rate=False, ds_interval=0, ds_agg=0, exact=False):
+    g = core.run_spanset(ctx, spanset, start, end, agg, rate, ds_interval, ds_agg, exact=exact)
+    o = oracle.spangroup(spanset, start, end, agg, rate, ds_interval, ds_agg)
+    return g, o
+
+
+def assert_same(g, o, rtol=1e-9, exact_double=False, check_err_index=True):
+    rc, ts, isi, bits, n_in, err_at = g
+    assert rc == o.code, f"code gpu={_abi.ERR_NAMES.get(rc, rc)} oracle={_abi.ERR_NAMES.get(o.code, o.code)}"
+    assert n_in == o.n_input_points, f"aggregatedSize gpu={n_in} oracle={o.n_input_points}"
+    if rc == 0 or check_err_index:
+        assert len(ts) == len(o.ts), f"n_out gpu={len(ts)} oracle={len(o.ts)}"
+    n = min(len(ts), len(o.ts))
+    np.testing.assert_array_equal(ts[:n], o.ts[:n], err_msg="timestamps")
+    np.testing.assert_array_equal(isi[:n], o.is_int[:n], err_msg="isInteger")
+    ints = o.is_int[:n].astype(bool)
+    np.testing.assert_array_equal(bits[:n][ints], o.bits[:n][ints], err_msg="long values")
+    gd = bits[:n][~ints].view(np.float64)
+    od = o.bits[:n][~ints].view(np.float64)
+    if exact_double:
+        np.testing.assert_array_equal(bits[:n][~ints], o.bits[:n][~ints], err_msg="double bits")
+    else:
+        np.testing.assert_allclose(gd, od, rtol=rtol, atol=0, err_msg="double values")

@@ -1,0 +1,249 @@
+"""GPU parity: libtsdbhip (HIP kernels, called through the C-ABI) vs the CPU
+oracle (restatement of the reference, pinned by tests/golden) on the same
+seeded inputs. Integer results are bit-exact; double results within 1e-9
+relative, and bit-exact with TSDBHIP_EXACT_ORDER (one span chunk, the
+reference's summation order)."""
+import numpy as np
+import pytest
+
+from helpers import I, F, M, T0, U32MAX, run_both, assert_same
+from opentsdb_amd import _abi, core, packing, synth
+
+pytestmark = pytest.mark.gpu
+
+AGGS = [0, 1, 2, 3, 4]
+
+
+def ka_groups():
+    T = T0
+    return {
+        "KA1": [I([(T + 100, 10), (T + 110, 20)]), I([(T + 105, 100), (T + 115, 200)])],
+        "KA2": [I([(T + 100, 0), (T + 103, -10)]), I([(T + 101, 5)])],
+        "KA3": [I([(T + 100, 10), (T + 110, 30), (T + 120, 60)]), I([(T + 105, 1000), (T + 115, 1100)])],
+        "KA6": [I([(T + 100, 1), (T + 110, 2)]), F([(T + 200, 1.5), (T + 210, 2.5)])],
+    }
+
+
+@pytest.mark.parametrize("name", ["KA1", "KA2", "KA3", "KA6"])
+@pytest.mark.parametrize("agg", AGGS)
+@pytest.mark.parametrize("rate", [False, True])
+def test_known_answers(ctx, name, agg, rate):
+    ss = packing.pack_spans(ka_groups()[name])
+    g, o = run_both(ctx, ss, agg=agg, rate=rate)
+    assert_same(g, o)
+    g2, _ = run_both(ctx, ss, agg=agg, rate=rate, exact=True)
+    assert_same(g2, o, exact_double=True)
+
+
+def test_ka8_bracket_after_end(ctx):
+    T = T0
+    ss = packing.pack_spans([I([(T + 100, 0), (T + 200, 100)]), I([(T + 150, 7)])])
+    g, o = run_both(ctx, ss, end=T + 160)
+    assert_same(g, o, exact_double=True)
+    assert list(g[1] - T) == [100, 150] and list(g[3]) == [0, 57]
+
+
+@pytest.mark.parametrize("agg", AGGS)
+@pytest.mark.parametrize("ds_agg", AGGS)
+def test_downsample_ka4_ka5(ctx, agg, ds_agg):
+    T = T0
+    spans = [I([(T + 100 + i, i) for i in range(120)]),
+             I([(T + 100, 1), (T + 130, 2), (T + 161, 3), (T + 170, 4), (T + 230, 5)])]
+    ss = packing.pack_spans(spans)
+    g, o = run_both(ctx, ss, agg=agg, ds_interval=60, ds_agg=ds_agg)
+    assert_same(g, o)
+    g, o = run_both(ctx, ss, agg=agg, ds_interval=60, ds_agg=ds_agg, exact=True)
+    assert_same(g, o, exact_double=True)
+
+
+@pytest.mark.parametrize("kind", [_abi.SYN_INT64_COUNTER, _abi.SYN_FLOAT32, _abi.SYN_FLOAT64])
+@pytest.mark.parametrize("agg", AGGS)
+def test_regular_nods(ctx, kind, agg):
+    ss = synth.regular(40, 700, kind, seed=3, step=10)
+    g, o = run_both(ctx, ss, agg=agg)
+    assert_same(g, o)
+    g, o = run_both(ctx, ss, agg=agg, exact=True)
+    assert_same(g, o, exact_double=True)
+
+
+@pytest.mark.parametrize("kind", [_abi.SYN_INT64_COUNTER, _abi.SYN_FLOAT32])
+@pytest.mark.parametrize("agg,ds_agg", [(0, 3), (3, 3), (0, 0), (2, 1), (1, 2), (4, 4), (3, 4)])
+@pytest.mark.parametrize("rate", [False, True])
+def test_regular_ds(ctx, kind, agg, ds_agg, rate):
+    ss = synth.regular(30, 2000, kind, seed=5, step=10)
+    g, o = run_both(ctx, ss, agg=agg, rate=rate, ds_interval=60, ds_agg=ds_agg)
+    assert_same(g, o)
+    g, o = run_both(ctx, ss, agg=agg, rate=rate, ds_interval=60, ds_agg=ds_agg, exact=True)
+    assert_same(g, o, exact_double=True)
+
+
+@pytest.mark.parametrize("seed", [1, 2, 3])
+@pytest.mark.parametrize("agg", AGGS)
+@pytest.mark.parametrize("rate", [False, True])
+def test_jittered_mixed(ctx, seed, agg, rate):
+    ss = synth.jittered(12, 60, seed=seed, span_range=400_000, max_gap=700)
+    g, o = run_both(ctx, ss, agg=agg, rate=rate)
+    assert_same(g, o)
+    g, o = run_both(ctx, ss, agg=agg, rate=rate, exact=True)
+    assert_same(g, o, exact_double=True)
+
+
+@pytest.mark.parametrize("seed", [4, 5])
+@pytest.mark.parametrize("agg", AGGS)
+def test_jittered_int_lerp(ctx, seed, agg):
+    """C4-int: all-integer series exercise the bit-exact int64 lerp."""
+    ss = synth.jittered(15, 80, seed=seed, span_range=300_000, max_gap=900, float_frac=0.0,
+                        float_cell_frac=0.0)
+    g, o = run_both(ctx, ss, agg=agg)
+    assert_same(g, o, exact_double=True)
+
+
+@pytest.mark.parametrize("seed", [6, 7])
+@pytest.mark.parametrize("ds", [(300, 0), (300, 3), (900, 4), (120, 1)])
+def test_jittered_ds(ctx, seed, ds):
+    ss = synth.jittered(10, 80, seed=seed, span_range=200_000, max_gap=400)
+    for agg in AGGS:
+        g, o = run_both(ctx, ss, agg=agg, ds_interval=ds[0], ds_agg=ds[1], exact=True)
+        assert_same(g, o, exact_double=True)
+
+
+@pytest.mark.parametrize("window", [(100, 2000), (500, 1500), (0, 700), (1700, U32MAX)])
+def test_start_end_windows(ctx, window):
+    """start inside the data (seek), end cutting spans (brackets past end)."""
+    T = T0
+    spans = [I([(T + 10 * i, i * 7) for i in range(200)]),
+             I([(T + 5 + 13 * i, -3 * i) for i in range(150)]),
+             F([(T + 300 + 11 * i, 0.5 * i) for i in range(100)])]
+    ss = packing.pack_spans(spans)
+    lo, hi = window
+    for agg in AGGS:
+        for rate in (False, True):
+            g, o = run_both(ctx, ss, start=T + lo, end=min(U32MAX, T + hi), agg=agg, rate=rate, exact=True)
+            assert_same(g, o, exact_double=True)
+
+
+def test_q1_seek_inside_row_minimal_widths(ctx):
+    """Quirk Q1: a seek inside a row with non-1-byte values shifts offsets."""
+    T = T0
+    spans = [I([(T + i, 1000 + i) for i in range(50)], minimal=True),
+             I([(T + i, 10 ** 6 + i) for i in range(50)], minimal=False)]
+    ss = packing.pack_spans(spans)
+    for agg in AGGS:
+        g, o = run_both(ctx, ss, start=T + 20, agg=agg, exact=True)
+        assert_same(g, o, exact_double=True)
+
+
+def test_minimal_width_ints(ctx):
+    T = T0
+    rng = np.random.default_rng(9)
+    spans = []
+    for s in range(6):
+        vals = rng.integers(-(1 << 40), 1 << 40, 300) >> rng.integers(0, 40, 300)
+        spans.append(I([(T + 3 * i + s, int(v)) for i, v in enumerate(vals)], minimal=True))
+    ss = packing.pack_spans(spans)
+    for agg in AGGS:
+        g, o = run_both(ctx, ss, agg=agg)
+        assert_same(g, o, exact_double=True)
+
+
+def test_empty_and_disjoint(ctx):
+    T = T0
+    ss = packing.pack_spans([I([(T + 100, 1)])])
+    g, o = run_both(ctx, ss, start=T + 200, end=T + 300)
+    assert_same(g, o)
+    assert len(g[1]) == 0
+    ss = packing.pack_spans([])
+    g, o = run_both(ctx, ss)
+    assert_same(g, o)
+
+
+def test_single_point_rate(ctx):
+    T = T0
+    ss = packing.pack_spans([I([(T + 100, 5)]), I([(T + 50, 1), (T + 150, 9)])])
+    for agg in AGGS:
+        g, o = run_both(ctx, ss, agg=agg, rate=True)
+        assert_same(g, o, exact_double=True)
+
+
+def test_illegal_width(ctx):
+    T = T0
+    bad = packing.KeyValue(T, bytes([0x00, 0x02, 0x00, 0x12]), bytes([1, 2, 3, 4, 5, 6, 0]))  # len 3 ints
+    spans = [I([(T + i, i) for i in range(5)]), [bad]]
+    ss = packing.pack_spans(spans)
+    g, o = run_both(ctx, ss)
+    assert_same(g, o)
+    assert g[0] == _abi.E_ILLEGAL_DATA
+
+
+def test_nan_result(ctx):
+    T = T0
+    spans = [F([(T + 1, float("inf")), (T + 2, 1.0)]), F([(T + 1, 1.0), (T + 2, 1.0)])]
+    ss = packing.pack_spans(spans)
+    g, o = run_both(ctx, ss)
+    assert_same(g, o)
+    assert g[0] == _abi.E_NAN_INF
+
+
+def test_row_assembly_rules(ctx):
+    """Span.addRow: out-of-order rows dropped, merges of close rows."""
+    T = T0
+    r1 = synth.compact_cells(T, [(T + i, 0x7, int(i).to_bytes(8, "big")) for i in range(0, 3600, 7)])
+    r2 = synth.compact_cells(T + 3600, [(T + 3600 + i, 0x7, int(i).to_bytes(8, "big")) for i in range(0, 400, 3)])
+    r_old = synth.compact_cells(T, [(T + 5, 0x0, bytes([9]))])
+    r3 = synth.compact_cells(T + 7200, [(T + 7200 + i, 0x3, int(i).to_bytes(4, "big")) for i in range(0, 3600, 11)])
+    spans = [[r1, r2, r3], [r1, r_old, r3], [r2, r1]]
+    ss = packing.pack_spans(spans)
+    for agg in AGGS:
+        for ds in ((0, 0), (60, 3)):
+            g, o = run_both(ctx, ss, agg=agg, ds_interval=ds[0], ds_agg=ds[1], exact=True)
+            assert_same(g, o, exact_double=True)
+
+
+def test_short_overflow_merged_rowseq(ctx):
+    """RowSeq.Iterator's short value_index overflows past 32767 value bytes."""
+    T = T0
+    r1 = synth.compact_cells(T, [(T + i, 0x7, int(i).to_bytes(8, "big")) for i in range(3600)])
+    r2 = synth.compact_cells(T + 3600, [(T + 3600 + i, 0x7, int(i).to_bytes(8, "big")) for i in range(496)])
+    ss = packing.pack_spans([[r1, r2]])
+    g, o = run_both(ctx, ss)
+    assert_same(g, o)
+    assert g[0] == o.code
+
+
+def test_device_generator_matches_host(ctx):
+    import ctypes as C
+    from opentsdb_amd import _lib
+    L = _lib.lib()
+    for kind in (_abi.SYN_INT64_COUNTER, _abi.SYN_FLOAT32, _abi.SYN_FLOAT64):
+        host = synth.regular(7, 5000, kind, seed=11, step=5)
+        p = _abi.SynthParams(seed=11, n_spans=7, n_points=5000, t0=T0, step=5, kind=kind)
+        d = _abi.SgDesc()
+        ctx.check(L.tsdbhip_synth_generate(ctx.handle, C.byref(p), C.byref(d)))
+        R = d.n_rows
+        arrs = [np.zeros(7 + 1, np.uint64), np.zeros(R, np.uint32), np.zeros(R, np.uint32),
+                np.zeros(R, np.uint64), np.zeros(R, np.uint64), np.zeros(R, np.uint32),
+                np.zeros(d.qual_nbytes, np.uint8), np.zeros(d.val_nbytes, np.uint8)]
+        ctx.check(L.tsdbhip_desc_download(ctx.handle, C.byref(d), *[a.ctypes.data for a in arrs]))
+        for a, b in zip(arrs, [host.span_row_start, host.row_base, host.row_ncells, host.row_qual_off,
+                               host.row_val_off, host.row_val_len, host.qual_bytes, host.val_bytes]):
+            np.testing.assert_array_equal(a, b)
+        # run on the device-resident desc and compare with the oracle
+        rc, ts, isi, bits, n_in, _ = core.run_spanset(ctx, host, 0, U32MAX, 0, False, 60, 3, device_desc=d)
+        import oracle
+        o = oracle.spangroup(host, 0, U32MAX, 0, False, 60, 3)
+        assert_same((rc, ts, isi, bits, n_in, -1), o)
+        L.tsdbhip_synth_free(ctx.handle, C.byref(d))
+
+
+def test_spangroup_api_lazy_errors(ctx):
+    T = T0
+    sg = core.SpanGroup(None, 0, U32MAX, [core.Span(I([(T + 1, 1), (T + 2, 2)])),
+                                          core.Span(F([(T + 1, 1.0), (T + 3, float("nan"))]))],
+                        False, core.Aggregators.get("sum"), ctx=ctx)
+    pts = []
+    with pytest.raises(core.IllegalStateException):
+        for dp in sg:
+            pts.append(dp)
+    import oracle
+    o = oracle.spangroup(packing.pack_spans([s.rows for s in sg.spans]), 0, U32MAX, 0)
+    assert len(pts) == len(o.ts)
