@@ -30,6 +30,7 @@
 #include "k_grid.hip"
 #include "k_reduce.hip"
 #include "k_util.hip"
+#include "k_decode_fast.hip"
 
 using namespace tsdb;
 
@@ -455,7 +456,52 @@ static int spangroup_run(tsdbhip_ctx* ctx, const tsdbhip_sg_desc* d, tsdbhip_sg_
   HIPCHK(hipEventRecord(ctx->ev[1], st));
   if (n_kept) {
     const unsigned blocks = grid_for(n_kept, 4, 65536);
-    if (interval == 0) {
+    // wide rows (the reference's hourly compacted rows) take the streaming
+    // kernel; rows of a few cells (sparse series) the general one.
+    const char* force = getenv("TSDBHIP_DECODE");
+    bool fast = R > 0 && h.n_input / R >= 64;
+    if (force && !strcmp(force, "general")) fast = false;
+    if (force && !strcmp(force, "fast")) fast = true;
+    da.fb_list = scratch<uint32_t>(ctx, "fb_list", n_kept);
+    da.fb_count = scratch<uint32_t>(ctx, "fb_count", 1, true);
+    da.use_fb = 0;
+    if (fast) {
+      // spans the streaming kernel cannot take are queued for the general one
+      DecodeArgs ga = da;
+      ga.use_fb = 1;
+      if (interval == 0) {
+        hipLaunchKernelGGL((k_decode_fast<0, false>), dim3(blocks), dim3(256), 0, st, da, row_ncells, row_val_len);
+        hipLaunchKernelGGL(k_decode_nods, dim3(blocks), dim3(256), 0, st, ga);
+      } else {
+        switch (ds_agg) {
+          case 0: hipLaunchKernelGGL((k_decode_fast<0, true>), dim3(blocks), dim3(256), 0, st, da, row_ncells, row_val_len); break;
+          case 1: hipLaunchKernelGGL((k_decode_fast<1, true>), dim3(blocks), dim3(256), 0, st, da, row_ncells, row_val_len); break;
+          case 2: hipLaunchKernelGGL((k_decode_fast<2, true>), dim3(blocks), dim3(256), 0, st, da, row_ncells, row_val_len); break;
+          case 3: hipLaunchKernelGGL((k_decode_fast<3, true>), dim3(blocks), dim3(256), 0, st, da, row_ncells, row_val_len); break;
+          default: hipLaunchKernelGGL((k_decode_fast<4, true>), dim3(blocks), dim3(256), 0, st, da, row_ncells, row_val_len); break;
+        }
+        HIPCHK(hipEventRecord(ctx->ev[6], st));
+        switch (ds_agg) {
+          case 0: launch_decode_ds<0>(ctx, blocks, ga); break;
+          case 1: launch_decode_ds<1>(ctx, blocks, ga); break;
+          case 2: launch_decode_ds<2>(ctx, blocks, ga); break;
+          case 3: launch_decode_ds<3>(ctx, blocks, ga); break;
+          default: launch_decode_ds<4>(ctx, blocks, ga); break;
+        }
+      }
+    } else if (fast) {
+      if (interval == 0) {
+        hipLaunchKernelGGL((k_decode_fast<0, false>), dim3(blocks), dim3(256), 0, st, da, row_ncells, row_val_len);
+      } else {
+        switch (ds_agg) {
+          case 0: hipLaunchKernelGGL((k_decode_fast<0, true>), dim3(blocks), dim3(256), 0, st, da, row_ncells, row_val_len); break;
+          case 1: hipLaunchKernelGGL((k_decode_fast<1, true>), dim3(blocks), dim3(256), 0, st, da, row_ncells, row_val_len); break;
+          case 2: hipLaunchKernelGGL((k_decode_fast<2, true>), dim3(blocks), dim3(256), 0, st, da, row_ncells, row_val_len); break;
+          case 3: hipLaunchKernelGGL((k_decode_fast<3, true>), dim3(blocks), dim3(256), 0, st, da, row_ncells, row_val_len); break;
+          default: hipLaunchKernelGGL((k_decode_fast<4, true>), dim3(blocks), dim3(256), 0, st, da, row_ncells, row_val_len); break;
+        }
+      }
+    } else if (interval == 0) {
       hipLaunchKernelGGL(k_decode_nods, dim3(blocks), dim3(256), 0, st, da);
     } else {
       switch (ds_agg) {

@@ -33,6 +33,14 @@ DEVI uint64_t ballot(bool p) { return __ballot(p); }
 DEVI uint64_t lanemask_le(int lane) { return lane == 63 ? ~0ull : ((2ull << lane) - 1); }
 DEVI uint64_t lanemask_lt(int lane) { return (1ull << lane) - 1; }
 
+// Lanes of one wave exchanging data through LDS: the wave's LDS operations
+// execute in order, so only the compiler must not move accesses across.
+DEVI void wave_lds_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
 // Position of the (j+1)-th set bit of m (j per lane); requires j < popc(m).
 DEVI int select_bit(uint64_t m, int j) {
   int p = 0;

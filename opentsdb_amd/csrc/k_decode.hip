@@ -54,6 +54,9 @@ struct DecodeArgs {
   unsigned int* gflags;       // [0] any float E point, [1] any int E point
   unsigned long long* range;  // [0] min grid-candidate ts, [1] max E ts
   unsigned long long* fstar;  // max first-E ts over spans whose first E point is float
+  uint32_t* fb_list;          // spans the fast kernel handed to the general one
+  uint32_t* fb_count;         // [1]; general kernels iterate this list when `use_fb`
+  int32_t use_fb;
 };
 
 #define BAD_ILLEGAL 1
@@ -117,11 +120,18 @@ DEVI void decode_chunk(const DecodeArgs& a, uint64_t r0, uint64_t r1, uint32_t n
   }
 }
 
+__device__ void span_nods_general(const DecodeArgs& a, uint32_t k);
+
 __global__ void __launch_bounds__(256) k_decode_nods(DecodeArgs a) {
-  const int lane = lane_id();
   const uint32_t wave = (blockIdx.x * blockDim.x + threadIdx.x) / WAVE;
   const uint32_t nwaves = gridDim.x * blockDim.x / WAVE;
-  for (uint32_t k = wave; k < a.n_kept; k += nwaves) {
+  const uint32_t n = a.use_fb ? *a.fb_count : a.n_kept;
+  for (uint32_t i = wave; i < n; i += nwaves) span_nods_general(a, a.use_fb ? a.fb_list[i] : i);
+}
+
+__device__ void span_nods_general(const DecodeArgs& a, uint32_t k) {
+  const int lane = lane_id();
+  {
     const uint32_t s = a.kept[k];
     const uint64_t r0 = a.span_row_start[s], r1 = a.span_row_start[s + 1];
     const uint32_t n = a.sp_ncells[s];
@@ -221,15 +231,12 @@ DEVI void finalize_bucket(const DecodeArgs& a, const Bucket& b, uint64_t eidx, u
   a.e_flt[eo + eidx] = !allint;
 }
 
+// One span, any row structure (general path; also the fallback of the fast
+// kernel). s_bits/s_flt: this wave's 64-entry LDS staging.
 template <int AGG>
-__global__ void __launch_bounds__(256) k_decode_ds(DecodeArgs a) {
-  __shared__ int64_t s_bits[4][WAVE];
-  __shared__ uint8_t s_flt[4][WAVE];
+__device__ void span_ds_general(const DecodeArgs& a, uint32_t k, int64_t* s_bits_w, uint8_t* s_flt_w) {
   const int lane = lane_id();
-  const int wib = threadIdx.x / WAVE;
-  const uint32_t wave = (blockIdx.x * blockDim.x + threadIdx.x) / WAVE;
-  const uint32_t nwaves = gridDim.x * blockDim.x / WAVE;
-  for (uint32_t k = wave; k < a.n_kept; k += nwaves) {
+  {
     const uint32_t s = a.kept[k];
     const uint64_t r0 = a.span_row_start[s], r1 = a.span_row_start[s + 1];
     const uint32_t n = a.sp_ncells[s];
@@ -333,16 +340,14 @@ __global__ void __launch_bounds__(256) k_decode_ds(DecodeArgs a) {
       }
       // ---- ordered double path / Welford: one lane per segment ----
       if (seq) {
-        s_bits[wib][lane] = o.bits;
-        s_flt[wib][lane] = o.isflt;
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-        __builtin_amdgcn_wave_barrier();
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+        s_bits_w[lane] = o.bits;
+        s_flt_w[lane] = o.isflt;
+        wave_lds_sync();
         if (lane < nseg) {
           bool first = true;
           if (lane == 0 && cont) { b.dsum = cb.dsum; b.dmm = cb.dmm; b.wf = cb.wf; first = false; }
           for (int i = seg_a; i <= seg_b; i++) {
-            const double x = to_double(s_bits[wib][i], s_flt[wib][i] != 0);
+            const double x = to_double(s_bits_w[i], s_flt_w[i] != 0);
             seq_push<AGG>(b, x, first);
             first = false;
           }
@@ -393,6 +398,18 @@ __global__ void __launch_bounds__(256) k_decode_ds(DecodeArgs a) {
       if (anyi) atomicOr(&a.gflags[1], 1u);
     }
   }
+}
+
+template <int AGG>
+__global__ void __launch_bounds__(256) k_decode_ds(DecodeArgs a) {
+  __shared__ int64_t s_bits[4][WAVE];
+  __shared__ uint8_t s_flt[4][WAVE];
+  const int wib = threadIdx.x / WAVE;
+  const uint32_t wave = (blockIdx.x * blockDim.x + threadIdx.x) / WAVE;
+  const uint32_t nwaves = gridDim.x * blockDim.x / WAVE;
+  const uint32_t n = a.use_fb ? *a.fb_count : a.n_kept;
+  for (uint32_t i = wave; i < n; i += nwaves)
+    span_ds_general<AGG>(a, a.use_fb ? a.fb_list[i] : i, s_bits[wib], s_flt[wib]);
 }
 
 // Per-span summary of E after decode: grid range, F* (float first points).

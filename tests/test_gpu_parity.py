@@ -14,6 +14,17 @@ pytestmark = pytest.mark.gpu
 AGGS = [0, 1, 2, 3, 4]
 
 
+@pytest.fixture(autouse=True, params=["auto", "general", "fast"])
+def decode_path(request, monkeypatch):
+    """Run every case through the streaming decode kernel (with its fallback
+    queue) and through the general per-span kernel."""
+    if request.param != "auto":
+        monkeypatch.setenv("TSDBHIP_DECODE", request.param)
+    else:
+        monkeypatch.delenv("TSDBHIP_DECODE", raising=False)
+    return request.param
+
+
 def ka_groups():
     T = T0
     return {
