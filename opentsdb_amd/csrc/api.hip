@@ -31,6 +31,7 @@
 #include "k_reduce.hip"
 #include "k_util.hip"
 #include "k_decode_fast.hip"
+#include "k_ds_chunks.hip"
 
 using namespace tsdb;
 
@@ -257,10 +258,71 @@ static void readback(tsdbhip_ctx* ctx, void* host, const void* dev, size_t bytes
   std::memcpy(host, ctx->host_small, bytes);
 }
 
-template <int AGG>
-static void launch_decode_ds(tsdbhip_ctx* ctx, unsigned blocks, const DecodeArgs& a) {
-  hipLaunchKernelGGL(k_decode_ds<AGG>, dim3(blocks), dim3(256), 0, ctx->stream, a);
+// runtime aggregator id -> F::template run<AGG>(args...)
+template <typename F, typename... A>
+static void launch_agg(int agg, A&&... args) {
+  switch (agg) {
+    case 0: F::template run<0>(args...); break;
+    case 1: F::template run<1>(args...); break;
+    case 2: F::template run<2>(args...); break;
+    case 3: F::template run<3>(args...); break;
+    default: F::template run<4>(args...); break;
+  }
 }
+
+struct LaunchGeneralDs {
+  template <int AGG>
+  static void run(tsdbhip_ctx* ctx, unsigned blocks, const DecodeArgs& a) {
+    hipLaunchKernelGGL(k_decode_ds<AGG>, dim3(blocks), dim3(256), 0, ctx->stream, a);
+  }
+};
+
+struct LaunchFastDs {
+  template <int AGG>
+  static void run(tsdbhip_ctx* ctx, unsigned blocks, const DecodeArgs& a, const uint32_t* ncells,
+                  const uint32_t* vlen) {
+    hipLaunchKernelGGL((k_decode_fast<AGG, true>), dim3(blocks), dim3(256), 0, ctx->stream, a, ncells, vlen);
+  }
+};
+
+// Chunk-parallel downsampling of regular-cadence integer spans; leaves the
+// list of spans it did not take in fa.span_list for k_decode_fast.
+struct LaunchChunks {
+  template <int AGG>
+  static void run(tsdbhip_ctx* ctx, const DecodeArgs& da, DecodeArgs& fa, const uint32_t* ncells,
+                  const uint32_t* vlen, uint64_t R, uint64_t e_total, uint64_t chunk_bound) {
+    if (AGG == 4) return;  // dev: Welford is order-dependent, serial kernels only
+    hipStream_t st = ctx->stream;
+    const uint32_t n_kept = da.n_kept;
+    ChunkPlanArgs p;
+    p.row_kidx = scratch<int32_t>(ctx, "ck_row_kidx", R);
+    HIPCHK(hipMemsetAsync(p.row_kidx, 0xFF, R * sizeof(int32_t), st));
+    uint64_t* nch = scratch<uint64_t>(ctx, "ck_row_nch", R);
+    uint64_t* rc0 = scratch<uint64_t>(ctx, "ck_row_chunk0", R);
+    hipLaunchKernelGGL(k_row_chunks, dim3(grid_for(R, 256)), dim3(256), 0, st, ncells, R, nch);
+    dscan_u64(ctx, nch, rc0, R, scratch<uint64_t>(ctx, "ck_nch_total", 1), "ck");
+    p.row_chunk0 = rc0;
+    p.plan_k = scratch<uint32_t>(ctx, "ck_plan_k", n_kept);
+    p.plan_nb = scratch<uint32_t>(ctx, "ck_plan_nb", n_kept);
+    p.fail = scratch<uint32_t>(ctx, "ck_fail", n_kept);
+    p.hp_n = scratch<uint32_t>(ctx, "ck_hp_n", e_total);
+    p.hp_ref = scratch<uint32_t>(ctx, "ck_hp_ref", e_total);
+    p.hp_rel = scratch<uint32_t>(ctx, "ck_hp_rel", e_total);
+    p.hp_v = scratch<int64_t>(ctx, "ck_hp_v", e_total);
+    p.lp_n = scratch<uint32_t>(ctx, "ck_lp_n", chunk_bound);
+    p.lp_ts = scratch<uint64_t>(ctx, "ck_lp_ts", chunk_bound);
+    p.lp_v = scratch<int64_t>(ctx, "ck_lp_v", chunk_bound);
+    p.list = scratch<uint32_t>(ctx, "ck_list", n_kept);
+    p.list_count = scratch<uint32_t>(ctx, "ck_list_count", 1, true);
+    const unsigned span_blocks = grid_for(n_kept, 4, 65536);
+    hipLaunchKernelGGL(k_ds_plan, dim3(span_blocks), dim3(256), 0, st, da, p, ncells);
+    hipLaunchKernelGGL(k_ds_chunks<AGG>, dim3(grid_for(R, 4, 1u << 20)), dim3(256), 0, st, da, p, ncells, vlen, R);
+    hipLaunchKernelGGL(k_ds_finalize<AGG>, dim3(span_blocks), dim3(256), 0, st, da, p);
+    hipLaunchKernelGGL(k_ds_collect, dim3(grid_for(n_kept, 256)), dim3(256), 0, st, da, p);
+    fa.span_list = p.list;
+    fa.span_count = p.list_count;
+  }
+};
 
 template <int AGG, int MODE, bool RATE>
 static void launch_reduce(tsdbhip_ctx* ctx, unsigned blocks, const ReduceArgs& r, const FinalArgs& f,
@@ -457,60 +519,35 @@ static int spangroup_run(tsdbhip_ctx* ctx, const tsdbhip_sg_desc* d, tsdbhip_sg_
   if (n_kept) {
     const unsigned blocks = grid_for(n_kept, 4, 65536);
     // wide rows (the reference's hourly compacted rows) take the streaming
-    // kernel; rows of a few cells (sparse series) the general one.
+    // kernels; rows of a few cells (sparse series) the general one. With
+    // downsampling, regular-cadence integer spans go chunk-parallel first.
     const char* force = getenv("TSDBHIP_DECODE");
     bool fast = R > 0 && h.n_input / R >= 64;
-    if (force && !strcmp(force, "general")) fast = false;
-    if (force && !strcmp(force, "fast")) fast = true;
+    bool chunks = fast;
+    if (force && !strcmp(force, "general")) fast = chunks = false;
+    if (force && !strcmp(force, "fast")) { fast = true; chunks = false; }
+    if (force && !strcmp(force, "chunks")) fast = chunks = true;
     da.fb_list = scratch<uint32_t>(ctx, "fb_list", n_kept);
     da.fb_count = scratch<uint32_t>(ctx, "fb_count", 1, true);
     da.use_fb = 0;
-    if (fast) {
-      // spans the streaming kernel cannot take are queued for the general one
-      DecodeArgs ga = da;
-      ga.use_fb = 1;
-      if (interval == 0) {
-        hipLaunchKernelGGL((k_decode_fast<0, false>), dim3(blocks), dim3(256), 0, st, da, row_ncells, row_val_len);
-        hipLaunchKernelGGL(k_decode_nods, dim3(blocks), dim3(256), 0, st, ga);
-      } else {
-        switch (ds_agg) {
-          case 0: hipLaunchKernelGGL((k_decode_fast<0, true>), dim3(blocks), dim3(256), 0, st, da, row_ncells, row_val_len); break;
-          case 1: hipLaunchKernelGGL((k_decode_fast<1, true>), dim3(blocks), dim3(256), 0, st, da, row_ncells, row_val_len); break;
-          case 2: hipLaunchKernelGGL((k_decode_fast<2, true>), dim3(blocks), dim3(256), 0, st, da, row_ncells, row_val_len); break;
-          case 3: hipLaunchKernelGGL((k_decode_fast<3, true>), dim3(blocks), dim3(256), 0, st, da, row_ncells, row_val_len); break;
-          default: hipLaunchKernelGGL((k_decode_fast<4, true>), dim3(blocks), dim3(256), 0, st, da, row_ncells, row_val_len); break;
-        }
-        HIPCHK(hipEventRecord(ctx->ev[6], st));
-        switch (ds_agg) {
-          case 0: launch_decode_ds<0>(ctx, blocks, ga); break;
-          case 1: launch_decode_ds<1>(ctx, blocks, ga); break;
-          case 2: launch_decode_ds<2>(ctx, blocks, ga); break;
-          case 3: launch_decode_ds<3>(ctx, blocks, ga); break;
-          default: launch_decode_ds<4>(ctx, blocks, ga); break;
-        }
-      }
-    } else if (fast) {
-      if (interval == 0) {
-        hipLaunchKernelGGL((k_decode_fast<0, false>), dim3(blocks), dim3(256), 0, st, da, row_ncells, row_val_len);
-      } else {
-        switch (ds_agg) {
-          case 0: hipLaunchKernelGGL((k_decode_fast<0, true>), dim3(blocks), dim3(256), 0, st, da, row_ncells, row_val_len); break;
-          case 1: hipLaunchKernelGGL((k_decode_fast<1, true>), dim3(blocks), dim3(256), 0, st, da, row_ncells, row_val_len); break;
-          case 2: hipLaunchKernelGGL((k_decode_fast<2, true>), dim3(blocks), dim3(256), 0, st, da, row_ncells, row_val_len); break;
-          case 3: hipLaunchKernelGGL((k_decode_fast<3, true>), dim3(blocks), dim3(256), 0, st, da, row_ncells, row_val_len); break;
-          default: hipLaunchKernelGGL((k_decode_fast<4, true>), dim3(blocks), dim3(256), 0, st, da, row_ncells, row_val_len); break;
-        }
-      }
+    da.span_list = nullptr;
+    da.span_count = nullptr;
+    DecodeArgs ga = da;  // spans the streaming kernels hand to the general ones
+    ga.use_fb = 1;
+    if (!fast) {
+      if (interval == 0) hipLaunchKernelGGL(k_decode_nods, dim3(blocks), dim3(256), 0, st, da);
+      else launch_agg<LaunchGeneralDs>(ds_agg, ctx, blocks, da);
     } else if (interval == 0) {
-      hipLaunchKernelGGL(k_decode_nods, dim3(blocks), dim3(256), 0, st, da);
+      hipLaunchKernelGGL((k_decode_fast<0, false>), dim3(blocks), dim3(256), 0, st, da, row_ncells, row_val_len);
+      hipLaunchKernelGGL(k_decode_nods, dim3(blocks), dim3(256), 0, st, ga);
     } else {
-      switch (ds_agg) {
-        case 0: launch_decode_ds<0>(ctx, blocks, da); break;
-        case 1: launch_decode_ds<1>(ctx, blocks, da); break;
-        case 2: launch_decode_ds<2>(ctx, blocks, da); break;
-        case 3: launch_decode_ds<3>(ctx, blocks, da); break;
-        default: launch_decode_ds<4>(ctx, blocks, da); break;
+      DecodeArgs fa = da;
+      if (chunks && ds_agg != 4) {
+        const uint64_t chunk_bound = d->qual_nbytes / 2 / FCH + R + 1;
+        launch_agg<LaunchChunks>(ds_agg, ctx, da, fa, row_ncells, row_val_len, R, e_total, chunk_bound);
       }
+      launch_agg<LaunchFastDs>(ds_agg, ctx, blocks, fa, row_ncells, row_val_len);
+      launch_agg<LaunchGeneralDs>(ds_agg, ctx, blocks, ga);
     }
   }
   HIPCHK(hipEventRecord(ctx->ev[2], st));

@@ -33,6 +33,57 @@ DEVI uint64_t ballot(bool p) { return __ballot(p); }
 DEVI uint64_t lanemask_le(int lane) { return lane == 63 ? ~0ull : ((2ull << lane) - 1); }
 DEVI uint64_t lanemask_lt(int lane) { return (1ull << lane) - 1; }
 
+// ---- DPP wave scans (row_shr within 16-lane rows, then row_bcast 15/31) ----
+// Pure VALU: no LDS traffic, unlike __shfl (ds_bpermute).
+template <int CTRL, int ROWMASK>
+DEVI uint32_t dpp_u32(uint32_t x) {
+  return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, CTRL, ROWMASK, 0xf, false);
+}
+DEVI uint32_t wave_incl_scan_u32_dpp(uint32_t x) {
+  x += dpp_u32<0x111, 0xf>(x);
+  x += dpp_u32<0x112, 0xf>(x);
+  x += dpp_u32<0x114, 0xf>(x);
+  x += dpp_u32<0x118, 0xf>(x);
+  x += dpp_u32<0x142, 0xa>(x);
+  x += dpp_u32<0x143, 0xc>(x);
+  return x;
+}
+template <int CTRL, int ROWMASK>
+DEVI uint64_t dpp_u64(uint64_t x) {
+  const uint32_t lo = dpp_u32<CTRL, ROWMASK>((uint32_t)x);
+  const uint32_t hi = dpp_u32<CTRL, ROWMASK>((uint32_t)(x >> 32));
+  return ((uint64_t)hi << 32) | lo;
+}
+DEVI uint64_t wave_incl_scan_u64_dpp(uint64_t x) {
+  x += dpp_u64<0x111, 0xf>(x);
+  x += dpp_u64<0x112, 0xf>(x);
+  x += dpp_u64<0x114, 0xf>(x);
+  x += dpp_u64<0x118, 0xf>(x);
+  x += dpp_u64<0x142, 0xa>(x);
+  x += dpp_u64<0x143, 0xc>(x);
+  return x;
+}
+
+// floor(a / n) for u64 a, u32 n > 0: 32-bit path when possible.
+DEVI uint64_t udiv64_32(uint64_t a, uint32_t n) {
+  if ((a >> 32) == 0) return (uint32_t)a / n;
+  if (n == 1) return a;
+  uint64_t q = (uint64_t)((double)a / (double)n);
+  int64_t r = (int64_t)(a - q * (uint64_t)n);
+  q += (int64_t)floor((double)r / (double)n);
+  r = (int64_t)(a - q * (uint64_t)n);
+  while (r < 0) { q--; r += n; }
+  while (r >= (int64_t)n) { q++; r -= n; }
+  return q;
+}
+// Java long / int with truncation toward zero (n >= 1).
+DEVI int64_t ldiv64_32(int64_t a, uint32_t n) {
+  if (a >= INT32_MIN && a <= INT32_MAX && n <= (uint32_t)INT32_MAX) return (int64_t)((int32_t)a / (int32_t)n);
+  const uint64_t ua = a < 0 ? (uint64_t)0 - (uint64_t)a : (uint64_t)a;
+  const uint64_t q = udiv64_32(ua, n);
+  return a < 0 ? (int64_t)((uint64_t)0 - q) : (int64_t)q;
+}
+
 // Lanes of one wave exchanging data through LDS: the wave's LDS operations
 // execute in order, so only the compiler must not move accesses across.
 DEVI void wave_lds_sync() {

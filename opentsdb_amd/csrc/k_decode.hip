@@ -57,6 +57,8 @@ struct DecodeArgs {
   uint32_t* fb_list;          // spans the fast kernel handed to the general one
   uint32_t* fb_count;         // [1]; general kernels iterate this list when `use_fb`
   int32_t use_fb;
+  const uint32_t* span_list;  // k_decode_fast: spans to take (null = all kept)
+  const uint32_t* span_count;
 };
 
 #define BAD_ILLEGAL 1

@@ -14,10 +14,11 @@ pytestmark = pytest.mark.gpu
 AGGS = [0, 1, 2, 3, 4]
 
 
-@pytest.fixture(autouse=True, params=["auto", "general", "fast"])
+@pytest.fixture(autouse=True, params=["auto", "general", "fast", "chunks"])
 def decode_path(request, monkeypatch):
-    """Run every case through the streaming decode kernel (with its fallback
-    queue) and through the general per-span kernel."""
+    """Run every case through the chunk-parallel downsampler, the streaming
+    decode kernel (each with its fallback queue) and the general per-span
+    kernel."""
     if request.param != "auto":
         monkeypatch.setenv("TSDBHIP_DECODE", request.param)
     else:
@@ -116,6 +117,86 @@ def test_jittered_ds(ctx, seed, ds):
     for agg in AGGS:
         g, o = run_both(ctx, ss, agg=agg, ds_interval=ds[0], ds_agg=ds[1], exact=True)
         assert_same(g, o, exact_double=True)
+
+
+def regular_int_spans(n_spans, n_pts, step, seed, wide=True, perturb=None, offset_step=7):
+    """Regular-cadence integer series, 8-byte cells (wide) or 4-byte ints;
+    `perturb(s, ts_list)` may drop / shift points to break the cadence."""
+    rng = np.random.default_rng(seed)
+    spans = []
+    for s in range(n_spans):
+        ts = [T0 + 3 + s * offset_step + step * i for i in range(n_pts)]
+        if perturb:
+            ts = perturb(s, ts)
+        if wide:
+            vals = [int(v) for v in rng.integers(-(1 << 40), 1 << 40, len(ts))]
+            spans.append(I(list(zip(ts, vals)), minimal=False))
+        else:
+            vals = [int(v) for v in rng.integers(1 << 17, 1 << 30, len(ts)) * rng.choice([-1, 1], len(ts))]
+            spans.append(I(list(zip(ts, vals)), minimal=True))
+    return packing.pack_spans(spans)
+
+
+@pytest.mark.parametrize("step,interval", [(1, 60), (1, 45), (10, 60), (1, 7), (1, 1000), (2, 5000),
+                                           (1, 1), (3, 2), (1, 100000)])
+@pytest.mark.parametrize("ds_agg", [0, 1, 2, 3])
+def test_chunk_regular(ctx, step, interval, ds_agg):
+    """Chunk-parallel downsampling: buckets inside a chunk, spilling over
+    chunks and hour rows, longer than a row, one cell per bucket, and a
+    single bucket for the whole span."""
+    ss = regular_int_spans(6, 3000, step, seed=interval + ds_agg)
+    for agg in (0, 3, 1):
+        g, o = run_both(ctx, ss, agg=agg, ds_interval=interval, ds_agg=ds_agg)
+        assert_same(g, o, exact_double=True)
+
+
+@pytest.mark.parametrize("ds_agg", [0, 1, 2, 3])
+def test_chunk_regular_int32_rows(ctx, ds_agg):
+    ss = regular_int_spans(5, 2500, 1, seed=11, wide=False)
+    g, o = run_both(ctx, ss, agg=0, ds_interval=60, ds_agg=ds_agg)
+    assert_same(g, o, exact_double=True)
+
+
+def _drop_one(s, ts):
+    return ts[:700 + 97 * s] + ts[701 + 97 * s:]
+
+
+def _shift_one(s, ts):
+    out = list(ts)
+    i = 1000 + 31 * s
+    out[i] = out[i] - 1 if out[i] - 1 > out[i - 1] else out[i]
+    return out
+
+
+def _gap(s, ts):
+    return ts[:500] + [t + 37 for t in ts[500:]] if s % 2 else ts
+
+
+@pytest.mark.parametrize("perturb", [_drop_one, _shift_one, _gap])
+@pytest.mark.parametrize("ds_agg", [0, 1, 2, 3])
+def test_chunk_cadence_breaks(ctx, perturb, ds_agg):
+    """A missing, shifted or gapped point breaks the regular-head hypothesis:
+    the span must fall back to the serial kernels with identical results."""
+    ss = regular_int_spans(8, 3000, 1, seed=21, perturb=perturb)
+    for interval in (60, 13):
+        g, o = run_both(ctx, ss, agg=0, ds_interval=interval, ds_agg=ds_agg)
+        assert_same(g, o, exact_double=True)
+
+
+def test_chunk_mixed_eligibility(ctx):
+    """Regular wide int spans next to float, minimal-width, sparse and
+    seek-start spans in one group."""
+    T = T0
+    spans = [I([(T + 3 + s * 7 + i, (i * 7919 + s) << 20) for i in range(2000)], minimal=False)
+             for s in range(4)]
+    spans += [F([(T + 3 + 2 * i, 0.25 * i) for i in range(1500)]),
+              I([(T + 11 * i, i % 300) for i in range(400)]),
+              I([(T + 500 + 997 * i, 5 * i) for i in range(6)])]
+    ss = packing.pack_spans(spans)
+    for ds_agg in (0, 1, 2, 3):
+        for start in (0, T + 700):
+            g, o = run_both(ctx, ss, start=start, agg=0, ds_interval=60, ds_agg=ds_agg)
+            assert_same(g, o, exact_double=True)
 
 
 @pytest.mark.parametrize("window", [(100, 2000), (500, 1500), (0, 700), (1700, U32MAX)])
