@@ -302,12 +302,13 @@ struct LaunchChunks {
     hipLaunchKernelGGL(k_row_chunks, dim3(grid_for(R, 256)), dim3(256), 0, st, ncells, R, nch);
     dscan_u64(ctx, nch, rc0, R, scratch<uint64_t>(ctx, "ck_nch_total", 1), "ck");
     p.row_chunk0 = rc0;
-    p.plan_k = scratch<uint32_t>(ctx, "ck_plan_k", n_kept);
-    p.plan_nb = scratch<uint32_t>(ctx, "ck_plan_nb", n_kept);
+    p.row_prev_ts = scratch<uint32_t>(ctx, "ck_row_prev_ts", R);
+    p.plan = scratch<SpanPlan>(ctx, "ck_plan", n_kept);
     p.fail = scratch<uint32_t>(ctx, "ck_fail", n_kept);
-    p.hp_n = scratch<uint32_t>(ctx, "ck_hp_n", e_total);
+    p.tail_ts = scratch<uint32_t>(ctx, "ck_tail_ts", n_kept);
+    p.hp_nrel = scratch<uint32_t>(ctx, "ck_hp_nrel", e_total);
     p.hp_ref = scratch<uint32_t>(ctx, "ck_hp_ref", e_total);
-    p.hp_rel = scratch<uint32_t>(ctx, "ck_hp_rel", e_total);
+    p.hp_pre = scratch<uint32_t>(ctx, "ck_hp_pre", e_total);
     p.hp_v = scratch<int64_t>(ctx, "ck_hp_v", e_total);
     p.lp_n = scratch<uint32_t>(ctx, "ck_lp_n", chunk_bound);
     p.lp_ts = scratch<uint64_t>(ctx, "ck_lp_ts", chunk_bound);
