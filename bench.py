@@ -59,6 +59,20 @@ def ref_row_bytes(n_series, n_points, step, kind):
     return n_series * per_span
 
 
+def pmc_traffic(config, kernel, world):
+    """HBM bytes per launch of `kernel` from the committed rocprofv3 PMC
+    summary of this config (profiles/pmc_<config>.json, made by
+    profiles/profile.sh + pmc_summary.py: 2 x FETCH_SIZE + WRITE_SIZE)."""
+    path = os.path.join(ROOT, "profiles", f"pmc_{config}.json")
+    if world != 1 or not os.path.exists(path):
+        return None, None
+    ks = json.load(open(path)).get("kernels", {})
+    for name, e in ks.items():
+        if name.split("<")[0] == kernel and e.get("hbm_bytes_per_launch"):
+            return e["hbm_bytes_per_launch"], os.path.relpath(path, ROOT)
+    return None, None
+
+
 def dist_setup(n_gpus):
     world = int(os.environ.get("WORLD_SIZE", "1"))
     if world == 1:
@@ -169,13 +183,14 @@ def main():
     import torch
     barrier()
     torch.cuda.synchronize()
-    decode_ms, total_ms = [], []
+    hot_ms, total_ms, hot_kernel = [], [], 0
     t0 = time.perf_counter()
     for _ in range(args.steps):
         step_once()
         tm = ctx.timing()
-        decode_ms.append(tm.decode_ms)
+        hot_ms.append(tm.hot_ms)
         total_ms.append(tm.total_ms)
+        hot_kernel = tm.hot_kernel
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
     barrier()
@@ -188,9 +203,13 @@ def main():
     ms_step = elapsed / args.steps * 1e3
     value = n_input / (elapsed / args.steps)
 
+    # roofline of the dominant kernel: SURVEY.md §8(d) algorithmic bytes (the
+    # row bytes it streams) over its own duration (HIP events on its stream)
     local_bytes = ref_row_bytes(hi - lo, n_points, step, kind)
-    dec = float(np.mean(decode_ms))
-    achieved = local_bytes / (dec * 1e-3) / 1e9
+    hot = float(np.mean(hot_ms))
+    achieved = local_bytes / (hot * 1e-3) / 1e9
+    kname = _abi.HOT_NAMES.get(hot_kernel, "none")
+    traffic, traffic_src = pmc_traffic(args.config, kname, world)
     if rank == 0:
         res = {
             "metric": METRIC,
@@ -216,14 +235,15 @@ def main():
             },
             "roofline": {
                 "bound": "hbm",
-                "kernel": "k_decode_ds (RowSeq decode + greedy downsample)" if dsi else "k_decode_nods",
+                "kernel": kname,
                 "achieved": achieved,
                 "peak": HBM_PEAK_GBS,
                 "unit": "GB/s",
                 "frac": achieved / HBM_PEAK_GBS,
-                "traffic": None,
+                "traffic": traffic,
+                "traffic_source": traffic_src,
                 "alg_bytes_per_launch": local_bytes,
-                "kernel_ms": dec,
+                "kernel_ms": hot,
                 "step_device_ms": float(np.mean(total_ms)),
             },
         }

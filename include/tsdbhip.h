@@ -72,6 +72,12 @@ extern "C" {
 #define TSDBHIP_AGG_AVG 3
 #define TSDBHIP_AGG_DEV 4
 
+/* tsdbhip_timing.hot_kernel */
+#define TSDBHIP_HOT_NONE        0
+#define TSDBHIP_HOT_DS_CHUNKS   1 /* chunk-parallel decode + downsample     */
+#define TSDBHIP_HOT_DECODE_FAST 2 /* streaming per-span decode(+downsample) */
+#define TSDBHIP_HOT_DECODE_GEN  3 /* general per-span decode(+downsample)   */
+
 /* ---- desc flags ------------------------------------------------------- */
 #define TSDBHIP_DESC_DEVICE   0x1u /* every array pointer in the desc is a
                                       device pointer (data already in HBM) */
@@ -135,7 +141,9 @@ typedef struct tsdbhip_timing {
   float    grid_ms;         /* union-grid construction                      */
   float    reduce_ms;       /* cross-span reduction + combine               */
   float    exchange_ms;     /* RCCL exchange (sharded runs)                 */
-  float    reserved[3];
+  float    hot_ms;          /* the dominant HBM-streaming kernel alone      */
+  uint32_t hot_kernel;      /* TSDBHIP_HOT_*: which kernel hot_ms timed      */
+  float    reserved;
   uint64_t decode_bytes;    /* algorithmic bytes read+written by decode      */
   uint64_t alg_bytes;       /* SURVEY §8(d) algorithmic bytes of the call   */
   uint64_t n_grid;          /* |G|                                           */

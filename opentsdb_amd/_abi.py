@@ -85,6 +85,10 @@ class SgOut(C.Structure):
     ]
 
 
+HOT_NONE, HOT_DS_CHUNKS, HOT_DECODE_FAST, HOT_DECODE_GEN = 0, 1, 2, 3
+HOT_NAMES = {1: "k_ds_chunks", 2: "k_decode_fast", 3: "k_decode_general"}
+
+
 class Timing(C.Structure):
     _fields_ = [
         ("total_ms", C.c_float),
@@ -92,7 +96,9 @@ class Timing(C.Structure):
         ("grid_ms", C.c_float),
         ("reduce_ms", C.c_float),
         ("exchange_ms", C.c_float),
-        ("reserved", C.c_float * 3),
+        ("hot_ms", C.c_float),
+        ("hot_kernel", C.c_uint32),
+        ("reserved", C.c_float),
         ("decode_bytes", C.c_uint64),
         ("alg_bytes", C.c_uint64),
         ("n_grid", C.c_uint64),

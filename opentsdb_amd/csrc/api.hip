@@ -55,7 +55,8 @@ struct tsdbhip_ctx {
   std::string err;
   std::map<std::string, Buf> bufs;
   void* host_small = nullptr;  // pinned readback area
-  hipEvent_t ev[8] = {};
+  hipEvent_t ev[10] = {};  // [8],[9] bracket the dominant kernel
+  uint32_t hot_kernel = 0;
   tsdbhip_timing timing = {};
   ncclComm_t comm = nullptr;
   int nranks = 1, rank = 0;
@@ -317,7 +318,10 @@ struct LaunchChunks {
     p.list_count = scratch<uint32_t>(ctx, "ck_list_count", 1, true);
     const unsigned span_blocks = grid_for(n_kept, 4, 65536);
     hipLaunchKernelGGL(k_ds_plan, dim3(span_blocks), dim3(256), 0, st, da, p, ncells);
+    HIPCHK(hipEventRecord(ctx->ev[8], st));
     hipLaunchKernelGGL(k_ds_chunks<AGG>, dim3(grid_for(R, 4, 1u << 20)), dim3(256), 0, st, da, p, ncells, vlen, R);
+    HIPCHK(hipEventRecord(ctx->ev[9], st));
+    ctx->hot_kernel = TSDBHIP_HOT_DS_CHUNKS;
     hipLaunchKernelGGL(k_ds_finalize<AGG>, dim3(span_blocks), dim3(256), 0, st, da, p);
     hipLaunchKernelGGL(k_ds_collect, dim3(grid_for(n_kept, 256)), dim3(256), 0, st, da, p);
     fa.span_list = p.list;
@@ -419,6 +423,7 @@ static int spangroup_run(tsdbhip_ctx* ctx, const tsdbhip_sg_desc* d, tsdbhip_sg_
   const int32_t interval = d->ds_interval > 0 ? d->ds_interval : 0;
   hipStream_t st = ctx->stream;
   tsdbhip_timing tm = {};
+  ctx->hot_kernel = TSDBHIP_HOT_NONE;
   out->n_out = 0;
   out->n_input_points = 0;
   out->err_code = 0;
@@ -535,11 +540,15 @@ static int spangroup_run(tsdbhip_ctx* ctx, const tsdbhip_sg_desc* d, tsdbhip_sg_
     da.span_count = nullptr;
     DecodeArgs ga = da;  // spans the streaming kernels hand to the general ones
     ga.use_fb = 1;
+    ctx->hot_kernel = fast ? TSDBHIP_HOT_DECODE_FAST : TSDBHIP_HOT_DECODE_GEN;
+    HIPCHK(hipEventRecord(ctx->ev[8], st));
     if (!fast) {
       if (interval == 0) hipLaunchKernelGGL(k_decode_nods, dim3(blocks), dim3(256), 0, st, da);
       else launch_agg<LaunchGeneralDs>(ds_agg, ctx, blocks, da);
+      HIPCHK(hipEventRecord(ctx->ev[9], st));
     } else if (interval == 0) {
       hipLaunchKernelGGL((k_decode_fast<0, false>), dim3(blocks), dim3(256), 0, st, da, row_ncells, row_val_len);
+      HIPCHK(hipEventRecord(ctx->ev[9], st));
       hipLaunchKernelGGL(k_decode_nods, dim3(blocks), dim3(256), 0, st, ga);
     } else {
       DecodeArgs fa = da;
@@ -548,6 +557,7 @@ static int spangroup_run(tsdbhip_ctx* ctx, const tsdbhip_sg_desc* d, tsdbhip_sg_
         launch_agg<LaunchChunks>(ds_agg, ctx, da, fa, row_ncells, row_val_len, R, e_total, chunk_bound);
       }
       launch_agg<LaunchFastDs>(ds_agg, ctx, blocks, fa, row_ncells, row_val_len);
+      if (ctx->hot_kernel == TSDBHIP_HOT_DECODE_FAST) HIPCHK(hipEventRecord(ctx->ev[9], st));
       launch_agg<LaunchGeneralDs>(ds_agg, ctx, blocks, ga);
     }
   }
@@ -744,6 +754,8 @@ static int spangroup_run(tsdbhip_ctx* ctx, const tsdbhip_sg_desc* d, tsdbhip_sg_
   }
   HIPCHK(hipStreamSynchronize(st));
   tm.decode_ms = ev_ms(ctx->ev[1], ctx->ev[2]);
+  if (ctx->hot_kernel) tm.hot_ms = ev_ms(ctx->ev[8], ctx->ev[9]);
+  tm.hot_kernel = ctx->hot_kernel;
   tm.grid_ms = ev_ms(ctx->ev[3], ctx->ev[4]);
   tm.reduce_ms = ev_ms(ctx->ev[4], ctx->ev[5]);
   tm.total_ms = ev_ms(ctx->ev[0], ctx->ev[5]);
