@@ -44,7 +44,7 @@
 extern "C" {
 #endif
 
-#define TSDBHIP_ABI_VERSION 1
+#define TSDBHIP_ABI_VERSION 2
 
 /* ---- return codes ---------------------------------------------------- */
 #define TSDBHIP_OK               0
@@ -77,6 +77,8 @@ extern "C" {
 #define TSDBHIP_HOT_DS_CHUNKS   1 /* chunk-parallel decode + downsample     */
 #define TSDBHIP_HOT_DECODE_FAST 2 /* streaming per-span decode(+downsample) */
 #define TSDBHIP_HOT_DECODE_GEN  3 /* general per-span decode(+downsample)   */
+#define TSDBHIP_HOT_COMPACT     4 /* row classification + single/trivial
+                                     compaction (tsdbhip_compact_rows)      */
 
 /* ---- desc flags ------------------------------------------------------- */
 #define TSDBHIP_DESC_DEVICE   0x1u /* every array pointer in the desc is a
@@ -133,7 +135,8 @@ typedef struct tsdbhip_sg_out {
                                lazy reference, or -1 if unknown / no error  */
 } tsdbhip_sg_out;
 
-/* Per-call device timings of the last tsdbhip_spangroup_run on a ctx,
+/* Per-call device timings of the last tsdbhip_spangroup_run (or
+ * tsdbhip_compact_rows: total_ms, hot_ms, hot_kernel only) on a ctx,
  * measured with HIP events on the ctx stream (milliseconds). */
 typedef struct tsdbhip_timing {
   float    total_ms;        /* first kernel start .. last kernel end        */
@@ -154,18 +157,30 @@ typedef struct tsdbhip_timing {
 /*
  * A batch of HBase rows, each a list of KeyValues (qualifier, value) in the
  * order HBase returns them (sorted by qualifier bytes). For every row the
- * library computes compacted[0] of CompactionQueue.compact(row, compacted).
+ * library computes compacted[0] of CompactionQueue.compact(row, compacted)
+ * (CompactionQueue.java:243-435) — the cell TsdbQuery.findSpans hands to
+ * Span.addRow (TsdbQuery.java:264-266).
+ *
+ * Layout (chosen so the per-KV metadata stays small next to the ~7 bytes of
+ * cell data per KV): the qualifiers of row r's KVs are packed back to back,
+ * in KV order, in qual_bytes[row_qual_off[r], row_qual_off[r+1]); likewise
+ * the values in val_bytes[row_val_off[r], row_val_off[r+1]). Per KV only the
+ * two lengths are passed (u16: an OpenTSDB qualifier is at most 2*4096 bytes
+ * and a compacted value at most 8*4096+1). Offsets must be non-decreasing
+ * and each row's lengths must add up to its extents, else
+ * TSDBHIP_E_INVALID_ARG.
  */
 typedef struct tsdbhip_rows_desc {
-  uint32_t flags;            /* TSDBHIP_DESC_DEVICE                          */
+  uint32_t flags;               /* TSDBHIP_DESC_DEVICE: desc AND out arrays
+                                   are device pointers                      */
   uint32_t reserved0;
   uint64_t n_rows;
   uint64_t n_kvs;
-  const uint64_t* row_kv_start; /* [n_rows+1]                                */
-  const uint64_t* kv_qual_off;  /* [n_kvs] byte offset into qual_bytes       */
-  const uint32_t* kv_qual_len;  /* [n_kvs]                                   */
-  const uint64_t* kv_val_off;   /* [n_kvs] byte offset into val_bytes        */
-  const uint32_t* kv_val_len;   /* [n_kvs]                                   */
+  const uint64_t* row_kv_start; /* [n_rows+1] KVs of row r                   */
+  const uint64_t* row_qual_off; /* [n_rows+1] qualifier bytes of row r       */
+  const uint64_t* row_val_off;  /* [n_rows+1] value bytes of row r           */
+  const uint16_t* kv_qual_len;  /* [n_kvs] qualifier().length                */
+  const uint16_t* kv_val_len;   /* [n_kvs] value().length                    */
   const uint8_t*  qual_bytes;
   uint64_t        qual_nbytes;
   const uint8_t*  val_bytes;
@@ -178,7 +193,20 @@ typedef struct tsdbhip_rows_desc {
 #define TSDBHIP_ROW_TRIVIAL  2  /* trivialCompact                             */
 #define TSDBHIP_ROW_COMPLEX  3  /* complexCompact                             */
 #define TSDBHIP_ROW_ERROR    4  /* IllegalDataException                       */
+#define TSDBHIP_ROW_OOB      5  /* ArrayIndexOutOfBoundsException
+                                   (breakDownValues on a malformed compacted
+                                   cell, CompactionQueue.java:708,722)       */
 
+/*
+ * Output: row r's compacted qualifier is written at
+ *   qual_bytes[row_qual_off[r] - row_qual_off[0]]   (never longer than the
+ *   row's input qualifiers), its value at
+ *   val_bytes[row_val_off[r] - row_val_off[0] + r]  (never longer than the
+ *   row's input values + 1 meta byte),
+ * so one pass needs no output scan: qual_capacity >= qualifier extent and
+ * val_capacity >= value extent + n_rows. Bytes between rows are undefined.
+ * Rows with status NONE/ERROR/OOB have length 0.
+ */
 typedef struct tsdbhip_rows_out {
   uint64_t qual_capacity;    /* in: bytes available in qual_bytes           */
   uint64_t val_capacity;     /* in: bytes available in val_bytes            */
@@ -189,8 +217,10 @@ typedef struct tsdbhip_rows_out {
   uint32_t* row_val_len;     /* [n_rows]                                     */
   uint8_t*  qual_bytes;      /* out                                          */
   uint8_t*  val_bytes;       /* out                                          */
-  uint64_t  qual_used;
-  uint64_t  val_used;
+  uint64_t  qual_used;       /* out: qualifier extent written               */
+  uint64_t  val_used;        /* out: value extent written                   */
+  uint64_t  n_complex;       /* out: rows that reached complexCompact
+                                (status COMPLEX, ERROR or OOB)             */
 } tsdbhip_rows_out;
 
 /* ---- synthetic, HBM-resident inputs (bench / tests) -------------------- */

@@ -6,7 +6,7 @@ and the test harness.
 """
 import ctypes as C
 
-ABI_VERSION = 1
+ABI_VERSION = 2
 
 OK = 0
 E_ILLEGAL_DATA = -1
@@ -34,13 +34,14 @@ DESC_DEVICE = 0x1
 EXACT_ORDER = 0x2
 SHARDED = 0x4
 
-ROW_NONE, ROW_SINGLE, ROW_TRIVIAL, ROW_COMPLEX, ROW_ERROR = 0, 1, 2, 3, 4
+ROW_NONE, ROW_SINGLE, ROW_TRIVIAL, ROW_COMPLEX, ROW_ERROR, ROW_OOB = 0, 1, 2, 3, 4, 5
 
 SYN_INT64_COUNTER, SYN_FLOAT32, SYN_FLOAT64 = 0, 1, 2
 
 UNIQUE_ID_BYTES = 128
 
 P8 = C.POINTER(C.c_uint8)
+P16 = C.POINTER(C.c_uint16)
 P32 = C.POINTER(C.c_uint32)
 P64 = C.POINTER(C.c_uint64)
 PI64 = C.POINTER(C.c_int64)
@@ -113,10 +114,10 @@ class RowsDesc(C.Structure):
         ("n_rows", C.c_uint64),
         ("n_kvs", C.c_uint64),
         ("row_kv_start", P64),
-        ("kv_qual_off", P64),
-        ("kv_qual_len", P32),
-        ("kv_val_off", P64),
-        ("kv_val_len", P32),
+        ("row_qual_off", P64),
+        ("row_val_off", P64),
+        ("kv_qual_len", P16),
+        ("kv_val_len", P16),
         ("qual_bytes", P8),
         ("qual_nbytes", C.c_uint64),
         ("val_bytes", P8),
@@ -137,6 +138,7 @@ class RowsOut(C.Structure):
         ("val_bytes", P8),
         ("qual_used", C.c_uint64),
         ("val_used", C.c_uint64),
+        ("n_complex", C.c_uint64),
     ]
 
 

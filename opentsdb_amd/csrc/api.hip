@@ -32,6 +32,7 @@
 #include "k_util.hip"
 #include "k_decode_fast.hip"
 #include "k_ds_chunks.hip"
+#include "k_compact.hip"
 
 using namespace tsdb;
 
@@ -926,8 +927,121 @@ extern "C" int tsdbhip_desc_download(tsdbhip_ctx* ctx, const tsdbhip_sg_desc* d,
 }
 
 // ------------------------------------------------------- compaction ------
-extern "C" int tsdbhip_compact_rows(tsdbhip_ctx* ctx, const tsdbhip_rows_desc* desc, tsdbhip_rows_out* out) {
-  if (!ctx || !desc || !out) return TSDBHIP_E_INVALID_ARG;
-  set_error(ctx, "tsdbhip_compact_rows: GPU compaction not built yet");
-  return TSDBHIP_E_UNSUPPORTED;
+// CompactionQueue.compact (CompactionQueue.java:243-743) for a batch of rows:
+// k_compact_rows (wave per row) then k_compact_complex for the rows holding a
+// compacted cell (LDS cell table, or global scratch for very long rows).
+extern "C" int tsdbhip_compact_rows(tsdbhip_ctx* ctx, const tsdbhip_rows_desc* d, tsdbhip_rows_out* out) {
+  if (!ctx || !d || !out) return TSDBHIP_E_INVALID_ARG;
+  std::lock_guard<std::mutex> lock(ctx->mu);
+  out->qual_used = out->val_used = out->n_complex = 0;
+  const uint64_t R = d->n_rows;
+  if (R == 0) return TSDBHIP_OK;
+  if (!d->row_kv_start || !d->row_qual_off || !d->row_val_off || (d->n_kvs && (!d->kv_qual_len || !d->kv_val_len)) ||
+      !d->qual_bytes || !d->val_bytes || !out->row_status || !out->row_qual_off || !out->row_qual_len ||
+      !out->row_val_off || !out->row_val_len || !out->qual_bytes || !out->val_bytes || R >= (1ull << 32)) {
+    set_error(ctx, "tsdbhip_compact_rows: null array or too many rows");
+    return TSDBHIP_E_INVALID_ARG;
+  }
+  try {
+    HIPCHK(hipSetDevice(ctx->device));
+    const bool dev = (d->flags & TSDBHIP_DESC_DEVICE) != 0;
+    uint64_t ext[4];  // row_qual_off[0], [R], row_val_off[0], [R]
+    if (dev) {
+      uint64_t* h = (uint64_t*)ctx->host_small;
+      HIPCHK(hipMemcpyAsync(h + 0, d->row_qual_off, 8, hipMemcpyDeviceToHost, ctx->stream));
+      HIPCHK(hipMemcpyAsync(h + 1, d->row_qual_off + R, 8, hipMemcpyDeviceToHost, ctx->stream));
+      HIPCHK(hipMemcpyAsync(h + 2, d->row_val_off, 8, hipMemcpyDeviceToHost, ctx->stream));
+      HIPCHK(hipMemcpyAsync(h + 3, d->row_val_off + R, 8, hipMemcpyDeviceToHost, ctx->stream));
+      HIPCHK(hipStreamSynchronize(ctx->stream));
+      std::memcpy(ext, h, sizeof ext);
+    } else {
+      ext[0] = d->row_qual_off[0];
+      ext[1] = d->row_qual_off[R];
+      ext[2] = d->row_val_off[0];
+      ext[3] = d->row_val_off[R];
+    }
+    if (ext[1] < ext[0] || ext[3] < ext[2] || ext[1] > d->qual_nbytes || ext[3] > d->val_nbytes) {
+      set_error(ctx, "tsdbhip_compact_rows: row offsets out of range");
+      return TSDBHIP_E_INVALID_ARG;
+    }
+    const uint64_t qext = ext[1] - ext[0], vext = ext[3] - ext[2];
+    if (out->qual_capacity < qext || out->val_capacity < vext + R) {
+      set_error(ctx, "tsdbhip_compact_rows: output needs %llu qualifier / %llu value bytes",
+                (unsigned long long)qext, (unsigned long long)(vext + R));
+      return TSDBHIP_E_CAPACITY;
+    }
+    CompactArgs a;
+    a.n_rows = R;
+    a.n_kvs = d->n_kvs;
+    a.row_kv_start = stage(ctx, "c_rks", d->row_kv_start, R + 1, dev);
+    a.row_qual_off = stage(ctx, "c_rqo", d->row_qual_off, R + 1, dev);
+    a.row_val_off = stage(ctx, "c_rvo", d->row_val_off, R + 1, dev);
+    a.kv_qual_len = stage(ctx, "c_kql", d->kv_qual_len, d->n_kvs, dev);
+    a.kv_val_len = stage(ctx, "c_kvl", d->kv_val_len, d->n_kvs, dev);
+    a.qual = stage(ctx, "c_qual", d->qual_bytes, d->qual_nbytes, dev, 64);
+    a.val = stage(ctx, "c_val", d->val_bytes, d->val_nbytes, dev, 64);
+    a.qual_nbytes = d->qual_nbytes;
+    a.val_nbytes = d->val_nbytes;
+    a.qcap = out->qual_capacity;
+    a.vcap = out->val_capacity;
+    if (dev) {
+      a.status = out->row_status;
+      a.out_qoff = out->row_qual_off;
+      a.out_qlen = out->row_qual_len;
+      a.out_voff = out->row_val_off;
+      a.out_vlen = out->row_val_len;
+      a.oq = out->qual_bytes;
+      a.ov = out->val_bytes;
+    } else {
+      a.status = scratch<uint8_t>(ctx, "c_st", R);
+      a.out_qoff = scratch<uint64_t>(ctx, "c_oqo", R);
+      a.out_qlen = scratch<uint32_t>(ctx, "c_oql", R);
+      a.out_voff = scratch<uint64_t>(ctx, "c_ovo", R);
+      a.out_vlen = scratch<uint32_t>(ctx, "c_ovl", R);
+      a.oq = scratch<uint8_t>(ctx, "c_oq", qext);
+      a.ov = scratch<uint8_t>(ctx, "c_ov", vext + R);
+      a.qcap = qext;
+      a.vcap = vext + R;
+    }
+    a.counters = scratch<uint32_t>(ctx, "c_cnt", 4, true);
+    a.list_lds = scratch<uint32_t>(ctx, "c_llds", R);
+    a.list_big = scratch<uint32_t>(ctx, "c_lbig", R);
+    a.big_cells = scratch<uint64_t>(ctx, "c_cells", qext / 2 + R + 1);
+    HIPCHK(hipEventRecord(ctx->ev[0], ctx->stream));
+    HIPCHK(hipEventRecord(ctx->ev[8], ctx->stream));
+    hipLaunchKernelGGL(k_compact_rows, dim3(grid_for(R, 4, 1u << 16)), dim3(256), 0, ctx->stream, a);
+    HIPCHK(hipGetLastError());
+    HIPCHK(hipEventRecord(ctx->ev[9], ctx->stream));
+    hipLaunchKernelGGL(k_compact_complex<true>, dim3(1024), dim3(256), 0, ctx->stream, a);
+    hipLaunchKernelGGL(k_compact_complex<false>, dim3(256), dim3(256), 0, ctx->stream, a);
+    HIPCHK(hipGetLastError());
+    HIPCHK(hipEventRecord(ctx->ev[1], ctx->stream));
+    uint32_t cnt[4];
+    readback(ctx, cnt, a.counters, sizeof cnt);
+    if (cnt[2]) {
+      set_error(ctx, "tsdbhip_compact_rows: a row's KV lengths do not match its offsets");
+      return TSDBHIP_E_INVALID_ARG;
+    }
+    if (!dev) {
+      HIPCHK(hipMemcpyAsync(out->row_status, a.status, R, hipMemcpyDeviceToHost, ctx->stream));
+      HIPCHK(hipMemcpyAsync(out->row_qual_off, a.out_qoff, 8 * R, hipMemcpyDeviceToHost, ctx->stream));
+      HIPCHK(hipMemcpyAsync(out->row_qual_len, a.out_qlen, 4 * R, hipMemcpyDeviceToHost, ctx->stream));
+      HIPCHK(hipMemcpyAsync(out->row_val_off, a.out_voff, 8 * R, hipMemcpyDeviceToHost, ctx->stream));
+      HIPCHK(hipMemcpyAsync(out->row_val_len, a.out_vlen, 4 * R, hipMemcpyDeviceToHost, ctx->stream));
+      if (qext) HIPCHK(hipMemcpyAsync(out->qual_bytes, a.oq, qext, hipMemcpyDeviceToHost, ctx->stream));
+      HIPCHK(hipMemcpyAsync(out->val_bytes, a.ov, vext + R, hipMemcpyDeviceToHost, ctx->stream));
+      HIPCHK(hipStreamSynchronize(ctx->stream));
+    }
+    tsdbhip_timing t = {};
+    t.total_ms = ev_ms(ctx->ev[0], ctx->ev[1]);
+    t.hot_ms = ev_ms(ctx->ev[8], ctx->ev[9]);
+    t.hot_kernel = TSDBHIP_HOT_COMPACT;
+    ctx->timing = t;
+    out->qual_used = qext;
+    out->val_used = vext + R;
+    out->n_complex = (uint64_t)cnt[0] + cnt[1];
+  } catch (Fail& f) {
+    return f.code;
+  }
+  return TSDBHIP_OK;
 }

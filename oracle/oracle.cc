@@ -746,7 +746,9 @@ static std::vector<Cell> breakDownValues(const std::vector<KeyValue>& row) {  //
   }
   return cells;
 }
+static thread_local bool g_entered_complex = false;  // rows that reached complexCompact
 static CompactResult complexCompact(const std::vector<KeyValue>& row) {  // :600-679
+  g_entered_complex = true;
   std::vector<Cell> cells = breakDownValues(row);
   std::stable_sort(cells.begin(), cells.end(),
                    [](const Cell& a, const Cell& b) { return memcmp_u(a.q, b.q) < 0; });
@@ -945,38 +947,51 @@ int oracle_agg_double(int agg, const double* v, size_t n, double* out) {
 }
 
 // CompactionQueue.compact(row, compacted) for a batch of rows; host only.
+// Same batch layout and output placement as tsdbhip_compact_rows
+// (include/tsdbhip.h): row r's KVs are packed back to back in
+// [row_qual_off[r], row_qual_off[r+1]) / [row_val_off[r], row_val_off[r+1]).
 int oracle_compact_rows(const tsdbhip_rows_desc* d, tsdbhip_rows_out* out) {
-  uint64_t qu = 0, vu = 0;
+  const uint64_t q0 = d->n_rows ? d->row_qual_off[0] : 0, v0 = d->n_rows ? d->row_val_off[0] : 0;
+  uint64_t qu = 0, vu = 0, nc = 0;
   for (uint64_t r = 0; r < d->n_rows; r++) {
     std::vector<KeyValue> row;
+    uint64_t qp = d->row_qual_off[r], vp = d->row_val_off[r];
     for (uint64_t k = d->row_kv_start[r]; k < d->row_kv_start[r + 1]; k++) {
       KeyValue kv;
       kv.base_time = 0;
-      kv.qualifier = slice(d->qual_bytes, d->kv_qual_off[k], d->kv_qual_len[k]);
-      kv.value = slice(d->val_bytes, d->kv_val_off[k], d->kv_val_len[k]);
+      kv.qualifier = slice(d->qual_bytes, qp, d->kv_qual_len[k]);
+      kv.value = slice(d->val_bytes, vp, d->kv_val_len[k]);
+      qp += d->kv_qual_len[k];
+      vp += d->kv_val_len[k];
       row.push_back(kv);
     }
+    if (qp != d->row_qual_off[r + 1] || vp != d->row_val_off[r + 1]) return TSDBHIP_E_INVALID_ARG;
     CompactResult res;
+    g_entered_complex = false;
     try {
       res = compact(row);
-    } catch (JavaException&) {
-      res.status = TSDBHIP_ROW_ERROR;
+    } catch (JavaException& e) {
+      res.status = e.code == TSDBHIP_E_OUT_OF_BOUNDS ? TSDBHIP_ROW_OOB : TSDBHIP_ROW_ERROR;
       res.qual.clear(); res.val.clear();
     }
-    if (qu + res.qual.size() > out->qual_capacity || vu + res.val.size() > out->val_capacity)
+    const uint64_t oq = d->row_qual_off[r] - q0, ov = d->row_val_off[r] - v0 + r;
+    if (oq + res.qual.size() > out->qual_capacity || ov + res.val.size() > out->val_capacity)
       return TSDBHIP_E_CAPACITY;
+    if (g_entered_complex) nc++;
     out->row_status[r] = (uint8_t)res.status;
-    out->row_qual_off[r] = qu;
+    out->row_qual_off[r] = oq;
     out->row_qual_len[r] = (uint32_t)res.qual.size();
-    out->row_val_off[r] = vu;
+    out->row_val_off[r] = ov;
     out->row_val_len[r] = (uint32_t)res.val.size();
-    if (!res.qual.empty()) std::memcpy(out->qual_bytes + qu, res.qual.data(), res.qual.size());
-    if (!res.val.empty()) std::memcpy(out->val_bytes + vu, res.val.data(), res.val.size());
-    qu += res.qual.size();
-    vu += res.val.size();
+    if (!res.qual.empty()) std::memcpy(out->qual_bytes + oq, res.qual.data(), res.qual.size());
+    if (!res.val.empty()) std::memcpy(out->val_bytes + ov, res.val.data(), res.val.size());
+    qu = std::max<uint64_t>(qu, oq + res.qual.size());
+    vu = std::max<uint64_t>(vu, ov + res.val.size());
   }
-  out->qual_used = qu;
-  out->val_used = vu;
+  (void)qu; (void)vu;
+  out->qual_used = d->n_rows ? d->row_qual_off[d->n_rows] - q0 : 0;  // the extents, as tsdbhip_compact_rows
+  out->val_used = d->n_rows ? d->row_val_off[d->n_rows] - v0 + d->n_rows : 0;
+  out->n_complex = nc;
   return TSDBHIP_OK;
 }
 

@@ -96,32 +96,13 @@ def agg_double(agg, values):
 
 
 def compact_rows(rowbatch):
-    """rowbatch: opentsdb_amd.compaction.RowBatch -> list of (status, qual, val)."""
+    """rowbatch: opentsdb_amd.compaction.RowBatch -> compaction.RowsResult
+    (same placement of the compacted rows as tsdbhip_compact_rows)."""
+    from opentsdb_amd import compaction
     desc = rowbatch.fill_desc(_abi.RowsDesc())
-    n = rowbatch.n_rows
-    qcap = max(16, 2 * len(rowbatch.qual_bytes) + 16)
-    vcap = max(16, 2 * len(rowbatch.val_bytes) + 16 + n)
-    st = np.zeros(n, np.uint8)
-    qo = np.zeros(n, np.uint64)
-    ql = np.zeros(n, np.uint32)
-    vo = np.zeros(n, np.uint64)
-    vl = np.zeros(n, np.uint32)
-    qb = np.zeros(qcap, np.uint8)
-    vb = np.zeros(vcap, np.uint8)
-    out = _abi.RowsOut()
-    out.qual_capacity, out.val_capacity = qcap, vcap
-    out.row_status = _abi.ptr(st, C.c_uint8)
-    out.row_qual_off = _abi.ptr(qo, C.c_uint64)
-    out.row_qual_len = _abi.ptr(ql, C.c_uint32)
-    out.row_val_off = _abi.ptr(vo, C.c_uint64)
-    out.row_val_len = _abi.ptr(vl, C.c_uint32)
-    out.qual_bytes = _abi.ptr(qb, C.c_uint8)
-    out.val_bytes = _abi.ptr(vb, C.c_uint8)
+    res, out = compaction.out_buffers(rowbatch)
     rc = lib().oracle_compact_rows(C.byref(desc), C.byref(out))
     if rc:
         raise RuntimeError(rc)
-    res = []
-    for r in range(n):
-        res.append((int(st[r]), bytes(qb[int(qo[r]):int(qo[r]) + int(ql[r])]),
-                    bytes(vb[int(vo[r]):int(vo[r]) + int(vl[r])])))
-    return res
+    res.n_complex = int(out.n_complex)
+    return compaction._trim(res, rowbatch.n_rows)

@@ -18,7 +18,7 @@ from opentsdb_amd import _abi, compaction, packing, synth
 GOLD = json.load(open(os.path.join(os.path.dirname(__file__), "golden", "known_answers.json")))
 AGG = {"sum": 0, "min": 1, "max": 2, "avg": 3, "dev": 4}
 STATUS = {"none": _abi.ROW_NONE, "single": _abi.ROW_SINGLE, "trivial": _abi.ROW_TRIVIAL,
-          "complex": _abi.ROW_COMPLEX, "error": _abi.ROW_ERROR}
+          "complex": _abi.ROW_COMPLEX, "error": _abi.ROW_ERROR, "oob": _abi.ROW_OOB}
 
 
 def spans_from_golden(case):
@@ -75,7 +75,7 @@ def test_oracle_stddev_random_values_seeded():
 def test_oracle_compaction_vectors(case):
     rows = [[(bytes.fromhex(q), bytes.fromhex(v)) for q, v in case["kvs"]]]
     res = oracle.compact_rows(compaction.pack_rows(rows))
-    st, q, v = res[0]
+    st, q, v = res.row(0)
     assert st == STATUS[case["status"]]
     if "qual" in case:
         assert q.hex() == case["qual"] and v.hex() == case["val"]
