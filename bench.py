@@ -45,6 +45,10 @@ CONFIGS = {
            "C1: 100 int series x 3600 pts @1s, sum, no downsample"),
     "c3": (1_000_000, 3600, 1, _abi.SYN_INT64_COUNTER, _abi.AGG_SUM, 0, 0,
            "C3 (sum, no rate): 1M series x 3600 pts @1s, int64 counters"),
+    # secondary path (configs[4]): row compaction, see bench_c5
+    "c5": (1_000_000, 0, 0, 0, 0, 0, 0,
+           "C5: row compaction, 1M rows / ~48M raw cells (1..99 per row, mixed widths, legacy floats, "
+           "10% pre-compacted rows with late singles + exact dups, 0.1% conflicting dups)"),
 }
 
 
@@ -127,6 +131,139 @@ def cpu_baseline(cfg, seconds=10.0):
     }
 
 
+def cpu_baseline_c5(batch, seconds=10.0):
+    """oracle_compact_rows (C++ restatement of CompactionQueue.compact) on
+    the host cores: independent row batches per thread, a bounded sample."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle
+    from opentsdb_amd import compaction
+    rows = min(batch.n_rows, 20000)
+    k1 = int(batch.row_kv_start[rows])
+    sub = compaction.RowBatch(batch.row_kv_start[:rows + 1].copy(), batch.row_qual_off[:rows + 1].copy(),
+                              batch.row_val_off[:rows + 1].copy(), batch.kv_qual_len[:k1].copy(),
+                              batch.kv_val_len[:k1].copy(), batch.qual_bytes, batch.val_bytes)
+    cells = int(sub.kv_qual_len.astype(np.int64).sum() // 2)  # raw cells (2 qualifier bytes each)
+    t = time.perf_counter()
+    oracle.compact_rows(sub)
+    probe = time.perf_counter() - t
+    threads = max(1, min(16, os.cpu_count() or 1))
+    reps = max(1, int(seconds / max(probe, 1e-3)))
+    done = [0]
+    lock = threading.Lock()
+
+    def work():
+        for _ in range(reps):
+            oracle.compact_rows(sub)
+        with lock:
+            done[0] += reps
+
+    ths = [threading.Thread(target=work) for _ in range(threads)]
+    t = time.perf_counter()
+    for th in ths:
+        th.start()
+    for th in ths:
+        th.join()
+    wall = time.perf_counter() - t
+    return {"value": done[0] * cells / wall, "unit": "raw cells/s", "cores": threads, "kind": "port",
+            "value_1core": cells / probe,
+            "sample": f"first {rows} rows ({cells} cells) of the same batch, {threads} threads x {reps} "
+                      f"batches, {wall:.1f} s wall (oracle/oracle.cc: C++ restatement of "
+                      f"CompactionQueue.compact; no JVM in the image)"}
+
+
+def bench_c5(args):
+    """C5 (configs[4]): tsdbhip_compact_rows over 1M HBM-resident rows."""
+    import torch
+    from opentsdb_amd import compaction
+    t0 = time.perf_counter()
+    mix = {}
+    if args.c5_mix == "plain":  # no row needs a fix: trivialCompact is a copy
+        mix = dict(p_complex=0.0, p_conflict=0.0, p_junk=0.0,
+                   kind_p=np.array([0.25, 0.2, 0.2, 0.2, 0.1, 0.05, 0.0, 0.0]))
+    elif args.c5_mix == "nocomplex":
+        mix = dict(p_complex=0.0, p_conflict=0.0)
+    b = compaction.synth_rows(args.series or 1_000_000, seed=5, **mix)
+    gen_s = time.perf_counter() - t0
+    ctx = Context(0)
+    L = lib()
+    dev = torch.device("cuda", 0)
+    keep = []
+
+    def up(a, ctype):
+        t = torch.from_numpy(a.view(np.uint8)).to(dev)
+        keep.append(t)
+        return C.cast(C.c_void_p(t.data_ptr()), C.POINTER(ctype))
+
+    d = _abi.RowsDesc(flags=_abi.DESC_DEVICE, n_rows=b.n_rows, n_kvs=b.n_kvs,
+                      row_kv_start=up(b.row_kv_start, C.c_uint64), row_qual_off=up(b.row_qual_off, C.c_uint64),
+                      row_val_off=up(b.row_val_off, C.c_uint64), kv_qual_len=up(b.kv_qual_len, C.c_uint16),
+                      kv_val_len=up(b.kv_val_len, C.c_uint16), qual_bytes=up(b.qual_bytes, C.c_uint8),
+                      qual_nbytes=len(b.qual_bytes), val_bytes=up(b.val_bytes, C.c_uint8),
+                      val_nbytes=len(b.val_bytes))
+    R = b.n_rows
+    qcap, vcap = b.qual_extent + 64, b.val_extent + R + 64
+    o = {k: torch.zeros(n, dtype=dt, device=dev) for k, n, dt in
+         [("st", R, torch.uint8), ("qo", R, torch.int64), ("ql", R, torch.int32), ("vo", R, torch.int64),
+          ("vl", R, torch.int32), ("q", qcap, torch.uint8), ("v", vcap, torch.uint8)]}
+    P = lambda t, ct: C.cast(C.c_void_p(t.data_ptr()), C.POINTER(ct))  # noqa: E731
+    out = _abi.RowsOut(qual_capacity=qcap, val_capacity=vcap, row_status=P(o["st"], C.c_uint8),
+                       row_qual_off=P(o["qo"], C.c_uint64), row_qual_len=P(o["ql"], C.c_uint32),
+                       row_val_off=P(o["vo"], C.c_uint64), row_val_len=P(o["vl"], C.c_uint32),
+                       qual_bytes=P(o["q"], C.c_uint8), val_bytes=P(o["v"], C.c_uint8))
+
+    def step_once():
+        ctx.check(L.tsdbhip_compact_rows(ctx.handle, C.byref(d), C.byref(out)))
+
+    for _ in range(args.warmup):
+        step_once()
+    torch.cuda.synchronize()
+    hot, tot, cx = [], [], []
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step_once()
+        tm = ctx.timing()
+        hot.append(tm.hot_ms)
+        tot.append(tm.total_ms)
+        cx.append(tm.reduce_ms)
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    st = o["st"].cpu().numpy()
+    ql = o["ql"].cpu().numpy().astype(np.int64)
+    vl = o["vl"].cpu().numpy().astype(np.int64)
+    # SURVEY.md §8(d) C5: input cell bytes + output compacted bytes
+    row_q = np.diff(b.row_qual_off.astype(np.int64))
+    row_v = np.diff(b.row_val_off.astype(np.int64))
+    n_cx = int(out.n_complex)
+    alg_all = int(row_q.sum() + row_v.sum() + ql.sum() + vl.sum())
+    # k_compact_tiles finishes every row except complexCompact rows of > 256
+    # cells (none in C5), which k_compact_complex redoes: all bytes are its.
+    alg_rows = alg_all
+    cells = int(b.kv_qual_len.astype(np.int64).sum() // 2)
+    hot_ms = float(np.mean(hot))
+    achieved = alg_rows / (hot_ms * 1e-3) / 1e9
+    traffic, traffic_src = pmc_traffic("c5", "k_compact_tiles", 1)
+    res = {
+        "metric": "raw cells/sec compacted (CompactionQueue.compact) + % HBM roofline, 1 MI355X",
+        "value": cells / (elapsed / args.steps), "unit": "raw cells/s", "n_gpus": 1, "steps": args.steps,
+        "warmup": args.warmup, "ms_per_step": elapsed / args.steps * 1e3, "higher_is_better": True,
+        "scaling": "weak", "vs_baseline": None, "dtype": "u8",
+        "data": f"synthetic HBase rows in the reference byte encoding (host-generated in {gen_s:.0f} s, "
+                f"HBM-resident before timing)",
+        "config": {"workload": CONFIGS["c5"][7], "n_rows": R, "n_kvs": b.n_kvs, "raw_cells": cells,
+                   "rows_complex": n_cx, "status_counts": np.bincount(st, minlength=6).tolist()},
+        "roofline": {"bound": "hbm", "kernel": "k_compact_tiles", "achieved": achieved, "peak": HBM_PEAK_GBS,
+                     "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
+                     "traffic_source": traffic_src, "alg_bytes_per_launch": alg_rows, "kernel_ms": hot_ms,
+                     "complex_kernel_ms": float(np.mean(cx)), "step_device_ms": float(np.mean(tot)),
+                     "call_alg_bytes": alg_all,
+                     "call_achieved": alg_all / (float(np.mean(tot)) * 1e-3) / 1e9},
+    }
+    if not args.no_cpu:
+        res["cpu_baseline"] = cpu_baseline_c5(b, args.cpu_seconds)
+    print(json.dumps(res), flush=True)
+    ctx.close()
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -137,7 +274,11 @@ def main():
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--exact", action="store_true", help="TSDBHIP_EXACT_ORDER")
+    ap.add_argument("--c5-mix", default="c5", choices=["c5", "plain", "nocomplex"],
+                    help="C5 row mix (diagnostics; the C5 line is 'c5')")
     args = ap.parse_args()
+    if args.config == "c5":
+        return bench_c5(args)
 
     dist, rank, world, local_rank = dist_setup(args.gpus)
     n_series, n_points, step, kind, agg, dsi, dsa, desc_txt = CONFIGS[args.config]

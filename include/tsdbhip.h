@@ -77,7 +77,7 @@ extern "C" {
 #define TSDBHIP_HOT_DS_CHUNKS   1 /* chunk-parallel decode + downsample     */
 #define TSDBHIP_HOT_DECODE_FAST 2 /* streaming per-span decode(+downsample) */
 #define TSDBHIP_HOT_DECODE_GEN  3 /* general per-span decode(+downsample)   */
-#define TSDBHIP_HOT_COMPACT     4 /* row classification + single/trivial
+#define TSDBHIP_HOT_COMPACT     4 /* k_compact_tiles: classification + single/trivial/short complex
                                      compaction (tsdbhip_compact_rows)      */
 
 /* ---- desc flags ------------------------------------------------------- */
@@ -135,9 +135,10 @@ typedef struct tsdbhip_sg_out {
                                lazy reference, or -1 if unknown / no error  */
 } tsdbhip_sg_out;
 
-/* Per-call device timings of the last tsdbhip_spangroup_run (or
- * tsdbhip_compact_rows: total_ms, hot_ms, hot_kernel only) on a ctx,
- * measured with HIP events on the ctx stream (milliseconds). */
+/* Per-call device timings of the last tsdbhip_spangroup_run on a ctx,
+ * measured with HIP events on the ctx stream (milliseconds). After
+ * tsdbhip_compact_rows: total_ms, hot_ms = decode_ms = k_compact_rows,
+ * reduce_ms = k_compact_complex, hot_kernel = TSDBHIP_HOT_COMPACT. */
 typedef struct tsdbhip_timing {
   float    total_ms;        /* first kernel start .. last kernel end        */
   float    decode_ms;       /* decode(+downsample) kernel — dominant, HBM   */

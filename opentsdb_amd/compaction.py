@@ -194,7 +194,7 @@ _KIND_P = np.array([0.22, 0.18, 0.18, 0.18, 0.12, 0.10, 0.01, 0.01])
 
 
 def synth_rows(n_rows, seed=5, min_cells=1, max_cells=99, p_complex=0.10, p_conflict=0.001,
-               p_junk=0.001, p_dup=0.2):
+               p_junk=0.001, p_dup=0.2, kind_p=None):
     """C5: n_rows rows with U{min..max} points each; returns a RowBatch."""
     rng = np.random.default_rng(seed)
     n = rng.integers(min_cells, max_cells + 1, n_rows).astype(np.int64)
@@ -212,7 +212,7 @@ def synth_rows(n_rows, seed=5, min_cells=1, max_cells=99, p_complex=0.10, p_conf
     pos = np.repeat(es, n) + cidx
     uu = (cs[pos] - lo[crow]) / tot[crow]
     delta = np.minimum((uu * (3601 - n[crow])).astype(np.int64), 3600 - n[crow]) + cidx
-    kind = rng.choice(len(_KINDS), N, p=_KIND_P)
+    kind = rng.choice(len(_KINDS), N, p=_KIND_P if kind_p is None else kind_p)
     kk = _KINDS[kind]
     rflag, rlen, fflag, flen = kk[:, 0], kk[:, 1], kk[:, 2], kk[:, 3]
     rq = (delta << 4) | rflag

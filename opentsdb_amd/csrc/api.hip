@@ -928,7 +928,7 @@ extern "C" int tsdbhip_desc_download(tsdbhip_ctx* ctx, const tsdbhip_sg_desc* d,
 
 // ------------------------------------------------------- compaction ------
 // CompactionQueue.compact (CompactionQueue.java:243-743) for a batch of rows:
-// k_compact_rows (wave per row) then k_compact_complex for the rows holding a
+// k_compact_tiles (16-row LDS tiles, wave per row) then k_compact_complex for the rows holding a
 // compacted cell (LDS cell table, or global scratch for very long rows).
 extern "C" int tsdbhip_compact_rows(tsdbhip_ctx* ctx, const tsdbhip_rows_desc* d, tsdbhip_rows_out* out) {
   if (!ctx || !d || !out) return TSDBHIP_E_INVALID_ARG;
@@ -1009,7 +1009,7 @@ extern "C" int tsdbhip_compact_rows(tsdbhip_ctx* ctx, const tsdbhip_rows_desc* d
     a.big_cells = scratch<uint64_t>(ctx, "c_cells", qext / 2 + R + 1);
     HIPCHK(hipEventRecord(ctx->ev[0], ctx->stream));
     HIPCHK(hipEventRecord(ctx->ev[8], ctx->stream));
-    hipLaunchKernelGGL(k_compact_rows, dim3(grid_for(R, 4, 1u << 16)), dim3(256), 0, ctx->stream, a);
+    hipLaunchKernelGGL(k_compact_tiles, dim3(grid_for(R, CT_ROWS, 1u << 16)), dim3(256), 0, ctx->stream, a);
     HIPCHK(hipGetLastError());
     HIPCHK(hipEventRecord(ctx->ev[9], ctx->stream));
     hipLaunchKernelGGL(k_compact_complex<true>, dim3(1024), dim3(256), 0, ctx->stream, a);
@@ -1036,10 +1036,12 @@ extern "C" int tsdbhip_compact_rows(tsdbhip_ctx* ctx, const tsdbhip_rows_desc* d
     t.total_ms = ev_ms(ctx->ev[0], ctx->ev[1]);
     t.hot_ms = ev_ms(ctx->ev[8], ctx->ev[9]);
     t.hot_kernel = TSDBHIP_HOT_COMPACT;
+    t.decode_ms = t.hot_ms;                                 // k_compact_rows
+    t.reduce_ms = ev_ms(ctx->ev[9], ctx->ev[1]);            // k_compact_complex
     ctx->timing = t;
     out->qual_used = qext;
     out->val_used = vext + R;
-    out->n_complex = (uint64_t)cnt[0] + cnt[1];
+    out->n_complex = (uint64_t)cnt[0] + cnt[1] + cnt[3];
   } catch (Fail& f) {
     return f.code;
   }

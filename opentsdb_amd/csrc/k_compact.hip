@@ -1,14 +1,16 @@
 // k_compact.hip — CompactionQueue.compact(row, compacted) on gfx950
 // (reference: src/core/CompactionQueue.java:243-743), the secondary path.
 //
-// Two launches over a batch of rows (tsdbhip_rows_desc):
-//   k_compact_rows     one wave per row (grid-stride). Reads the KV lengths
-//                      and the 2-byte qualifiers, classifies the row exactly
-//                      as compact() does (junk KVs, single KV, the in-order
-//                      delta check of the trivial pre-pass :286-333, legacy
-//                      floats) and writes single / trivial / error rows
-//                      directly. Rows holding a compacted cell (complex) go
-//                      to a work list.
+// Launches over a batch of rows (tsdbhip_rows_desc):
+//   k_compact_tiles    the main kernel (see its comment below): tiles of 16
+//                      consecutive rows staged in LDS with 16-B loads; each
+//                      wave classifies a row exactly as compact() does (junk
+//                      KVs, single KV, the in-order delta check of the trivial
+//                      pre-pass :286-333, legacy floats) and compacts it
+//                      LDS -> LDS, complex rows of <= 256 cells included;
+//                      the tile is written back with 16-B stores.
+//                      cq_row_global is the same per-row logic straight from
+//                      global memory, for tiles over the LDS budget.
 //   k_compact_complex  one 256-thread block per complex row: breakDownValues
 //                      (:690-743) into a cell table (LDS, or global scratch
 //                      for rows over LDS_CELLS cells), then the stable sort +
@@ -51,7 +53,8 @@ struct CompactArgs {
   uint32_t* out_vlen;
   uint8_t* oq;
   uint8_t* ov;
-  uint32_t* counters;   // [0] complex rows in LDS list, [1] in big list, [2] bad-argument flag
+  uint32_t* counters;   // [0] complex rows in LDS list, [1] in big list, [2] bad-argument flag,
+                        // [3] complex rows finished in-wave by k_compact_tiles
   uint32_t* list_lds;   // complex rows with <= CQ_LDS_CELLS cells
   uint32_t* list_big;   // the others
   uint64_t* big_cells;  // scratch: row r's cells at (row_qual_off[r]-row_qual_off[0])/2 + r
@@ -98,10 +101,10 @@ DEVI void wave_copy(uint8_t* dst, const uint8_t* src, uint64_t n, int lane) {
 }
 
 // ---------------------------------------------------------------------------
-__global__ void __launch_bounds__(256) k_compact_rows(CompactArgs a) {
-  const int lane = lane_id();
-  const uint64_t nwaves = (uint64_t)gridDim.x * blockDim.x / WAVE;
-  for (uint64_t r = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) / WAVE; r < a.n_rows; r += nwaves) {
+// One row by one wave straight from global memory: the fallback of
+// k_compact_tiles for tiles that do not fit its LDS budget.
+DEVI void cq_row_global(const CompactArgs& a, uint64_t r, int lane) {
+  {
     const RowHdr h = cq_row(a, r);
     if (lane == 0) {
       a.out_qoff[r] = h.oqo;
@@ -160,11 +163,11 @@ __global__ void __launch_bounds__(256) k_compact_rows(CompactArgs a) {
         atomicOr(&a.counters[2], 1u);
         cq_finish(a, r, CQ_NONE, 0, 0);
       }
-      continue;
+      return;
     }
     if (nvalid == 0) {  // empty row, or only junk (:245-247, :301-306, :335-337)
       if (lane == 0) cq_finish(a, r, CQ_NONE, 0, 0);
-      continue;
+      return;
     }
     if (nvalid == 1) {  // one KV (left): compacted[0] = kv, float-fixed (:248-266)
       if (f_ql == 2 && cq_legacy(f_q & 0xFF, f_vl)) {
@@ -184,18 +187,18 @@ __global__ void __launch_bounds__(256) k_compact_rows(CompactArgs a) {
         wave_copy(a.ov + h.ovo, a.val + f_vpos, f_vl, lane);
         if (lane == 0) cq_finish(a, r, CQ_SINGLE, f_ql, f_vl);
       }
-      continue;
+      return;
     }
     if (err_delta || (nmulti == 0 && legacy_bad)) {  // :324-327, fixFloatingPointValue :538
       if (lane == 0) cq_finish(a, r, CQ_ERROR, 0, 0);
-      continue;
+      return;
     }
     if (nmulti) {  // complexCompact: handed to k_compact_complex
       if (lane == 0) {
         if (ncells <= CQ_LDS_CELLS) a.list_lds[atomicAdd(&a.counters[0], 1u)] = (uint32_t)r;
         else a.list_big[atomicAdd(&a.counters[1], 1u)] = (uint32_t)r;
       }
-      continue;
+      return;
     }
     // ---- trivialCompact (:450-474): q[0], fixed q[1]; fixed values; 0x00 ----
     if (!any_legacy && !any_junk) {
@@ -427,4 +430,491 @@ __global__ void __launch_bounds__(256) k_compact_complex(CompactArgs a) {
   }
 }
 
+
+// ===========================================================================
+// k_compact_tiles: the main compaction kernel. A 256-thread block takes a tile
+// of CT_ROWS consecutive rows; their KV lengths, qualifier bytes and value
+// bytes are contiguous in the batch, so the block stages them into LDS with
+// 16-B loads (one round trip for the whole tile), each wave compacts rows of
+// the tile LDS -> LDS, and the block writes the tile's output ranges back with
+// 16-B stores (byte stores only at the tile's two edges). Rows holding a
+// compacted cell are finished in-wave when they break down into at most
+// CT_SORT cells (bitonic sort of (qualifier, cell index) keys = the stable
+// Collections.sort of complexCompact, :607); longer ones go to the
+// k_compact_complex lists. Tiles over the LDS budget fall back to
+// cq_row_global.
+// ===========================================================================
+constexpr int CT_ROWS = 16;    // rows per tile
+constexpr int CT_QB = 4096;    // qualifier bytes per tile
+constexpr int CT_VB = 8192;    // value bytes per tile
+constexpr int CT_KB = 1536;    // KVs per tile
+constexpr int CT_SORT = 256;   // cells of an in-wave complexCompact
+constexpr int CQ_RUNS_SLOTS = 12;
+
+struct __attribute__((aligned(16))) TileLds {
+  uint8_t qin[CT_QB + 32];
+  uint8_t vin[CT_VB + 32];
+  uint8_t qout[CT_QB + 32];
+  uint8_t vout[CT_VB + 32 + CT_ROWS];
+  uint8_t qlen[2 * CT_KB + 32];
+  uint8_t vlen[2 * CT_KB + 32];
+  uint32_t keys[4][CT_SORT];
+  uint32_t pay[4][CT_SORT];
+  uint32_t runs[4][CQ_RUNS_SLOTS];
+  uint64_t hdr[3][CT_ROWS + 1];
+  uint32_t n_complex;  // rows of this block that reached complexCompact in-wave
+};
+
+// Stages src[b0, b1) into lds with 16-B loads; byte x of src lands at
+// lds[x - b0 + head], head = the misalignment of src + b0. Every loaded chunk
+// holds at least one byte of the range, so no load leaves the range's pages.
+DEVI uint32_t cq_stage(uint8_t* lds, const uint8_t* src, uint64_t b0, uint64_t b1, int tid) {
+  const uintptr_t s = (uintptr_t)(src + b0);
+  const uint32_t head = (uint32_t)(s & 15u);
+  if (b1 <= b0) return head;
+  const uint64_t nch = (head + (b1 - b0) + 15) / 16;
+  const uint4* g = (const uint4*)(s - head);
+  for (uint64_t c = tid; c < nch; c += 256) *(uint4*)(lds + 16 * c) = g[c];
+  return head;
+}
+
+// Writes lds[i0 + (x - b0)] to dst[x] for x in [b0, b1): 16-B stores where a
+// whole aligned chunk of dst lies inside the range, byte stores at the edges.
+// lds must be laid out so that (i0 - (dst+b0)) is a multiple of 16.
+DEVI void cq_unstage(uint8_t* dst, const uint8_t* lds, uint32_t i0, uint64_t b0, uint64_t b1, int tid) {
+  if (b1 <= b0) return;
+  const uintptr_t s = (uintptr_t)(dst + b0), e = (uintptr_t)(dst + b1);
+  const uintptr_t a0 = s & ~(uintptr_t)15;
+  const uint64_t nch = (e - a0 + 15) / 16;
+  for (uint64_t c = tid; c < nch; c += 256) {
+    const uintptr_t cs = a0 + 16 * c;
+    const uint32_t li = (uint32_t)(i0 - (s - a0) + 16 * c);  // lds index of byte cs
+    if (cs >= s && cs + 16 <= e) {
+      *(uint4*)cs = *(const uint4*)(lds + li);
+    } else {
+      for (int j = 0; j < 16; j++)
+        if (cs + j >= s && cs + j < e) *(uint8_t*)(cs + j) = lds[li + j];
+    }
+  }
+}
+
+DEVI uint32_t lds_q16(const uint8_t* p, uint32_t i) { return ((uint32_t)p[i] << 8) | p[i + 1]; }
+DEVI uint32_t lds_u16(const uint8_t* p, uint32_t i) { return (uint32_t)p[i] | ((uint32_t)p[i + 1] << 8); }
+
+// Row positions inside the tile's LDS buffers.
+struct RowLds {
+  uint32_t k0;   // byte index of the row's first KV length in qlen
+  uint32_t kv0;  // ... in vlen
+  uint32_t qi;   // index of the row's first qualifier byte in qin
+  uint32_t vi;   // ... first value byte in vin
+  uint32_t qo;   // index in qout of the row's compacted qualifier
+  uint32_t vo;   // index in vout of the row's compacted value
+};
+
+// Bitonic sort (ascending) of keys[0, n) by one wave; n <= CT_SORT.
+DEVI void cq_sort(uint32_t* keys, uint32_t n, int lane) {
+  uint32_t P = 2;
+  while (P < n) P <<= 1;
+  for (uint32_t i = n + lane; i < P; i += WAVE) keys[i] = ~0u;
+  wave_lds_sync();
+  for (uint32_t k = 2; k <= P; k <<= 1) {
+    for (uint32_t j = k >> 1; j > 0; j >>= 1) {
+      for (uint32_t i = lane; i < P; i += WAVE) {
+        const uint32_t l = i ^ j;
+        if (l > i) {
+          const uint32_t x = keys[i], y = keys[l];
+          if ((x > y) == ((i & k) == 0)) {
+            keys[i] = y;
+            keys[l] = x;
+          }
+        }
+      }
+      wave_lds_sync();
+    }
+  }
+}
+
+// Number of keys in the sorted run A[rs, re) below `key` (keys are unique).
+DEVI uint32_t cq_lower_bound(const uint32_t* A, uint32_t rs, uint32_t re, uint32_t key) {
+  uint32_t lo = rs, hi = re;
+  while (lo < hi) {
+    const uint32_t mid = (lo + hi) >> 1;
+    if (A[mid] < key) lo = mid + 1;
+    else hi = mid;
+  }
+  return lo - rs;
+}
+
+constexpr int CQ_RUNS = 8;  // sorted runs merged by rank before falling back to bitonic
+
+// complexCompact (:600-743) of one row from LDS. Returns the row status; on
+// COMPLEX, *qlen/*vlen are the output lengths (already in qout/vout).
+// The cells' stable sort order is the order of the composite key
+// (qualifier << 16 | breakdown index). The 2-byte KVs that reach here have
+// strictly increasing deltas (the trivial pre-pass threw otherwise), so they
+// form one sorted run; each multi-value cell is a run when its qualifiers
+// do not decrease (true for every cell trivialCompact/complexCompact wrote).
+// With <= CQ_RUNS runs a cell's final position is the sum of its ranks in
+// every run (binary searches); otherwise the keys are bitonic-sorted.
+DEVI uint8_t cq_complex_lds(TileLds& L, const RowLds& p, uint32_t nk, uint32_t n_single, uint32_t n_cells,
+                            uint32_t* A, uint32_t* pay, uint32_t* runs, int lane, uint32_t* qlen_out,
+                            uint32_t* vlen_out) {
+  // ---- breakDownValues: singles at A[0, n_single), multi cells after ----
+  uint32_t qcar = 0, vcar = 0, ccar = 0, scar = 0, mcar = n_single;
+  uint32_t err = ~0u;  // (kv << 1) | oob of the first failing KV
+  uint32_t nruns = n_single ? 1u : 0u;
+  bool monotone = true;
+  if (lane == 0) runs[0] = 0;
+  for (uint32_t base = 0; base < nk; base += WAVE) {
+    const uint32_t i = base + lane;
+    const bool act = i < nk;
+    const uint32_t ql = act ? lds_u16(L.qlen, p.k0 + 2 * i) : 0u;
+    const uint32_t vl = act ? lds_u16(L.vlen, p.kv0 + 2 * i) : 0u;
+    const bool valid = act && ql != 0 && (ql & 1) == 0;
+    const bool two = valid && ql == 2;
+    const uint32_t nc = valid ? ql >> 1 : 0u;
+    const uint32_t qx = wave_incl_scan_u32_dpp(ql), vx = wave_incl_scan_u32_dpp(vl), cx = wave_incl_scan_u32_dpp(nc);
+    const uint32_t qpos = p.qi + qcar + qx - ql, vpos = p.vi + vcar + vx - vl, cb = ccar + cx - nc;
+    qcar += readlane_u32(qx, 63);
+    vcar += readlane_u32(vx, 63);
+    ccar += readlane_u32(cx, 63);
+    const uint64_t m2 = ballot(two);
+    if (two) {
+      const uint32_t q = lds_q16(L.qin, qpos);
+      const bool leg = cq_legacy(q & 0xFF, vl);
+      const uint32_t flen = leg ? 4u : vl;
+      A[scar + __popcll(m2 & lanemask_lt(lane))] = (((q & 0xFF00) | cq_fixq(q & 0xFF, flen)) << 16) | cb;
+      pay[cb] = ((vpos + (leg ? 4u : 0u)) << 16) | flen;
+    }
+    const bool bad = two && cq_legacy(lds_q16(L.qin, qpos) & 0xFF, vl) &&
+                     (L.vin[vpos] | L.vin[vpos + 1] | L.vin[vpos + 2] | L.vin[vpos + 3]) != 0;
+    const uint64_t mb = ballot(bad);
+    if (mb) err = min(err, (base + (uint32_t)(__ffsll((long long)mb) - 1)) << 1);
+    scar += __popcll(m2);
+    uint64_t mm = ballot(valid && ql > 2);
+    while (mm) {  // multi-value cells, one at a time, wave-cooperative
+      const int l = __ffsll((long long)mm) - 1;
+      mm &= mm - 1;
+      const uint32_t kq = readlane_u32(qpos, l), kv = readlane_u32(vpos, l);
+      const uint32_t kvl = readlane_u32(vl, l), knc = readlane_u32(nc, l), kcb = readlane_u32(cb, l);
+      const uint32_t kid = base + l;
+      if (nruns < CQ_RUNS && lane == 0) runs[nruns] = mcar;
+      nruns++;
+      if (kvl == 0) {  // val[val.length - 1] of an empty value (:708)
+        err = min(err, (kid << 1) | 1u);
+        continue;
+      }
+      if (L.vin[kv + kvl - 1] != 0) {  // unknown meta byte (:709-714)
+        err = min(err, kid << 1);
+        continue;
+      }
+      uint32_t run = 0, prevq = 0;
+      bool over = false, desc = false;
+      for (uint32_t c0 = 0; c0 < knc; c0 += WAVE) {
+        const uint32_t c = c0 + lane;
+        const bool a2 = c < knc;
+        const uint32_t q = a2 ? lds_q16(L.qin, kq + 2 * c) : 0u;
+        const uint32_t len = a2 ? (q & 7u) + 1u : 0u;
+        const uint32_t incl = wave_incl_scan_u32_dpp(len);
+        const uint32_t off = run + incl - len;
+        uint32_t pq = (uint32_t)__shfl((int)q, lane == 0 ? 0 : lane - 1);
+        if (lane == 0) pq = prevq;
+        if (a2) {
+          over |= off + len > kvl;  // System.arraycopy past the value (:722)
+          desc |= q < pq;
+          A[mcar + c] = (q << 16) | (kcb + c);
+          pay[kcb + c] = ((kv + off) << 16) | len;
+        }
+        run += readlane_u32(incl, 63);
+        prevq = (uint32_t)__shfl((int)q, 63);
+      }
+      monotone = monotone && !ballot(desc);
+      mcar += knc;
+      if (ballot(over)) err = min(err, (kid << 1) | 1u);
+      else if (run != kvl - 1) err = min(err, kid << 1);  // (:730-736)
+    }
+  }
+  if (err != ~0u) return (err & 1u) ? CQ_OOB : CQ_ERROR;
+  const uint32_t n = n_cells;
+  wave_lds_sync();
+  if (monotone && nruns <= CQ_RUNS) {
+    // ---- merge the sorted runs by rank ----
+    if (lane == 0) runs[nruns] = n;
+    wave_lds_sync();
+    uint32_t key[CT_SORT / WAVE], rank[CT_SORT / WAVE];
+#pragma unroll
+    for (int k = 0; k < CT_SORT / WAVE; k++) {
+      const uint32_t i = lane + WAVE * k;
+      key[k] = i < n ? A[i] : 0u;
+      rank[k] = 0;
+      if (i < n) {
+        for (uint32_t r = 0; r < nruns; r++) {
+          const uint32_t rs = runs[r], re = runs[r + 1];
+          rank[k] += (i >= rs && i < re) ? i - rs : cq_lower_bound(A, rs, re, key[k]);
+        }
+      }
+    }
+    wave_lds_sync();
+#pragma unroll
+    for (int k = 0; k < CT_SORT / WAVE; k++)
+      if (lane + WAVE * k < n) A[rank[k]] = key[k];
+    wave_lds_sync();
+  } else {
+    cq_sort(A, n, lane);
+  }
+  // ---- duplicate check + emission in sorted order (:611-678) ----
+  int prev_d = -1;
+  uint32_t rep_key = 0, rank = 0, vrun = 0;
+  bool bad = false;
+  for (uint32_t p0 = 0; p0 < n; p0 += WAVE) {
+    const uint32_t i = p0 + lane;
+    const bool act = i < n;
+    const uint32_t key = act ? A[i] : ~0u;
+    const int d = (int)(key >> 20);
+    int pd = __shfl(d, lane == 0 ? 0 : lane - 1);
+    if (lane == 0) pd = prev_d;
+    const bool head = act && d != pd;
+    const uint64_t hm = ballot(head);
+    const uint64_t below = hm & lanemask_le(lane);
+    const uint32_t sk = (uint32_t)__shfl((int)key, below ? 63 - __clzll(below) : lane);
+    const uint32_t rk = below ? sk : rep_key;
+    const uint32_t pw = act ? pay[key & 0xFFFF] : 0u;
+    const uint32_t len = pw & 0xFFFF, off = pw >> 16;
+    if (act && !head) {
+      const uint32_t rw = pay[rk & 0xFFFF];
+      if (((key >> 16) & 0xFF) != ((rk >> 16) & 0xFF) || len != (rw & 0xFFFF)) {
+        bad = true;
+      } else {
+        for (uint32_t j = 0; j < len; j++) bad |= L.vin[off + j] != L.vin[(rw >> 16) + j];
+      }
+    }
+    const uint32_t hl = head ? len : 0u;
+    const uint32_t vi = wave_incl_scan_u32_dpp(hl);
+    if (head) {
+      const uint32_t r2 = rank + __popcll(hm & lanemask_lt(lane));
+      L.qout[p.qo + 2 * r2] = (uint8_t)(key >> 24);
+      L.qout[p.qo + 2 * r2 + 1] = (uint8_t)(key >> 16);
+      const uint32_t dst = p.vo + vrun + vi - hl;
+      for (uint32_t j = 0; j < len; j++) L.vout[dst + j] = L.vin[off + j];
+    }
+    rank += __popcll(hm);
+    vrun += readlane_u32(vi, 63);
+    prev_d = __shfl(d, 63);
+    if (hm) rep_key = (uint32_t)__shfl((int)key, 63 - __clzll(hm));
+  }
+  if (ballot(bad)) return CQ_ERROR;
+  if (lane == 0) L.vout[p.vo + vrun] = 0;
+  *qlen_out = 2 * rank;
+  *vlen_out = vrun + 1;
+  return CQ_COMPLEX;
+}
+
+// One row, LDS -> LDS (same classification as cq_row_global).
+DEVI void cq_row_lds(const CompactArgs& a, uint64_t r, const RowHdr& h, TileLds& L, const RowLds& p,
+                     uint32_t* keys, uint32_t* pay, uint32_t* runs, int lane) {
+  const uint32_t nk = (uint32_t)h.nk;
+  uint32_t qcar = 0, vcar = 0, nvalid = 0, nmulti = 0, ncells = 0;
+  int last_delta = -1;
+  bool err_delta = false, legacy_bad = false, any_fix = false, any_junk = false;
+  uint32_t f_qpos = 0, f_vpos = 0, f_ql = 0, f_vl = 0, f_q = 0;
+  for (uint32_t base = 0; base < nk; base += WAVE) {
+    const uint32_t i = base + lane;
+    const bool act = i < nk;
+    const uint32_t ql = act ? lds_u16(L.qlen, p.k0 + 2 * i) : 0u;
+    const uint32_t vl = act ? lds_u16(L.vlen, p.kv0 + 2 * i) : 0u;
+    const uint32_t qi = wave_incl_scan_u32_dpp(ql), vi = wave_incl_scan_u32_dpp(vl);
+    // (clamped: lengths that overrun the row are rejected after this pass)
+    const uint32_t qpos = min(p.qi + qcar + qi - ql, (uint32_t)CT_QB), vpos = min(p.vi + vcar + vi - vl, (uint32_t)CT_VB);
+    qcar += readlane_u32(qi, 63);
+    vcar += readlane_u32(vi, 63);
+    const bool valid = act && ql != 0 && (ql & 1) == 0;
+    const bool two = valid && ql == 2;
+    const uint32_t q = two ? lds_q16(L.qin, qpos) : 0u;
+    const int delta = (int)(q >> 4);
+    const bool leg = two && cq_legacy(q & 0xFF, vl);
+    const bool lbad = leg && (L.vin[vpos] | L.vin[vpos + 1] | L.vin[vpos + 2] | L.vin[vpos + 3]) != 0;
+    const uint64_t m2 = ballot(two);
+    const uint64_t lower = m2 & lanemask_lt(lane);
+    int pd = __shfl(delta, lower ? 63 - __clzll(lower) : lane);
+    if (!lower) pd = last_delta;
+    err_delta |= ballot(two && delta <= pd) != 0;
+    if (m2) last_delta = __shfl(delta, 63 - __clzll(m2));
+    legacy_bad |= ballot(lbad) != 0;
+    // a KV whose bytes change in trivialCompact: legacy float or wrong length flags
+    any_fix |= ballot(two && (leg || cq_fixq(q & 0xFF, vl) != (q & 0xFF))) != 0;
+    any_junk |= ballot(act && !valid) != 0;
+    const uint64_t mv = ballot(valid);
+    if (nvalid == 0 && mv) {
+      const int fl = __ffsll((long long)mv) - 1;
+      f_qpos = readlane_u32(qpos, fl);
+      f_vpos = readlane_u32(vpos, fl);
+      f_ql = readlane_u32(ql, fl);
+      f_vl = readlane_u32(vl, fl);
+      f_q = readlane_u32(q, fl);
+    }
+    nvalid += __popcll(mv);
+    nmulti += __popcll(ballot(valid && ql > 2));
+    ncells += readlane_u32(wave_incl_scan_u32_dpp(valid ? ql >> 1 : 0u), 63);
+  }
+  uint8_t st;
+  uint32_t oql = 0, ovl = 0;
+  if (qcar != h.qe - h.qs || vcar != h.ve - h.vs) {  // lengths vs extents: E_INVALID_ARG
+    if (lane == 0) atomicOr(&a.counters[2], 1u);
+    st = CQ_NONE;
+  } else if (nvalid == 0) {
+    st = CQ_NONE;
+  } else if (nvalid == 1) {
+    if (f_ql == 2 && cq_legacy(f_q & 0xFF, f_vl)) {
+      if ((L.vin[f_vpos] | L.vin[f_vpos + 1] | L.vin[f_vpos + 2] | L.vin[f_vpos + 3]) != 0) {
+        st = CQ_ERROR;
+      } else {
+        st = CQ_SINGLE;
+        if (lane < 4) L.vout[p.vo + lane] = L.vin[f_vpos + 4 + lane];
+        if (lane == 0) {
+          L.qout[p.qo] = (uint8_t)(f_q >> 8);
+          L.qout[p.qo + 1] = (uint8_t)cq_fixq(f_q & 0xFF, 4);
+        }
+        oql = 2;
+        ovl = 4;
+      }
+    } else {
+      st = CQ_SINGLE;
+      for (uint32_t j = lane; j < f_ql; j += WAVE) L.qout[p.qo + j] = L.qin[f_qpos + j];
+      for (uint32_t j = lane; j < f_vl; j += WAVE) L.vout[p.vo + j] = L.vin[f_vpos + j];
+      oql = f_ql;
+      ovl = f_vl;
+    }
+  } else if (err_delta || (nmulti == 0 && legacy_bad)) {
+    st = CQ_ERROR;
+  } else if (nmulti) {
+    if (ncells <= CT_SORT) {
+      st = cq_complex_lds(L, p, nk, nvalid - nmulti, ncells, keys, pay, runs, lane, &oql, &ovl);
+      if (lane == 0) atomicAdd(&L.n_complex, 1u);
+    } else {  // too many cells for the in-wave sort: block kernels
+      if (lane == 0) {
+        if (ncells <= CQ_LDS_CELLS) a.list_lds[atomicAdd(&a.counters[0], 1u)] = (uint32_t)r;
+        else a.list_big[atomicAdd(&a.counters[1], 1u)] = (uint32_t)r;
+      }
+      return;
+    }
+  } else if (!any_fix && !any_junk) {
+    // trivialCompact changes nothing: qualifiers and values pass through
+    st = CQ_TRIVIAL;
+    for (uint32_t j = lane; j < qcar; j += WAVE) L.qout[p.qo + j] = L.qin[p.qi + j];
+    for (uint32_t j = lane; j < vcar; j += WAVE) L.vout[p.vo + j] = L.vin[p.vi + j];
+    if (lane == 0) L.vout[p.vo + vcar] = 0;
+    oql = qcar;
+    ovl = vcar + 1;
+  } else {
+    // trivialCompact (:450-474) with flag / legacy-float fixes and junk skipped
+    st = CQ_TRIVIAL;
+    uint32_t qc2 = 0, vc2 = 0, nq = 0, nv = 0;
+    for (uint32_t base = 0; base < nk; base += WAVE) {
+      const uint32_t i = base + lane;
+      const bool act = i < nk;
+      const uint32_t ql = act ? lds_u16(L.qlen, p.k0 + 2 * i) : 0u;
+      const uint32_t vl = act ? lds_u16(L.vlen, p.kv0 + 2 * i) : 0u;
+      const uint32_t qi = wave_incl_scan_u32_dpp(ql), vi = wave_incl_scan_u32_dpp(vl);
+      const uint32_t qpos = p.qi + qc2 + qi - ql, vpos = p.vi + vc2 + vi - vl;
+      qc2 += readlane_u32(qi, 63);
+      vc2 += readlane_u32(vi, 63);
+      const bool valid = act && ql == 2;
+      const uint32_t q = valid ? lds_q16(L.qin, qpos) : 0u;
+      const bool leg = valid && cq_legacy(q & 0xFF, vl);
+      const uint32_t flen = valid ? (leg ? 4u : vl) : 0u;
+      const uint64_t mv = ballot(valid);
+      const uint32_t fi = wave_incl_scan_u32_dpp(flen);
+      if (valid) {
+        const uint32_t o = p.qo + 2 * (nq + __popcll(mv & lanemask_lt(lane)));
+        L.qout[o] = (uint8_t)(q >> 8);
+        L.qout[o + 1] = (uint8_t)cq_fixq(q & 0xFF, flen);
+        const uint32_t src = vpos + (leg ? 4u : 0u), dst = p.vo + nv + fi - flen;
+        for (uint32_t j = 0; j < flen; j++) L.vout[dst + j] = L.vin[src + j];
+      }
+      nq += __popcll(mv);
+      nv += readlane_u32(fi, 63);
+    }
+    if (lane == 0) L.vout[p.vo + nv] = 0;
+    oql = 2 * nq;
+    ovl = nv + 1;
+  }
+  if (lane == 0) cq_finish(a, r, st, oql, ovl);
+}
+
+__global__ void __launch_bounds__(256) k_compact_tiles(CompactArgs a) {
+  __shared__ TileLds L;
+  const int tid = threadIdx.x, lane = lane_id(), w = tid / WAVE;
+  const uint64_t n_tiles = (a.n_rows + CT_ROWS - 1) / CT_ROWS;
+  const uint64_t Q0 = a.row_qual_off[0], V0 = a.row_val_off[0];
+  if (tid == 0) L.n_complex = 0;
+  for (uint64_t t = blockIdx.x; t < n_tiles; t += gridDim.x) {
+    const uint64_t r0 = t * CT_ROWS;
+    const uint32_t nr = (uint32_t)min((uint64_t)CT_ROWS, a.n_rows - r0);
+    __syncthreads();  // previous tile's LDS fully consumed
+    if (tid <= (int)nr) {
+      L.hdr[0][tid] = a.row_kv_start[r0 + tid];
+      L.hdr[1][tid] = a.row_qual_off[r0 + tid];
+      L.hdr[2][tid] = a.row_val_off[r0 + tid];
+    }
+    __syncthreads();
+    const uint64_t kb0 = L.hdr[0][0], kb1 = L.hdr[0][nr];
+    const uint64_t qs0 = L.hdr[1][0], qs1 = L.hdr[1][nr];
+    const uint64_t vs0 = L.hdr[2][0], vs1 = L.hdr[2][nr];
+    const bool fits = kb0 <= kb1 && kb1 <= a.n_kvs && kb1 - kb0 <= CT_KB && qs0 <= qs1 && qs1 <= a.qual_nbytes &&
+                      qs1 - qs0 <= CT_QB && vs0 <= vs1 && vs1 <= a.val_nbytes && vs1 - vs0 <= CT_VB &&
+                      qs0 >= Q0 && vs0 >= V0 && qs1 - Q0 <= a.qcap && vs1 - V0 + r0 + nr <= a.vcap;
+    if (!fits) {
+      for (uint32_t j = w; j < nr; j += 4) cq_row_global(a, r0 + j, lane);
+      continue;
+    }
+    // ---- stage the tile (one round trip) ----
+    const uint32_t hq = cq_stage(L.qin, a.qual, qs0, qs1, tid);
+    const uint32_t hv = cq_stage(L.vin, a.val, vs0, vs1, tid);
+    const uint32_t hk = cq_stage(L.qlen, (const uint8_t*)a.kv_qual_len, 2 * kb0, 2 * kb1, tid);
+    const uint32_t hkv = cq_stage(L.vlen, (const uint8_t*)a.kv_val_len, 2 * kb0, 2 * kb1, tid);
+    // output buffers share the destination's 16-B phase (for cq_unstage)
+    const uint32_t oq_h = (uint32_t)((uintptr_t)(a.oq + (qs0 - Q0)) & 15u);
+    const uint32_t ov_h = (uint32_t)((uintptr_t)(a.ov + (vs0 - V0 + r0)) & 15u);
+    __syncthreads();
+    for (uint32_t j = w; j < nr; j += 4) {
+      const uint64_t r = r0 + j;
+      RowHdr h;
+      h.kb = L.hdr[0][j];
+      h.nk = L.hdr[0][j + 1] - h.kb;
+      h.qs = L.hdr[1][j];
+      h.qe = L.hdr[1][j + 1];
+      h.vs = L.hdr[2][j];
+      h.ve = L.hdr[2][j + 1];
+      h.oqo = h.qs - Q0;
+      h.ovo = h.vs - V0 + r;
+      if (lane == 0) {
+        a.out_qoff[r] = h.oqo;
+        a.out_voff[r] = h.ovo;
+      }
+      // offsets must not decrease (else E_INVALID_ARG); the lengths are
+      // checked against the extents in cq_row_lds
+      if (!(L.hdr[0][j + 1] >= h.kb && h.qe >= h.qs && h.ve >= h.vs)) {
+        if (lane == 0) {
+          atomicOr(&a.counters[2], 1u);
+          cq_finish(a, r, CQ_NONE, 0, 0);
+        }
+        continue;
+      }
+      RowLds p;
+      p.k0 = hk + 2 * (uint32_t)(h.kb - kb0);
+      p.kv0 = hkv + 2 * (uint32_t)(h.kb - kb0);
+      p.qi = hq + (uint32_t)(h.qs - qs0);
+      p.vi = hv + (uint32_t)(h.vs - vs0);
+      p.qo = oq_h + (uint32_t)(h.qs - qs0);
+      p.vo = ov_h + (uint32_t)(h.vs - vs0) + j;
+      cq_row_lds(a, r, h, L, p, L.keys[w], L.pay[w], L.runs[w], lane);
+    }
+    __syncthreads();
+    // ---- write the tile's compacted bytes back ----
+    cq_unstage(a.oq, L.qout, oq_h, qs0 - Q0, qs1 - Q0, tid);
+    cq_unstage(a.ov, L.vout, ov_h, vs0 - V0 + r0, vs1 - V0 + r0 + nr, tid);
+  }
+  __syncthreads();
+  if (tid == 0 && L.n_complex) atomicAdd(&a.counters[3], L.n_complex);
+}
 }  // namespace tsdb
