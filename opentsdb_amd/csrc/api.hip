@@ -287,46 +287,25 @@ struct LaunchFastDs {
   }
 };
 
-// Chunk-parallel downsampling of regular-cadence integer spans; leaves the
-// list of spans it did not take in fa.span_list for k_decode_fast.
+// Streaming downsampling of regular-cadence integer spans (k_ds_spans, wave
+// per span); leaves the spans it did not take in fa.span_list for
+// k_decode_fast.
 struct LaunchChunks {
   template <int AGG>
   static void run(tsdbhip_ctx* ctx, const DecodeArgs& da, DecodeArgs& fa, const uint32_t* ncells,
-                  const uint32_t* vlen, uint64_t R, uint64_t e_total, uint64_t chunk_bound) {
+                  const uint32_t* vlen, SpanDsArgs g) {
     if (AGG == 4) return;  // dev: Welford is order-dependent, serial kernels only
     hipStream_t st = ctx->stream;
     const uint32_t n_kept = da.n_kept;
-    ChunkPlanArgs p;
-    p.row_kidx = scratch<int32_t>(ctx, "ck_row_kidx", R);
-    HIPCHK(hipMemsetAsync(p.row_kidx, 0xFF, R * sizeof(int32_t), st));
-    uint64_t* nch = scratch<uint64_t>(ctx, "ck_row_nch", R);
-    uint64_t* rc0 = scratch<uint64_t>(ctx, "ck_row_chunk0", R);
-    hipLaunchKernelGGL(k_row_chunks, dim3(grid_for(R, 256)), dim3(256), 0, st, ncells, R, nch);
-    dscan_u64(ctx, nch, rc0, R, scratch<uint64_t>(ctx, "ck_nch_total", 1), "ck");
-    p.row_chunk0 = rc0;
-    p.row_prev_ts = scratch<uint32_t>(ctx, "ck_row_prev_ts", R);
-    p.plan = scratch<SpanPlan>(ctx, "ck_plan", n_kept);
-    p.fail = scratch<uint32_t>(ctx, "ck_fail", n_kept);
-    p.tail_ts = scratch<uint32_t>(ctx, "ck_tail_ts", n_kept);
-    p.hp_nrel = scratch<uint32_t>(ctx, "ck_hp_nrel", e_total);
-    p.hp_ref = scratch<uint32_t>(ctx, "ck_hp_ref", e_total);
-    p.hp_pre = scratch<uint32_t>(ctx, "ck_hp_pre", e_total);
-    p.hp_v = scratch<int64_t>(ctx, "ck_hp_v", e_total);
-    p.lp_n = scratch<uint32_t>(ctx, "ck_lp_n", chunk_bound);
-    p.lp_ts = scratch<uint64_t>(ctx, "ck_lp_ts", chunk_bound);
-    p.lp_v = scratch<int64_t>(ctx, "ck_lp_v", chunk_bound);
-    p.list = scratch<uint32_t>(ctx, "ck_list", n_kept);
-    p.list_count = scratch<uint32_t>(ctx, "ck_list_count", 1, true);
-    const unsigned span_blocks = grid_for(n_kept, 4, 65536);
-    hipLaunchKernelGGL(k_ds_plan, dim3(span_blocks), dim3(256), 0, st, da, p, ncells);
+    g.list = scratch<uint32_t>(ctx, "ck_list", n_kept);
+    g.list_count = scratch<uint32_t>(ctx, "ck_list_count", 1, true);
     HIPCHK(hipEventRecord(ctx->ev[8], st));
-    hipLaunchKernelGGL(k_ds_chunks<AGG>, dim3(grid_for(R, 4, 1u << 20)), dim3(256), 0, st, da, p, ncells, vlen, R);
+    hipLaunchKernelGGL(k_ds_spans<AGG>, dim3(grid_for(n_kept, 4, 1u << 20)), dim3(256), 0, st, da, g, ncells,
+                       vlen);
     HIPCHK(hipEventRecord(ctx->ev[9], st));
     ctx->hot_kernel = TSDBHIP_HOT_DS_CHUNKS;
-    hipLaunchKernelGGL(k_ds_finalize<AGG>, dim3(span_blocks), dim3(256), 0, st, da, p);
-    hipLaunchKernelGGL(k_ds_collect, dim3(grid_for(n_kept, 256)), dim3(256), 0, st, da, p);
-    fa.span_list = p.list;
-    fa.span_count = p.list_count;
+    fa.span_list = g.list;
+    fa.span_count = g.list_count;
   }
 };
 
@@ -453,6 +432,7 @@ static int spangroup_run(tsdbhip_ctx* ctx, const tsdbhip_sg_desc* d, tsdbhip_sg_
     uint64_t n_kept;
     uint64_t e_total;
     uint64_t T;
+    unsigned long long bound[2];  // [min first ts, max last ts] of the kept spans
   };
   Small* sm = scratch<Small>(ctx, "small", 1);
   {
@@ -462,6 +442,8 @@ static int spangroup_run(tsdbhip_ctx* ctx, const tsdbhip_sg_desc* d, tsdbhip_sg_
     init.range[1] = 0;
     init.nan_t = ~0ull;
     init.bad_at = ~0ull;
+    init.bound[0] = ~0ull;
+    init.bound[1] = 0;
     std::memcpy(ctx->host_small, &init, sizeof init);
     HIPCHK(hipMemcpyAsync(sm, ctx->host_small, sizeof init, hipMemcpyHostToDevice, st));
   }
@@ -498,7 +480,7 @@ static int spangroup_run(tsdbhip_ctx* ctx, const tsdbhip_sg_desc* d, tsdbhip_sg_
     dscan_u64(ctx, kflag, kidx, S, &sm->n_kept, "k");
     dscan_u64(ctx, sp_cap, eoff_s, S, &sm->e_total, "e");
     hipLaunchKernelGGL(k_kept_scatter, dim3(grid_for(S, 256)), dim3(256), 0, st, sp_kept, kidx, eoff_s,
-                       sp_ncells, S, kept, eoff, &sm->n_input);
+                       sp_ncells, S, kept, eoff, &sm->n_input, sp_first, sp_last, sm->bound);
   }
   Small h;
   readback(ctx, &h, sm, sizeof h);  // sync 1
@@ -506,6 +488,25 @@ static int spangroup_run(tsdbhip_ctx* ctx, const tsdbhip_sg_desc* d, tsdbhip_sg_
   const uint32_t n_kept = (uint32_t)h.n_kept;
   out->n_input_points = h.n_input;
   uint64_t n_input_global = h.n_input;
+
+  // ---- union-grid bitmap range: every E point lies in [first, last] of its
+  // span and in [start, ...]; G keeps those <= end (SURVEY.md §8a closed form)
+  int64_t lo = std::max<int64_t>(d->start_time, h.bound[0] == ~0ull ? INT64_MAX : (int64_t)h.bound[0]);
+  int64_t hi = std::min<int64_t>(d->end_time, (int64_t)h.bound[1]);
+  if (h.bound[0] == ~0ull) hi = -1;
+  if (sharded) {  // every rank needs the same bitmap geometry
+    unsigned long long* x = scratch<unsigned long long>(ctx, "xchg_bound", 2);
+    unsigned long long hv[2] = {lo <= hi ? (unsigned long long)lo : ~0ull, lo <= hi ? (unsigned long long)hi : 0ull};
+    HIPCHK(hipMemcpyAsync(x, hv, sizeof hv, hipMemcpyHostToDevice, st));
+    NCCLCHK(ncclAllReduce(x, x, 1, ncclUint64, ncclMin, ctx->comm, st));
+    NCCLCHK(ncclAllReduce(x + 1, x + 1, 1, ncclUint64, ncclMax, ctx->comm, st));
+    readback(ctx, hv, x, sizeof hv);
+    lo = hv[0] == ~0ull ? 1 : (int64_t)hv[0];
+    hi = hv[0] == ~0ull ? 0 : (int64_t)hv[1];
+  }
+  const bool empty_grid = lo > hi;
+  const uint64_t nwords = empty_grid ? 0 : (uint64_t)(hi - lo + 1 + 31) / 32;
+  uint32_t* bitmap = empty_grid ? nullptr : scratch<uint32_t>(ctx, "bitmap", nwords, true);
 
   // ---- decode (+ downsample) ----
   const uint64_t e_total = h.e_total;
@@ -523,6 +524,8 @@ static int spangroup_run(tsdbhip_ctx* ctx, const tsdbhip_sg_desc* d, tsdbhip_sg_
   da.interval = interval; da.ds_agg = ds_agg; da.rate = rate; da.err = &sm->err; da.gflags = sm->gflags;
   da.range = sm->range; da.fstar = &sm->fstar;
   HIPCHK(hipEventRecord(ctx->ev[1], st));
+  bool chunk_marked = false;     // k_ds_spans marked G for the spans it took
+  const uint32_t* mark_list = nullptr, *mark_count = nullptr;
   if (n_kept) {
     const unsigned blocks = grid_for(n_kept, 4, 65536);
     // wide rows (the reference's hourly compacted rows) take the streaming
@@ -554,8 +557,17 @@ static int spangroup_run(tsdbhip_ctx* ctx, const tsdbhip_sg_desc* d, tsdbhip_sg_
     } else {
       DecodeArgs fa = da;
       if (chunks && ds_agg != 4) {
-        const uint64_t chunk_bound = d->qual_nbytes / 2 / FCH + R + 1;
-        launch_agg<LaunchChunks>(ds_agg, ctx, da, fa, row_ncells, row_val_len, R, e_total, chunk_bound);
+        SpanDsArgs g = {};
+        g.bitmap = getenv("TSDBHIP_EXP_NOMARK") ? nullptr : bitmap;
+        g.lo = lo;
+        g.hi = hi;
+        g.rate = rate;
+        launch_agg<LaunchChunks>(ds_agg, ctx, da, fa, row_ncells, row_val_len, g);
+        chunk_marked = bitmap != nullptr && fa.span_list != nullptr;
+      }
+      if (chunk_marked) {
+        mark_list = fa.span_list;
+        mark_count = fa.span_count;
       }
       launch_agg<LaunchFastDs>(ds_agg, ctx, blocks, fa, row_ncells, row_val_len);
       if (ctx->hot_kernel == TSDBHIP_HOT_DECODE_FAST) HIPCHK(hipEventRecord(ctx->ev[9], st));
@@ -569,38 +581,27 @@ static int spangroup_run(tsdbhip_ctx* ctx, const tsdbhip_sg_desc* d, tsdbhip_sg_
 
   // ---- union grid ----
   bool anyf = h.gflags[0] != 0, anyi = h.gflags[1] != 0;
-  int64_t lo = (int64_t)h.range[0];
-  int64_t hi = std::min<int64_t>((int64_t)h.range[1], d->end_time);
   uint64_t fstar = h.fstar;
   if (sharded) {
-    // agree on range, flags, F* and the input count across ranks
+    // agree on flags, F* and the input count across ranks
     unsigned long long* x = scratch<unsigned long long>(ctx, "xchg_small", 8);
-    unsigned long long hv[8] = {(unsigned long long)(h.range[0] == ~0ull ? ~0ull : h.range[0]),
-                                (unsigned long long)h.range[1], (unsigned long long)fstar,
-                                (unsigned long long)anyf, (unsigned long long)anyi, h.n_input, 0, 0};
+    unsigned long long hv[8] = {(unsigned long long)fstar, (unsigned long long)anyf, (unsigned long long)anyi,
+                                h.n_input, 0, 0, 0, 0};
     HIPCHK(hipMemcpyAsync(x, hv, sizeof hv, hipMemcpyHostToDevice, st));
-    NCCLCHK(ncclAllReduce(x, x, 1, ncclUint64, ncclMin, ctx->comm, st));
-    NCCLCHK(ncclAllReduce(x + 1, x + 1, 4, ncclUint64, ncclMax, ctx->comm, st));
-    NCCLCHK(ncclAllReduce(x + 5, x + 5, 1, ncclUint64, ncclSum, ctx->comm, st));
+    NCCLCHK(ncclAllReduce(x, x, 3, ncclUint64, ncclMax, ctx->comm, st));
+    NCCLCHK(ncclAllReduce(x + 3, x + 3, 1, ncclUint64, ncclSum, ctx->comm, st));
     readback(ctx, hv, x, sizeof hv);
-    lo = (int64_t)hv[0];
-    hi = std::min<int64_t>((int64_t)hv[1], d->end_time);
-    fstar = hv[2];
-    anyf = hv[3] != 0;
-    anyi = hv[4] != 0;
-    n_input_global = hv[5];
+    fstar = hv[0];
+    anyf = hv[1] != 0;
+    anyi = hv[2] != 0;
+    n_input_global = hv[3];
     out->n_input_points = n_input_global;
   }
-  const bool empty_grid = h.range[0] == ~0ull && !sharded ? true : (lo > hi || (uint64_t)lo == ~0ull);
   uint64_t T = 0;
-  uint64_t nwords = 0;
-  uint32_t* bitmap = nullptr;
   uint32_t* word_rank = nullptr;
   uint32_t* gridv = nullptr;
   HIPCHK(hipEventRecord(ctx->ev[3], st));
   if (!empty_grid) {
-    nwords = (uint64_t)(hi - lo + 1 + 31) / 32;
-    bitmap = scratch<uint32_t>(ctx, "bitmap", nwords, true);
     word_rank = scratch<uint32_t>(ctx, "word_rank", nwords);
     const uint64_t nb = (nwords + 1023) / 1024;
     uint32_t* bsum = scratch<uint32_t>(ctx, "grid_bsum", nb);
@@ -608,6 +609,8 @@ static int spangroup_run(tsdbhip_ctx* ctx, const tsdbhip_sg_desc* d, tsdbhip_sg_
     ga.e_off = eoff; ga.e_len = e_len; ga.e_ts = e_ts; ga.n_kept = n_kept; ga.lo = lo; ga.hi = hi;
     ga.rate = rate; ga.bitmap = bitmap; ga.nwords = nwords; ga.word_rank = word_rank; ga.block_sum = bsum;
     ga.total = &sm->T;
+    ga.list = mark_list;  // spans k_ds_spans did not mark (null: all)
+    ga.list_count = mark_count;
     if (n_kept) hipLaunchKernelGGL(k_grid_mark, dim3(grid_for(n_kept, 4, 65536)), dim3(256), 0, st, ga);
     if (sharded) {
       uint32_t* all = scratch<uint32_t>(ctx, "bitmap_all", nwords * ctx->nranks);

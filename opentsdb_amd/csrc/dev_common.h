@@ -64,9 +64,8 @@ DEVI uint64_t wave_incl_scan_u64_dpp(uint64_t x) {
   return x;
 }
 
-// floor(a / n) for u64 a, u32 n > 0: 32-bit path when possible.
-DEVI uint64_t udiv64_32(uint64_t a, uint32_t n) {
-  if ((a >> 32) == 0) return (uint32_t)a / n;
+// floor(a / n) for u64 a, u32 n > 0 — the general case, out of line.
+__device__ __attribute__((noinline)) uint64_t udiv64_32_slow(uint64_t a, uint32_t n) {
   if (n == 1) return a;
   uint64_t q = (uint64_t)((double)a / (double)n);
   int64_t r = (int64_t)(a - q * (uint64_t)n);
@@ -74,6 +73,20 @@ DEVI uint64_t udiv64_32(uint64_t a, uint32_t n) {
   r = (int64_t)(a - q * (uint64_t)n);
   while (r < 0) { q--; r += n; }
   while (r >= (int64_t)n) { q++; r -= n; }
+  return q;
+}
+// floor(a / n): 32-bit path, or for a < 2^52 a refined double reciprocal
+// (error < 1) plus one exact correction step; larger a out of line.
+DEVI uint64_t udiv64_32(uint64_t a, uint32_t n) {
+  if ((a >> 32) == 0) return (uint32_t)a / n;
+  if ((a >> 52) != 0) return udiv64_32_slow(a, n);
+  const double dn = (double)n;
+  double r = __builtin_amdgcn_rcp(dn);
+  r = __builtin_fma(r, __builtin_fma(-dn, r, 1.0), r);  // one Newton step
+  uint64_t q = (uint64_t)__builtin_floor((double)a * r);
+  const int64_t rem = (int64_t)(a - q * (uint64_t)n);
+  if (rem < 0) q--;
+  else if (rem >= (int64_t)n) q++;
   return q;
 }
 // Java long / int with truncation toward zero (n >= 1).

@@ -415,20 +415,37 @@ __global__ void __launch_bounds__(256) k_decode_ds(DecodeArgs a) {
 }
 
 // Per-span summary of E after decode: grid range, F* (float first points).
-__global__ void k_span_summary(DecodeArgs a) {
+// One atomic per wave and field.
+__global__ void __launch_bounds__(256) k_span_summary(DecodeArgs a) {
   const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
-  if (k >= a.n_kept) return;
-  const uint32_t len = a.e_len[k];
-  if (len == 0) { atomicMin(a.err, -3 /*E_EMPTY_SPAN*/); return; }
-  const uint64_t eo = a.e_off[k];
-  const uint64_t first = a.e_ts[eo];
-  if (a.rate) {
-    if (len >= 2) atomicMin(&a.range[0], (unsigned long long)a.e_ts[eo + 1]);
-  } else {
-    atomicMin(&a.range[0], (unsigned long long)first);
-    if (a.e_flt[eo]) atomicMax(a.fstar, (unsigned long long)first + 1ull);  // +1: 0 = none
+  int64_t lo = INT64_MAX, hi = INT64_MIN, fs = 0;
+  bool empty = false;
+  if (k < a.n_kept) {
+    const uint32_t len = a.e_len[k];
+    const uint64_t eo = a.e_off[k];
+    if (len == 0) {
+      empty = true;
+    } else {
+      const int64_t first = a.e_ts[eo];
+      if (a.rate) {
+        if (len >= 2) lo = a.e_ts[eo + 1];
+      } else {
+        lo = first;
+        if (a.e_flt[eo]) fs = first + 1;  // +1: 0 = none
+      }
+      hi = a.e_ts[eo + len - 1];
+    }
   }
-  atomicMax(&a.range[1], (unsigned long long)a.e_ts[eo + len - 1]);
+  lo = wave_min_i64(lo);
+  hi = wave_max_i64(hi);
+  fs = wave_max_i64(fs);
+  const bool any_empty = ballot(empty) != 0;
+  if (lane_id() == 0) {
+    if (any_empty) atomicMin(a.err, -3 /*E_EMPTY_SPAN*/);
+    if (lo != INT64_MAX) atomicMin(&a.range[0], (unsigned long long)lo);
+    if (hi != INT64_MIN) atomicMax(&a.range[1], (unsigned long long)hi);
+    if (fs) atomicMax(a.fstar, (unsigned long long)fs);
+  }
 }
 
 }  // namespace tsdb

@@ -1,22 +1,30 @@
-// k_ds_chunks.hip — chunk-parallel greedy downsampling for regular-cadence
-// integer spans (the dominant case: series written at a fixed interval).
+// k_ds_chunks.hip — streaming greedy downsampling of regular-cadence integer
+// spans (the dominant case: series written at a fixed interval), one wave
+// per span, emitting E (the span's bucket sequence) directly.
 //
 // Span.DownsamplingIterator (Span.java:377-422) chains buckets serially: a
 // bucket starts at the first point >= previous start + interval. For a span
-// whose first bucket holds k cells and whose cadence is regular, the heads
-// are exactly the cells 0, k, 2k, ... The chunk kernel assumes that and
-// records, per head h, ts[h] and ts[h-1]; k_ds_finalize then proves it:
-// head h is exact iff ts[h] >= ts[h-k] + interval > ts[h-1], and the span's
-// last cell must stay inside the last bucket. Any miss, a float cell, a
-// mixed-width or unaligned row, unsorted cells, or cells before `start`
-// send the whole span to the serial kernels instead (k_decode_fast, then
-// k_decode.hip), which rewrite its E sequence.
+// whose second bucket starts at cell kk and whose cadence is regular, the
+// heads are exactly cells 0, kk, 2kk, ... The wave assumes that and proves it
+// as it goes: head h is exact iff ts[h] >= ts[h-kk] + interval > ts[h-1],
+// and the span's last cell must lie inside the last bucket. kk is found as
+// the first cell at/after ts[0] + interval (any distance, across chunks and
+// rows). Any miss, a float cell, a mixed-width or unaligned row, unsorted
+// cells, or a first cell before `start` send the whole span to the serial
+// kernels (k_decode_fast, then k_decode.hip), which rewrite its E.
 //
-// Pieces: the chunk holding a bucket's head writes the head piece (count,
-// timestamp sum relative to the head, integer sum/min/max); every chunk whose
-// first cell is not a head writes a lead piece for the bucket open at its
-// start. k_ds_finalize adds a bucket's head piece to the lead pieces of the
-// chunks it spills into (integer arithmetic: exact in any order).
+// The row streams through in 256-cell chunks (4 cells per lane: one 8-B
+// qualifier load and one or two 16-B value loads), two chunks of loads in
+// flight. Per chunk, DPP wave scans build ts-delta and value prefixes in LDS;
+// lane j owns the chunk's j-th head, and a bucket's count / ts sum / integer
+// sum are prefix differences (exact in any order). The bucket still open at
+// the end of a chunk (or row) is carried in registers and completed by the
+// next chunk's lead cells, so every bucket leaves the kernel finished: no
+// pieces, no second pass.
+//
+// Once a span is proven, the wave marks its E timestamps in the union-grid
+// bitmap (re-reading the E it just wrote; the span's loads have drained by
+// then), which saves the separate k_grid_mark pass for these spans.
 //
 // The chunk loop issues no global load besides the chunk stream itself: an
 // in-order vmcnt wait for any other load would also drain the prefetched
@@ -27,113 +35,13 @@
 
 namespace tsdb {
 
-struct alignas(16) SpanPlan {
-  uint32_t kk;    // first-bucket length in cells, 0 = not eligible
-  uint32_t nb;    // bucket count
-  uint32_t ncs;   // span cells
-  uint32_t pad;
-  uint64_t eo;    // E offset
-  uint64_t r0;    // first row
+struct SpanDsArgs {
+  uint32_t* list;        // spans left to the serial kernels
+  uint32_t* list_count;  // [1]
+  uint32_t* bitmap;      // union-grid bitmap over [lo, hi] (null: no marking)
+  int64_t lo, hi;
+  int32_t rate;
 };
-
-struct ChunkPlanArgs {
-  int32_t* row_kidx;            // [n_rows] kept index of the row's span, or -1
-  uint32_t* row_prev_ts;        // [n_rows] last ts of the previous row of the span
-  const uint64_t* row_chunk0;   // [n_rows] global id of the row's first chunk
-  SpanPlan* plan;               // [n_kept]
-  uint32_t* fail;               // [n_kept] set when verification fails
-  uint32_t* tail_ts;            // [n_kept] ts of the span's last cell
-  // head pieces [e_total], indexed e_off[k] + bucket
-  uint32_t* hp_nrel;            // n << 20 | sum of (ts - head ts) (n <= 256, sum < 2^20)
-  uint32_t* hp_ref;             // ts of the head
-  uint32_t* hp_pre;             // ts of the cell before the head
-  int64_t* hp_v;                // integer sum / min / max of the piece
-  // lead pieces [n_chunks]
-  uint32_t* lp_n;
-  uint64_t* lp_ts;              // absolute timestamp sum
-  int64_t* lp_v;
-  uint32_t* list;               // spans for the serial kernels
-  uint32_t* list_count;
-};
-
-// last row of [r0, r1) whose first span cell is <= cell
-DEVI uint64_t span_cell_row(const DecodeArgs& a, uint64_t r0, uint64_t r1, uint32_t cell) {
-  uint64_t lo = r0, hi = r1;
-  while (lo < hi) {
-    const uint64_t mid = (lo + hi) >> 1;
-    if (a.row_cell0[mid] <= cell) lo = mid + 1; else hi = mid;
-  }
-  return lo - 1;
-}
-DEVI uint64_t span_cell_chunk(const DecodeArgs& a, const ChunkPlanArgs& p, uint64_t r0, uint64_t r1,
-                              uint32_t cell) {
-  const uint64_t r = r1 - r0 == 1 ? r0 : span_cell_row(a, r0, r1, cell);
-  return p.row_chunk0[r] + (cell - a.row_cell0[r]) / FCH;
-}
-DEVI uint32_t row_last_ts(const DecodeArgs& a, uint64_t r, const uint32_t* ncells) {
-  return a.row_base[r] + (load_qual(a.qual, a.row_qual_off[r] + 2ull * (ncells[r] - 1)) >> 4);
-}
-
-// One wave per kept span: eligibility, k = cells of the first bucket.
-__global__ void __launch_bounds__(256) k_ds_plan(DecodeArgs a, ChunkPlanArgs p, const uint32_t* ncells) {
-  const int lane = lane_id();
-  const uint32_t wave = (blockIdx.x * blockDim.x + threadIdx.x) / WAVE;
-  const uint32_t nwaves = gridDim.x * blockDim.x / WAVE;
-  for (uint32_t k = wave; k < a.n_kept; k += nwaves) {
-    const uint32_t s = a.kept[k];
-    const uint64_t r0 = a.span_row_start[s], r1 = a.span_row_start[s + 1];
-    const uint32_t n = a.sp_ncells[s];
-    bool ok = a.sp_q1[s] < 0 && a.sp_ovf_cell[s] < 0 && n > 0 && r1 > r0;
-    for (uint64_t r = r0 + lane; r < r1 + lane; r += WAVE)
-      ok &= ballot(r < r1 && (a.row_ok[r] == 0 || ncells[r] == 0)) == 0;
-    for (uint64_t r = r0 + lane; r < r1; r += WAVE) {
-      p.row_kidx[r] = ok ? (int32_t)k : -1;
-      if (ok && r > r0) p.row_prev_ts[r] = row_last_ts(a, r - 1, ncells);
-    }
-    // common case: the first bucket ends within the first row's first 64 cells
-    int probe = -1;  // first probed cell at/after t0 + interval
-    int64_t t0 = 0;
-    if (ok) {
-      const uint32_t nc0 = ncells[r0];
-      const uint64_t qo = a.row_qual_off[r0];
-      const int64_t b0 = (int64_t)a.row_base[r0];
-      t0 = b0 + (load_qual(a.qual, qo) >> 4);
-      const bool in = (uint32_t)lane < nc0;
-      const int64_t t = in ? b0 + (load_qual(a.qual, qo + 2ull * lane) >> 4) : 0;
-      const uint64_t hit = ballot(in && t >= t0 + a.interval);
-      if (hit) probe = __builtin_ctzll(hit);
-    }
-    if (lane != 0) continue;
-    uint32_t kk = 0, nb = 0;
-    if (ok && t0 >= a.start) {
-      const int64_t end0 = t0 + a.interval;
-      if (probe > 0) {
-        kk = (uint32_t)probe;
-      } else {
-        uint64_t r = r0;
-        for (; r < r1; r++)
-          if ((int64_t)row_last_ts(a, r, ncells) >= end0) break;
-        if (r == r1) {
-          kk = n;  // one bucket holds the whole span
-        } else {
-          uint32_t lo = 0, hi = ncells[r];
-          while (lo < hi) {
-            const uint32_t mid = (lo + hi) >> 1;
-            const int64_t t = (int64_t)a.row_base[r] + (load_qual(a.qual, a.row_qual_off[r] + 2ull * mid) >> 4);
-            if (t < end0) lo = mid + 1; else hi = mid;
-          }
-          kk = a.row_cell0[r] + lo;
-        }
-      }
-      nb = kk ? (n + kk - 1) / kk : 0;
-      if (kk == 0 || nb > a.sp_cap[s]) { kk = 0; nb = 0; }
-    }
-    SpanPlan sp;
-    sp.kk = kk; sp.nb = nb; sp.ncs = n; sp.pad = 0; sp.eo = a.e_off[k]; sp.r0 = r0;
-    p.plan[k] = sp;
-    p.fail[k] = 0;
-  }
-}
 
 template <int W>
 struct RawW {
@@ -163,24 +71,84 @@ DEVI int64_t raw_value(const RawW<W>& x, int j) {
   return (int64_t)(int32_t)bswap32(w);
 }
 
-DEVI uint32_t raw_qual(uint2 q, int j) {
-  const uint32_t word = j < 2 ? q.x : q.y;
-  const uint32_t h = (j & 1) ? (word >> 16) : (word & 0xFFFF);
-  return ((h & 0xFF) << 8) | (h >> 8);
+// Two big-endian qualifiers of one dword -> (q0 | q1 << 16) in native order.
+DEVI uint32_t qpair(uint32_t word) { return __builtin_amdgcn_perm(word, word, 0x02030001u); }
+
+// Open-bucket / chain state of one span (wave-uniform).
+struct DsState {
+  uint32_t kk;       // cells per bucket (0 until the second head is found)
+  uint32_t hnext;    // span cell index of the next head (~0u: not in sight)
+  uint32_t bnext;    // bucket index of hnext
+  uint32_t t0;       // ts of the span's first cell
+  uint32_t lh_ts;    // ts of the latest head
+  uint32_t prev_ts;  // ts of the latest cell
+  bool open;         // bucket bnext-1 still takes cells
+  uint32_t o_n;      // its cells so far
+  uint64_t o_rel;    // its sum of (ts - o_ref)
+  uint32_t o_ref;    // its head ts
+  int64_t o_v;       // its value sum / min / max
+  uint32_t fbase;    // first bucket index held in the LDS buffer
+  uint32_t room;     // most buckets one chunk can close (256 / kk + 2)
+};
+
+// Closed buckets wait in a per-wave LDS buffer (count, ts offsets, value)
+// and leave it in batches, one lane per bucket, so the divisions of
+// Span.java:399 and the avg downsampler stay out of the chunk loop. A chunk
+// closes at most 256/kk + 2 <= 66 buckets (kk >= 4).
+constexpr uint32_t BKB = 80;
+struct BkLds {
+  uint32_t ref[BKB];  // head ts
+  uint32_t n[BKB];    // cells
+  uint64_t rel[BKB];  // sum of (ts - ref)
+  int64_t v[BKB];     // value sum / min / max
+};
+
+// wave-uniform copies (SGPR) of values every lane holds alike
+DEVI uint32_t ufl(uint32_t x) { return (uint32_t)__builtin_amdgcn_readfirstlane((int)x); }
+DEVI uint64_t ufl64(uint64_t x) { return ((uint64_t)ufl((uint32_t)(x >> 32)) << 32) | (uint64_t)ufl((uint32_t)x); }
+
+// Writes buckets [b0, b0 + cnt) of the span to E (Span.java:396-420, integer
+// buckets); returns each lane's bucket ts (lane < cnt).
+template <int AGG>
+DEVI uint32_t bk_flush(const DecodeArgs& a, const BkLds& B, uint64_t eo, uint32_t cap, uint32_t b0, uint32_t cnt,
+                       bool& bad) {
+  wave_lds_sync();
+  const int lane = lane_id();
+  uint32_t ts0 = 0;
+  for (uint32_t i = lane; i < cnt; i += WAVE) {
+    const uint32_t b = b0 + i;
+    const uint32_t n = B.n[i];
+    const uint32_t ts = B.ref[i] + (uint32_t)udiv64_32(B.rel[i], n);  // Span.java:399
+    if (i == (uint32_t)lane) ts0 = ts;
+    if (b < cap) {
+      a.e_ts[eo + b] = ts;
+      a.e_val[eo + b] = AGG == 3 ? ldiv64_32(B.v[i], n) : B.v[i];
+      a.e_flt[eo + b] = 0;
+    } else {
+      bad = true;  // more buckets than E holds: cannot be the greedy chain
+    }
+  }
+  wave_lds_sync();
+  return ts0;
 }
 
-// One row: its 256-cell chunks, two chunks of loads in flight. Returns true
-// if the row breaks a precondition (the span then goes to the serial path).
+template <int AGG>
+DEVI int64_t ds_combine(int64_t x, int64_t y) {
+  if (AGG == 0 || AGG == 3) return ladd(x, y);
+  if (AGG == 1) return y < x ? y : x;
+  return y > x ? y : x;
+}
+
+// One row of a span: its 256-cell chunks. Returns true if a precondition
+// breaks (the span then goes to the serial path).
 template <int AGG, int W>
-DEVI bool chunk_row(const DecodeArgs& a, const ChunkPlanArgs& p, const SpanPlan& sp, uint32_t kidx,
-                    uint64_t qoff, uint64_t voff, uint32_t base, uint32_t nc, uint32_t cell0, uint64_t chunk0,
-                    bool has_prev, uint32_t prev_ts, uint32_t* L_dt, uint32_t* L_pt, uint64_t* L_v) {
-  constexpr bool PREFIX = AGG == 0 || AGG == 3;  // sum / avg: prefix differences; min / max: lane loops
+DEVI bool ds_row(const DecodeArgs& a, const SpanDsArgs& g, DsState& st, uint64_t eo, uint32_t cap,
+                 uint32_t n_span, uint64_t qoff, uint64_t voff, uint32_t base, uint32_t nc, uint32_t cell0,
+                 uint32_t* L_dt, uint32_t* L_pt, uint64_t* L_v, BkLds& BK) {
+  constexpr bool PREFIX = AGG == 0 || AGG == 3;  // sum / avg: prefix differences; min / max: loops
   const int lane = lane_id();
-  const uint32_t kk = sp.kk;
+  const int64_t I = a.interval;
   const uint32_t clamp_c = (nc - 1) & ~3u;
-  // three register sets; the loop is unrolled by 3 so their roles rotate
-  // statically (a register copy of an in-flight load would wait for it)
   RawW<W> A, B, C;
   auto issue = [&](uint32_t c0, RawW<W>& x) {
     const uint32_t c = c0 + 4u * lane;
@@ -188,29 +156,44 @@ DEVI bool chunk_row(const DecodeArgs& a, const ChunkPlanArgs& p, const SpanPlan&
   };
   issue(0, A);
   issue(FCH, B);
-  uint32_t bfirst = (cell0 + kk - 1) / kk;  // first bucket whose head is at/after the row start
-  uint32_t hfirst = bfirst * kk;
   bool bad = false;
-  // process chunk c0 held in `cur`
   auto step = [&](uint32_t c0, const RawW<W>& cur) {
     const uint32_t nv = min((uint32_t)FCH, nc - c0);
     const uint32_t cs = cell0 + c0;  // span cell index of the chunk start
-    // ---- decode ----
+    // ---- decode: 4 cells per lane (loads past the row end were clamped) ----
+    const uint32_t p01 = qpair(cur.q.x), p23 = qpair(cur.q.y);
     uint32_t dt[4];
+    dt[0] = (p01 & 0xFFFF) >> 4;
+    dt[1] = p01 >> 20;
+    dt[2] = (p23 & 0xFFFF) >> 4;
+    dt[3] = p23 >> 20;
     int64_t bits[4];
 #pragma unroll
-    for (int j = 0; j < 4; j++) {
-      const bool valid = 4u * lane + j < nv;
-      const uint32_t q = raw_qual(cur.q, j);
-      dt[j] = valid ? q >> 4 : 0u;
-      bits[j] = valid ? raw_value<W>(cur, j) : 0;
-      bad |= valid && (q & 15) != (uint32_t)(W - 1);  // integer cell of this width
-      if (j > 0) bad |= valid && dt[j] <= dt[j - 1];  // sorted within the lane
+    for (int j = 0; j < 4; j++) bits[j] = raw_value<W>(cur, j);
+    // integer cells of width W (flags nibble of each qualifier), strictly
+    // increasing deltas (Span/RowSeq order)
+    const uint32_t fl = (W - 1) * 0x00010001u;
+    uint32_t nmine = 4;
+    if (nv == FCH) {  // full chunk: every lane holds 4 cells
+      bad |= (((p01 ^ fl) | (p23 ^ fl)) & 0x000F000Fu) != 0;
+      bad |= dt[1] <= dt[0] || dt[2] <= dt[1] || dt[3] <= dt[2];
+    } else {  // the row's last chunk: mask the lanes past its end
+      nmine = nv > 4u * lane ? min(4u, nv - 4u * lane) : 0u;
+      const uint32_t fm0 = nmine >= 2 ? 0x000F000Fu : (nmine == 1 ? 0x0000000Fu : 0u);
+      const uint32_t fm1 = nmine >= 4 ? 0x000F000Fu : (nmine == 3 ? 0x0000000Fu : 0u);
+      bad |= ((p01 ^ fl) & fm0) != 0 || ((p23 ^ fl) & fm1) != 0;
+      bad |= (nmine > 1 && dt[1] <= dt[0]) || (nmine > 2 && dt[2] <= dt[1]) || (nmine > 3 && dt[3] <= dt[2]);
+      if (nmine == 0) dt[0] = 0;
+#pragma unroll
+      for (int j = 0; j < 4; j++) {
+        if (j > 0 && (uint32_t)j >= nmine) dt[j] = dt[j - 1];  // ts prefix flat past the end
+        if ((uint32_t)j >= nmine) bits[j] = 0;
+      }
     }
     {
       const uint32_t pl = shfl_up_u32(dt[3], 1);
-      bad |= lane > 0 && 4u * lane < nv && dt[0] <= pl;
-      bad |= lane == 0 && has_prev && base + dt[0] <= prev_ts;  // previous chunk / row
+      bad |= lane > 0 && nmine > 0 && dt[0] <= pl;
+      bad |= lane == 0 && cs > 0 && base + dt[0] <= st.prev_ts;  // previous chunk / row
     }
     // ---- stage: ts deltas, ts prefix, value prefix (or raw values) ----
     uint32_t pt = 0;
@@ -219,7 +202,7 @@ DEVI bool chunk_row(const DecodeArgs& a, const ChunkPlanArgs& p, const SpanPlan&
     uint64_t pvi[4];
 #pragma unroll
     for (int j = 0; j < 4; j++) {
-      pt += dt[j];
+      pt += (uint32_t)j < nmine ? dt[j] : 0u;  // (nmine == 4 on full chunks)
       pv += (uint64_t)bits[j];
       pti[j] = pt;
       pvi[j] = PREFIX ? pv : (uint64_t)bits[j];
@@ -235,60 +218,130 @@ DEVI bool chunk_row(const DecodeArgs& a, const ChunkPlanArgs& p, const SpanPlan&
       *(ulonglong2*)&L_v[4 * lane + 2] = v23;
     }
     wave_lds_sync();
-    // ---- heads: lane j owns head hfirst + j*kk if it lies in the chunk ----
-    const uint64_t H64 = (uint64_t)hfirst + (uint64_t)lane * kk;
-    const bool mine = H64 < (uint64_t)cs + nv;
-    const uint64_t hm = ballot(mine);
-    bad |= hm == ~0ull;  // 64+ heads in one chunk: one lane per head cannot hold them
-    const uint32_t nh = (uint32_t)__builtin_popcountll(hm);
-    if (mine) {
-      const uint32_t H = (uint32_t)H64;
-      const int la = (int)(H - cs);
-      const int lb = (int)(min((uint64_t)cs + nv, H64 + kk) - 1 - cs);
-      const uint32_t n = (uint32_t)(lb - la + 1);
-      const uint32_t dta = L_dt[la];
-      const uint32_t rel = (L_pt[lb] - (la > 0 ? L_pt[la - 1] : 0u)) - n * dta;
-      int64_t v;
-      if (PREFIX) {
-        v = (int64_t)(L_v[lb] - (la > 0 ? L_v[la - 1] : 0ull));
-      } else {
-        v = (int64_t)L_v[la];
-        for (int i = la + 1; i <= lb; i++) {
-          const int64_t x = (int64_t)L_v[i];
-          if (AGG == 1 ? x < v : x > v) v = x;
-        }
-      }
-      const uint64_t e = sp.eo + bfirst + (uint32_t)lane;
-      p.hp_nrel[e] = (n << 20) | rel;
-      p.hp_ref[e] = base + dta;
-      p.hp_pre[e] = la > 0 ? base + L_dt[la - 1] : prev_ts;
-      p.hp_v[e] = v;
+    const uint32_t cend = cs + nv;
+    // ---- the span's first cell opens bucket 0 ----
+    if (cs == 0) {
+      st.t0 = ufl(base + L_dt[0]);
+      bad |= (int64_t)st.t0 < a.start;  // no seek inside the span
+      st.lh_ts = st.t0;
+      st.open = true;
+      st.o_n = 0;
+      st.o_rel = 0;
+      st.o_ref = st.t0;
+      st.o_v = AGG == 1 ? INT64_MAX : (AGG == 2 ? INT64_MIN : 0);
+      st.bnext = 1;
+      st.hnext = ~0u;
+      st.fbase = 0;
     }
-    const uint32_t last_ts = base + L_dt[nv - 1];
-    if (lane == 0) {
-      if (hfirst != cs) {  // lead piece: cells before the chunk's first head
-        const int lb = nh > 0 ? (int)(hfirst - cs) - 1 : (int)nv - 1;
-        int64_t v;
-        if (PREFIX) {
-          v = (int64_t)L_v[lb];
-        } else {
-          v = (int64_t)L_v[0];
-          for (int i = 1; i <= lb; i++) {
-            const int64_t x = (int64_t)L_v[i];
-            if (AGG == 1 ? x < v : x > v) v = x;
+    // ---- second head: the first cell at/after t0 + interval ----
+    if (st.kk == 0) {
+      const int64_t end0 = (int64_t)st.t0 + I;
+      uint64_t m = 0;
+      int q = 0;
+      for (; q < 4 && !m; q++) {
+        const uint32_t c = 64u * q + lane;
+        m = ballot(c < nv && (int64_t)(base + L_dt[c]) >= end0);
+      }
+      if (m) {
+        st.kk = cs + 64u * (q - 1) + (uint32_t)(__ffsll((long long)m) - 1);
+        st.hnext = st.kk;
+        st.room = FCH / max(st.kk, 4u) + 2;
+        bad |= st.kk < 4;  // more than 64 heads per chunk: the serial kernels
+      }
+    }
+    // ---- room in the bucket buffer for every bucket this chunk can close ----
+    if (st.kk != 0) {
+      const uint32_t closed = st.bnext - (st.open ? 1u : 0u);
+      if (closed + st.room - st.fbase > BKB) {
+        bk_flush<AGG>(a, BK, eo, cap, st.fbase, closed - st.fbase, bad);
+        st.fbase = closed;
+      }
+    }
+    // ---- lead cells [cs, min(hnext, cend)) complete the open bucket ----
+    const uint32_t lend = min(st.hnext, cend);
+    if (lend > cs) {
+      const uint32_t ln = lend - cs;
+      bad |= !st.open;
+      st.o_n += ln;
+      st.o_rel += (uint64_t)ln * base + ufl(L_pt[ln - 1]) - (uint64_t)ln * st.o_ref;
+      if (PREFIX) {
+        st.o_v = ladd(st.o_v, (int64_t)ufl64(L_v[ln - 1]));
+      } else {
+        int64_t v = AGG == 1 ? INT64_MAX : INT64_MIN;
+        for (uint32_t i = lane; i < ln; i += WAVE) v = ds_combine<AGG>(v, (int64_t)L_v[i]);
+        v = AGG == 1 ? wave_min_i64(v) : wave_max_i64(v);
+        st.o_v = ds_combine<AGG>(st.o_v, (int64_t)ufl64((uint64_t)v));
+      }
+    }
+    // ---- heads hnext, hnext + kk, ... inside the chunk ----
+    if (st.hnext < cend) {
+      const uint32_t kk = st.kk;
+      {  // the first head closes the open bucket: prove it against the latest head
+        const uint32_t la = st.hnext - cs;
+        const int64_t th = ufl(base + L_dt[la]);
+        const int64_t tp = la > 0 ? (int64_t)ufl(base + L_dt[la - 1]) : (int64_t)st.prev_ts;
+        const int64_t e = (int64_t)st.lh_ts + I;
+        bad |= !(th >= e && tp < e);
+        if (st.open) {
+          const uint32_t b = st.bnext - 1;
+          if (lane == 0) {
+            const uint32_t sl = b - st.fbase;
+            BK.ref[sl] = st.o_ref;
+            BK.n[sl] = st.o_n;
+            BK.rel[sl] = st.o_rel;
+            BK.v[sl] = st.o_v;
           }
         }
-        const uint64_t cid = chunk0 + c0 / FCH;
-        p.lp_n[cid] = (uint32_t)(lb + 1);
-        p.lp_ts[cid] = (uint64_t)(lb + 1) * (uint64_t)base + L_pt[lb];
-        p.lp_v[cid] = v;
+        st.open = false;
       }
-      if (cs + nv == sp.ncs) p.tail_ts[kidx] = last_ts;
+      const uint32_t nh = min((cend - 1 - st.hnext) / max(kk, 4u) + 1, (uint32_t)WAVE);  // kk >= 4
+      for (uint32_t jb = 0; jb < nh; jb += WAVE) {
+        const uint32_t j = jb + lane;
+        const bool mine = j < nh;
+        const uint32_t H = st.hnext + j * kk;
+        const uint32_t la = mine ? H - cs : 0;
+        const uint32_t lb = mine ? min(H + kk, cend) - 1 - cs : 0;
+        const uint32_t n = lb - la + 1;
+        const uint32_t dta = L_dt[la];
+        const uint32_t ref = base + dta;
+        const uint32_t rel = (L_pt[lb] - (la > 0 ? L_pt[la - 1] : 0u)) - n * dta;
+        int64_t v;
+        if (PREFIX) {
+          v = (int64_t)(L_v[lb] - (la > 0 ? L_v[la - 1] : 0ull));
+        } else {
+          v = (int64_t)L_v[la];
+          for (uint32_t i = la + 1; i <= lb; i++) v = ds_combine<AGG>(v, (int64_t)L_v[i]);
+        }
+        if (mine && j > 0) {  // chain proof against the previous head of the chunk
+          const uint32_t e = base + L_dt[la - kk] + (uint32_t)I;
+          const uint64_t e64 = (uint64_t)(base + L_dt[la - kk]) + (uint64_t)I;
+          bad |= e64 > 0xFFFFFFFFull ? true : !(ref >= e && base + L_dt[la - 1] < e);
+        }
+        // closed buckets st.bnext + j (complete inside the chunk) -> LDS buffer
+        if (mine && H + kk <= cend) {
+          const uint32_t sl = st.bnext + j - st.fbase;
+          BK.ref[sl] = ref;
+          BK.n[sl] = n;
+          BK.rel[sl] = rel;
+          BK.v[sl] = v;
+        }
+        if (jb + WAVE >= nh) {  // the chunk's last head: latest head, maybe still open
+          const int l = (int)(nh - 1 - jb);
+          st.lh_ts = readlane_u32(ref, l);
+          const uint32_t Hl = st.hnext + (nh - 1) * kk;
+          if (Hl + kk > cend) {
+            st.open = true;
+            st.o_n = readlane_u32(n, l);
+            st.o_rel = readlane_u32(rel, l);
+            st.o_ref = st.lh_ts;
+            st.o_v = (int64_t)readlane_u64((uint64_t)v, l);
+          }
+        }
+      }
+      st.hnext += nh * kk;
+      st.bnext += nh;
     }
-    prev_ts = last_ts;
-    has_prev = true;
-    hfirst += nh * kk;
-    bfirst += nh;
+    st.prev_ts = ufl(base + L_dt[nv - 1]);
     wave_lds_sync();
   };
   // loads past the row end are clamped (cache hits); steps past it skipped
@@ -300,112 +353,107 @@ DEVI bool chunk_row(const DecodeArgs& a, const ChunkPlanArgs& p, const SpanPlan&
     issue(c0 + 4 * FCH, B);
     if (c0 + 2 * FCH < nc) step(c0 + 2 * FCH, C);
   }
+  (void)n_span;
   return ballot(bad) != 0;
 }
 
-// One wave per row.
+// One wave per kept span.
 template <int AGG>
-__global__ void __launch_bounds__(256) k_ds_chunks(DecodeArgs a, ChunkPlanArgs p, const uint32_t* ncells,
-                                                   const uint32_t* vlen, uint64_t n_rows) {
+__global__ void __launch_bounds__(256) k_ds_spans(DecodeArgs a, SpanDsArgs g, const uint32_t* ncells,
+                                                  const uint32_t* vlen) {
   __shared__ uint32_t s_dt[4][FCH];
   __shared__ uint32_t s_pt[4][FCH];
   __shared__ uint64_t s_v[4][FCH];
+  __shared__ BkLds s_bk[4];
   const int lane = lane_id();
   const int wib = threadIdx.x / WAVE;
-  const uint64_t wave = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) / WAVE;
-  const uint64_t nwaves = (uint64_t)gridDim.x * blockDim.x / WAVE;
-  for (uint64_t r = wave; r < n_rows; r += nwaves) {
-    const int32_t kidx = p.row_kidx[r];
-    if (kidx < 0) continue;
-    const SpanPlan sp = p.plan[kidx];
-    if (sp.kk == 0) continue;
-    const uint32_t nc = ncells[r];
-    const uint32_t vl = vlen[r];
-    const uint64_t qoff = a.row_qual_off[r], voff = a.row_val_off[r];
-    const uint32_t vb = nc > 1 ? vl - 1 : vl;
-    const uint32_t w = vb / nc;
-    const bool aligned = vb == w * nc && (qoff & 7) == 0 && (voff & 15) == 0;
-    const bool first = r == sp.r0;
-    const uint32_t prev_ts = first ? 0u : p.row_prev_ts[r];
-    bool fail = true;
-    if (aligned && w == 8)
-      fail = chunk_row<AGG, 8>(a, p, sp, (uint32_t)kidx, qoff, voff, a.row_base[r], nc, a.row_cell0[r],
-                               p.row_chunk0[r], !first, prev_ts, s_dt[wib], s_pt[wib], s_v[wib]);
-    else if (aligned && w == 4)
-      fail = chunk_row<AGG, 4>(a, p, sp, (uint32_t)kidx, qoff, voff, a.row_base[r], nc, a.row_cell0[r],
-                               p.row_chunk0[r], !first, prev_ts, s_dt[wib], s_pt[wib], s_v[wib]);
-    if (fail && lane == 0) atomicOr(&p.fail[kidx], 1u);
-  }
-}
-
-// One wave per eligible span, one lane per bucket: proves the heads, then
-// combines the pieces into E.
-template <int AGG>
-__global__ void __launch_bounds__(256) k_ds_finalize(DecodeArgs a, ChunkPlanArgs p) {
-  const int lane = lane_id();
   const uint32_t wave = (blockIdx.x * blockDim.x + threadIdx.x) / WAVE;
   const uint32_t nwaves = gridDim.x * blockDim.x / WAVE;
   bool any = false;
-  for (uint32_t k = wave; k < a.n_kept; k += nwaves) {
-    const SpanPlan sp = p.plan[k];
-    if (sp.kk == 0 || p.fail[k]) continue;
-    const uint32_t kk = sp.kk, nb = sp.nb;
-    const uint64_t eo = sp.eo;
-    const uint64_t r0 = sp.r0, r1 = a.span_row_start[a.kept[k] + 1];
-    const int64_t I = a.interval;
-    bool bad = false;
-    for (uint32_t b = lane; b < nb; b += WAVE) {
-      const uint32_t nrel = p.hp_nrel[eo + b];
-      uint32_t n = nrel >> 20;
-      uint64_t rel = nrel & 0xFFFFFu;
-      const int64_t ref = p.hp_ref[eo + b];
-      int64_t v = p.hp_v[eo + b];
-      if (b > 0) {  // Span.java:389-398: the head is the first cell at/after the previous end
-        const int64_t end = (int64_t)p.hp_ref[eo + b - 1] + I;
-        bad |= !(ref >= end && (int64_t)p.hp_pre[eo + b] < end);
+  for (uint32_t k = ufl(wave); k < a.n_kept; k += nwaves) {
+    const uint32_t s = ufl(a.kept[k]);
+    const uint64_t r0 = ufl64(a.span_row_start[s]), r1 = ufl64(a.span_row_start[s + 1]);
+    const uint32_t n = ufl(a.sp_ncells[s]);
+    bool ok = a.sp_q1[s] < 0 && a.sp_ovf_cell[s] < 0 && n > 0 && r1 > r0 && a.interval > 0;
+    for (uint64_t r = r0 + lane; ok && r < r1 + lane; r += WAVE)
+      ok &= ballot(r < r1 && (a.row_ok[r] == 0 || ncells[r] == 0)) == 0;
+    // value width of the span's rows (all must match and be aligned)
+    uint32_t W = 0;
+    if (ok) {
+      const uint32_t nc = ncells[r0], vl = vlen[r0];
+      const uint32_t vb = nc > 1 ? vl - 1 : vl;
+      W = vb == (vb / nc) * nc ? vb / nc : 0;
+      ok = W == 8 || W == 4;
+    }
+    const uint64_t eo = ufl64(a.e_off[k]);
+    const uint32_t cap = ufl((uint32_t)a.sp_cap[s]);
+    DsState st = {};
+    uint32_t cell = 0;
+    for (uint64_t r = r0; ok && r < r1; r++) {
+      const uint32_t nc = ufl(ncells[r]);
+      const uint32_t vl = ufl(vlen[r]);
+      const uint64_t qoff = ufl64(a.row_qual_off[r]), voff = ufl64(a.row_val_off[r]);
+      const uint32_t rbase = ufl(a.row_base[r]);
+      const uint32_t vb = nc > 1 ? vl - 1 : vl;
+      if (!(vb == W * nc && (qoff & 7) == 0 && (voff & 15) == 0)) {
+        ok = false;
+        break;
       }
-      if (b == nb - 1) bad |= !((int64_t)p.tail_ts[k] < ref + I);
-      const uint32_t H = b * kk;
-      const uint32_t last = min(sp.ncs, H + kk) - 1;
-      if (last >= H + n) {  // the bucket spills into the following chunks
-        const uint64_t c_first = span_cell_chunk(a, p, r0, r1, H + n);
-        const uint64_t c_last = span_cell_chunk(a, p, r0, r1, last);
-        for (uint64_t c = c_first; c <= c_last; c++) {
-          const uint32_t ln = p.lp_n[c];
-          rel += p.lp_ts[c] - (uint64_t)ln * (uint64_t)ref;
-          n += ln;
-          const int64_t x = p.lp_v[c];
-          if (AGG == 0 || AGG == 3) v = ladd(v, x);
-          else if (AGG == 1 ? x < v : x > v) v = x;
+      const bool fail = W == 8 ? ds_row<AGG, 8>(a, g, st, eo, cap, n, qoff, voff, rbase, nc, cell,
+                                                 s_dt[wib], s_pt[wib], s_v[wib], s_bk[wib])
+                               : ds_row<AGG, 4>(a, g, st, eo, cap, n, qoff, voff, rbase, nc, cell,
+                                                 s_dt[wib], s_pt[wib], s_v[wib], s_bk[wib]);
+      ok = !fail;
+      cell += nc;
+    }
+    uint32_t ts_last = 0, n_last = 0;  // the final flush (one lane per bucket)
+    if (ok) {  // the last cell must lie inside the last bucket; then close it
+      bool bad = !((int64_t)st.prev_ts < (int64_t)st.lh_ts + a.interval) || st.bnext > cap;
+      const uint32_t b = st.bnext - 1;  // the open bucket
+      if (st.open) {
+        if (b - st.fbase >= BKB) {  // (cannot happen: a chunk left room for it)
+          bk_flush<AGG>(a, s_bk[wib], eo, cap, st.fbase, b - st.fbase, bad);
+          st.fbase = b;
+        }
+        if (lane == 0) {
+          const uint32_t sl = b - st.fbase;
+          s_bk[wib].ref[sl] = st.o_ref;
+          s_bk[wib].n[sl] = st.o_n;
+          s_bk[wib].rel[sl] = st.o_rel;
+          s_bk[wib].v[sl] = st.o_v;
         }
       }
-      a.e_ts[eo + b] = (uint32_t)(ref + (int64_t)udiv64_32(rel, n));  // Span.java:399
-      a.e_val[eo + b] = AGG == 3 ? ldiv64_32(v, n) : v;
-      a.e_flt[eo + b] = 0;
+      n_last = st.bnext - st.fbase;
+      ts_last = bk_flush<AGG>(a, s_bk[wib], eo, cap, st.fbase, n_last, bad);
+      ok = ballot(bad) == 0;
     }
-    if (ballot(bad)) {  // not the greedy chain: the serial kernels rewrite this span
-      if (lane == 0) p.fail[k] = 1;
-      continue;
+    if (ok) {
+      const uint32_t nb = st.bnext;
+      if (lane == 0) {
+        a.e_len[k] = nb;
+        a.e_bad[k] = -1;
+      }
+      any = true;
+      if (g.bitmap) {  // G: this span's E points <= end (rate: from the second)
+        auto mark = [&](int64_t t, uint32_t b) {
+          if ((g.rate && b == 0) || t > g.hi || t < g.lo) return;
+          const uint64_t off = (uint64_t)(t - g.lo);
+          const uint32_t bit = 1u << (off & 31);
+          uint32_t* w = &g.bitmap[off >> 5];
+          if (!(*w & bit)) atomicOr(w, bit);
+        };
+        if ((uint32_t)lane < min(n_last, (uint32_t)WAVE)) mark(ts_last, st.fbase + lane);
+        if (st.fbase > 0 || n_last > WAVE) {  // buckets not in registers: read their E back
+          __threadfence_block();
+          for (uint32_t i = lane; i < nb; i += WAVE)
+            if (i < st.fbase || i >= st.fbase + WAVE) mark(a.e_ts[eo + i], i);
+        }
+      }
+    } else if (lane == 0) {
+      g.list[atomicAdd(g.list_count, 1u)] = k;
     }
-    if (lane == 0) {
-      a.e_len[k] = nb;
-      a.e_bad[k] = -1;
-    }
-    any = true;
   }
   if (any && lane == 0 && !a.gflags[1]) atomicOr(&a.gflags[1], 1u);
-}
-
-// Spans not eligible or failing verification -> the serial kernels.
-__global__ void k_ds_collect(DecodeArgs a, ChunkPlanArgs p) {
-  const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
-  if (k >= a.n_kept) return;
-  if (p.plan[k].kk == 0 || p.fail[k]) p.list[atomicAdd(p.list_count, 1u)] = k;
-}
-
-__global__ void k_row_chunks(const uint32_t* ncells, uint64_t n_rows, uint64_t* out) {
-  const uint64_t r = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (r < n_rows) out[r] = (ncells[r] + FCH - 1) / FCH;
 }
 
 }  // namespace tsdb

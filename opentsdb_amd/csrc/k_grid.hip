@@ -25,6 +25,8 @@ struct GridArgs {
   uint32_t* block_sum;  // [nblocks]
   uint32_t* grid;       // [T] G
   uint64_t* total;      // [1] T
+  const uint32_t* list;       // k_grid_mark: only these kept spans (null: all)
+  const uint32_t* list_count;
 };
 
 // Mark every candidate point. Many spans share timestamps (regular cadence),
@@ -33,7 +35,9 @@ __global__ void __launch_bounds__(256) k_grid_mark(GridArgs g) {
   const int lane = lane_id();
   const uint32_t wave = (blockIdx.x * blockDim.x + threadIdx.x) / WAVE;
   const uint32_t nwaves = gridDim.x * blockDim.x / WAVE;
-  for (uint32_t k = wave; k < g.n_kept; k += nwaves) {
+  const uint32_t n = g.list ? *g.list_count : g.n_kept;
+  for (uint32_t w = wave; w < n; w += nwaves) {
+    const uint32_t k = g.list ? g.list[w] : w;
     const uint64_t eo = g.e_off[k];
     const uint32_t len = g.e_len[k];
     for (uint32_t i0 = g.rate ? 1 : 0; i0 < len; i0 += WAVE) {
