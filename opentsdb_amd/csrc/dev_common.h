@@ -54,14 +54,35 @@ DEVI uint64_t dpp_u64(uint64_t x) {
   const uint32_t hi = dpp_u32<CTRL, ROWMASK>((uint32_t)(x >> 32));
   return ((uint64_t)hi << 32) | lo;
 }
+// 64-bit inclusive wave scan: each DPP step is one add-with-carry pair
+// (lanes whose DPP source is out of range, or whose row is masked off, keep
+// their value: bound_ctrl off, so neither half is written there).
 DEVI uint64_t wave_incl_scan_u64_dpp(uint64_t x) {
-  x += dpp_u64<0x111, 0xf>(x);
-  x += dpp_u64<0x112, 0xf>(x);
-  x += dpp_u64<0x114, 0xf>(x);
-  x += dpp_u64<0x118, 0xf>(x);
-  x += dpp_u64<0x142, 0xa>(x);
-  x += dpp_u64<0x143, 0xc>(x);
-  return x;
+  uint32_t lo = (uint32_t)x, hi = (uint32_t)(x >> 32);
+  asm volatile(
+      "s_nop 1\n"
+      "v_add_co_u32_dpp %0, vcc, %0, %0 row_shr:1 row_mask:0xf bank_mask:0xf\n"
+      "v_addc_co_u32_dpp %1, vcc, %1, %1, vcc row_shr:1 row_mask:0xf bank_mask:0xf\n"
+      "s_nop 1\n"
+      "v_add_co_u32_dpp %0, vcc, %0, %0 row_shr:2 row_mask:0xf bank_mask:0xf\n"
+      "v_addc_co_u32_dpp %1, vcc, %1, %1, vcc row_shr:2 row_mask:0xf bank_mask:0xf\n"
+      "s_nop 1\n"
+      "v_add_co_u32_dpp %0, vcc, %0, %0 row_shr:4 row_mask:0xf bank_mask:0xf\n"
+      "v_addc_co_u32_dpp %1, vcc, %1, %1, vcc row_shr:4 row_mask:0xf bank_mask:0xf\n"
+      "s_nop 1\n"
+      "v_add_co_u32_dpp %0, vcc, %0, %0 row_shr:8 row_mask:0xf bank_mask:0xf\n"
+      "v_addc_co_u32_dpp %1, vcc, %1, %1, vcc row_shr:8 row_mask:0xf bank_mask:0xf\n"
+      "s_nop 1\n"
+      "v_add_co_u32_dpp %0, vcc, %0, %0 row_bcast:15 row_mask:0xa bank_mask:0xf\n"
+      "v_addc_co_u32_dpp %1, vcc, %1, %1, vcc row_bcast:15 row_mask:0xa bank_mask:0xf\n"
+      "s_nop 1\n"
+      "v_add_co_u32_dpp %0, vcc, %0, %0 row_bcast:31 row_mask:0xc bank_mask:0xf\n"
+      "v_addc_co_u32_dpp %1, vcc, %1, %1, vcc row_bcast:31 row_mask:0xc bank_mask:0xf\n"
+      "s_nop 1\n"
+      : "+v"(lo), "+v"(hi)
+      :
+      : "vcc");
+  return ((uint64_t)hi << 32) | lo;
 }
 
 // floor(a / n) for u64 a, u32 n > 0 — the general case, out of line.

@@ -375,8 +375,10 @@ __global__ void __launch_bounds__(256) k_ds_spans(DecodeArgs a, SpanDsArgs g, co
     const uint64_t r0 = ufl64(a.span_row_start[s]), r1 = ufl64(a.span_row_start[s + 1]);
     const uint32_t n = ufl(a.sp_ncells[s]);
     bool ok = a.sp_q1[s] < 0 && a.sp_ovf_cell[s] < 0 && n > 0 && r1 > r0 && a.interval > 0;
-    for (uint64_t r = r0 + lane; ok && r < r1 + lane; r += WAVE)
-      ok &= ballot(r < r1 && (a.row_ok[r] == 0 || ncells[r] == 0)) == 0;
+    for (uint64_t rb = r0; ok && rb < r1; rb += WAVE) {  // (uniform loop: keeps `ok` scalar)
+      const uint64_t r = rb + lane;
+      ok = ballot(r < r1 && (a.row_ok[r] == 0 || ncells[r] == 0)) == 0;
+    }
     // value width of the span's rows (all must match and be aligned)
     uint32_t W = 0;
     if (ok) {
