@@ -468,7 +468,13 @@ static int spangroup_run(tsdbhip_ctx* ctx, const tsdbhip_sg_desc* d, tsdbhip_sg_
     a.row_ok = row_ok; a.row_cell0 = row_cell0; a.sp_ncells = sp_ncells; a.sp_first = sp_first;
     a.sp_last = sp_last; a.sp_kept = sp_kept; a.sp_cap = sp_cap; a.sp_q1 = sp_q1;
     a.sp_q1_shift = sp_q1s; a.sp_ovf_cell = sp_ovf; a.err = &sm->err;
-    if (S) hipLaunchKernelGGL(k_assemble, dim3(grid_for(S, 4, 65536)), dim3(256), 0, st, a);
+    if (S) {  // thread per span, then a wave per span for the ones it queued
+      uint32_t* alist = scratch<uint32_t>(ctx, "asm_list", S);
+      uint32_t* acount = scratch<uint32_t>(ctx, "asm_count", 1, true);
+      hipLaunchKernelGGL(k_assemble_fast, dim3(grid_for(S, 256)), dim3(256), 0, st, a, alist, acount);
+      hipLaunchKernelGGL(k_assemble, dim3(grid_for(S, 4, 4096)), dim3(256), 0, st, a, (const uint32_t*)alist,
+                         (const uint32_t*)acount);
+    }
   }
   uint64_t* kflag = scratch<uint64_t>(ctx, "kflag", S);
   uint64_t* kidx = scratch<uint64_t>(ctx, "kidx", S);
@@ -479,7 +485,7 @@ static int spangroup_run(tsdbhip_ctx* ctx, const tsdbhip_sg_desc* d, tsdbhip_sg_
     hipLaunchKernelGGL(k_kept_flags, dim3(grid_for(S, 256)), dim3(256), 0, st, sp_kept, kflag, S);
     dscan_u64(ctx, kflag, kidx, S, &sm->n_kept, "k");
     dscan_u64(ctx, sp_cap, eoff_s, S, &sm->e_total, "e");
-    hipLaunchKernelGGL(k_kept_scatter, dim3(grid_for(S, 256)), dim3(256), 0, st, sp_kept, kidx, eoff_s,
+    hipLaunchKernelGGL(k_kept_scatter, dim3(grid_for(S, 256, 1024)), dim3(256), 0, st, sp_kept, kidx, eoff_s,
                        sp_ncells, S, kept, eoff, &sm->n_input, sp_first, sp_last, sm->bound);
   }
   Small h;
@@ -575,7 +581,7 @@ static int spangroup_run(tsdbhip_ctx* ctx, const tsdbhip_sg_desc* d, tsdbhip_sg_
     }
   }
   HIPCHK(hipEventRecord(ctx->ev[2], st));
-  if (n_kept) hipLaunchKernelGGL(k_span_summary, dim3(grid_for(n_kept, 256)), dim3(256), 0, st, da);
+  if (n_kept) hipLaunchKernelGGL(k_span_summary, dim3(grid_for(n_kept, 256, 1024)), dim3(256), 0, st, da);
   readback(ctx, &h, sm, sizeof h);  // sync 2
   if (h.err) throw Fail{h.err};
 

@@ -210,6 +210,25 @@ DEVI int64_t wave_max_i64(int64_t x) {
   return x;
 }
 
+// Block-level (256 threads) combine of one 64-bit value per thread; the
+// result is valid in thread 0. Few atomics per launch: same-address atomics
+// serialise at one L2 channel (~10 ns each).
+template <typename T, typename F>
+DEVI T block_reduce_256(T x, F op, T* sh /* [4] */) {
+#pragma unroll
+  for (int m = 1; m < 64; m <<= 1) {
+    T y;
+    if (sizeof(T) == 8) y = (T)shfl_xor_u64((uint64_t)x, m);
+    else y = (T)__shfl_xor((int)x, m);
+    x = op(x, y);
+  }
+  __syncthreads();
+  if (lane_id() == 0) sh[threadIdx.x / 64] = x;
+  __syncthreads();
+  if (threadIdx.x == 0) x = op(op(sh[0], sh[1]), op(sh[2], sh[3]));
+  return x;
+}
+
 // ---- big-endian cell decoding (org.hbase.async.Bytes, restated) -----------
 DEVI uint32_t bswap32(uint32_t x) { return __builtin_bswap32(x); }
 DEVI uint64_t bswap64(uint64_t x) { return __builtin_bswap64(x); }

@@ -169,11 +169,91 @@ __device__ void assemble_slow(const AssembleArgs& a, uint32_t s, uint64_t r0, ui
   }
 }
 
-__global__ void __launch_bounds__(256) k_assemble(AssembleArgs a) {
+// S7 keep rule and the span's E capacity (lane 0 / the span's thread).
+DEVI void assemble_finish(const AssembleArgs& a, uint32_t s, bool has_rows) {
+  const uint32_t n = a.sp_ncells[s];
+  const int64_t f = a.sp_first[s], l = a.sp_last[s];
+  if (has_rows && n == 0) set_err(a.err, -3 /*E_EMPTY_SPAN*/);
+  const bool kept = n > 0 && f <= a.end && l >= a.start;  // SpanGroup.java:135-139
+  a.sp_kept[s] = kept;
+  uint64_t cap = 0;
+  if (kept) {
+    cap = n;
+    if (a.interval > 0) {
+      const int64_t lo = f > a.start ? f : a.start;
+      const uint64_t b = (uint64_t)((l - lo) / a.interval) + 1;
+      cap = b < cap ? b : cap;
+    }
+  }
+  a.sp_cap[s] = cap;
+}
+
+// One thread per span: the common case (at most ASM_ROWS rows, each starting
+// after the previous one ended with no RowSeq merge possible, no seek inside
+// the first row) written directly; every other span is queued for the
+// wave-per-span kernel below.
+constexpr uint32_t ASM_ROWS = 64;
+__global__ void __launch_bounds__(256) k_assemble_fast(AssembleArgs a, uint32_t* list, uint32_t* count) {
+  const uint32_t s = blockIdx.x * blockDim.x + threadIdx.x;
+  bool defer = false;
+  if (s < a.n_spans) {
+    const uint64_t r0 = a.span_row_start[s], r1 = a.span_row_start[s + 1];
+    bool ok = r1 > r0 && r1 - r0 <= ASM_ROWS;
+    int64_t pb = -1, pl = -1, first_ts = 0;
+    uint32_t cell = 0;
+    for (uint64_t r = r0; ok && r < r1; r++) {
+      const uint32_t n = a.row_ncells[r];
+      if (n == 0 || row_value_bytes(a, r) >= 32768u) { ok = false; break; }
+      const int64_t base = a.row_base[r], first = row_first_ts(a, r), last = row_last_ts(a, r);
+      if (pb >= 0 && (base <= pb || first <= pl || last - pb < 4096)) { ok = false; break; }
+      if (r == r0) {
+        if (first < a.start) { ok = false; break; }  // Q1 seek inside the row
+        first_ts = first;
+      }
+      pb = base;
+      pl = last;
+      cell += n;
+    }
+    if (ok) {
+      uint32_t c = 0;
+      for (uint64_t r = r0; r < r1; r++) {  // (second pass: rows written only after the checks)
+        a.row_ok[r] = 2;
+        a.row_cell0[r] = c;
+        c += a.row_ncells[r];
+      }
+      a.sp_ncells[s] = cell;
+      a.sp_first[s] = first_ts;
+      a.sp_last[s] = pl;
+      a.sp_ovf_cell[s] = -1;
+      a.sp_q1[s] = -1;
+      a.sp_q1_shift[s] = 0;
+      assemble_finish(a, s, true);
+    } else {
+      defer = true;
+    }
+  }
+  // queue the deferred spans (one atomic per wave)
+  const uint64_t m = ballot(defer);
+  if (m) {
+    uint32_t base = 0;
+    if (lane_id() == __ffsll((long long)m) - 1) base = atomicAdd(count, (uint32_t)__popcll(m));
+    base = __shfl(base, __ffsll((long long)m) - 1);
+    if (defer) list[base + __popcll(m & lanemask_lt(lane_id()))] = s;
+  }
+}
+
+// One wave per span (of `list`, or of all spans when list is null). The
+// common case (rows in strictly increasing base order, each row starting
+// after the previous one ended, no RowSeq merge possible) is verified
+// wave-parallel; anything else falls back to an exact sequential walk by
+// lane 0 (the reference's own algorithm, O(rows)).
+__global__ void __launch_bounds__(256) k_assemble(AssembleArgs a, const uint32_t* list, const uint32_t* count) {
   const int lane = lane_id();
   const uint32_t wave = (blockIdx.x * blockDim.x + threadIdx.x) / WAVE;
   const uint32_t nwaves = gridDim.x * blockDim.x / WAVE;
-  for (uint32_t s = wave; s < a.n_spans; s += nwaves) {
+  const uint32_t nw = list ? *count : a.n_spans;
+  for (uint32_t w = wave; w < nw; w += nwaves) {
+    const uint32_t s = list ? list[w] : w;
     const uint64_t r0 = a.span_row_start[s], r1 = a.span_row_start[s + 1];
     bool ok = r1 > r0;
     int64_t prev_last = -1, prev_base = -1;
@@ -222,21 +302,7 @@ __global__ void __launch_bounds__(256) k_assemble(AssembleArgs a) {
     }
     if (lane == 0) {
       __threadfence_block();
-      const uint32_t n = a.sp_ncells[s];
-      const int64_t f = a.sp_first[s], l = a.sp_last[s];
-      if (r1 > r0 && n == 0) set_err(a.err, -3 /*E_EMPTY_SPAN*/);
-      const bool kept = n > 0 && f <= a.end && l >= a.start;  // SpanGroup.java:135-139
-      a.sp_kept[s] = kept;
-      uint64_t cap = 0;
-      if (kept) {
-        cap = n;
-        if (a.interval > 0) {
-          const int64_t lo = f > a.start ? f : a.start;
-          const uint64_t b = (uint64_t)((l - lo) / a.interval) + 1;
-          cap = b < cap ? b : cap;
-        }
-      }
-      a.sp_cap[s] = cap;
+      assemble_finish(a, s, r1 > r0);
     }
   }
 }

@@ -415,33 +415,34 @@ __global__ void __launch_bounds__(256) k_decode_ds(DecodeArgs a) {
 }
 
 // Per-span summary of E after decode: grid range, F* (float first points).
-// One atomic per wave and field.
+// Grid-stride, one atomic per block and field.
 __global__ void __launch_bounds__(256) k_span_summary(DecodeArgs a) {
-  const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
-  int64_t lo = INT64_MAX, hi = INT64_MIN, fs = 0;
-  bool empty = false;
-  if (k < a.n_kept) {
+  __shared__ int64_t sh_lo[4], sh_hi[4], sh_fs[4], sh_e[4];
+  int64_t lo = INT64_MAX, hi = INT64_MIN, fs = 0, empty = 0;
+  for (uint32_t k = blockIdx.x * blockDim.x + threadIdx.x; k < a.n_kept; k += gridDim.x * blockDim.x) {
     const uint32_t len = a.e_len[k];
     const uint64_t eo = a.e_off[k];
     if (len == 0) {
-      empty = true;
-    } else {
-      const int64_t first = a.e_ts[eo];
-      if (a.rate) {
-        if (len >= 2) lo = a.e_ts[eo + 1];
-      } else {
-        lo = first;
-        if (a.e_flt[eo]) fs = first + 1;  // +1: 0 = none
-      }
-      hi = a.e_ts[eo + len - 1];
+      empty = 1;
+      continue;
     }
+    const int64_t first = a.e_ts[eo];
+    if (a.rate) {
+      if (len >= 2) lo = min(lo, (int64_t)a.e_ts[eo + 1]);
+    } else {
+      lo = min(lo, first);
+      if (a.e_flt[eo]) fs = max(fs, first + 1);  // +1: 0 = none
+    }
+    hi = max(hi, (int64_t)a.e_ts[eo + len - 1]);
   }
-  lo = wave_min_i64(lo);
-  hi = wave_max_i64(hi);
-  fs = wave_max_i64(fs);
-  const bool any_empty = ballot(empty) != 0;
-  if (lane_id() == 0) {
-    if (any_empty) atomicMin(a.err, -3 /*E_EMPTY_SPAN*/);
+  auto mn = [](int64_t x, int64_t y) { return min(x, y); };
+  auto mx = [](int64_t x, int64_t y) { return max(x, y); };
+  lo = block_reduce_256(lo, mn, sh_lo);
+  hi = block_reduce_256(hi, mx, sh_hi);
+  fs = block_reduce_256(fs, mx, sh_fs);
+  empty = block_reduce_256(empty, mx, sh_e);
+  if (threadIdx.x == 0) {
+    if (empty) atomicMin(a.err, -3 /*E_EMPTY_SPAN*/);
     if (lo != INT64_MAX) atomicMin(&a.range[0], (unsigned long long)lo);
     if (hi != INT64_MIN) atomicMax(&a.range[1], (unsigned long long)hi);
     if (fs) atomicMax(a.fstar, (unsigned long long)fs);

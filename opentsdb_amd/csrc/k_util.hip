@@ -68,29 +68,31 @@ __global__ void k_kept_flags(const uint8_t* kept, uint64_t* kflag, uint32_t n) {
   const uint32_t s = blockIdx.x * blockDim.x + threadIdx.x;
   if (s < n) kflag[s] = kept[s];
 }
-// Kept-span list, E offsets, and (one atomic per wave) SpanGroup.aggregatedSize
-// and the [min first, max last] ts bounds of the kept spans.
+// Kept-span list, E offsets, and (one atomic per block, grid-stride)
+// SpanGroup.aggregatedSize and the [min first, max last] ts bounds of the
+// kept spans.
 __global__ void __launch_bounds__(256) k_kept_scatter(const uint8_t* kept, const uint64_t* kidx,
                                                       const uint64_t* eoff_s, const uint32_t* ncells, uint32_t n,
                                                       uint32_t* kept_list, uint64_t* eoff_k,
                                                       unsigned long long* n_input, const int64_t* sp_first,
                                                       const int64_t* sp_last, unsigned long long* bound) {
-  const uint32_t s = blockIdx.x * blockDim.x + threadIdx.x;
-  const bool k_ = s < n && kept[s];
+  __shared__ uint64_t sh_c[4];
+  __shared__ int64_t sh_f[4], sh_l[4];
   uint64_t cnt = 0;
   int64_t f = INT64_MAX, l = INT64_MIN;
-  if (k_) {
+  for (uint32_t s = blockIdx.x * blockDim.x + threadIdx.x; s < n; s += gridDim.x * blockDim.x) {
+    if (!kept[s]) continue;
     const uint64_t k = kidx[s];
     kept_list[k] = s;
     eoff_k[k] = eoff_s[s];
-    cnt = ncells[s];
-    f = sp_first[s];
-    l = sp_last[s];
+    cnt += ncells[s];
+    f = min(f, sp_first[s]);
+    l = max(l, sp_last[s]);
   }
-  cnt = wave_sum_u64(cnt);
-  f = wave_min_i64(f);
-  l = wave_max_i64(l);
-  if (lane_id() == 0 && cnt) {
+  cnt = block_reduce_256(cnt, [](uint64_t x, uint64_t y) { return x + y; }, sh_c);
+  f = block_reduce_256(f, [](int64_t x, int64_t y) { return min(x, y); }, sh_f);
+  l = block_reduce_256(l, [](int64_t x, int64_t y) { return max(x, y); }, sh_l);
+  if (threadIdx.x == 0 && cnt) {
     atomicAdd(n_input, (unsigned long long)cnt);
     atomicMin(&bound[0], (unsigned long long)f);
     atomicMax(&bound[1], (unsigned long long)l);
