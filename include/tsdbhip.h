@@ -74,7 +74,7 @@ extern "C" {
 
 /* tsdbhip_timing.hot_kernel */
 #define TSDBHIP_HOT_NONE        0
-#define TSDBHIP_HOT_DS_CHUNKS   1 /* chunk-parallel decode + downsample     */
+#define TSDBHIP_HOT_DS_CHUNKS   1 /* k_ds_spans: streaming decode+downsample */
 #define TSDBHIP_HOT_DECODE_FAST 2 /* streaming per-span decode(+downsample) */
 #define TSDBHIP_HOT_DECODE_GEN  3 /* general per-span decode(+downsample)   */
 #define TSDBHIP_HOT_COMPACT     4 /* k_compact_tiles: classification + single/trivial/short complex

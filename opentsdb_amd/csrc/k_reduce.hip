@@ -208,14 +208,18 @@ __global__ void __launch_bounds__(256) k_reduce(ReduceArgs r) {
     const int64_t t_last = (int64_t)r.grid[g0 + nvalid - 1];
     Acc acc;
     acc_init(acc);
-    for (uint32_t k = k0; k < k1; k++) {
-      const uint64_t eo = r.e_off[k];
-      const uint32_t len = r.e_len[k];
+    // Spans in order, 64 at a time: their E offsets/lengths come in with one
+    // load per lane. A span whose E holds exactly this tile's grid points
+    // (E[g0 .. g0+n) == G[g0 .. g0+n): aligned series) needs no bracket
+    // search and no lerp: lane l takes E[g0 + l]; runs of such spans load
+    // their values up to 8 spans ahead. Every other span takes the general
+    // path (cursor, grid ranks, lerp / rate).
+    auto general = [&](uint32_t k, uint64_t eo, uint32_t len) {
       const int64_t first = r.e_ts[eo], last = r.e_ts[eo + len - 1];
       if (RATE) {
-        if (len < 2 || last < t_first) continue;
+        if (len < 2 || last < t_first) return;
       } else {
-        if (first > t_last || last < t_first) continue;  // not started (F*) / expired
+        if (first > t_last || last < t_first) return;  // not started (F*) / expired
       }
       const uint32_t j = ptr[k - k0];
       const uint32_t idx = j + lane;
@@ -238,24 +242,24 @@ __global__ void __launch_bounds__(256) k_reduce(ReduceArgs r) {
       const int64_t cur = (int64_t)j + cl - 1;
       // bracket timestamps: inside the tile they are this wave's loaded points
       const int64_t ts_in = (int64_t)shfl_u64((uint64_t)pts, cl > 0 ? cl - 1 : 0);
-      if (!gv) continue;
+      if (!gv) return;
       if (RATE) {
-        if (tl > last) continue;
+        if (tl > last) return;
         const int64_t xc = cl > 0 ? ts_in : (int64_t)r.e_ts[eo + cur];
         const double yc = to_double(r.e_val[eo + cur], r.e_flt[eo + cur] != 0);
         double yp = 0.0;
         int64_t xp = 0;
         if (cur >= 1) { xp = r.e_ts[eo + cur - 1]; yp = to_double(r.e_val[eo + cur - 1], r.e_flt[eo + cur - 1] != 0); }
         acc_push<AGG, MODE>(acc, 0, (yc - yp) / (double)(xc - xp));
-        continue;
+        return;
       }
       if (cur < 0) {  // not started: next slot holds e_0
         if (MODE == MODE_DUAL && r.e_flt[eo]) acc.flag |= 1u;
-        continue;
+        return;
       }
       const int64_t xc = cl > 0 ? ts_in : (int64_t)r.e_ts[eo + cur];
       const bool active = (uint32_t)cur < len - 1 || xc == tl;
-      if (!active) continue;  // expired: nothing in either slot
+      if (!active) return;  // expired: nothing in either slot
       const int64_t vc = r.e_val[eo + cur];
       bool fc = false, fn = false;
       if (MODE == MODE_DUAL) {
@@ -275,6 +279,42 @@ __global__ void __launch_bounds__(256) k_reduce(ReduceArgs r) {
           yd = lerp_double(tl, xc, to_double(vc, MODE == MODE_DBL || fc), xn,
                            to_double(vn, MODE == MODE_DBL || fn));
         acc_push<AGG, MODE>(acc, yi, yd);
+      }
+    };
+    constexpr bool ALIGNED_OK = !RATE && MODE != MODE_DUAL;
+    for (uint32_t kb = k0; kb < k1; kb += WAVE) {
+      const uint32_t kl = kb + lane;
+      const bool kv = kl < k1;
+      const uint64_t eo_l = kv ? r.e_off[kl] : 0;
+      const uint32_t len_l = kv ? r.e_len[kl] : 0;
+      uint64_t almask = 0;
+      if (ALIGNED_OK) {
+        const bool al = kv && (uint64_t)len_l >= g0 + (uint64_t)nvalid &&
+                        (int64_t)r.e_ts[eo_l + g0] == t_first && (int64_t)r.e_ts[eo_l + g0 + nvalid - 1] == t_last;
+        almask = ballot(al);
+      }
+      const uint32_t nb = min((uint32_t)WAVE, k1 - kb);
+      for (uint32_t i = 0; i < nb;) {
+        if (ALIGNED_OK && ((almask >> i) & 1)) {
+          const uint64_t m = almask >> i;  // bit 0: span kb + i
+          const uint32_t run = min(8u, ~m == 0 ? 64u : (uint32_t)__builtin_ctzll(~m));
+          int64_t v[8];
+#pragma unroll
+          for (uint32_t u = 0; u < 8; u++) {
+            const uint64_t eo_u = readlane_u64(eo_l, (int)min(i + u, 63u));
+            v[u] = (u < run && gv) ? r.e_val[eo_u + g0 + lane] : 0;
+          }
+#pragma unroll
+          for (uint32_t u = 0; u < 8; u++) {
+            if (u >= run) break;
+            if (gv) acc_push<AGG, MODE>(acc, v[u], MODE == MODE_INT ? 0.0 : to_double(v[u], true));
+            if (lane == 0) ptr[kb + i + u - k0] = (uint32_t)(g0 + nvalid);
+          }
+          i += run;
+          continue;
+        }
+        general(kb + i, readlane_u64(eo_l, (int)i), readlane_u32(len_l, (int)i));
+        i++;
       }
     }
     if (gv) acc_store<AGG, MODE>(r, (uint64_t)chunk * r.T + g, acc);
