@@ -264,6 +264,38 @@ def bench_c5(args):
     ctx.close()
 
 
+def shard_ranges(n_series, world):
+    """Contiguous span ranges, one per rank, span (TreeMap) order preserved."""
+    return [(n_series * r // world, n_series * (r + 1) // world) for r in range(world)]
+
+
+def timed_loop(step_once, sync, barrier, steps, warmup, after_step=None):
+    """W untimed steps, then exactly K steps bracketed by barrier + device
+    sync on both sides; returns this rank's elapsed seconds."""
+    for _ in range(warmup):
+        step_once()
+    barrier()
+    sync()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        step_once()
+        if after_step:
+            after_step()
+    sync()
+    elapsed = time.perf_counter() - t0
+    barrier()
+    return elapsed
+
+
+def max_over_ranks(dist, x):
+    if dist is None:
+        return x
+    import torch as _t
+    t = _t.tensor([x], dtype=_t.float64)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item())
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -276,6 +308,9 @@ def main():
     ap.add_argument("--exact", action="store_true", help="TSDBHIP_EXACT_ORDER")
     ap.add_argument("--c5-mix", default="c5", choices=["c5", "plain", "nocomplex"],
                     help="C5 row mix (diagnostics; the C5 line is 'c5')")
+    ap.add_argument("--dry-run", action="store_true",
+                    help="harness check without a GPU: the multi-rank timing/barrier/report path with a "
+                         "no-op step (its value is meaningless and says so)")
     args = ap.parse_args()
     if args.config == "c5":
         return bench_c5(args)
@@ -284,9 +319,27 @@ def main():
     n_series, n_points, step, kind, agg, dsi, dsa, desc_txt = CONFIGS[args.config]
     if args.series:
         n_series = args.series
-    lo = n_series * rank // world
-    hi = n_series * (rank + 1) // world
+    shards = shard_ranges(n_series, world)
+    lo, hi = shards[rank]
 
+    def barrier():
+        if dist is not None:
+            dist.barrier()
+
+    if args.dry_run:
+        elapsed = max_over_ranks(dist, timed_loop(lambda: time.sleep(0.001), lambda: None, barrier,
+                                                   args.steps, args.warmup))
+        if rank == 0:
+            print(json.dumps({"metric": METRIC, "value": n_series * n_points / (elapsed / args.steps),
+                              "unit": "input points/s", "n_gpus": world, "steps": args.steps,
+                              "warmup": args.warmup, "ms_per_step": elapsed / args.steps * 1e3,
+                              "dry_run": True, "config": {"workload": desc_txt, "shards": shards}}), flush=True)
+        if dist is not None:
+            dist.destroy_process_group()
+        return
+
+    import torch
+    torch.cuda.set_device(local_rank)
     ctx = Context(local_rank)
     L = lib()
     if world > 1:
@@ -315,31 +368,17 @@ def main():
     def step_once():
         ctx.check(L.tsdbhip_spangroup_run(ctx.handle, C.byref(d), C.byref(out)))
 
-    def barrier():
-        if dist is not None:
-            dist.barrier()
+    hot_ms, total_ms, hot_kernel = [], [], [0]
 
-    for _ in range(args.warmup):
-        step_once()
-    import torch
-    barrier()
-    torch.cuda.synchronize()
-    hot_ms, total_ms, hot_kernel = [], [], 0
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        step_once()
+    def record():
         tm = ctx.timing()
         hot_ms.append(tm.hot_ms)
         total_ms.append(tm.total_ms)
-        hot_kernel = tm.hot_kernel
-    torch.cuda.synchronize()
-    elapsed = time.perf_counter() - t0
-    barrier()
-    if dist is not None:
-        import torch as _t
-        x = _t.tensor([elapsed], dtype=_t.float64)
-        dist.all_reduce(x, op=dist.ReduceOp.MAX)
-        elapsed = float(x.item())
+        hot_kernel[0] = tm.hot_kernel
+
+    elapsed = max_over_ranks(dist, timed_loop(step_once, torch.cuda.synchronize, barrier, args.steps,
+                                              args.warmup, record))
+    hot_kernel = hot_kernel[0]
     n_input = int(out.n_input_points)  # global (allreduced when sharded)
     ms_step = elapsed / args.steps * 1e3
     value = n_input / (elapsed / args.steps)
@@ -373,6 +412,7 @@ def main():
                 "downsample": f"{dsi}s-{['sum', 'min', 'max', 'avg', 'dev'][dsa]}" if dsi else "none",
                 "parallelism": f"series-sharded x{world} (RCCL exchange of per-t partials)" if world > 1
                                else "single GPU",
+                "shards": shards,
             },
             "roofline": {
                 "bound": "hbm",

@@ -12,7 +12,7 @@ import subprocess
 from . import _abi
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "libtsdbhip.so")
+LIB_PATH = os.environ.get("TSDBHIP_LIB") or os.path.join(HERE, "libtsdbhip.so")  # (override: A/B builds)
 CSRC = os.path.join(HERE, "csrc")
 
 _LIB = None

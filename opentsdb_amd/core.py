@@ -125,7 +125,7 @@ class Span:
 
 
 def run_spanset(ctx, spanset: SpanSet, start, end, agg, rate=False, ds_interval=0, ds_agg=0,
-                exact=False, capacity=None, device_desc=None):
+                exact=False, capacity=None, device_desc=None, sharded=False):
     """Low-level: one tsdbhip_spangroup_run. Returns (code, ts, is_int, bits,
     n_input_points, err_index)."""
     desc = _abi.SgDesc()
@@ -139,6 +139,8 @@ def run_spanset(ctx, spanset: SpanSet, start, end, agg, rate=False, ds_interval=
     desc.ds_interval = int(ds_interval)
     if exact:
         desc.flags |= _abi.EXACT_ORDER
+    if sharded:  # this rank's shard; exchange over the ctx communicator
+        desc.flags |= _abi.SHARDED
     cap = capacity
     if cap is None:
         cap = max(1, spanset.n_cells()) if spanset is not None else 1 << 20

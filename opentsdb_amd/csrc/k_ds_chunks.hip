@@ -53,6 +53,7 @@ struct RawW {
 // to 3 cells past the row end (inside the buffers' 64-byte slack).
 template <int W>
 DEVI void load_raw(const DecodeArgs& a, uint64_t qoff, uint64_t voff, uint32_t c, RawW<W>& x) {
+  // (plain loads: non-temporal ones measured 15 % slower on this stream)
   x.q = *(const uint2*)(a.qual + qoff + 2ull * c);
   const uint4* pv = (const uint4*)(a.val + voff + (uint64_t)W * c);
 #pragma unroll

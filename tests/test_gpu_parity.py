@@ -247,6 +247,12 @@ def test_empty_and_disjoint(ctx):
     ss = packing.pack_spans([])
     g, o = run_both(ctx, ss)
     assert_same(g, o)
+    # a span without rows: Span.timestamp(0) throws in SpanGroup.add
+    ss = packing.pack_spans([I([(T + 1, 1), (T + 2, 2)])])
+    ss.span_row_start = np.array([0, 1, 1], np.uint64)
+    g, o = run_both(ctx, ss)
+    assert o.code == _abi.E_EMPTY_SPAN
+    assert_same(g, o)
 
 
 def test_single_point_rate(ctx):
