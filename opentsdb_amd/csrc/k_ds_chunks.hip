@@ -13,9 +13,9 @@
 // cells, or a first cell before `start` send the whole span to the serial
 // kernels (k_decode_fast, then k_decode.hip), which rewrite its E.
 //
-// The row streams through in 256-cell chunks (4 cells per lane: one 8-B
-// qualifier load and one or two 16-B value loads), two chunks of loads in
-// flight. Per chunk, DPP wave scans build ts-delta and value prefixes in LDS;
+// The row streams through in 512-cell chunks (8 consecutive cells per lane:
+// one 16-B qualifier load and two or four 16-B value loads), the next chunk's
+// loads in flight while one is processed. Per chunk, DPP wave scans build ts-delta and value prefixes in LDS;
 // lane j owns the chunk's j-th head, and a bucket's count / ts sum / integer
 // sum are prefix differences (exact in any order). The bucket still open at
 // the end of a chunk (or row) is carried in registers and completed by the
@@ -43,21 +43,24 @@ struct SpanDsArgs {
   int32_t rate;
 };
 
+constexpr uint32_t DCH = 512;  // cells per chunk: 8 per lane
+
 template <int W>
 struct RawW {
-  uint2 q;             // 4 big-endian qualifiers
-  uint4 v[W / 4];      // 4 values
+  uint4 q;              // 8 big-endian qualifiers
+  uint4 v[2 * W / 4];   // 8 values
 };
 
-// Branch-free chunk load; c is clamped into the row by the caller. Reads up
-// to 3 cells past the row end (inside the buffers' 64-byte slack).
+// Branch-free chunk load of 8 consecutive cells per lane; c is clamped into
+// the row by the caller. Reads up to 7 cells past the row end (inside the
+// buffers' 64-byte slack). Lanes read 16 B of qualifiers and 8W bytes of
+// values each (plain loads: non-temporal ones measured 15 % slower).
 template <int W>
 DEVI void load_raw(const DecodeArgs& a, uint64_t qoff, uint64_t voff, uint32_t c, RawW<W>& x) {
-  // (plain loads: non-temporal ones measured 15 % slower on this stream)
-  x.q = *(const uint2*)(a.qual + qoff + 2ull * c);
+  x.q = *(const uint4*)(a.qual + qoff + 2ull * c);
   const uint4* pv = (const uint4*)(a.val + voff + (uint64_t)W * c);
 #pragma unroll
-  for (int i = 0; i < W / 4; i++) x.v[i] = pv[i];
+  for (int i = 0; i < 2 * W / 4; i++) x.v[i] = pv[i];
 }
 
 template <int W>
@@ -67,8 +70,9 @@ DEVI int64_t raw_value(const RawW<W>& x, int j) {
     const uint32_t lo = (j & 1) ? u.z : u.x, hi = (j & 1) ? u.w : u.y;
     return (int64_t)bswap64((uint64_t)lo | ((uint64_t)hi << 32));
   }
-  const uint4 u = x.v[0];
-  const uint32_t w = j == 0 ? u.x : j == 1 ? u.y : j == 2 ? u.z : u.w;
+  const uint4 u = x.v[j >> 2];
+  const int k = j & 3;
+  const uint32_t w = k == 0 ? u.x : k == 1 ? u.y : k == 2 ? u.z : u.w;
   return (int64_t)(int32_t)bswap32(w);
 }
 
@@ -95,8 +99,8 @@ struct DsState {
 // Closed buckets wait in a per-wave LDS buffer (count, ts offsets, value)
 // and leave it in batches, one lane per bucket, so the divisions of
 // Span.java:399 and the avg downsampler stay out of the chunk loop. A chunk
-// closes at most 256/kk + 2 <= 66 buckets (kk >= 4).
-constexpr uint32_t BKB = 80;
+// closes at most 512/kk + 2 <= 130 buckets (kk >= 4).
+constexpr uint32_t BKB = 136;
 struct BkLds {
   uint32_t ref[BKB];  // head ts
   uint32_t n[BKB];    // cells
@@ -140,89 +144,103 @@ DEVI int64_t ds_combine(int64_t x, int64_t y) {
   return y > x ? y : x;
 }
 
-// One row of a span: its 256-cell chunks. Returns true if a precondition
+// One row of a span: its 512-cell chunks. Returns true if a precondition
 // breaks (the span then goes to the serial path).
 template <int AGG, int W>
 DEVI bool ds_row(const DecodeArgs& a, const SpanDsArgs& g, DsState& st, uint64_t eo, uint32_t cap,
-                 uint32_t n_span, uint64_t qoff, uint64_t voff, uint32_t base, uint32_t nc, uint32_t cell0,
-                 uint32_t* L_dt, uint32_t* L_pt, uint64_t* L_v, BkLds& BK) {
+                 uint64_t qoff, uint64_t voff, uint32_t base, uint32_t nc, uint32_t cell0, uint32_t* L_pt,
+                 uint64_t* L_v, BkLds& BK) {
   constexpr bool PREFIX = AGG == 0 || AGG == 3;  // sum / avg: prefix differences; min / max: loops
   const int lane = lane_id();
   const int64_t I = a.interval;
-  const uint32_t clamp_c = (nc - 1) & ~3u;
-  RawW<W> A, B, C;
+  const uint32_t clamp_c = (nc - 1) & ~7u;
+  // ts delta (from the row base) of chunk cell x: the ts prefix differenced
+  auto dtx = [&](uint32_t x) { return L_pt[x] - (x > 0 ? L_pt[x - 1] : 0u); };
+  RawW<W> A, B;
   auto issue = [&](uint32_t c0, RawW<W>& x) {
-    const uint32_t c = c0 + 4u * lane;
+    const uint32_t c = c0 + 8u * lane;
     load_raw<W>(a, qoff, voff, c < nc ? c : clamp_c, x);
   };
   issue(0, A);
-  issue(FCH, B);
+  issue(DCH, B);
   bool bad = false;
   auto step = [&](uint32_t c0, const RawW<W>& cur) {
-    const uint32_t nv = min((uint32_t)FCH, nc - c0);
+    const uint32_t nv = min(DCH, nc - c0);
     const uint32_t cs = cell0 + c0;  // span cell index of the chunk start
-    // ---- decode: 4 cells per lane (loads past the row end were clamped) ----
-    const uint32_t p01 = qpair(cur.q.x), p23 = qpair(cur.q.y);
-    uint32_t dt[4];
-    dt[0] = (p01 & 0xFFFF) >> 4;
-    dt[1] = p01 >> 20;
-    dt[2] = (p23 & 0xFFFF) >> 4;
-    dt[3] = p23 >> 20;
-    int64_t bits[4];
+    // ---- decode: 8 cells per lane (loads past the row end were clamped) ----
+    uint32_t qp[4];
+    qp[0] = qpair(cur.q.x);
+    qp[1] = qpair(cur.q.y);
+    qp[2] = qpair(cur.q.z);
+    qp[3] = qpair(cur.q.w);
+    uint32_t dt[8];
 #pragma unroll
-    for (int j = 0; j < 4; j++) bits[j] = raw_value<W>(cur, j);
+    for (int i = 0; i < 4; i++) {
+      dt[2 * i] = (qp[i] & 0xFFFF) >> 4;
+      dt[2 * i + 1] = qp[i] >> 20;
+    }
+    int64_t bits[8];
+#pragma unroll
+    for (int j = 0; j < 8; j++) bits[j] = raw_value<W>(cur, j);
     // integer cells of width W (flags nibble of each qualifier), strictly
     // increasing deltas (Span/RowSeq order)
     const uint32_t fl = (W - 1) * 0x00010001u;
-    uint32_t nmine = 4;
-    if (nv == FCH) {  // full chunk: every lane holds 4 cells
-      bad |= (((p01 ^ fl) | (p23 ^ fl)) & 0x000F000Fu) != 0;
-      bad |= dt[1] <= dt[0] || dt[2] <= dt[1] || dt[3] <= dt[2];
+    uint32_t nmine = 8;
+    if (nv == DCH) {  // full chunk: every lane holds 8 cells
+      bad |= (((qp[0] ^ fl) | (qp[1] ^ fl) | (qp[2] ^ fl) | (qp[3] ^ fl)) & 0x000F000Fu) != 0;
+#pragma unroll
+      for (int j = 1; j < 8; j++) bad |= dt[j] <= dt[j - 1];
     } else {  // the row's last chunk: mask the lanes past its end
-      nmine = nv > 4u * lane ? min(4u, nv - 4u * lane) : 0u;
-      const uint32_t fm0 = nmine >= 2 ? 0x000F000Fu : (nmine == 1 ? 0x0000000Fu : 0u);
-      const uint32_t fm1 = nmine >= 4 ? 0x000F000Fu : (nmine == 3 ? 0x0000000Fu : 0u);
-      bad |= ((p01 ^ fl) & fm0) != 0 || ((p23 ^ fl) & fm1) != 0;
-      bad |= (nmine > 1 && dt[1] <= dt[0]) || (nmine > 2 && dt[2] <= dt[1]) || (nmine > 3 && dt[3] <= dt[2]);
+      nmine = nv > 8u * lane ? min(8u, nv - 8u * lane) : 0u;
+#pragma unroll
+      for (int i = 0; i < 4; i++) {
+        const uint32_t fm = nmine >= 2u * i + 2 ? 0x000F000Fu : (nmine == 2u * i + 1 ? 0x0000000Fu : 0u);
+        bad |= ((qp[i] ^ fl) & fm) != 0;
+      }
+#pragma unroll
+      for (int j = 1; j < 8; j++) bad |= (uint32_t)j < nmine && dt[j] <= dt[j - 1];
       if (nmine == 0) dt[0] = 0;
 #pragma unroll
-      for (int j = 0; j < 4; j++) {
+      for (int j = 0; j < 8; j++) {
         if (j > 0 && (uint32_t)j >= nmine) dt[j] = dt[j - 1];  // ts prefix flat past the end
         if ((uint32_t)j >= nmine) bits[j] = 0;
       }
     }
     {
-      const uint32_t pl = shfl_up_u32(dt[3], 1);
+      const uint32_t pl = shfl_up_u32(dt[7], 1);
       bad |= lane > 0 && nmine > 0 && dt[0] <= pl;
       bad |= lane == 0 && cs > 0 && base + dt[0] <= st.prev_ts;  // previous chunk / row
     }
-    // ---- stage: ts deltas, ts prefix, value prefix (or raw values) ----
+    // ---- stage: ts prefix, value prefix (or raw values) ----
     uint32_t pt = 0;
     uint64_t pv = 0;
-    uint32_t pti[4];
-    uint64_t pvi[4];
+    uint32_t pti[8];
+    uint64_t pvi[8];
 #pragma unroll
-    for (int j = 0; j < 4; j++) {
-      pt += (uint32_t)j < nmine ? dt[j] : 0u;  // (nmine == 4 on full chunks)
+    for (int j = 0; j < 8; j++) {
+      pt += (uint32_t)j < nmine ? dt[j] : 0u;  // (nmine == 8 on full chunks)
       pv += (uint64_t)bits[j];
       pti[j] = pt;
       pvi[j] = PREFIX ? pv : (uint64_t)bits[j];
     }
     const uint32_t xt = wave_incl_scan_u32_dpp(pt) - pt;
-    *(uint4*)&L_pt[4 * lane] = make_uint4(pti[0] + xt, pti[1] + xt, pti[2] + xt, pti[3] + xt);
-    *(uint4*)&L_dt[4 * lane] = make_uint4(dt[0], dt[1], dt[2], dt[3]);
+    *(uint4*)&L_pt[8 * lane] = make_uint4(pti[0] + xt, pti[1] + xt, pti[2] + xt, pti[3] + xt);
+    *(uint4*)&L_pt[8 * lane + 4] = make_uint4(pti[4] + xt, pti[5] + xt, pti[6] + xt, pti[7] + xt);
     {
       const uint64_t xv = PREFIX ? wave_incl_scan_u64_dpp(pv) - pv : 0ull;
-      ulonglong2 v01, v23;
-      v01.x = pvi[0] + xv; v01.y = pvi[1] + xv; v23.x = pvi[2] + xv; v23.y = pvi[3] + xv;
-      *(ulonglong2*)&L_v[4 * lane] = v01;
-      *(ulonglong2*)&L_v[4 * lane + 2] = v23;
+#pragma unroll
+      for (int j = 0; j < 8; j += 2) {
+        ulonglong2 v2;
+        v2.x = pvi[j] + xv;
+        v2.y = pvi[j + 1] + xv;
+        *(ulonglong2*)&L_v[8 * lane + j] = v2;
+      }
     }
     wave_lds_sync();
     const uint32_t cend = cs + nv;
     // ---- the span's first cell opens bucket 0 ----
     if (cs == 0) {
-      st.t0 = ufl(base + L_dt[0]);
+      st.t0 = ufl(base + L_pt[0]);
       bad |= (int64_t)st.t0 < a.start;  // no seek inside the span
       st.lh_ts = st.t0;
       st.open = true;
@@ -239,15 +257,15 @@ DEVI bool ds_row(const DecodeArgs& a, const SpanDsArgs& g, DsState& st, uint64_t
       const int64_t end0 = (int64_t)st.t0 + I;
       uint64_t m = 0;
       int q = 0;
-      for (; q < 4 && !m; q++) {
+      for (; q < (int)(DCH / WAVE) && !m; q++) {
         const uint32_t c = 64u * q + lane;
-        m = ballot(c < nv && (int64_t)(base + L_dt[c]) >= end0);
+        m = ballot(c < nv && (int64_t)(base + L_pt[c] - (c > 0 ? L_pt[c - 1] : 0u)) >= end0);
       }
       if (m) {
         st.kk = cs + 64u * (q - 1) + (uint32_t)(__ffsll((long long)m) - 1);
         st.hnext = st.kk;
-        st.room = FCH / max(st.kk, 4u) + 2;
-        bad |= st.kk < 4;  // more than 64 heads per chunk: the serial kernels
+        st.room = DCH / max(st.kk, 4u) + 2;
+        bad |= st.kk < 4;  // more than 128 heads per chunk: the serial kernels
       }
     }
     // ---- room in the bucket buffer for every bucket this chunk can close ----
@@ -279,8 +297,8 @@ DEVI bool ds_row(const DecodeArgs& a, const SpanDsArgs& g, DsState& st, uint64_t
       const uint32_t kk = st.kk;
       {  // the first head closes the open bucket: prove it against the latest head
         const uint32_t la = st.hnext - cs;
-        const int64_t th = ufl(base + L_dt[la]);
-        const int64_t tp = la > 0 ? (int64_t)ufl(base + L_dt[la - 1]) : (int64_t)st.prev_ts;
+        const int64_t th = ufl(base + dtx(la));
+        const int64_t tp = la > 0 ? (int64_t)ufl(base + dtx(la - 1)) : (int64_t)st.prev_ts;
         const int64_t e = (int64_t)st.lh_ts + I;
         bad |= !(th >= e && tp < e);
         if (st.open) {
@@ -295,7 +313,7 @@ DEVI bool ds_row(const DecodeArgs& a, const SpanDsArgs& g, DsState& st, uint64_t
         }
         st.open = false;
       }
-      const uint32_t nh = min((cend - 1 - st.hnext) / max(kk, 4u) + 1, (uint32_t)WAVE);  // kk >= 4
+      const uint32_t nh = min((cend - 1 - st.hnext) / max(kk, 4u) + 1, 2u * WAVE);  // kk >= 4
       for (uint32_t jb = 0; jb < nh; jb += WAVE) {
         const uint32_t j = jb + lane;
         const bool mine = j < nh;
@@ -303,9 +321,10 @@ DEVI bool ds_row(const DecodeArgs& a, const SpanDsArgs& g, DsState& st, uint64_t
         const uint32_t la = mine ? H - cs : 0;
         const uint32_t lb = mine ? min(H + kk, cend) - 1 - cs : 0;
         const uint32_t n = lb - la + 1;
-        const uint32_t dta = L_dt[la];
+        const uint32_t pa = la > 0 ? L_pt[la - 1] : 0u;
+        const uint32_t dta = L_pt[la] - pa;
         const uint32_t ref = base + dta;
-        const uint32_t rel = (L_pt[lb] - (la > 0 ? L_pt[la - 1] : 0u)) - n * dta;
+        const uint32_t rel = (L_pt[lb] - pa) - n * dta;
         int64_t v;
         if (PREFIX) {
           v = (int64_t)(L_v[lb] - (la > 0 ? L_v[la - 1] : 0ull));
@@ -314,9 +333,10 @@ DEVI bool ds_row(const DecodeArgs& a, const SpanDsArgs& g, DsState& st, uint64_t
           for (uint32_t i = la + 1; i <= lb; i++) v = ds_combine<AGG>(v, (int64_t)L_v[i]);
         }
         if (mine && j > 0) {  // chain proof against the previous head of the chunk
-          const uint32_t e = base + L_dt[la - kk] + (uint32_t)I;
-          const uint64_t e64 = (uint64_t)(base + L_dt[la - kk]) + (uint64_t)I;
-          bad |= e64 > 0xFFFFFFFFull ? true : !(ref >= e && base + L_dt[la - 1] < e);
+          const uint32_t tprev = base + dtx(la - kk);
+          const uint64_t e64 = (uint64_t)tprev + (uint64_t)I;
+          const uint32_t e = (uint32_t)e64;
+          bad |= e64 > 0xFFFFFFFFull ? true : !(ref >= e && base + (pa - (la > 1 ? L_pt[la - 2] : 0u)) < e);
         }
         // closed buckets st.bnext + j (complete inside the chunk) -> LDS buffer
         if (mine && H + kk <= cend) {
@@ -342,19 +362,16 @@ DEVI bool ds_row(const DecodeArgs& a, const SpanDsArgs& g, DsState& st, uint64_t
       st.hnext += nh * kk;
       st.bnext += nh;
     }
-    st.prev_ts = ufl(base + L_dt[nv - 1]);
+    st.prev_ts = ufl(base + dtx(nv - 1));
     wave_lds_sync();
   };
-  // loads past the row end are clamped (cache hits); steps past it skipped
-  for (uint32_t c0 = 0; c0 < nc; c0 += 3 * FCH) {
-    issue(c0 + 2 * FCH, C);
+  // two register sets: one chunk in flight while the other is processed
+  for (uint32_t c0 = 0; c0 < nc; c0 += 2 * DCH) {
     step(c0, A);
-    issue(c0 + 3 * FCH, A);
-    if (c0 + FCH < nc) step(c0 + FCH, B);
-    issue(c0 + 4 * FCH, B);
-    if (c0 + 2 * FCH < nc) step(c0 + 2 * FCH, C);
+    issue(c0 + 2 * DCH, A);
+    if (c0 + DCH < nc) step(c0 + DCH, B);
+    issue(c0 + 3 * DCH, B);
   }
-  (void)n_span;
   return ballot(bad) != 0;
 }
 
@@ -362,9 +379,8 @@ DEVI bool ds_row(const DecodeArgs& a, const SpanDsArgs& g, DsState& st, uint64_t
 template <int AGG>
 __global__ void __launch_bounds__(256) k_ds_spans(DecodeArgs a, SpanDsArgs g, const uint32_t* ncells,
                                                   const uint32_t* vlen) {
-  __shared__ uint32_t s_dt[4][FCH];
-  __shared__ uint32_t s_pt[4][FCH];
-  __shared__ uint64_t s_v[4][FCH];
+  __shared__ uint32_t s_pt[4][DCH];
+  __shared__ uint64_t s_v[4][DCH];
   __shared__ BkLds s_bk[4];
   const int lane = lane_id();
   const int wib = threadIdx.x / WAVE;
@@ -402,10 +418,10 @@ __global__ void __launch_bounds__(256) k_ds_spans(DecodeArgs a, SpanDsArgs g, co
         ok = false;
         break;
       }
-      const bool fail = W == 8 ? ds_row<AGG, 8>(a, g, st, eo, cap, n, qoff, voff, rbase, nc, cell,
-                                                 s_dt[wib], s_pt[wib], s_v[wib], s_bk[wib])
-                               : ds_row<AGG, 4>(a, g, st, eo, cap, n, qoff, voff, rbase, nc, cell,
-                                                 s_dt[wib], s_pt[wib], s_v[wib], s_bk[wib]);
+      const bool fail = W == 8 ? ds_row<AGG, 8>(a, g, st, eo, cap, qoff, voff, rbase, nc, cell, s_pt[wib],
+                                                 s_v[wib], s_bk[wib])
+                               : ds_row<AGG, 4>(a, g, st, eo, cap, qoff, voff, rbase, nc, cell, s_pt[wib],
+                                                 s_v[wib], s_bk[wib]);
       ok = !fail;
       cell += nc;
     }
