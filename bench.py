@@ -379,6 +379,18 @@ def main():
     elapsed = max_over_ranks(dist, timed_loop(step_once, torch.cuda.synchronize, barrier, args.steps,
                                               args.warmup, record))
     hot_kernel = hot_kernel[0]
+    # achievable bandwidth on this box, same buffers (tsdbhip_bw_probe): a
+    # streaming read with the downsampler's geometry and a D2D copy
+    probe = {}
+    width = 4 if kind == _abi.SYN_FLOAT32 else 8
+    for mode, name in ((0, "read_stream"), (1, "d2d_copy")):
+        ms, nb = C.c_float(), C.c_uint64()
+        best = None
+        for _ in range(3):
+            ctx.check(L.tsdbhip_bw_probe(ctx.handle, C.byref(d), mode, width, C.byref(ms), C.byref(nb)))
+            gbs = nb.value / (ms.value * 1e-3) / 1e9
+            best = gbs if best is None else max(best, gbs)
+        probe[name] = best
     n_input = int(out.n_input_points)  # global (allreduced when sharded)
     ms_step = elapsed / args.steps * 1e3
     value = n_input / (elapsed / args.steps)
@@ -426,6 +438,8 @@ def main():
                 "alg_bytes_per_launch": local_bytes,
                 "kernel_ms": hot,
                 "step_device_ms": float(np.mean(total_ms)),
+                "achievable_GBs": {k: round(v, 1) for k, v in probe.items()},
+                "frac_of_read_stream": achieved / probe["read_stream"],
             },
         }
         if not args.no_cpu and world == 1:

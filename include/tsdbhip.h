@@ -282,6 +282,16 @@ int tsdbhip_desc_download(tsdbhip_ctx* ctx, const tsdbhip_sg_desc* ddesc,
                           uint64_t* row_val_off, uint32_t* row_val_len,
                           uint8_t* qual_bytes, uint8_t* val_bytes);
 
+/* ---- measurement ------------------------------------------------------- */
+/* Bandwidth probe over a device-resident desc (TSDBHIP_DESC_DEVICE):
+ * mode 0 streams its qualifier + value rows with the geometry of the
+ * downsampling kernel (one wave per span, 16-B loads), mode 1 copies its
+ * value bytes device-to-device. *ms = kernel time, *bytes = bytes moved.
+ * `width` = value bytes per cell (4 or 8). Not part of the reference API:
+ * it reports the achievable bandwidth beside the 8 TB/s peak. */
+int tsdbhip_bw_probe(tsdbhip_ctx* ctx, const tsdbhip_sg_desc* desc, int32_t mode, uint32_t width,
+                     float* ms, uint64_t* bytes);
+
 #ifdef __cplusplus
 }
 #endif

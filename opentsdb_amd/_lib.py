@@ -22,7 +22,7 @@ EXPORTS = [
     "tsdbhip_host_register", "tsdbhip_host_unregister", "tsdbhip_spangroup_run",
     "tsdbhip_last_timing", "tsdbhip_compact_rows", "tsdbhip_comm_unique_id",
     "tsdbhip_comm_init", "tsdbhip_synth_generate", "tsdbhip_synth_free",
-    "tsdbhip_desc_download",
+    "tsdbhip_desc_download", "tsdbhip_bw_probe",
 ]
 
 
@@ -71,6 +71,9 @@ def lib():
     L.tsdbhip_synth_generate.argtypes = [C.c_void_p, P(_abi.SynthParams), P(_abi.SgDesc)]
     L.tsdbhip_synth_free.argtypes = [C.c_void_p, P(_abi.SgDesc)]
     L.tsdbhip_desc_download.argtypes = [C.c_void_p, P(_abi.SgDesc)] + [C.c_void_p] * 8
+    L.tsdbhip_bw_probe.argtypes = [C.c_void_p, P(_abi.SgDesc), C.c_int32, C.c_uint32, P(C.c_float),
+                                   P(C.c_uint64)]
+    L.tsdbhip_bw_probe.restype = C.c_int
     if L.tsdbhip_abi_version() != _abi.ABI_VERSION:
         raise TsdbHipError(_abi.E_INVALID_ARG, "ABI version mismatch")
     _LIB = L

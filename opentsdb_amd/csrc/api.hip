@@ -1063,3 +1063,39 @@ extern "C" int tsdbhip_compact_rows(tsdbhip_ctx* ctx, const tsdbhip_rows_desc* d
   }
   return TSDBHIP_OK;
 }
+
+// ------------------------------------------------------ bandwidth probe ---
+// mode 0: streaming read of a device desc's row bytes with k_ds_spans'
+// geometry; mode 1: device-to-device copy of its value bytes. Returns the
+// kernel time (HIP events) and the bytes it moved.
+extern "C" int tsdbhip_bw_probe(tsdbhip_ctx* ctx, const tsdbhip_sg_desc* d, int32_t mode, uint32_t width,
+                                float* ms, uint64_t* bytes) {
+  if (!ctx || !d || !ms || !bytes || !(d->flags & TSDBHIP_DESC_DEVICE) || (width != 4 && width != 8))
+    return TSDBHIP_E_INVALID_ARG;
+  std::lock_guard<std::mutex> lock(ctx->mu);
+  try {
+    HIPCHK(hipSetDevice(ctx->device));
+    hipStream_t st = ctx->stream;
+    uint32_t* sink = scratch<uint32_t>(ctx, "probe_sink", 1);
+    HIPCHK(hipEventRecord(ctx->ev[0], st));
+    if (mode == 0) {
+      hipLaunchKernelGGL(k_probe_read, dim3(grid_for(d->n_spans, 4, 1u << 20)), dim3(256), 0, st, d->span_row_start,
+                         d->row_ncells, d->row_qual_off, d->row_val_off, d->qual_bytes, d->val_bytes, d->n_spans,
+                         width, sink);
+      *bytes = d->qual_nbytes + d->val_nbytes;
+    } else {
+      const uint64_t n16 = d->val_nbytes / 16;
+      uint4* dst = scratch<uint4>(ctx, "probe_dst", n16);
+      hipLaunchKernelGGL(k_probe_copy, dim3(grid_for(n16, 256, 1u << 16)), dim3(256), 0, st,
+                         (const uint4*)d->val_bytes, dst, n16);
+      *bytes = 2 * n16 * 16;
+    }
+    HIPCHK(hipGetLastError());
+    HIPCHK(hipEventRecord(ctx->ev[1], st));
+    HIPCHK(hipStreamSynchronize(st));
+    *ms = ev_ms(ctx->ev[0], ctx->ev[1]);
+  } catch (Fail& f) {
+    return f.code;
+  }
+  return TSDBHIP_OK;
+}

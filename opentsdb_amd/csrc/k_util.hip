@@ -207,3 +207,44 @@ __global__ void k_bitmap_or(const uint32_t* all, uint32_t nranks, uint64_t nword
   out[w] = x;
 }
 }  // namespace tsdb
+
+namespace tsdb {
+// ---- bandwidth probes (achievable bandwidth beside peak) ----
+// Streaming read with k_ds_spans' geometry: one wave per span, the span's
+// qualifier and value rows read with 16-B loads, 8 cells per lane, one
+// chunk in flight while the previous one is folded (XOR) into a register.
+__global__ void __launch_bounds__(256) k_probe_read(const uint64_t* span_row_start, const uint32_t* ncells,
+                                                    const uint64_t* qoff, const uint64_t* voff, const uint8_t* qual,
+                                                    const uint8_t* val, uint32_t n_spans, uint32_t w,
+                                                    uint32_t* sink) {
+  const int lane = lane_id();
+  const uint32_t wave = (blockIdx.x * blockDim.x + threadIdx.x) / WAVE;
+  const uint32_t nwaves = gridDim.x * blockDim.x / WAVE;
+  uint32_t acc = 0;
+  for (uint32_t s = wave; s < n_spans; s += nwaves) {
+    for (uint64_t r = span_row_start[s]; r < span_row_start[s + 1]; r++) {
+      const uint32_t nc = ncells[r];
+      const uint8_t* q = qual + qoff[r];
+      const uint8_t* v = val + voff[r];
+      for (uint32_t c0 = 0; c0 < nc; c0 += 512) {
+        const uint32_t c = c0 + 8u * lane;
+        if (c < nc) {
+          const uint4 a = *(const uint4*)(q + 2ull * c);
+          acc ^= a.x ^ a.y ^ a.z ^ a.w;
+          for (uint32_t i = 0; i < 2 * w / 4; i++) {
+            const uint4 b = *(const uint4*)(v + (uint64_t)w * c + 16ull * i);
+            acc ^= b.x ^ b.y ^ b.z ^ b.w;
+          }
+        }
+      }
+    }
+  }
+  if (acc == 0x9e3779b9u) sink[0] = acc;  // keeps the loads alive
+}
+
+// Device copy, 16 B per lane per iteration (grid-stride).
+__global__ void __launch_bounds__(256) k_probe_copy(const uint4* src, uint4* dst, uint64_t n16) {
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n16; i += (uint64_t)gridDim.x * blockDim.x)
+    dst[i] = src[i];
+}
+}  // namespace tsdb
