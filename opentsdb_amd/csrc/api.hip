@@ -563,7 +563,7 @@ static int spangroup_run(tsdbhip_ctx* ctx, const tsdbhip_sg_desc* d, tsdbhip_sg_
     } else if (interval == 0) {
       hipLaunchKernelGGL((k_decode_fast<0, false>), dim3(blocks), dim3(256), 0, st, da, row_ncells, row_val_len);
       HIPCHK(hipEventRecord(ctx->ev[9], st));
-      hipLaunchKernelGGL(k_decode_nods, dim3(blocks), dim3(256), 0, st, ga);
+      hipLaunchKernelGGL(k_decode_nods, dim3(std::min(blocks, 2048u)), dim3(256), 0, st, ga);
     } else {
       DecodeArgs fa = da;
       if (chunks && ds_agg != 4) {
@@ -579,13 +579,16 @@ static int spangroup_run(tsdbhip_ctx* ctx, const tsdbhip_sg_desc* d, tsdbhip_sg_
         mark_list = fa.span_list;
         mark_count = fa.span_count;
       }
-      launch_agg<LaunchFastDs>(ds_agg, ctx, blocks, fa, row_ncells, row_val_len);
+      // (grid-stride over the spans left by k_ds_spans: usually few)
+      const unsigned lblocks = fa.span_list ? std::min(blocks, 2048u) : blocks;
+      launch_agg<LaunchFastDs>(ds_agg, ctx, lblocks, fa, row_ncells, row_val_len);
       if (ctx->hot_kernel == TSDBHIP_HOT_DECODE_FAST) HIPCHK(hipEventRecord(ctx->ev[9], st));
-      launch_agg<LaunchGeneralDs>(ds_agg, ctx, blocks, ga);
+      launch_agg<LaunchGeneralDs>(ds_agg, ctx, std::min(blocks, 2048u), ga);
     }
   }
   HIPCHK(hipEventRecord(ctx->ev[2], st));
-  if (n_kept) hipLaunchKernelGGL(k_span_summary, dim3(grid_for(n_kept, 256, 1024)), dim3(256), 0, st, da);
+  if (n_kept)
+    hipLaunchKernelGGL(k_span_summary, dim3(grid_for(n_kept, 256, 1024)), dim3(256), 0, st, da, mark_list, mark_count);
   readback(ctx, &h, sm, sizeof h);  // sync 2
   if (h.err && !sharded) throw Fail{h.err};
 
@@ -652,7 +655,11 @@ static int spangroup_run(tsdbhip_ctx* ctx, const tsdbhip_sg_desc* d, tsdbhip_sg_
         n_chunks = 1;
         spc = std::max<uint32_t>(n_kept, 1);
       } else {
+        // chunks of ~256 spans (fewer partials for the combine), but at
+        // least ~2048 waves when the group is small
         uint64_t want = std::max<uint64_t>(1, target / n_tiles);
+        const uint64_t by_size = std::max<uint64_t>((n_kept + 255) / 256, (2048 + n_tiles - 1) / n_tiles);
+        want = std::min<uint64_t>(want, by_size);
         want = std::min<uint64_t>(want, std::max<uint32_t>(1, n_kept / 16));
         n_chunks = (uint32_t)std::max<uint64_t>(1, want);
         spc = (n_kept + n_chunks - 1) / n_chunks;

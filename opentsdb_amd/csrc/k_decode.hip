@@ -414,37 +414,29 @@ __global__ void __launch_bounds__(256) k_decode_ds(DecodeArgs a) {
     span_ds_general<AGG>(a, a.use_fb ? a.fb_list[i] : i, s_bits[wib], s_flt[wib]);
 }
 
-// Per-span summary of E after decode: grid range, F* (float first points).
-// Grid-stride, one atomic per block and field.
-__global__ void __launch_bounds__(256) k_span_summary(DecodeArgs a) {
-  __shared__ int64_t sh_lo[4], sh_hi[4], sh_fs[4], sh_e[4];
-  int64_t lo = INT64_MAX, hi = INT64_MIN, fs = 0, empty = 0;
-  for (uint32_t k = blockIdx.x * blockDim.x + threadIdx.x; k < a.n_kept; k += gridDim.x * blockDim.x) {
+// Per-span summary of E after decode: empty spans (E_EMPTY_SPAN) and F*
+// (the latest first point that is a float). Over `list` only when given: the
+// spans k_ds_spans finished are integer and non-empty. Grid-stride, one
+// atomic per block and field.
+__global__ void __launch_bounds__(256) k_span_summary(DecodeArgs a, const uint32_t* list, const uint32_t* count) {
+  __shared__ int64_t sh_fs[4], sh_e[4];
+  int64_t fs = 0, empty = 0;
+  const uint32_t n = list ? *count : a.n_kept;
+  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+    const uint32_t k = list ? list[i] : i;
     const uint32_t len = a.e_len[k];
     const uint64_t eo = a.e_off[k];
     if (len == 0) {
       empty = 1;
       continue;
     }
-    const int64_t first = a.e_ts[eo];
-    if (a.rate) {
-      if (len >= 2) lo = min(lo, (int64_t)a.e_ts[eo + 1]);
-    } else {
-      lo = min(lo, first);
-      if (a.e_flt[eo]) fs = max(fs, first + 1);  // +1: 0 = none
-    }
-    hi = max(hi, (int64_t)a.e_ts[eo + len - 1]);
+    if (!a.rate && a.e_flt[eo]) fs = max(fs, (int64_t)a.e_ts[eo] + 1);  // +1: 0 = none
   }
-  auto mn = [](int64_t x, int64_t y) { return min(x, y); };
   auto mx = [](int64_t x, int64_t y) { return max(x, y); };
-  lo = block_reduce_256(lo, mn, sh_lo);
-  hi = block_reduce_256(hi, mx, sh_hi);
   fs = block_reduce_256(fs, mx, sh_fs);
   empty = block_reduce_256(empty, mx, sh_e);
   if (threadIdx.x == 0) {
     if (empty) atomicMin(a.err, -3 /*E_EMPTY_SPAN*/);
-    if (lo != INT64_MAX) atomicMin(&a.range[0], (unsigned long long)lo);
-    if (hi != INT64_MIN) atomicMax(&a.range[1], (unsigned long long)hi);
     if (fs) atomicMax(a.fstar, (unsigned long long)fs);
   }
 }
