@@ -35,21 +35,54 @@ from opentsdb_amd._lib import Context, lib  # noqa: E402
 METRIC = "input data points/sec aggregated (node) + % HBM roofline, 1/2/4/8 MI355X"
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: 8.0 TB/s spec
 
+def _cfg(n_series, n_points, step, kind, agg, dsi=0, dsa=0, rate=False, gen="device", desc=""):
+    return dict(n_series=n_series, n_points=n_points, step=step, kind=kind, agg=agg, dsi=dsi, dsa=dsa,
+                rate=rate, gen=gen, desc=desc)
+
+
+I64, F32 = _abi.SYN_INT64_COUNTER, _abi.SYN_FLOAT32
+SUM, MIN, MAX, AVG, DEV = _abi.AGG_SUM, _abi.AGG_MIN, _abi.AGG_MAX, _abi.AGG_AVG, _abi.AGG_DEV
 CONFIGS = {
-    # name: (n_series, points/series, step s, kind, agg, ds_interval, ds_agg, description)
-    "c3s": (1_000_000, 3600, 1, _abi.SYN_INT64_COUNTER, _abi.AGG_SUM, 60, _abi.AGG_AVG,
-            "C3*: 1M series x 3600 pts @1s (3.6G pts), int64 counters, sum + 1m-avg downsample"),
-    "c2": (10_000, 8640, 10, _abi.SYN_FLOAT32, _abi.AGG_AVG, 60, _abi.AGG_AVG,
-           "C2: 10k float32 series x 1 day @10s (86.4M pts), avg + 1m-avg downsample"),
-    "c1": (100, 3600, 1, _abi.SYN_INT64_COUNTER, _abi.AGG_SUM, 0, 0,
-           "C1: 100 int series x 3600 pts @1s, sum, no downsample"),
-    "c3": (1_000_000, 3600, 1, _abi.SYN_INT64_COUNTER, _abi.AGG_SUM, 0, 0,
-           "C3 (sum, no rate): 1M series x 3600 pts @1s, int64 counters"),
+    # BASELINE.json configs; the default line is c3s (the north-star target)
+    "c3s": _cfg(1_000_000, 3600, 1, I64, SUM, 60, AVG,
+                desc="C3*: 1M series x 3600 pts @1s (3.6G pts), int64 counters, sum + 1m-avg downsample"),
+    "c1": _cfg(100, 3600, 1, I64, SUM, desc="C1: 100 int series x 3600 pts @1s, sum, no downsample"),
+    "c2": _cfg(10_000, 8640, 10, F32, AVG, 60, AVG,
+               desc="C2: 10k float32 series x 1 day @10s (86.4M pts), avg + 1m-avg downsample"),
+    "c3": _cfg(1_000_000, 3600, 1, I64, SUM, desc="C3 (sum, no rate): 1M series x 3600 pts @1s, int64 counters"),
+    "c3r_sum": _cfg(1_000_000, 3600, 1, I64, SUM, rate=True, desc="C3: 1M series x 3600 pts @1s, rate, sum"),
+    "c3r_max": _cfg(1_000_000, 3600, 1, I64, MAX, rate=True, desc="C3: 1M series x 3600 pts @1s, rate, max"),
+    "c3r_dev": _cfg(1_000_000, 3600, 1, I64, DEV, rate=True, desc="C3: 1M series x 3600 pts @1s, rate, dev"),
+    "c4": _cfg(1000, 11500, 0, -1, SUM, gen="jitter",
+               desc="C4: 1000 jittered series (gaps U{1..6960}s, ~11.5k pts each, 50% float32 series, "
+                    "1% float cells), ~10M-point union grid, sum"),
+    "c4i": _cfg(1000, 11500, 0, -1, SUM, gen="jitter_int",
+                desc="C4-int: the C4 timestamps with all-int series (the int64 lerp path), sum"),
     # secondary path (configs[4]): row compaction, see bench_c5
-    "c5": (1_000_000, 0, 0, 0, 0, 0, 0,
-           "C5: row compaction, 1M rows / ~48M raw cells (1..99 per row, mixed widths, legacy floats, "
-           "10% pre-compacted rows with late singles + exact dups, 0.1% conflicting dups)"),
+    "c5": _cfg(1_000_000, 0, 0, 0, 0, gen="rows",
+               desc="C5: row compaction, 1M rows / ~48M raw cells (1..99 per row, mixed widths, legacy floats, "
+                    "10% pre-compacted rows with late singles + exact dups, 0.1% conflicting dups)"),
 }
+
+
+def host_spanset(cfg, lo, hi, seed=4):
+    """Host-generated SpanGroup of a config (the jittered C4 shapes), spans [lo, hi)."""
+    ff = 0.5 if cfg["gen"] == "jitter" else 0.0
+    fc = 0.01 if cfg["gen"] == "jitter" else 0.0
+    ss = synth.jittered_packed(cfg["n_series"], cfg["n_points"], seed=seed, float_frac=ff, float_cell_frac=fc)
+    if (lo, hi) == (0, cfg["n_series"]):
+        return ss
+    r0, r1 = int(ss.span_row_start[lo]), int(ss.span_row_start[hi])
+    from opentsdb_amd.packing import SpanSet
+    return SpanSet((ss.span_row_start[lo:hi + 1] - r0).astype(np.uint64), ss.row_base[r0:r1],
+                   ss.row_ncells[r0:r1], ss.row_qual_off[r0:r1], ss.row_val_off[r0:r1], ss.row_val_len[r0:r1],
+                   ss.qual_bytes, ss.val_bytes)
+
+
+def spanset_row_bytes(ss):
+    """SURVEY.md §8(d) algorithmic input bytes of a SpanSet's rows."""
+    n = ss.row_ncells.astype(np.int64)
+    return int((4 + 2 * n + ss.row_val_len.astype(np.int64)).sum())
 
 
 def ref_row_bytes(n_series, n_points, step, kind):
@@ -86,19 +119,27 @@ def dist_setup(n_gpus):
     return dist, dist.get_rank(), dist.get_world_size(), int(os.environ.get("LOCAL_RANK", "0"))
 
 
-def cpu_baseline(cfg, seconds=10.0):
+def cpu_baseline(cfg_name, seconds=10.0):
     """The oracle (C++ restatement of the reference's Java iterators) on the
     host cores, independent SpanGroups per thread (group-by style,
     TsdbQuery.java:322-362); a bounded sample of the same workload shape."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle
-    n_series, n_points, step, kind, agg, dsi, dsa, _ = CONFIGS[cfg]
-    sample_series = max(1, min(n_series, 200_000 // max(1, n_points // 100)))
-    ss = synth.regular(sample_series, n_points, kind, seed=1, step=step)
+    cfg = CONFIGS[cfg_name]
+    if cfg["gen"] == "device":
+        n_points = cfg["n_points"]
+        sample_series = max(1, min(cfg["n_series"], 200_000 // max(1, n_points // 100)))
+        ss = synth.regular(sample_series, n_points, cfg["kind"], seed=1, step=cfg["step"])
+        what = f"{sample_series} series x {n_points} pts of the same workload"
+    else:
+        sample_series = 20
+        ss = host_spanset(dict(cfg, n_series=sample_series), 0, sample_series, seed=11)
+        what = f"{sample_series} series of the same generator (~{cfg['n_points']} pts each)"
+    args = (0, (1 << 32) - 1, cfg["agg"], cfg["rate"], cfg["dsi"], cfg["dsa"])
     oracle.lib()
     # probe one run, then size the sample to ~`seconds` of CPU work
     t = time.perf_counter()
-    r = oracle.spangroup(ss, 0, (1 << 32) - 1, agg, False, dsi, dsa, capacity=ss.n_cells())
+    r = oracle.spangroup(ss, *args, capacity=ss.n_cells())
     probe = time.perf_counter() - t
     threads = max(1, min(16, os.cpu_count() or 1))
     reps_per_thread = max(1, int(seconds / max(probe, 1e-3)))
@@ -108,7 +149,7 @@ def cpu_baseline(cfg, seconds=10.0):
     def work():
         n = 0
         for _ in range(reps_per_thread):
-            rr = oracle.spangroup(ss, 0, (1 << 32) - 1, agg, False, dsi, dsa, capacity=ss.n_cells())
+            rr = oracle.spangroup(ss, *args, capacity=ss.n_cells())
             n += rr.n_input_points
         with lock:
             total[0] += n
@@ -124,8 +165,7 @@ def cpu_baseline(cfg, seconds=10.0):
     return {
         "value": total[0] / wall, "unit": "input points/s", "cores": threads, "kind": "port",
         "value_1core": one_core,
-        "sample": f"{sample_series} series x {n_points} pts of the same workload, "
-                  f"{threads} threads x {reps_per_thread} SpanGroups, {wall:.1f} s wall "
+        "sample": f"{what}, {threads} threads x {reps_per_thread} SpanGroups, {wall:.1f} s wall "
                   f"(oracle/oracle.cc: C++ restatement of SpanGroup/Span/RowSeq/Aggregators; "
                   f"no JVM in the image)",
     }
@@ -249,7 +289,7 @@ def bench_c5(args):
         "scaling": "weak", "vs_baseline": None, "dtype": "u8",
         "data": f"synthetic HBase rows in the reference byte encoding (host-generated in {gen_s:.0f} s, "
                 f"HBM-resident before timing)",
-        "config": {"workload": CONFIGS["c5"][7], "n_rows": R, "n_kvs": b.n_kvs, "raw_cells": cells,
+        "config": {"workload": CONFIGS["c5"]["desc"], "n_rows": R, "n_kvs": b.n_kvs, "raw_cells": cells,
                    "rows_complex": n_cx, "status_counts": np.bincount(st, minlength=6).tolist()},
         "roofline": {"bound": "hbm", "kernel": "k_compact_tiles", "achieved": achieved, "peak": HBM_PEAK_GBS,
                      "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
@@ -316,9 +356,12 @@ def main():
         return bench_c5(args)
 
     dist, rank, world, local_rank = dist_setup(args.gpus)
-    n_series, n_points, step, kind, agg, dsi, dsa, desc_txt = CONFIGS[args.config]
+    cfg = CONFIGS[args.config]
+    n_series, n_points, step, kind = cfg["n_series"], cfg["n_points"], cfg["step"], cfg["kind"]
+    agg, dsi, dsa, rate, desc_txt = cfg["agg"], cfg["dsi"], cfg["dsa"], cfg["rate"], cfg["desc"]
     if args.series:
         n_series = args.series
+        cfg = dict(cfg, n_series=n_series)
     shards = shard_ranges(n_series, world)
     lo, hi = shards[rank]
 
@@ -347,18 +390,45 @@ def main():
         dist.broadcast_object_list(uid, src=0)
         ctx.comm_init(world, rank, uid[0])
 
-    p = _abi.SynthParams(seed=3, n_spans=hi - lo, n_points=n_points, t0=synth.T0, step=step,
-                         kind=kind, span0=lo)
     d = _abi.SgDesc()
-    ctx.check(L.tsdbhip_synth_generate(ctx.handle, C.byref(p), C.byref(d)))
+    keep = []
+    if cfg["gen"] == "device":  # the reference's byte format generated straight into HBM
+        p = _abi.SynthParams(seed=3, n_spans=hi - lo, n_points=n_points, t0=synth.T0, step=step,
+                             kind=kind, span0=lo)
+        ctx.check(L.tsdbhip_synth_generate(ctx.handle, C.byref(p), C.byref(d)))
+        local_bytes = ref_row_bytes(hi - lo, n_points, step, kind)
+    else:  # host-generated (jittered C4 shapes), uploaded to HBM before timing
+        ss = host_spanset(cfg, lo, hi)
+        dev = torch.device("cuda", local_rank)
+
+        def up(arr, ctype):
+            t = torch.from_numpy(np.ascontiguousarray(arr).view(np.uint8)).to(dev)
+            keep.append(t)
+            return C.cast(C.c_void_p(t.data_ptr()), C.POINTER(ctype))
+
+        ss.fill_desc(d)
+        d.flags = _abi.DESC_DEVICE
+        d.span_row_start = up(ss.span_row_start, C.c_uint64)
+        d.row_base = up(ss.row_base, C.c_uint32)
+        d.row_ncells = up(ss.row_ncells, C.c_uint32)
+        d.row_qual_off = up(ss.row_qual_off, C.c_uint64)
+        d.row_val_off = up(ss.row_val_off, C.c_uint64)
+        d.row_val_len = up(ss.row_val_len, C.c_uint32)
+        d.qual_bytes = up(ss.qual_bytes, C.c_uint8)
+        d.val_bytes = up(ss.val_bytes, C.c_uint8)
+        local_bytes = spanset_row_bytes(ss)
+        n_points = int(cfg["n_points"] * 1.5 * n_series)  # bound on the union grid
     d.start_time = 0
     d.end_time = (1 << 32) - 1
-    d.agg, d.rate, d.ds_interval, d.ds_agg = agg, 0, dsi, dsa
+    d.agg, d.rate, d.ds_interval, d.ds_agg = agg, int(rate), dsi, dsa
     if world > 1:
         d.flags |= _abi.SHARDED
     if args.exact:
         d.flags |= _abi.EXACT_ORDER
-    cap = max(1, n_points if dsi == 0 else (n_points * step) // dsi + 2)
+    if cfg["gen"] == "device":
+        cap = max(1, n_points if dsi == 0 else (n_points * step) // dsi + 2)
+    else:  # union of all timestamps (bounded by all ranks' input points)
+        cap = max(1, n_points + 16)
     ts = np.zeros(cap, np.int64)
     isi = np.zeros(cap, np.uint8)
     bits = np.zeros(cap, np.int64)
@@ -383,7 +453,7 @@ def main():
     # streaming read with the downsampler's geometry and a D2D copy
     probe = {}
     width = 4 if kind == _abi.SYN_FLOAT32 else 8
-    for mode, name in ((0, "read_stream"), (1, "d2d_copy")):
+    for mode, name in (((0, "read_stream"), (1, "d2d_copy")) if cfg["gen"] == "device" else ()):
         ms, nb = C.c_float(), C.c_uint64()
         best = None
         for _ in range(3):
@@ -397,7 +467,6 @@ def main():
 
     # roofline of the dominant kernel: SURVEY.md §8(d) algorithmic bytes (the
     # row bytes it streams) over its own duration (HIP events on its stream)
-    local_bytes = ref_row_bytes(hi - lo, n_points, step, kind)
     hot = float(np.mean(hot_ms))
     achieved = local_bytes / (hot * 1e-3) / 1e9
     kname = _abi.HOT_NAMES.get(hot_kernel, "none")
@@ -414,12 +483,14 @@ def main():
             "higher_is_better": True,
             "scaling": "strong",
             "vs_baseline": None,
-            "dtype": "int64" if kind == _abi.SYN_INT64_COUNTER else "f64",
+            "dtype": "int64" if (kind == _abi.SYN_INT64_COUNTER and not rate) or cfg["gen"] == "jitter_int"
+                     else "f64",
             "data": "synthetic (device-generated KeyValue bytes in the reference encoding)",
             "config": {
                 "workload": desc_txt,
                 "n_series": n_series,
-                "points_per_series": n_points,
+                "points_per_series": cfg["n_points"],
+                "rate": bool(rate),
                 "aggregator": ["sum", "min", "max", "avg", "dev"][agg],
                 "downsample": f"{dsi}s-{['sum', 'min', 'max', 'avg', 'dev'][dsa]}" if dsi else "none",
                 "parallelism": f"series-sharded x{world} (RCCL exchange of per-t partials)" if world > 1
@@ -439,13 +510,14 @@ def main():
                 "kernel_ms": hot,
                 "step_device_ms": float(np.mean(total_ms)),
                 "achievable_GBs": {k: round(v, 1) for k, v in probe.items()},
-                "frac_of_read_stream": achieved / probe["read_stream"],
+                "frac_of_read_stream": achieved / probe["read_stream"] if probe else None,
             },
         }
         if not args.no_cpu and world == 1:
             res["cpu_baseline"] = cpu_baseline(args.config, args.cpu_seconds)
         print(json.dumps(res), flush=True)
-    L.tsdbhip_synth_free(ctx.handle, C.byref(d))
+    if cfg["gen"] == "device":
+        L.tsdbhip_synth_free(ctx.handle, C.byref(d))
     ctx.close()
     if dist is not None:
         dist.destroy_process_group()

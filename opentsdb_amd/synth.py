@@ -197,3 +197,70 @@ def jittered(n_spans, mean_pts, seed=4, t0=T0, span_range=40_000_000, max_gap=69
                 pts.append((int(t),) + encode_long(int(rng.integers(-10**6, 10**6)), minimal))
         spans.append(series_rows(pts))
     return pack_spans(spans)
+
+
+def jittered_packed(n_spans, mean_pts, seed=4, t0=T0, span_range=40_000_000, max_gap=6960,
+                    float_frac=0.5, float_cell_frac=0.01):
+    """C4, vectorised: ~mean_pts points per series with
+    jittered gaps U{1..max_gap} s from a start in the first quarter of
+    `span_range`; `float_frac` of the series float32 (~100 + N(0,1)), the
+    others minimal-width longs with `float_cell_frac` float cells. One
+    compacted KeyValue per hour row (trivialCompact layout, as series_rows),
+    packed like packing.pack_spans (rows 8-B / 16-B aligned)."""
+    rng = np.random.default_rng(seed)
+    n = rng.integers(max(2, mean_pts // 2), mean_pts * 3 // 2 + 1, n_spans).astype(np.int64)
+    N = int(n.sum())
+    sid = np.repeat(np.arange(n_spans, dtype=np.int64), n)
+    first = np.cumsum(n) - n
+    gaps = rng.integers(1, max_gap + 1, N).astype(np.int64)
+    gaps[first] = 0
+    start = t0 + rng.integers(0, max(1, span_range // 4), n_spans).astype(np.int64)
+    cs = np.cumsum(gaps)
+    ts = start[sid] + cs - cs[first][sid]
+    is_fs = rng.random(n_spans) < float_frac
+    flt = is_fs[sid] | (rng.random(N) < float_cell_frac)
+    fval = np.where(is_fs[sid], 100.0 + rng.standard_normal(N),
+                    rng.integers(-1000, 1000, N).astype(np.float64) + 0.5).astype(">f4")
+    ival = rng.integers(-10**6, 10**6, N).astype(np.int64)
+    # minimal long widths (TSDB.java:240-250)
+    iw = np.where((ival >= -128) & (ival <= 127), 1,
+                  np.where((ival >= -32768) & (ival <= 32767), 2,
+                           np.where((ival >= -(1 << 31)) & (ival < (1 << 31)), 4, 8)))
+    w = np.where(flt, 4, iw)
+    flags = np.where(flt, FLAG_FLOAT | 0x3, w - 1)
+    base = ts - ts % MAX_TIMESPAN
+    # rows: runs of equal (span, base)
+    newrow = np.ones(N, bool)
+    newrow[1:] = (sid[1:] != sid[:-1]) | (base[1:] != base[:-1])
+    rid = np.cumsum(newrow) - 1
+    R = int(rid[-1]) + 1
+    rfirst = np.nonzero(newrow)[0]
+    rcells = np.diff(np.append(rfirst, N))
+    rvraw = np.add.reduceat(w, rfirst)
+    rvlen = rvraw + (rcells > 1)
+    qlen_al = (2 * rcells + 7) // 8 * 8
+    vlen_al = (rvlen + 15) // 16 * 16
+    qoff = np.cumsum(qlen_al) - qlen_al
+    voff = np.cumsum(vlen_al) - vlen_al
+    idx_in_row = np.arange(N) - rfirst[rid]
+    qb = np.zeros(int(qlen_al.sum()) + 64, np.uint8)
+    q = ((ts - base[rfirst][rid]) << 4) | flags
+    qp = qoff[rid] + 2 * idx_in_row
+    qb[qp] = (q >> 8).astype(np.uint8)
+    qb[qp + 1] = (q & 0xFF).astype(np.uint8)
+    wcs = np.cumsum(w) - w
+    vpos = voff[rid] + wcs - wcs[rfirst][rid]
+    vb = np.zeros(int(vlen_al.sum()) + 64, np.uint8)
+    fbytes = fval.view(np.uint8).reshape(N, 4)
+    ibytes = ival.astype(">i8").view(np.uint8).reshape(N, 8)
+    for width in (1, 2, 4, 8):
+        sel = np.nonzero(~flt & (w == width))[0]
+        for j in range(width):
+            vb[vpos[sel] + j] = ibytes[sel, 8 - width + j]
+    sel = np.nonzero(flt)[0]
+    for j in range(4):
+        vb[vpos[sel] + j] = fbytes[sel, j]
+    srs = np.zeros(n_spans + 1, np.uint64)
+    srs[1:] = np.cumsum(np.bincount(sid[rfirst], minlength=n_spans))
+    return SpanSet(srs, base[rfirst].astype(np.uint32), rcells.astype(np.uint32), qoff.astype(np.uint64),
+                   voff.astype(np.uint64), rvlen.astype(np.uint32), qb, vb)
