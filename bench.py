@@ -468,8 +468,15 @@ def main():
     # roofline of the dominant kernel: SURVEY.md §8(d) algorithmic bytes (the
     # row bytes it streams) over its own duration (HIP events on its stream)
     hot = float(np.mean(hot_ms))
-    achieved = local_bytes / (hot * 1e-3) / 1e9
     kname = _abi.HOT_NAMES.get(hot_kernel, "none")
+    hot_bytes = local_bytes
+    if kname == "k_reduce":  # direct path: the reducer streams the value bytes only
+        if cfg["gen"] == "device":
+            hot_bytes = (hi - lo) * cfg["n_points"] * width
+        else:
+            nc = ss.row_ncells.astype(np.int64)
+            hot_bytes = int((ss.row_val_len.astype(np.int64) - (nc > 1)).sum())
+    achieved = hot_bytes / (hot * 1e-3) / 1e9
     traffic, traffic_src = pmc_traffic(args.config, kname, world)
     if rank == 0:
         res = {
@@ -506,9 +513,11 @@ def main():
                 "frac": achieved / HBM_PEAK_GBS,
                 "traffic": traffic,
                 "traffic_source": traffic_src,
-                "alg_bytes_per_launch": local_bytes,
+                "alg_bytes_per_launch": hot_bytes,
                 "kernel_ms": hot,
                 "step_device_ms": float(np.mean(total_ms)),
+                "path_alg_bytes": local_bytes,
+                "path_GBs": local_bytes / (float(np.mean(total_ms)) * 1e-3) / 1e9,
                 "achievable_GBs": {k: round(v, 1) for k, v in probe.items()},
                 "frac_of_read_stream": achieved / probe["read_stream"] if probe else None,
             },

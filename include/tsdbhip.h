@@ -77,6 +77,7 @@ extern "C" {
 #define TSDBHIP_HOT_DS_CHUNKS   1 /* k_ds_spans: streaming decode+downsample */
 #define TSDBHIP_HOT_DECODE_FAST 2 /* streaming per-span decode(+downsample) */
 #define TSDBHIP_HOT_DECODE_GEN  3 /* general per-span decode(+downsample)   */
+#define TSDBHIP_HOT_REDUCE_DIRECT 5 /* k_reduce over direct spans (no-downsampling path) */
 #define TSDBHIP_HOT_COMPACT     4 /* k_compact_tiles: classification + single/trivial/short complex
                                      compaction (tsdbhip_compact_rows)      */
 

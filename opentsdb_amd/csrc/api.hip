@@ -33,6 +33,7 @@
 #include "k_decode_fast.hip"
 #include "k_ds_chunks.hip"
 #include "k_compact.hip"
+#include "k_direct.hip"
 
 using namespace tsdb;
 
@@ -57,6 +58,7 @@ struct tsdbhip_ctx {
   std::map<std::string, Buf> bufs;
   void* host_small = nullptr;  // pinned readback area
   hipEvent_t ev[10] = {};  // [8],[9] bracket the dominant kernel
+  bool time_reduce = false;  // the dominant kernel is k_reduce (direct path)
   uint32_t hot_kernel = 0;
   tsdbhip_timing timing = {};
   ncclComm_t comm = nullptr;
@@ -312,7 +314,9 @@ struct LaunchChunks {
 template <int AGG, int MODE, bool RATE>
 static void launch_reduce(tsdbhip_ctx* ctx, unsigned blocks, const ReduceArgs& r, const FinalArgs& f,
                           bool par, bool finalize) {
+  if (ctx->time_reduce) HIPCHK(hipEventRecord(ctx->ev[8], ctx->stream));
   hipLaunchKernelGGL((k_reduce<AGG, MODE, RATE>), dim3(blocks), dim3(256), 0, ctx->stream, r);
+  if (ctx->time_reduce) HIPCHK(hipEventRecord(ctx->ev[9], ctx->stream));
   if (!finalize) return;
   if (par)
     hipLaunchKernelGGL((k_finalize_par<AGG, MODE, RATE>), dim3((unsigned)f.T), dim3(256), 0, ctx->stream, r, f);
@@ -405,6 +409,7 @@ static int spangroup_run(tsdbhip_ctx* ctx, const tsdbhip_sg_desc* d, tsdbhip_sg_
   hipStream_t st = ctx->stream;
   tsdbhip_timing tm = {};
   ctx->hot_kernel = TSDBHIP_HOT_NONE;
+  ctx->time_reduce = false;
   out->n_out = 0;
   out->n_input_points = 0;
   out->err_code = 0;
@@ -535,6 +540,8 @@ static int spangroup_run(tsdbhip_ctx* ctx, const tsdbhip_sg_desc* d, tsdbhip_sg_
   da.range = sm->range; da.fstar = &sm->fstar;
   HIPCHK(hipEventRecord(ctx->ev[1], st));
   bool chunk_marked = false;     // k_ds_spans marked G for the spans it took
+  bool direct = false;           // k_direct_scan took the no-downsampling path
+  DirectArgs dg = {};
   const uint32_t* mark_list = nullptr, *mark_count = nullptr;
   if (n_kept) {
     const unsigned blocks = grid_for(n_kept, 4, 65536);
@@ -544,9 +551,11 @@ static int spangroup_run(tsdbhip_ctx* ctx, const tsdbhip_sg_desc* d, tsdbhip_sg_
     const char* force = getenv("TSDBHIP_DECODE");
     bool fast = R > 0 && h.n_input / R >= 64;
     bool chunks = fast;
-    if (force && !strcmp(force, "general")) fast = chunks = false;
-    if (force && !strcmp(force, "fast")) { fast = true; chunks = false; }
-    if (force && !strcmp(force, "chunks")) fast = chunks = true;
+    direct = fast && interval == 0 && bitmap != nullptr;
+    if (force && !strcmp(force, "general")) fast = chunks = direct = false;
+    if (force && !strcmp(force, "fast")) { fast = true; chunks = direct = false; }
+    if (force && !strcmp(force, "chunks")) { fast = chunks = true; direct = false; }
+    if (force && !strcmp(force, "direct")) { fast = chunks = true; direct = interval == 0 && bitmap != nullptr; }
     da.fb_list = scratch<uint32_t>(ctx, "fb_list", n_kept);
     da.fb_count = scratch<uint32_t>(ctx, "fb_count", 1, true);
     da.use_fb = 0;
@@ -561,8 +570,35 @@ static int spangroup_run(tsdbhip_ctx* ctx, const tsdbhip_sg_desc* d, tsdbhip_sg_
       else launch_agg<LaunchGeneralDs>(ds_agg, ctx, blocks, da);
       HIPCHK(hipEventRecord(ctx->ev[9], st));
     } else if (interval == 0) {
-      hipLaunchKernelGGL((k_decode_fast<0, false>), dim3(blocks), dim3(256), 0, st, da, row_ncells, row_val_len);
-      HIPCHK(hipEventRecord(ctx->ev[9], st));
+      DecodeArgs fa = da;
+      if (direct) {
+        // regular-cadence spans on consecutive grid ranks skip E (k_direct.hip)
+        dg.info = scratch<uint32_t>(ctx, "d_info", n_kept);
+        dg.n = scratch<uint32_t>(ctx, "d_n", n_kept);
+        dg.x0 = scratch<uint32_t>(ctx, "d_x0", n_kept);
+        dg.step = scratch<uint32_t>(ctx, "d_step", n_kept);
+        dg.voff = scratch<uint64_t>(ctx, "d_voff", n_kept);
+        dg.c0 = scratch<uint32_t>(ctx, "d_c0", n_kept);
+        dg.r0 = scratch<uint64_t>(ctx, "d_r0", n_kept);
+        dg.ga = scratch<uint32_t>(ctx, "d_ga", n_kept);
+        dg.row_cpre = scratch<uint32_t>(ctx, "row_cpre", R);
+        dg.list = scratch<uint32_t>(ctx, "d_list", n_kept);
+        dg.list_count = scratch<uint32_t>(ctx, "d_list_count", 1, true);
+        dg.bitmap = bitmap;
+        dg.lo = lo;
+        dg.hi = hi;
+        dg.rate = rate;
+        ctx->hot_kernel = TSDBHIP_HOT_REDUCE_DIRECT;  // timed around k_reduce
+        hipLaunchKernelGGL(k_direct_scan, dim3(grid_for(n_kept, 256, 1u << 20)), dim3(256), 0, st, da, dg,
+                           row_ncells, row_val_len);
+        fa.span_list = dg.list;
+        fa.span_count = dg.list_count;
+        mark_list = dg.list;
+        mark_count = dg.list_count;
+      }
+      const unsigned lblocks = fa.span_list ? std::min(blocks, 2048u) : blocks;
+      hipLaunchKernelGGL((k_decode_fast<0, false>), dim3(lblocks), dim3(256), 0, st, fa, row_ncells, row_val_len);
+      if (!direct) HIPCHK(hipEventRecord(ctx->ev[9], st));
       hipLaunchKernelGGL(k_decode_nods, dim3(std::min(blocks, 2048u)), dim3(256), 0, st, ga);
     } else {
       DecodeArgs fa = da;
@@ -640,6 +676,23 @@ static int spangroup_run(tsdbhip_ctx* ctx, const tsdbhip_sg_desc* d, tsdbhip_sg_
     gridv = scratch<uint32_t>(ctx, "grid", T);
     ga.grid = gridv;
     hipLaunchKernelGGL(k_grid_emit, dim3(grid_for(nwords, 256)), dim3(256), 0, st, ga);
+    if (direct && n_kept) {
+      // candidates whose points are not consecutive grid ranks need E (their
+      // grid points are already marked; types, F* and errors already counted)
+      dg.word_rank = word_rank;
+      dg.bitmap = bitmap;
+      HIPCHK(hipMemsetAsync(dg.list_count, 0, 4, st));
+      HIPCHK(hipMemsetAsync(da.fb_count, 0, 4, st));
+      hipLaunchKernelGGL(k_direct_verify, dim3(grid_for(n_kept, 256)), dim3(256), 0, st, dg, n_kept);
+      DecodeArgs fa = da;
+      fa.span_list = dg.list;
+      fa.span_count = dg.list_count;
+      hipLaunchKernelGGL((k_decode_fast<0, false>), dim3(std::min(grid_for(n_kept, 4, 65536), 2048u)), dim3(256), 0,
+                         st, fa, row_ncells, row_val_len);
+      DecodeArgs gfa = da;
+      gfa.use_fb = 1;
+      hipLaunchKernelGGL(k_decode_nods, dim3(std::min(grid_for(n_kept, 4, 65536), 2048u)), dim3(256), 0, st, gfa);
+    }
   }
   HIPCHK(hipEventRecord(ctx->ev[4], st));
   tm.n_grid = T;
@@ -647,6 +700,7 @@ static int spangroup_run(tsdbhip_ctx* ctx, const tsdbhip_sg_desc* d, tsdbhip_sg_
   // ---- reduce ----
   if (T > 0) {
     const int mode = rate ? MODE_DBL : (!anyf ? MODE_INT : (!anyi ? MODE_DBL : MODE_DUAL));
+    ctx->time_reduce = direct;
     auto run_reduce = [&](bool one_chunk, bool finalize) {
       const uint64_t n_tiles = (T + 63) / 64;
       const uint64_t target = 16384;  // waves in flight over 256 CUs
@@ -672,6 +726,10 @@ static int spangroup_run(tsdbhip_ctx* ctx, const tsdbhip_sg_desc* d, tsdbhip_sg_
       r.e_off = eoff; r.e_len = e_len; r.e_ts = e_ts; r.e_val = e_val; r.e_flt = e_flt; r.n_kept = n_kept;
       r.grid = gridv; r.T = T; r.bitmap = bitmap; r.word_rank = word_rank; r.lo = lo;
       r.spans_per_chunk = spc; r.n_chunks = n_chunks; r.tiles_per_wave = tpw; r.n_tile_groups = ntg;
+      r.d_info = direct ? dg.info : nullptr;
+      r.d_n = dg.n; r.d_ga = dg.ga; r.d_voff = dg.voff; r.d_x0 = dg.x0; r.d_step = dg.step; r.d_c0 = dg.c0;
+      r.d_r0 = dg.r0; r.span_row_start = span_row_start; r.kept = kept; r.row_cpre = dg.row_cpre;
+      r.row_ncells = row_ncells; r.row_val_off = row_val_off; r.val = val;
       r.ptr = scratch<uint32_t>(ctx, "cursor", n_waves * spc);
       const uint64_t np = (uint64_t)n_chunks * T;
       r.p_cnt = scratch<uint32_t>(ctx, "p_cnt", np);

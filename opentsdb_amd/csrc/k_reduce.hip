@@ -53,7 +53,49 @@ struct ReduceArgs {
   double* p_wdm;
   double* p_wdv;
   uint32_t* p_dhas;     // double min/max: a non-NaN value was seen
+  // direct spans (k_direct.hip; d_info null: none): values read from the
+  // reference's value bytes at grid rank - d_ga
+  const uint32_t* d_info;
+  const uint32_t* d_n;
+  const uint32_t* d_ga;
+  const uint64_t* d_voff;
+  const uint32_t* d_x0;
+  const uint32_t* d_step;
+  const uint32_t* d_c0;
+  const uint64_t* d_r0;
+  const uint64_t* span_row_start;
+  const uint32_t* kept;
+  const uint32_t* row_cpre;
+  const uint32_t* row_ncells;
+  const uint64_t* row_val_off;
+  const uint8_t* val;
 };
+
+// value bits of a direct span's cell (width 8: long / double bits; width 4:
+// int or float widened to double, RowSeq.java:194-226)
+DEVI int64_t direct_bits(uint64_t raw, uint32_t info) {
+  if (info & 4u /*DIR_W8*/) return (int64_t)bswap64(raw);
+  const uint32_t u = bswap32((uint32_t)raw);
+  if (info & 2u /*DIR_FLT*/) return dbits((double)__uint_as_float(u));
+  return (int64_t)(int32_t)u;
+}
+DEVI uint64_t direct_load(const uint8_t* p, uint32_t info) {
+  return (info & 4u) ? *(const uint64_t*)p : (uint64_t)*(const uint32_t*)p;
+}
+
+// byte offset of E index e of a direct span whose points cross rows
+DEVI uint64_t direct_multi_off(const ReduceArgs& r, uint32_t k, int64_t e) {
+  const uint32_t s = r.kept[k];
+  const uint64_t r0 = r.span_row_start[s], r1 = r.span_row_start[s + 1];
+  const uint32_t c = r.d_c0[k] + (uint32_t)e;
+  uint64_t lo = r0, hi = r1 - 1;  // last row with cpre <= c
+  while (lo < hi) {
+    const uint64_t mid = (lo + hi + 1) >> 1;
+    if (r.row_cpre[mid] <= c) lo = mid; else hi = mid - 1;
+  }
+  const uint32_t w = (r.d_info[k] & 4u) ? 8u : 4u;
+  return r.row_val_off[lo] + (uint64_t)w * (c - r.row_cpre[lo]);
+}
 
 struct Acc {
   uint32_t cnt;
@@ -156,6 +198,88 @@ DEVI double lerp_double(int64_t x, int64_t x0, double y0, int64_t x1, double y1)
   return y0 + ((double)(x - x0) * (y1 - y0)) / (double)(x1 - x0);
 }
 
+// acc_push on active lanes only, without a branch: the push is computed on
+// a copy and selected (no exec-mask juggling on the scalar unit).
+template <int AGG, int MODE>
+DEVI void acc_push_if(Acc& a, bool act, int64_t yi, double yd) {
+  Acc b = a;
+  acc_push<AGG, MODE>(b, yi, yd);
+  a.cnt = act ? b.cnt : a.cnt;
+  a.flag = act ? b.flag : a.flag;
+  a.dhas = act ? b.dhas : a.dhas;
+  a.ia = act ? b.ia : a.ia;
+  a.da = act ? b.da : a.da;
+  a.wi.n = act ? b.wi.n : a.wi.n;
+  a.wi.mean = act ? b.wi.mean : a.wi.mean;
+  a.wi.var = act ? b.wi.var : a.wi.var;
+  a.wd.n = act ? b.wd.n : a.wd.n;
+  a.wd.mean = act ? b.wd.mean : a.wd.mean;
+  a.wd.var = act ? b.wd.var : a.wd.var;
+}
+
+template <uint32_t W, bool FLT>
+DEVI int64_t dbits_of(uint64_t raw) {
+  if (W == 8) return (int64_t)bswap64(raw);
+  const uint32_t u = bswap32((uint32_t)raw);
+  if (FLT) return dbits((double)__uint_as_float(u));
+  return (int64_t)(int32_t)u;
+}
+template <uint32_t W>
+DEVI uint64_t dload(const uint8_t* p) {
+  if (W == 8) return *(const uint64_t*)p;
+  return (uint64_t)*(const uint32_t*)p;
+}
+
+// A run of `run` (<= 8) single-row direct spans of one value width and type,
+// batch lanes i..i+run-1: all value loads issued first, branch-free
+// (inactive lanes read E[0]), then pushed in span order.
+template <int AGG, int MODE, bool RATE, uint32_t W, bool FLT>
+DEVI void direct_run(const ReduceArgs& r, Acc& acc, uint32_t run, uint32_t i, uint64_t dvo_l, uint32_t dga_l,
+                     uint32_t dn_l, uint32_t dx0_l, uint32_t dstep_l, uint64_t g, bool gv) {
+  uint64_t raw[8], rawp0[8];
+  bool act[8];
+  int64_t ev[8];
+#pragma unroll
+  for (uint32_t u = 0; u < 8; u++) {
+    // (past the run: repeat its last span, so the loads stay straight-line)
+    const int ln = (int)(i + min(u, run - 1));
+    const uint32_t ga = readlane_u32(dga_l, ln), n = readlane_u32(dn_l, ln);
+    const uint64_t vo = readlane_u64(dvo_l, ln);
+    const int64_t e = (int64_t)g - (int64_t)ga;
+    ev[u] = e;
+    act[u] = gv && (RATE ? (n >= 2 && e <= (int64_t)n - 2) : (e >= 0 && e < (int64_t)n));
+    const int64_t ec = act[u] ? (RATE ? (e < 0 ? 0 : e + 1) : e) : 0;
+    raw[u] = dload<W>(r.val + vo + W * (uint64_t)ec);
+    if (RATE) {  // lane 0's previous cell (the other lanes take their neighbour's)
+      const int64_t ep = (lane_id() == 0 && act[u] && e >= 0) ? e : ec;
+      rawp0[u] = dload<W>(r.val + vo + W * (uint64_t)ep);
+    }
+  }
+  __builtin_amdgcn_sched_barrier(0);  // keep every load of the run ahead of the first use
+#pragma unroll
+  for (uint32_t u = 0; u < 8; u++) {
+    if (u >= run) break;
+    const int64_t b = dbits_of<W, FLT>(raw[u]);
+    if (RATE) {
+      const uint32_t step = readlane_u32(dstep_l, (int)(i + u));
+      const double diff = to_double(b, FLT) - to_double(dbits_of<W, FLT>(wave_shr1_u64(raw[u], rawp0[u])), FLT);
+      double v;
+      // x_cur - x_prev = step; a power-of-two step divides exactly as a
+      // product with its (exact) reciprocal: same IEEE result, no divide
+      if ((step & (step - 1)) == 0) v = diff * __builtin_amdgcn_ldexp(1.0, -(int)__builtin_ctz(step));
+      else v = diff / (double)(int64_t)step;
+      if (ballot(act[u] && ev[u] < 0)) {  // Q5: before the span's second point, y0 / x0
+        const uint32_t x0 = readlane_u32(dx0_l, (int)(i + u));
+        if (ev[u] < 0) v = to_double(b, FLT) / (double)(int64_t)x0;
+      }
+      acc_push_if<AGG, MODE>(acc, act[u], 0, v);
+    } else {
+      if (MODE == MODE_DUAL && FLT && act[u]) acc.flag |= 1u;
+      acc_push_if<AGG, MODE>(acc, act[u], b, MODE == MODE_INT ? 0.0 : to_double(b, MODE == MODE_DBL || FLT));
+    }
+  }
+}
+
 template <int AGG, int MODE, bool RATE>
 __global__ void __launch_bounds__(256) k_reduce(ReduceArgs r) {
   const int lane = lane_id();
@@ -183,6 +307,7 @@ __global__ void __launch_bounds__(256) k_reduce(ReduceArgs r) {
   {
     const int64_t t0 = r.grid[tb * WAVE];
     for (uint32_t k = k0 + lane; k < k1; k += WAVE) {
+      if (r.d_info && (r.d_info[k] & 1u)) { ptr[k - k0] = 0; continue; }
       const uint64_t eo = r.e_off[k];
       uint32_t lo = base_idx, hi = r.e_len[k];
       if (hi < lo) hi = lo;
@@ -281,20 +406,98 @@ __global__ void __launch_bounds__(256) k_reduce(ReduceArgs r) {
         acc_push<AGG, MODE>(acc, yi, yd);
       }
     };
+    // A direct span (k_direct.hip) at lane g: E index e = g - ga; its value
+    // is the cell itself (non-rate: active iff 0 <= e < n), or its constant-
+    // step difference (rate: e = j - 1 for point j; e < 0 is the Q5 state
+    // cur = e_0, prev = (0, 0); active iff n >= 2 and e <= n - 2).
+    auto direct_push = [&](uint32_t info, bool act, int64_t e, uint64_t raw, uint64_t rawp, uint32_t x0,
+                           uint32_t step) {
+      if (!act) return;
+      const bool flt = (info & 2u) != 0;
+      const int64_t b = direct_bits(raw, info);
+      if (RATE) {
+        double v;
+        if (e < 0) {
+          v = to_double(b, flt) / (double)(int64_t)x0;
+        } else {
+          const double diff = to_double(b, flt) - to_double(direct_bits(rawp, info), flt);
+          // x_cur - x_prev = step; a power-of-two step divides exactly as a
+          // product with its (exact) reciprocal: same IEEE result, no divide
+          if ((step & (step - 1)) == 0) v = diff * __builtin_amdgcn_ldexp(1.0, -(int)__builtin_ctz(step));
+          else v = diff / (double)(int64_t)step;
+        }
+        acc_push<AGG, MODE>(acc, 0, v);
+        return;
+      }
+      if (MODE == MODE_DUAL && flt) acc.flag |= 1u;
+      acc_push<AGG, MODE>(acc, b, MODE == MODE_INT ? 0.0 : to_double(b, MODE == MODE_DBL || flt));
+    };
+    // one direct span, any row layout
+    auto direct_one = [&](uint32_t k, uint32_t info, uint32_t ga, uint32_t n, uint64_t vo) {
+      const int64_t e = (int64_t)g - (int64_t)ga;
+      const bool act = gv && (RATE ? (n >= 2 && e <= (int64_t)n - 2) : (e >= 0 && e < (int64_t)n));
+      const int64_t ec = RATE ? (e < 0 ? 0 : e + 1) : e;  // the cell read
+      const bool multi = (info & 8u) != 0;
+      uint64_t raw = 0, rawp = 0;
+      if (act) raw = direct_load(r.val + (multi ? direct_multi_off(r, k, ec) : vo + ((info & 4u) ? 8 : 4) * ec), info);
+      uint32_t x0 = 0, step = 0;
+      if (RATE) {
+        rawp = shfl_up_u64(raw, 1);
+        if (lane == 0 && act && e >= 0)
+          rawp = direct_load(r.val + (multi ? direct_multi_off(r, k, e) : vo + ((info & 4u) ? 8 : 4) * e), info);
+        x0 = r.d_x0[k];
+        step = r.d_step[k];
+      }
+      direct_push(info, act, e, raw, rawp, x0, step);
+    };
     constexpr bool ALIGNED_OK = !RATE && MODE != MODE_DUAL;
     for (uint32_t kb = k0; kb < k1; kb += WAVE) {
       const uint32_t kl = kb + lane;
       const bool kv = kl < k1;
-      const uint64_t eo_l = kv ? r.e_off[kl] : 0;
-      const uint32_t len_l = kv ? r.e_len[kl] : 0;
+      const uint32_t dinfo_l = (r.d_info && kv) ? r.d_info[kl] : 0u;
+      const bool dl = (dinfo_l & 1u) != 0;
+      const uint64_t eo_l = kv && !dl ? r.e_off[kl] : 0;
+      const uint32_t len_l = kv && !dl ? r.e_len[kl] : 0;
+      const uint64_t dmask = ballot(dl);
+      uint32_t dga_l = 0, dn_l = 0, dx0_l = 0, dstep_l = 0;
+      uint64_t dvo_l = 0;
+      uint64_t dsingle = 0;  // direct spans held in one row
+      if (dmask) {
+        if (dl) {
+          dga_l = r.d_ga[kl]; dn_l = r.d_n[kl]; dvo_l = r.d_voff[kl];
+          if (RATE) { dx0_l = r.d_x0[kl]; dstep_l = r.d_step[kl]; }
+        }
+        dsingle = ballot(dl && !(dinfo_l & 8u));
+      }
       uint64_t almask = 0;
       if (ALIGNED_OK) {
-        const bool al = kv && (uint64_t)len_l >= g0 + (uint64_t)nvalid &&
+        const bool al = kv && !dl && (uint64_t)len_l >= g0 + (uint64_t)nvalid &&
                         (int64_t)r.e_ts[eo_l + g0] == t_first && (int64_t)r.e_ts[eo_l + g0 + nvalid - 1] == t_last;
         almask = ballot(al);
       }
       const uint32_t nb = min((uint32_t)WAVE, k1 - kb);
       for (uint32_t i = 0; i < nb;) {
+        if ((dsingle >> i) & 1) {
+          // a run of single-row direct spans with this span's width and type
+          const uint32_t info0 = readlane_u32(dinfo_l, (int)i);
+          const uint64_t m = ballot(dl && !(dinfo_l & 8u) && dinfo_l == info0) >> i;
+          const uint32_t run = min(8u, ~m == 0 ? 64u : (uint32_t)__builtin_ctzll(~m));
+          if (info0 & 4u) {
+            if (info0 & 2u) direct_run<AGG, MODE, RATE, 8, true>(r, acc, run, i, dvo_l, dga_l, dn_l, dx0_l, dstep_l, g, gv);
+            else direct_run<AGG, MODE, RATE, 8, false>(r, acc, run, i, dvo_l, dga_l, dn_l, dx0_l, dstep_l, g, gv);
+          } else {
+            if (info0 & 2u) direct_run<AGG, MODE, RATE, 4, true>(r, acc, run, i, dvo_l, dga_l, dn_l, dx0_l, dstep_l, g, gv);
+            else direct_run<AGG, MODE, RATE, 4, false>(r, acc, run, i, dvo_l, dga_l, dn_l, dx0_l, dstep_l, g, gv);
+          }
+          i += run;
+          continue;
+        }
+        if ((dmask >> i) & 1) {
+          direct_one(kb + i, readlane_u32(dinfo_l, (int)i), readlane_u32(dga_l, (int)i), readlane_u32(dn_l, (int)i),
+                     readlane_u64(dvo_l, (int)i));
+          i++;
+          continue;
+        }
         if (ALIGNED_OK && ((almask >> i) & 1)) {
           const uint64_t m = almask >> i;  // bit 0: span kb + i
           const uint32_t run = min(8u, ~m == 0 ? 64u : (uint32_t)__builtin_ctzll(~m));
