@@ -589,7 +589,7 @@ static int spangroup_run(tsdbhip_ctx* ctx, const tsdbhip_sg_desc* d, tsdbhip_sg_
         dg.hi = hi;
         dg.rate = rate;
         ctx->hot_kernel = TSDBHIP_HOT_REDUCE_DIRECT;  // timed around k_reduce
-        hipLaunchKernelGGL(k_direct_scan, dim3(grid_for(n_kept, 256, 1u << 20)), dim3(256), 0, st, da, dg,
+        hipLaunchKernelGGL(k_direct_scan, dim3(grid_for(n_kept, 4 * DIRB, 1u << 20)), dim3(256), 0, st, da, dg,
                            row_ncells, row_val_len);
         fa.span_list = dg.list;
         fa.span_count = dg.list_count;

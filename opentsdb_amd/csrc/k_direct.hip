@@ -86,6 +86,17 @@ DEVI void pend_push(Pending& p, uint32_t k, uint32_t* list, uint32_t* count) {
   if (++p.cnt == WAVE) pend_flush(p, list, count);
 }
 
+// A row's qualifier bytes as a buffer resource (range rounded to the 8-byte
+// loads; the packer aligns rows to 8 B and buffers carry slack).
+DEVI __amdgpu_buffer_rsrc_t qual_rsrc(const uint8_t* p, uint32_t nc) {
+  return __builtin_amdgcn_make_buffer_rsrc((void*)p, 0, (int)((2u * nc + 7u) & ~7u), 0x00020000);
+}
+DEVI uint2 qload(__amdgpu_buffer_rsrc_t rs, uint32_t voff, uint32_t soff) {
+  const auto v = __builtin_amdgcn_raw_buffer_load_b64(rs, (int)voff, (int)soff, 0);
+  return make_uint2(v[0], v[1]);
+}
+
+#define DIRB 32           // spans per wave batch
 #define DIRG 8            // groups of 256 cells per wave iteration (4 cells per lane each)
 #define DIRQ (256 * DIRG)
 
@@ -103,12 +114,12 @@ __global__ void __launch_bounds__(256) k_direct_scan(DecodeArgs a, DirectArgs g,
   // the last marked pattern (regular series repeat it span after span)
   int64_t m_xf = -1;
   uint32_t m_step = 0, m_np = 0;
-  for (uint32_t kb = ufl(wave) * WAVE; kb < a.n_kept; kb += nwaves * WAVE) {
+  for (uint32_t kb = ufl(wave) * DIRB; kb < a.n_kept; kb += nwaves * DIRB) {
     const uint32_t kl = kb + lane;
     uint32_t s_l = 0, n_l = 0, nc_l = 0, vl_l = 0, base_l = 0;
     uint64_t r0_l = 0, r1_l = 0, qoff_l = 0, voff_l = 0;
     bool ok_l = false;
-    if (kl < a.n_kept) {
+    if (lane < DIRB && kl < a.n_kept) {
       s_l = a.kept[kl];
       r0_l = a.span_row_start[s_l];
       r1_l = a.span_row_start[s_l + 1];
@@ -123,7 +134,7 @@ __global__ void __launch_bounds__(256) k_direct_scan(DecodeArgs a, DirectArgs g,
         ok_l = a.row_ok[r0_l] != 0 && nc_l > 0;
       }
     }
-    const uint32_t nb = min((uint32_t)WAVE, a.n_kept - kb);
+    const uint32_t nb = min((uint32_t)DIRB, a.n_kept - kb);
     const uint64_t okm = ballot(ok_l);
     // qualifier chunks; the next span's first chunk is loaded while the
     // current span's last chunk is processed (`carry`)
@@ -181,12 +192,12 @@ __global__ void __launch_bounds__(256) k_direct_scan(DecodeArgs a, DirectArgs g,
         }
         if (lane == 0) g.row_cpre[r] = cell;
         if (lane == (int)(r - r0)) my_cpre = cell;
+        // the row's qualifiers through a buffer descriptor: 32-bit offsets with
+        // immediate group offsets, and loads past the row return 0 (no clamp)
+        const __amdgpu_buffer_rsrc_t rs = qual_rsrc(a.qual + qoff, nc);
         if (!(r == r0 && carry)) {
 #pragma unroll
-          for (int j = 0; j < DIRG; j++) {
-            const uint32_t c = 256 * j + 4 * lane;
-            cur[j] = *(const uint2*)(a.qual + qoff + 2ull * (c < nc ? c : 0));
-          }
+          for (int j = 0; j < DIRG; j++) cur[j] = qload(rs, 8u * lane + 512u * j, 0u);
         }
         carry = false;
         // cadence from the first two cells (lane 0 holds cells 0..3 of the row)
@@ -207,19 +218,14 @@ __global__ void __launch_bounds__(256) k_direct_scan(DecodeArgs a, DirectArgs g,
           const uint32_t nc0 = c0 + DIRQ;
           if (nc0 < nc) {
 #pragma unroll
-            for (int j = 0; j < DIRG; j++) {
-              const uint32_t c = nc0 + 256 * j + 4 * lane;
-              nxt[j] = *(const uint2*)(a.qual + qoff + 2ull * (c < nc ? c : 0));
-            }
+            for (int j = 0; j < DIRG; j++) nxt[j] = qload(rs, 8u * lane + 512u * j, 2u * nc0);
           } else if (r + 1 == r1 && i + 1 < nb && ((okm >> (i + 1)) & 1)) {
             const uint64_t nq = readlane_u64(qoff_l, (int)(i + 1));
             const uint32_t nn = readlane_u32(nc_l, (int)(i + 1));
             if ((nq & 7) == 0) {
+              const __amdgpu_buffer_rsrc_t ns = qual_rsrc(a.qual + nq, nn);
 #pragma unroll
-              for (int j = 0; j < DIRG; j++) {
-                const uint32_t c = 256 * j + 4 * lane;
-                nxt[j] = *(const uint2*)(a.qual + nq + 2ull * (c < nn ? c : 0));
-              }
+              for (int j = 0; j < DIRG; j++) nxt[j] = qload(ns, 8u * lane + 512u * j, 0u);
               carry_next = true;
             }
           }
@@ -228,26 +234,32 @@ __global__ void __launch_bounds__(256) k_direct_scan(DecodeArgs a, DirectArgs g,
             const uint32_t g0 = c0 + 256 * j;
             if (g0 >= nc) break;  // (uniform)
             // expected delta of this lane's first cell in the group
-            const uint32_t e0 = first - base + (cell + g0) * step + lane_off;
+            const uint32_t e0 = ufl(first - base + (cell + g0) * step) + lane_off;
             uint32_t q[4];
             q[0] = __builtin_amdgcn_perm(0u, cur[j].x, 0x0C0C0001u);
             q[1] = __builtin_amdgcn_perm(0u, cur[j].x, 0x0C0C0203u);
             q[2] = __builtin_amdgcn_perm(0u, cur[j].y, 0x0C0C0001u);
             q[3] = __builtin_amdgcn_perm(0u, cur[j].y, 0x0C0C0203u);
+            // lane's first cell against its expected delta, the next three
+            // against their predecessor + step
             if (g0 + 256 <= nc) {  // full group (uniform): no masking
+              accx |= (q[0] >> 4) ^ e0;
+#pragma unroll
+              for (int c = 1; c < 4; c++) accx |= ((q[c] >> 4) - (q[c - 1] >> 4)) ^ step;
 #pragma unroll
               for (int c = 0; c < 4; c++) {
-                accx |= (q[c] >> 4) ^ (e0 + (uint32_t)c * step);
                 qor |= q[c];
                 qand &= q[c];
               }
             } else {
+              const uint32_t cl = g0 + 4 * (uint32_t)lane;
+              accx |= cl < nc ? (q[0] >> 4) ^ e0 : 0u;
+#pragma unroll
+              for (int c = 1; c < 4; c++) accx |= cl + c < nc ? ((q[c] >> 4) - (q[c - 1] >> 4)) ^ step : 0u;
 #pragma unroll
               for (int c = 0; c < 4; c++) {
-                const bool v = g0 + 4 * (uint32_t)lane + (uint32_t)c < nc;
-                accx |= v ? (q[c] >> 4) ^ (e0 + (uint32_t)c * step) : 0u;
-                qor |= v ? q[c] : 0u;
-                qand &= v ? q[c] : 0xFFFFu;
+                qor |= cl + c < nc ? q[c] : 0u;
+                qand &= cl + c < nc ? q[c] : 0xFFFFu;
               }
             }
           }
