@@ -244,6 +244,73 @@ __global__ void __launch_bounds__(256) k_assemble_fast(AssembleArgs a, uint32_t*
   }
 }
 
+// Span.addRow / RowSeq.addRow walk (the first loop of assemble_slow) with
+// the rows' metadata loaded 64 at a time by the wave and the decision chain
+// run uniformly over lanes (readlane): exact for every span whose rows never
+// restart a RowSeq (time_adj <= 0), never overflow the `short` value index,
+// and whose first accepted cell is at or after start (no seek inside a row).
+// Returns false (nothing written that the slow walk does not rewrite) when
+// the span needs the slow walk.
+DEVI bool assemble_walk(const AssembleArgs& a, uint32_t s, uint64_t r0, uint64_t r1) {
+  const int lane = lane_id();
+  int64_t rs_base = -1, last_ts = 0;
+  uint32_t cum = 0;           // value bytes of the current RowSeq
+  uint32_t cell = 0;
+  int64_t first_ts = -1, last_all = 0;
+  for (uint64_t rb = r0; rb < r1; rb += WAVE) {
+    const uint64_t r = rb + lane;
+    const bool valid = r < r1;
+    uint32_t n = 0, base = 0, fdt = 0, ldt = 0, vb = 0;
+    if (valid) {
+      n = a.row_ncells[r];
+      base = a.row_base[r];
+      if (n > 0) {
+        fdt = load_qual(a.qual, a.row_qual_off[r]) >> 4;
+        ldt = load_qual(a.qual, a.row_qual_off[r] + 2ull * (n - 1)) >> 4;
+        vb = row_value_bytes(a, r);
+      }
+    }
+    if (ballot(valid && n == 0)) return false;  // (the slow walk reports it)
+    const uint32_t nb = (uint32_t)min((uint64_t)WAVE, r1 - rb);
+    uint32_t st = 0;  // this lane's row: 0 dropped, 1 merged, 2 starts a RowSeq
+    for (uint32_t j = 0; j < nb; j++) {
+      const int64_t b = (int64_t)readlane_u32(base, (int)j);
+      const int64_t first = b + readlane_u32(fdt, (int)j), last = b + readlane_u32(ldt, (int)j);
+      const uint32_t v = readlane_u32(vb, (int)j);
+      uint32_t x = 0;
+      if (rs_base < 0) {
+        x = 2; rs_base = b; last_ts = last; cum = v;
+      } else if (last - rs_base < 4096) {  // merge into the last RowSeq (Span.java:117-121)
+        if (b - rs_base <= 0) return false;  // restart / illegal: slow walk
+        if (last_ts < first) { x = 1; last_ts = last; cum += v; }  // else RowSeq.java:142-148
+      } else if (last_ts < first) {        // else Span.java:126-130: dropped
+        x = 2; rs_base = b; last_ts = last; cum = v;
+      }
+      if (cum >= 32768u) return false;     // short value_index overflow: slow walk
+      if (x && first_ts < 0) first_ts = first;
+      if (x) last_all = last;
+      st = lane == (int)j ? x : st;
+    }
+    const uint32_t acc = st ? n : 0u;
+    const uint32_t incl = wave_incl_scan_u32(acc);
+    if (valid) {
+      a.row_ok[r] = (uint8_t)st;
+      a.row_cell0[r] = cell + incl - acc;
+    }
+    cell += readlane_u32(incl, 63);
+  }
+  if (first_ts < a.start) return false;  // seek inside the first RowSeq (Q1): slow walk
+  if (lane == 0) {
+    a.sp_ncells[s] = cell;
+    a.sp_first[s] = first_ts;
+    a.sp_last[s] = last_all;
+    a.sp_ovf_cell[s] = -1;
+    a.sp_q1[s] = -1;
+    a.sp_q1_shift[s] = 0;
+  }
+  return true;
+}
+
 // One wave per span (of `list`, or of all spans when list is null). The
 // common case (rows in strictly increasing base order, each row starting
 // after the previous one ended, no RowSeq merge possible) is verified
@@ -294,13 +361,14 @@ __global__ void __launch_bounds__(256) k_assemble(AssembleArgs a, const uint32_t
         a.sp_q1[s] = -1;
         a.sp_q1_shift[s] = 0;
       }
-    } else if (lane == 0) {
-      if (r1 == r0) {
+    } else if (r1 == r0) {
+      if (lane == 0) {
         a.sp_ncells[s] = 0; a.sp_first[s] = 0; a.sp_last[s] = -1;
         a.sp_ovf_cell[s] = -1; a.sp_q1[s] = -1; a.sp_q1_shift[s] = 0;
-      } else {
-        assemble_slow(a, s, r0, r1);
       }
+    } else if (!assemble_walk(a, s, r0, r1)) {
+      __threadfence_block();
+      if (lane == 0) assemble_slow(a, s, r0, r1);
     }
     if (lane == 0) {
       __threadfence_block();

@@ -46,6 +46,17 @@ def test_sharded_regular_ds(sctx, agg, rate):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("agg", [0, 2, 4])
+@pytest.mark.parametrize("rate", [False, True])
+def test_sharded_regular_nods_direct(sctx, agg, rate):
+    """no downsampling on regular series: the direct path (k_direct.hip), whose
+    consecutive-rank test runs against the exchanged (global) grid"""
+    ss = synth.regular(30, 1200, _abi.SYN_INT64_COUNTER, seed=5, step=5)
+    g, o = run_sharded(sctx, ss, agg=agg, rate=rate)
+    assert_same(g, o)
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("agg", [0, 3, 4])
 def test_sharded_c3s_shape(sctx, agg):
     ss = synth.regular(300, 3600, _abi.SYN_INT64_COUNTER, seed=3, step=1)
