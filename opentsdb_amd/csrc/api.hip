@@ -315,7 +315,8 @@ template <int AGG, int MODE, bool RATE>
 static void launch_reduce(tsdbhip_ctx* ctx, unsigned blocks, const ReduceArgs& r, const FinalArgs& f,
                           bool par, bool finalize) {
   if (ctx->time_reduce) HIPCHK(hipEventRecord(ctx->ev[8], ctx->stream));
-  hipLaunchKernelGGL((k_reduce<AGG, MODE, RATE>), dim3(blocks), dim3(256), 0, ctx->stream, r);
+  if (r.d_info) hipLaunchKernelGGL((k_reduce<AGG, MODE, RATE, true>), dim3(blocks), dim3(256), 0, ctx->stream, r);
+  hipLaunchKernelGGL((k_reduce<AGG, MODE, RATE, false>), dim3(blocks), dim3(256), 0, ctx->stream, r);
   if (ctx->time_reduce) HIPCHK(hipEventRecord(ctx->ev[9], ctx->stream));
   if (!finalize) return;
   if (par)
@@ -730,7 +731,18 @@ static int spangroup_run(tsdbhip_ctx* ctx, const tsdbhip_sg_desc* d, tsdbhip_sg_
       r.d_n = dg.n; r.d_ga = dg.ga; r.d_voff = dg.voff; r.d_x0 = dg.x0; r.d_step = dg.step; r.d_c0 = dg.c0;
       r.d_r0 = dg.r0; r.span_row_start = span_row_start; r.kept = kept; r.row_cpre = dg.row_cpre;
       r.row_ncells = row_ncells; r.row_val_off = row_val_off; r.val = val;
+      r.chunk_e = nullptr;
+      if (direct) {
+        uint32_t* ce = scratch<uint32_t>(ctx, "chunk_e", n_chunks, true);
+        if (n_kept)
+          hipLaunchKernelGGL(k_chunk_flags, dim3(grid_for(n_kept, 256)), dim3(256), 0, st, dg.info, n_kept, spc, ce);
+        r.chunk_e = ce;
+      }
       r.ptr = scratch<uint32_t>(ctx, "cursor", n_waves * spc);
+      r.st_x = scratch<uint2>(ctx, "st_x", n_waves * spc);
+      r.st_y = scratch<longlong2>(ctx, "st_y", n_waves * spc);
+      r.st_rv = scratch<double>(ctx, "st_rv", n_waves * spc);
+      r.st_f = scratch<uint32_t>(ctx, "st_f", n_waves * spc);
       const uint64_t np = (uint64_t)n_chunks * T;
       r.p_cnt = scratch<uint32_t>(ctx, "p_cnt", np);
       r.p_flag = scratch<uint8_t>(ctx, "p_flag", np);

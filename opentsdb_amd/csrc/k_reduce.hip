@@ -42,7 +42,15 @@ struct ReduceArgs {
   uint32_t n_chunks;
   uint32_t tiles_per_wave;
   uint32_t n_tile_groups;
-  uint32_t* ptr;        // [n_waves * spans_per_chunk] per-wave span cursors
+  uint32_t* ptr;        // [n_waves * spans_per_chunk] per-wave span cursors j
+  // per-wave span bracket cache (same indexing as ptr): after a tile, for
+  // cursor j (first point past the tile): x/y/type of points j-1 and j (rate:
+  // the rate value of point j-1), so a span without points in the next tile
+  // is evaluated from registers
+  uint2* st_x;          // (x_{j-1}, x_j)    x_j = UINT32_MAX past the end
+  longlong2* st_y;      // (y_{j-1}, y_j)
+  double* st_rv;        // rate value at point j-1
+  uint32_t* st_f;       // bit0 float(j-1), bit1 float(j), bit2 cache valid
   // partials [n_chunks][T]
   uint32_t* p_cnt;
   uint8_t* p_flag;      // bit0 isFloat contribution, bit1 first double is NaN
@@ -53,6 +61,7 @@ struct ReduceArgs {
   double* p_wdm;
   double* p_wdv;
   uint32_t* p_dhas;     // double min/max: a non-NaN value was seen
+  const uint32_t* chunk_e;  // [n_chunks] chunk holds an E (non-direct) span
   // direct spans (k_direct.hip; d_info null: none): values read from the
   // reference's value bytes at grid rank - d_ga
   const uint32_t* d_info;
@@ -280,7 +289,10 @@ DEVI void direct_run(const ReduceArgs& r, Acc& acc, uint32_t run, uint32_t i, ui
   }
 }
 
-template <int AGG, int MODE, bool RATE>
+// DONLY: the instantiation for span chunks holding direct spans only (no E
+// span state, fewer registers); with direct spans present both are launched
+// and each takes the chunks r.chunk_e marks as its own.
+template <int AGG, int MODE, bool RATE, bool DONLY>
 __global__ void __launch_bounds__(256) k_reduce(ReduceArgs r) {
   const int lane = lane_id();
   const uint32_t wave = (blockIdx.x * blockDim.x + threadIdx.x) / WAVE;
@@ -288,6 +300,8 @@ __global__ void __launch_bounds__(256) k_reduce(ReduceArgs r) {
   if (wave >= n_waves) return;
   const uint32_t chunk = wave % r.n_chunks;
   const uint32_t tg = wave / r.n_chunks;
+  if (r.d_info && (r.chunk_e[chunk] != 0) == DONLY) return;  // the other instantiation's chunk
+  if (!r.d_info && DONLY) return;
   const uint32_t k0 = chunk * r.spans_per_chunk;
   const uint32_t k1 = min(r.n_kept, k0 + r.spans_per_chunk);
   const uint64_t n_tiles = (r.T + WAVE - 1) / WAVE;
@@ -304,9 +318,10 @@ __global__ void __launch_bounds__(256) k_reduce(ReduceArgs r) {
   uint32_t* ptr = r.ptr + (uint64_t)wave * r.spans_per_chunk;
   const uint32_t base_idx = RATE ? 1u : 0u;
   // cursor init: first point index >= base_idx with ts >= G[tb*64]
-  {
+  if (!DONLY) {
     const int64_t t0 = r.grid[tb * WAVE];
     for (uint32_t k = k0 + lane; k < k1; k += WAVE) {
+      r.st_f[(uint64_t)wave * r.spans_per_chunk + (k - k0)] = 0;
       if (r.d_info && (r.d_info[k] & 1u)) { ptr[k - k0] = 0; continue; }
       const uint64_t eo = r.e_off[k];
       uint32_t lo = base_idx, hi = r.e_len[k];
@@ -339,14 +354,13 @@ __global__ void __launch_bounds__(256) k_reduce(ReduceArgs r) {
     // search and no lerp: lane l takes E[g0 + l]; runs of such spans load
     // their values up to 8 spans ahead. Every other span takes the general
     // path (cursor, grid ranks, lerp / rate).
-    auto general = [&](uint32_t k, uint64_t eo, uint32_t len) {
+    auto general = [&](uint32_t k, uint64_t eo, uint32_t len, uint32_t j) -> uint32_t {
       const int64_t first = r.e_ts[eo], last = r.e_ts[eo + len - 1];
       if (RATE) {
-        if (len < 2 || last < t_first) return;
+        if (len < 2 || last < t_first) return j;
       } else {
-        if (first > t_last || last < t_first) return;  // not started (F*) / expired
+        if (first > t_last || last < t_first) return j;  // not started (F*) / expired
       }
-      const uint32_t j = ptr[k - k0];
       const uint32_t idx = j + lane;
       const int64_t pts = idx < len ? (int64_t)r.e_ts[eo + idx] : INT64_MAX;
       const bool in = pts <= t_last;
@@ -362,29 +376,29 @@ __global__ void __launch_bounds__(256) k_reduce(ReduceArgs r) {
       } else {
         M = 0;
       }
-      if (lane == 0) ptr[k - k0] = j + kk;
+      const uint32_t jn = j + kk;
       const int cl = __popcll(M & lanemask_le(lane));
       const int64_t cur = (int64_t)j + cl - 1;
       // bracket timestamps: inside the tile they are this wave's loaded points
       const int64_t ts_in = (int64_t)shfl_u64((uint64_t)pts, cl > 0 ? cl - 1 : 0);
-      if (!gv) return;
+      if (!gv) return jn;
       if (RATE) {
-        if (tl > last) return;
+        if (tl > last) return jn;
         const int64_t xc = cl > 0 ? ts_in : (int64_t)r.e_ts[eo + cur];
         const double yc = to_double(r.e_val[eo + cur], r.e_flt[eo + cur] != 0);
         double yp = 0.0;
         int64_t xp = 0;
         if (cur >= 1) { xp = r.e_ts[eo + cur - 1]; yp = to_double(r.e_val[eo + cur - 1], r.e_flt[eo + cur - 1] != 0); }
         acc_push<AGG, MODE>(acc, 0, (yc - yp) / (double)(xc - xp));
-        return;
+        return jn;
       }
       if (cur < 0) {  // not started: next slot holds e_0
         if (MODE == MODE_DUAL && r.e_flt[eo]) acc.flag |= 1u;
-        return;
+        return jn;
       }
       const int64_t xc = cl > 0 ? ts_in : (int64_t)r.e_ts[eo + cur];
       const bool active = (uint32_t)cur < len - 1 || xc == tl;
-      if (!active) return;  // expired: nothing in either slot
+      if (!active) return jn;  // expired: nothing in either slot
       const int64_t vc = r.e_val[eo + cur];
       bool fc = false, fn = false;
       if (MODE == MODE_DUAL) {
@@ -405,6 +419,26 @@ __global__ void __launch_bounds__(256) k_reduce(ReduceArgs r) {
                            to_double(vn, MODE == MODE_DBL || fn));
         acc_push<AGG, MODE>(acc, yi, yd);
       }
+      return jn;
+    };
+    // A span with no point in this tile (its next point j lies past t_last):
+    // every lane's bracket is (j-1, j), all from the cache.
+    auto cached = [&](uint32_t j, uint32_t len, uint2 x, longlong2 y, double rv, uint32_t f) {
+      if (!gv || j >= len) return;  // expired (all points consumed before this tile)
+      if (RATE) {  // cur = j-1 (j >= 1), constant over the tile; active: tl <= last
+        if (len >= 2) acc_push<AGG, MODE>(acc, 0, rv);
+        return;
+      }
+      if (j == 0) return;  // not started (F* covers the float look-ahead)
+      const bool fc = (f & 1u) != 0, fn = (f & 2u) != 0;
+      if (MODE == MODE_DUAL && (fc || fn)) acc.flag |= 1u;
+      int64_t yi = 0;
+      double yd = 0.0;
+      if (MODE != MODE_DBL) yi = lerp_long(tl, (int64_t)x.x, y.x, (int64_t)x.y, y.y);
+      if (MODE != MODE_INT)
+        yd = lerp_double(tl, (int64_t)x.x, to_double(y.x, MODE == MODE_DBL || fc), (int64_t)x.y,
+                         to_double(y.y, MODE == MODE_DBL || fn));
+      acc_push<AGG, MODE>(acc, yi, yd);
     };
     // A direct span (k_direct.hip) at lane g: E index e = g - ga; its value
     // is the cell itself (non-rate: active iff 0 <= e < n), or its constant-
@@ -455,9 +489,26 @@ __global__ void __launch_bounds__(256) k_reduce(ReduceArgs r) {
       const uint32_t kl = kb + lane;
       const bool kv = kl < k1;
       const uint32_t dinfo_l = (r.d_info && kv) ? r.d_info[kl] : 0u;
-      const bool dl = (dinfo_l & 1u) != 0;
+      const bool dl = DONLY || (dinfo_l & 1u) != 0;
       const uint64_t eo_l = kv && !dl ? r.e_off[kl] : 0;
       const uint32_t len_l = kv && !dl ? r.e_len[kl] : 0;
+      // E spans: cursor and bracket cache, lane = span
+      const uint64_t sl = (uint64_t)wave * r.spans_per_chunk + (kl - k0);
+      const bool el = !DONLY && kv && !dl;
+      uint32_t j_l = 0, f_l = 0;
+      uint2 x_l = make_uint2(0, 0);
+      longlong2 y_l = make_longlong2(0, 0);
+      double rv_l = 0.0;
+      if (el) {
+        j_l = ptr[kl - k0];
+        f_l = r.st_f[sl];
+        if (f_l & 4u) {
+          x_l = r.st_x[sl];
+          if (RATE) rv_l = r.st_rv[sl];
+          else y_l = r.st_y[sl];
+        }
+      }
+      bool dirty_l = false;
       const uint64_t dmask = ballot(dl);
       uint32_t dga_l = 0, dn_l = 0, dx0_l = 0, dstep_l = 0;
       uint64_t dvo_l = 0;
@@ -470,11 +521,13 @@ __global__ void __launch_bounds__(256) k_reduce(ReduceArgs r) {
         dsingle = ballot(dl && !(dinfo_l & 8u));
       }
       uint64_t almask = 0;
-      if (ALIGNED_OK) {
-        const bool al = kv && !dl && (uint64_t)len_l >= g0 + (uint64_t)nvalid &&
-                        (int64_t)r.e_ts[eo_l + g0] == t_first && (int64_t)r.e_ts[eo_l + g0 + nvalid - 1] == t_last;
+      if (ALIGNED_OK) {  // (cursor at g0 first: the end check loads only then)
+        bool al = el && j_l == g0 && (uint64_t)len_l >= g0 + (uint64_t)nvalid;
+        if (al) al = (int64_t)r.e_ts[eo_l + g0] == t_first && (int64_t)r.e_ts[eo_l + g0 + nvalid - 1] == t_last;
         almask = ballot(al);
       }
+      // spans with no point in this tile take the cache
+      const uint64_t cmask = ballot(el && !((almask >> lane) & 1) && (f_l & 4u) && (j_l >= len_l || (int64_t)x_l.y > t_last));
       const uint32_t nb = min((uint32_t)WAVE, k1 - kb);
       for (uint32_t i = 0; i < nb;) {
         if ((dsingle >> i) & 1) {
@@ -492,7 +545,7 @@ __global__ void __launch_bounds__(256) k_reduce(ReduceArgs r) {
           i += run;
           continue;
         }
-        if ((dmask >> i) & 1) {
+        if (DONLY || ((dmask >> i) & 1)) {
           direct_one(kb + i, readlane_u32(dinfo_l, (int)i), readlane_u32(dga_l, (int)i), readlane_u32(dn_l, (int)i),
                      readlane_u64(dvo_l, (int)i));
           i++;
@@ -511,13 +564,66 @@ __global__ void __launch_bounds__(256) k_reduce(ReduceArgs r) {
           for (uint32_t u = 0; u < 8; u++) {
             if (u >= run) break;
             if (gv) acc_push<AGG, MODE>(acc, v[u], MODE == MODE_INT ? 0.0 : to_double(v[u], true));
-            if (lane == 0) ptr[kb + i + u - k0] = (uint32_t)(g0 + nvalid);
           }
+          // cursor past the tile; cache stale (refilled by the general path)
+          if ((uint32_t)lane >= i && (uint32_t)lane < i + run) { j_l = (uint32_t)(g0 + nvalid); f_l = 0; dirty_l = true; }
           i += run;
           continue;
         }
-        general(kb + i, readlane_u64(eo_l, (int)i), readlane_u32(len_l, (int)i));
+        if ((cmask >> i) & 1) {
+          const uint2 x = make_uint2(readlane_u32(x_l.x, (int)i), readlane_u32(x_l.y, (int)i));
+          longlong2 y = make_longlong2(0, 0);
+          double rv = 0.0;
+          if (RATE) rv = __longlong_as_double((long long)readlane_u64((uint64_t)__double_as_longlong(rv_l), (int)i));
+          else y = make_longlong2((long long)readlane_u64((uint64_t)y_l.x, (int)i),
+                                  (long long)readlane_u64((uint64_t)y_l.y, (int)i));
+          cached(readlane_u32(j_l, (int)i), readlane_u32(len_l, (int)i), x, y, rv, readlane_u32(f_l, (int)i));
+          i++;
+          continue;
+        }
+        {
+          const uint64_t eo = readlane_u64(eo_l, (int)i);
+          const uint32_t len = readlane_u32(len_l, (int)i);
+          const uint32_t jn = general(kb + i, eo, len, readlane_u32(j_l, (int)i));
+          // refill the cache for cursor jn: points jn-1 and jn (rate: the
+          // rate value of jn-1, SpanGroup.java:741-755)
+          uint2 x = make_uint2(0, UINT32_MAX);
+          longlong2 y = make_longlong2(0, 0);
+          double rv = 0.0;
+          uint32_t f = 4u;
+          if (jn >= 1) {
+            x.x = r.e_ts[eo + jn - 1];
+            y.x = r.e_val[eo + jn - 1];
+            if (r.e_flt[eo + jn - 1]) f |= 1u;
+          }
+          if (jn < len) {
+            x.y = r.e_ts[eo + jn];
+            y.y = r.e_val[eo + jn];
+            if (r.e_flt[eo + jn]) f |= 2u;
+          }
+          if (RATE && jn >= 1) {
+            const double yc = to_double(y.x, (f & 1u) != 0);
+            if (jn >= 2) {
+              const int64_t xp = r.e_ts[eo + jn - 2];
+              const double yp = to_double(r.e_val[eo + jn - 2], r.e_flt[eo + jn - 2] != 0);
+              rv = (yc - yp) / (double)((int64_t)x.x - xp);
+            } else {
+              rv = yc / (double)(int64_t)x.x;  // Q5: prev = (0, 0)
+            }
+          }
+          if (lane == (int)i) { j_l = jn; x_l = x; y_l = y; rv_l = rv; f_l = f; dirty_l = true; }
+        }
         i++;
+      }
+      // write back the cursors and caches that changed
+      if (dirty_l) {
+        ptr[kl - k0] = j_l;
+        r.st_f[sl] = f_l;
+        if (f_l & 4u) {
+          r.st_x[sl] = x_l;
+          if (RATE) r.st_rv[sl] = rv_l;
+          else r.st_y[sl] = y_l;
+        }
       }
     }
     if (gv) acc_store<AGG, MODE>(r, (uint64_t)chunk * r.T + g, acc);
@@ -525,6 +631,11 @@ __global__ void __launch_bounds__(256) k_reduce(ReduceArgs r) {
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
   }
+}
+
+__global__ void k_chunk_flags(const uint32_t* d_info, uint32_t n_kept, uint32_t spc, uint32_t* chunk_e) {
+  const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
+  if (k < n_kept && !(d_info[k] & 1u)) chunk_e[k / spc] = 1u;
 }
 
 // ------------------------------------------------------------- finalize ---
