@@ -197,9 +197,9 @@ DEVI void acc_load(const ReduceArgs& r, uint64_t p, Acc& a) {
 // Java long lerp: y0 + (x - x0) * (y1 - y0) / (x1 - x0), 0 < x1 - x0 < 2^32.
 DEVI int64_t lerp_long(int64_t x, int64_t x0, int64_t y0, int64_t x1, int64_t y1) {
   const int64_t num = lmul(x - x0, lsub(y1, y0));
-  const uint64_t d = (uint64_t)(x1 - x0);
+  const uint32_t d = (uint32_t)(x1 - x0);  // timestamps are u32: 0 < d < 2^32
   const uint64_t mag = num < 0 ? (uint64_t)0 - (uint64_t)num : (uint64_t)num;
-  const uint64_t q = mag / d;
+  const uint64_t q = udiv64_32(mag, d);
   const int64_t sq = num < 0 ? (int64_t)((uint64_t)0 - q) : (int64_t)q;
   return ladd(y0, sq);
 }
@@ -413,7 +413,9 @@ __global__ void __launch_bounds__(256) k_reduce(ReduceArgs r) {
         const int64_t vn = r.e_val[eo + cur + 1];
         int64_t yi = 0;
         double yd = 0.0;
-        if (MODE != MODE_DBL) yi = lerp_long(tl, xc, vc, xn, vn);
+        // (dual: a float in the bracket puts t on the double path; the long
+        // lerp of this span is then never read)
+        if (MODE == MODE_INT || (MODE == MODE_DUAL && !fc && !fn)) yi = lerp_long(tl, xc, vc, xn, vn);
         if (MODE != MODE_INT)
           yd = lerp_double(tl, xc, to_double(vc, MODE == MODE_DBL || fc), xn,
                            to_double(vn, MODE == MODE_DBL || fn));
@@ -434,7 +436,7 @@ __global__ void __launch_bounds__(256) k_reduce(ReduceArgs r) {
       if (MODE == MODE_DUAL && (fc || fn)) acc.flag |= 1u;
       int64_t yi = 0;
       double yd = 0.0;
-      if (MODE != MODE_DBL) yi = lerp_long(tl, (int64_t)x.x, y.x, (int64_t)x.y, y.y);
+      if (MODE == MODE_INT || (MODE == MODE_DUAL && !fc && !fn)) yi = lerp_long(tl, (int64_t)x.x, y.x, (int64_t)x.y, y.y);
       if (MODE != MODE_INT)
         yd = lerp_double(tl, (int64_t)x.x, to_double(y.x, MODE == MODE_DBL || fc), (int64_t)x.y,
                          to_double(y.y, MODE == MODE_DBL || fn));
