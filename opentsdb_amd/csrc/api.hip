@@ -301,13 +301,23 @@ struct LaunchChunks {
     const uint32_t n_kept = da.n_kept;
     g.list = scratch<uint32_t>(ctx, "ck_list", n_kept);
     g.list_count = scratch<uint32_t>(ctx, "ck_list_count", 1, true);
+    g.in_list = nullptr;
+    g.in_count = nullptr;
+    // integer spans over every kept span, then float spans over the ones left
+    SpanDsArgs gf = g;
+    gf.in_list = g.list;
+    gf.in_count = g.list_count;
+    gf.list = scratch<uint32_t>(ctx, "ck_list2", n_kept);
+    gf.list_count = scratch<uint32_t>(ctx, "ck_list2_count", 1, true);
     HIPCHK(hipEventRecord(ctx->ev[8], st));
-    hipLaunchKernelGGL(k_ds_spans<AGG>, dim3(grid_for(n_kept, 4, 1u << 20)), dim3(256), 0, st, da, g, ncells,
-                       vlen);
+    hipLaunchKernelGGL((k_ds_spans<AGG, false>), dim3(grid_for(n_kept, 4, 1u << 20)), dim3(256), 0, st, da, g,
+                       ncells, vlen);
+    hipLaunchKernelGGL((k_ds_spans<AGG, true>), dim3(std::min(grid_for(n_kept, 4, 1u << 20), 2048u)), dim3(256), 0,
+                       st, da, gf, ncells, vlen);
     HIPCHK(hipEventRecord(ctx->ev[9], st));
     ctx->hot_kernel = TSDBHIP_HOT_DS_CHUNKS;
-    fa.span_list = g.list;
-    fa.span_count = g.list_count;
+    fa.span_list = gf.list;
+    fa.span_count = gf.list_count;
   }
 };
 

@@ -38,6 +38,8 @@ namespace tsdb {
 struct SpanDsArgs {
   uint32_t* list;        // spans left to the serial kernels
   uint32_t* list_count;  // [1]
+  const uint32_t* in_list;   // spans to take (null: every kept span)
+  const uint32_t* in_count;
   uint32_t* bitmap;      // union-grid bitmap over [lo, hi] (null: no marking)
   int64_t lo, hi;
   int32_t rate;
@@ -116,7 +118,7 @@ DEVI uint64_t ufl64(uint64_t x) { return ((uint64_t)ufl((uint32_t)(x >> 32)) << 
 // buckets); returns each lane's bucket ts (lane < cnt).
 template <int AGG>
 DEVI uint32_t bk_flush(const DecodeArgs& a, const BkLds& B, uint64_t eo, uint32_t cap, uint32_t b0, uint32_t cnt,
-                       bool& bad) {
+                       bool flt, bool& bad) {
   wave_lds_sync();
   const int lane = lane_id();
   uint32_t ts0 = 0;
@@ -127,14 +129,26 @@ DEVI uint32_t bk_flush(const DecodeArgs& a, const BkLds& B, uint64_t eo, uint32_
     if (i == (uint32_t)lane) ts0 = ts;
     if (b < cap) {
       a.e_ts[eo + b] = ts;
-      a.e_val[eo + b] = AGG == 3 ? ldiv64_32(B.v[i], n) : B.v[i];
-      a.e_flt[eo + b] = 0;
+      if (flt)  // Aggregators.Avg.runDouble: sum / n (Aggregators.java:172-180)
+        a.e_val[eo + b] = AGG == 3 ? dbits(bitsd(B.v[i]) / (double)(int32_t)n) : B.v[i];
+      else
+        a.e_val[eo + b] = AGG == 3 ? ldiv64_32(B.v[i], n) : B.v[i];
+      a.e_flt[eo + b] = flt ? 1 : 0;
     } else {
       bad = true;  // more buckets than E holds: cannot be the greedy chain
     }
   }
   wave_lds_sync();
   return ts0;
+}
+
+// runDouble of sum / min / max / avg, one value at a time in point order,
+// seeded with the first (Aggregators.java:86-180)
+template <int AGG>
+DEVI double ds_dcombine(double x, double y) {
+  if (AGG == 0 || AGG == 3) return x + y;
+  if (AGG == 1) return y < x ? y : x;
+  return y > x ? y : x;
 }
 
 template <int AGG>
@@ -146,7 +160,7 @@ DEVI int64_t ds_combine(int64_t x, int64_t y) {
 
 // One row of a span: its 512-cell chunks. Returns true if a precondition
 // breaks (the span then goes to the serial path).
-template <int AGG, int W>
+template <int AGG, int W, bool FLT>
 DEVI bool ds_row(const DecodeArgs& a, const SpanDsArgs& g, DsState& st, uint64_t eo, uint32_t cap,
                  uint64_t qoff, uint64_t voff, uint32_t base, uint32_t nc, uint32_t cell0, uint32_t* L_pt,
                  uint64_t* L_v, BkLds& BK) {
@@ -173,6 +187,7 @@ DEVI bool ds_row(const DecodeArgs& a, const SpanDsArgs& g, DsState& st, uint64_t
     qp[1] = qpair(cur.q.y);
     qp[2] = qpair(cur.q.z);
     qp[3] = qpair(cur.q.w);
+    constexpr bool prefix = PREFIX && !FLT;
     uint32_t dt[8];
 #pragma unroll
     for (int i = 0; i < 4; i++) {
@@ -182,9 +197,13 @@ DEVI bool ds_row(const DecodeArgs& a, const SpanDsArgs& g, DsState& st, uint64_t
     int64_t bits[8];
 #pragma unroll
     for (int j = 0; j < 8; j++) bits[j] = raw_value<W>(cur, j);
+    if (W == 4 && FLT) {  // float32 cells widened to double (RowSeq.java:216-226)
+#pragma unroll
+      for (int j = 0; j < 8; j++) bits[j] = dbits((double)__int_as_float((int32_t)bits[j]));
+    }
     // integer cells of width W (flags nibble of each qualifier), strictly
     // increasing deltas (Span/RowSeq order)
-    const uint32_t fl = (W - 1) * 0x00010001u;
+    const uint32_t fl = ((FLT ? 8u : 0u) | (W - 1)) * 0x00010001u;
     uint32_t nmine = 8;
     if (nv == DCH) {  // full chunk: every lane holds 8 cells
       bad |= (((qp[0] ^ fl) | (qp[1] ^ fl) | (qp[2] ^ fl) | (qp[3] ^ fl)) & 0x000F000Fu) != 0;
@@ -221,13 +240,13 @@ DEVI bool ds_row(const DecodeArgs& a, const SpanDsArgs& g, DsState& st, uint64_t
       pt += (uint32_t)j < nmine ? dt[j] : 0u;  // (nmine == 8 on full chunks)
       pv += (uint64_t)bits[j];
       pti[j] = pt;
-      pvi[j] = PREFIX ? pv : (uint64_t)bits[j];
+      pvi[j] = prefix ? pv : (uint64_t)bits[j];
     }
     const uint32_t xt = wave_incl_scan_u32_dpp(pt) - pt;
     *(uint4*)&L_pt[8 * lane] = make_uint4(pti[0] + xt, pti[1] + xt, pti[2] + xt, pti[3] + xt);
     *(uint4*)&L_pt[8 * lane + 4] = make_uint4(pti[4] + xt, pti[5] + xt, pti[6] + xt, pti[7] + xt);
     {
-      const uint64_t xv = PREFIX ? wave_incl_scan_u64_dpp(pv) - pv : 0ull;
+      const uint64_t xv = prefix ? wave_incl_scan_u64_dpp(pv) - pv : 0ull;
 #pragma unroll
       for (int j = 0; j < 8; j += 2) {
         ulonglong2 v2;
@@ -272,7 +291,7 @@ DEVI bool ds_row(const DecodeArgs& a, const SpanDsArgs& g, DsState& st, uint64_t
     if (st.kk != 0) {
       const uint32_t closed = st.bnext - (st.open ? 1u : 0u);
       if (closed + st.room - st.fbase > BKB) {
-        bk_flush<AGG>(a, BK, eo, cap, st.fbase, closed - st.fbase, bad);
+        bk_flush<AGG>(a, BK, eo, cap, st.fbase, closed - st.fbase, FLT, bad);
         st.fbase = closed;
       }
     }
@@ -281,10 +300,18 @@ DEVI bool ds_row(const DecodeArgs& a, const SpanDsArgs& g, DsState& st, uint64_t
     if (lend > cs) {
       const uint32_t ln = lend - cs;
       bad |= !st.open;
+      const bool seed = st.o_n == 0;
       st.o_n += ln;
       st.o_rel += (uint64_t)ln * base + ufl(L_pt[ln - 1]) - (uint64_t)ln * st.o_ref;
-      if (PREFIX) {
+      if (prefix) {
         st.o_v = ladd(st.o_v, (int64_t)ufl64(L_v[ln - 1]));
+      } else if (FLT) {  // the open double bucket continues in point order
+        double v = bitsd(st.o_v);
+        for (uint32_t i = 0; i < ln; i++) {
+          const double x = bitsd((int64_t)L_v[i]);
+          v = (seed && i == 0) ? x : ds_dcombine<AGG>(v, x);
+        }
+        st.o_v = dbits(v);
       } else {
         int64_t v = AGG == 1 ? INT64_MAX : INT64_MIN;
         for (uint32_t i = lane; i < ln; i += WAVE) v = ds_combine<AGG>(v, (int64_t)L_v[i]);
@@ -326,8 +353,12 @@ DEVI bool ds_row(const DecodeArgs& a, const SpanDsArgs& g, DsState& st, uint64_t
         const uint32_t ref = base + dta;
         const uint32_t rel = (L_pt[lb] - pa) - n * dta;
         int64_t v;
-        if (PREFIX) {
+        if (prefix) {
           v = (int64_t)(L_v[lb] - (la > 0 ? L_v[la - 1] : 0ull));
+        } else if (FLT) {
+          double d = bitsd((int64_t)L_v[la]);
+          for (uint32_t i = la + 1; i <= lb; i++) d = ds_dcombine<AGG>(d, bitsd((int64_t)L_v[i]));
+          v = dbits(d);
         } else {
           v = (int64_t)L_v[la];
           for (uint32_t i = la + 1; i <= lb; i++) v = ds_combine<AGG>(v, (int64_t)L_v[i]);
@@ -376,7 +407,10 @@ DEVI bool ds_row(const DecodeArgs& a, const SpanDsArgs& g, DsState& st, uint64_t
 }
 
 // One wave per kept span.
-template <int AGG>
+// FLT: spans whose cells are all float (double buckets); the integer
+// instantiation runs over every kept span first, the float one over the
+// spans it left (g.in_list), so neither carries the other's branches.
+template <int AGG, bool FLT>
 __global__ void __launch_bounds__(256) k_ds_spans(DecodeArgs a, SpanDsArgs g, const uint32_t* ncells,
                                                   const uint32_t* vlen) {
   __shared__ uint32_t s_pt[4][DCH];
@@ -386,8 +420,11 @@ __global__ void __launch_bounds__(256) k_ds_spans(DecodeArgs a, SpanDsArgs g, co
   const int wib = threadIdx.x / WAVE;
   const uint32_t wave = (blockIdx.x * blockDim.x + threadIdx.x) / WAVE;
   const uint32_t nwaves = gridDim.x * blockDim.x / WAVE;
-  bool any = false;
-  for (uint32_t k = ufl(wave); k < a.n_kept; k += nwaves) {
+  bool any_i = false, any_f = false;
+  int64_t fs = 0;  // F*: latest first bucket ts of a float span, + 1
+  const uint32_t n_in = g.in_list ? *g.in_count : a.n_kept;
+  for (uint32_t w = ufl(wave); w < n_in; w += nwaves) {
+    const uint32_t k = g.in_list ? ufl(g.in_list[w]) : w;
     const uint32_t s = ufl(a.kept[k]);
     const uint64_t r0 = ufl64(a.span_row_start[s]), r1 = ufl64(a.span_row_start[s + 1]);
     const uint32_t n = ufl(a.sp_ncells[s]);
@@ -418,9 +455,9 @@ __global__ void __launch_bounds__(256) k_ds_spans(DecodeArgs a, SpanDsArgs g, co
         ok = false;
         break;
       }
-      const bool fail = W == 8 ? ds_row<AGG, 8>(a, g, st, eo, cap, qoff, voff, rbase, nc, cell, s_pt[wib],
+      const bool fail = W == 8 ? ds_row<AGG, 8, FLT>(a, g, st, eo, cap, qoff, voff, rbase, nc, cell, s_pt[wib],
                                                  s_v[wib], s_bk[wib])
-                               : ds_row<AGG, 4>(a, g, st, eo, cap, qoff, voff, rbase, nc, cell, s_pt[wib],
+                               : ds_row<AGG, 4, FLT>(a, g, st, eo, cap, qoff, voff, rbase, nc, cell, s_pt[wib],
                                                  s_v[wib], s_bk[wib]);
       ok = !fail;
       cell += nc;
@@ -431,7 +468,7 @@ __global__ void __launch_bounds__(256) k_ds_spans(DecodeArgs a, SpanDsArgs g, co
       const uint32_t b = st.bnext - 1;  // the open bucket
       if (st.open) {
         if (b - st.fbase >= BKB) {  // (cannot happen: a chunk left room for it)
-          bk_flush<AGG>(a, s_bk[wib], eo, cap, st.fbase, b - st.fbase, bad);
+          bk_flush<AGG>(a, s_bk[wib], eo, cap, st.fbase, b - st.fbase, FLT, bad);
           st.fbase = b;
         }
         if (lane == 0) {
@@ -443,7 +480,7 @@ __global__ void __launch_bounds__(256) k_ds_spans(DecodeArgs a, SpanDsArgs g, co
         }
       }
       n_last = st.bnext - st.fbase;
-      ts_last = bk_flush<AGG>(a, s_bk[wib], eo, cap, st.fbase, n_last, bad);
+      ts_last = bk_flush<AGG>(a, s_bk[wib], eo, cap, st.fbase, n_last, FLT, bad);
       ok = ballot(bad) == 0;
     }
     if (ok) {
@@ -452,7 +489,21 @@ __global__ void __launch_bounds__(256) k_ds_spans(DecodeArgs a, SpanDsArgs g, co
         a.e_len[k] = nb;
         a.e_bad[k] = -1;
       }
-      any = true;
+      if (FLT) {
+        any_f = true;
+        if (!a.rate) {  // (the first bucket's ts: lane 0's of the last flush, or E)
+          uint32_t t0b;
+          if (st.fbase == 0) {
+            t0b = readlane_u32(ts_last, 0);
+          } else {
+            __threadfence_block();
+            t0b = ufl(a.e_ts[eo]);
+          }
+          fs = max(fs, (int64_t)t0b + 1);
+        }
+      } else {
+        any_i = true;
+      }
       if (g.bitmap) {  // G: this span's E points <= end (rate: from the second)
         auto mark = [&](int64_t t, uint32_t b) {
           if ((g.rate && b == 0) || t > g.hi || t < g.lo) return;
@@ -472,7 +523,12 @@ __global__ void __launch_bounds__(256) k_ds_spans(DecodeArgs a, SpanDsArgs g, co
       g.list[atomicAdd(g.list_count, 1u)] = k;
     }
   }
-  if (any && lane == 0 && !a.gflags[1]) atomicOr(&a.gflags[1], 1u);
+  if (lane == 0) {
+    if (any_i && !a.gflags[1]) atomicOr(&a.gflags[1], 1u);
+    if (any_f && !a.gflags[0]) atomicOr(&a.gflags[0], 1u);
+    if (fs && (unsigned long long)fs > *(volatile unsigned long long*)a.fstar)
+      atomicMax(a.fstar, (unsigned long long)fs);
+  }
 }
 
 }  // namespace tsdb
