@@ -312,7 +312,7 @@ struct LaunchChunks {
     HIPCHK(hipEventRecord(ctx->ev[8], st));
     hipLaunchKernelGGL((k_ds_spans<AGG, false>), dim3(grid_for(n_kept, 4, 1u << 20)), dim3(256), 0, st, da, g,
                        ncells, vlen);
-    hipLaunchKernelGGL((k_ds_spans<AGG, true>), dim3(std::min(grid_for(n_kept, 4, 1u << 20), 2048u)), dim3(256), 0,
+    hipLaunchKernelGGL((k_ds_spans<AGG, true>), dim3(std::min(grid_for(n_kept, 4, 1u << 20), 1024u)), dim3(256), 0,
                        st, da, gf, ncells, vlen);
     HIPCHK(hipEventRecord(ctx->ev[9], st));
     ctx->hot_kernel = TSDBHIP_HOT_DS_CHUNKS;
@@ -607,10 +607,10 @@ static int spangroup_run(tsdbhip_ctx* ctx, const tsdbhip_sg_desc* d, tsdbhip_sg_
         mark_list = dg.list;
         mark_count = dg.list_count;
       }
-      const unsigned lblocks = fa.span_list ? std::min(blocks, 2048u) : blocks;
+      const unsigned lblocks = fa.span_list ? std::min(blocks, 1024u) : blocks;
       hipLaunchKernelGGL((k_decode_fast<0, false>), dim3(lblocks), dim3(256), 0, st, fa, row_ncells, row_val_len);
       if (!direct) HIPCHK(hipEventRecord(ctx->ev[9], st));
-      hipLaunchKernelGGL(k_decode_nods, dim3(std::min(blocks, 2048u)), dim3(256), 0, st, ga);
+      hipLaunchKernelGGL(k_decode_nods, dim3(std::min(blocks, 1024u)), dim3(256), 0, st, ga);
     } else {
       DecodeArgs fa = da;
       if (chunks && ds_agg != 4) {
@@ -627,10 +627,10 @@ static int spangroup_run(tsdbhip_ctx* ctx, const tsdbhip_sg_desc* d, tsdbhip_sg_
         mark_count = fa.span_count;
       }
       // (grid-stride over the spans left by k_ds_spans: usually few)
-      const unsigned lblocks = fa.span_list ? std::min(blocks, 2048u) : blocks;
+      const unsigned lblocks = fa.span_list ? std::min(blocks, 1024u) : blocks;
       launch_agg<LaunchFastDs>(ds_agg, ctx, lblocks, fa, row_ncells, row_val_len);
       if (ctx->hot_kernel == TSDBHIP_HOT_DECODE_FAST) HIPCHK(hipEventRecord(ctx->ev[9], st));
-      launch_agg<LaunchGeneralDs>(ds_agg, ctx, std::min(blocks, 2048u), ga);
+      launch_agg<LaunchGeneralDs>(ds_agg, ctx, std::min(blocks, 1024u), ga);
     }
   }
   HIPCHK(hipEventRecord(ctx->ev[2], st));
@@ -674,7 +674,9 @@ static int spangroup_run(tsdbhip_ctx* ctx, const tsdbhip_sg_desc* d, tsdbhip_sg_
     ga.total = &sm->T;
     ga.list = mark_list;  // spans k_ds_spans did not mark (null: all)
     ga.list_count = mark_count;
-    if (n_kept) hipLaunchKernelGGL(k_grid_mark, dim3(grid_for(n_kept, 4, 65536)), dim3(256), 0, st, ga);
+    if (n_kept)
+      hipLaunchKernelGGL(k_grid_mark, dim3(mark_list ? std::min(grid_for(n_kept, 4, 65536), 1024u) : grid_for(n_kept, 4, 65536)),
+                         dim3(256), 0, st, ga);
     if (sharded) {
       uint32_t* all = scratch<uint32_t>(ctx, "bitmap_all", nwords * ctx->nranks);
       NCCLCHK(ncclAllGather(bitmap, all, nwords, ncclUint32, ctx->comm, st));
@@ -698,11 +700,11 @@ static int spangroup_run(tsdbhip_ctx* ctx, const tsdbhip_sg_desc* d, tsdbhip_sg_
       DecodeArgs fa = da;
       fa.span_list = dg.list;
       fa.span_count = dg.list_count;
-      hipLaunchKernelGGL((k_decode_fast<0, false>), dim3(std::min(grid_for(n_kept, 4, 65536), 2048u)), dim3(256), 0,
+      hipLaunchKernelGGL((k_decode_fast<0, false>), dim3(std::min(grid_for(n_kept, 4, 65536), 1024u)), dim3(256), 0,
                          st, fa, row_ncells, row_val_len);
       DecodeArgs gfa = da;
       gfa.use_fb = 1;
-      hipLaunchKernelGGL(k_decode_nods, dim3(std::min(grid_for(n_kept, 4, 65536), 2048u)), dim3(256), 0, st, gfa);
+      hipLaunchKernelGGL(k_decode_nods, dim3(std::min(grid_for(n_kept, 4, 65536), 1024u)), dim3(256), 0, st, gfa);
     }
   }
   HIPCHK(hipEventRecord(ctx->ev[4], st));
@@ -742,6 +744,7 @@ static int spangroup_run(tsdbhip_ctx* ctx, const tsdbhip_sg_desc* d, tsdbhip_sg_
       r.d_r0 = dg.r0; r.span_row_start = span_row_start; r.kept = kept; r.row_cpre = dg.row_cpre;
       r.row_ncells = row_ncells; r.row_val_off = row_val_off; r.val = val;
       r.chunk_e = nullptr;
+      r.fstar = fstar;
       if (direct) {
         uint32_t* ce = scratch<uint32_t>(ctx, "chunk_e", n_chunks, true);
         if (n_kept)

@@ -87,7 +87,7 @@ DEVI uint64_t wave_incl_scan_u64_dpp(uint64_t x) {
 
 // floor(a / n) for u64 a, u32 n > 0 — the general case, out of line.
 __device__ __attribute__((noinline)) uint64_t udiv64_32_slow(uint64_t a, uint32_t n) {
-  if (n == 1) return a;
+  if (n <= 1) return n ? a : 0;  // (n == 0 only on a discarded lane: no loop)
   uint64_t q = (uint64_t)((double)a / (double)n);
   int64_t r = (int64_t)(a - q * (uint64_t)n);
   q += (int64_t)floor((double)r / (double)n);

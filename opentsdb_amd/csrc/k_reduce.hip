@@ -62,6 +62,7 @@ struct ReduceArgs {
   double* p_wdv;
   uint32_t* p_dhas;     // double min/max: a non-NaN value was seen
   const uint32_t* chunk_e;  // [n_chunks] chunk holds an E (non-direct) span
+  uint64_t fstar;           // F* (FinalArgs.fstar): t + 1 < F* is a double t
   // direct spans (k_direct.hip; d_info null: none): values read from the
   // reference's value bytes at grid rank - d_ga
   const uint32_t* d_info;
@@ -321,16 +322,48 @@ __global__ void __launch_bounds__(256) k_reduce(ReduceArgs r) {
   if (!DONLY) {
     const int64_t t0 = r.grid[tb * WAVE];
     for (uint32_t k = k0 + lane; k < k1; k += WAVE) {
-      r.st_f[(uint64_t)wave * r.spans_per_chunk + (k - k0)] = 0;
-      if (r.d_info && (r.d_info[k] & 1u)) { ptr[k - k0] = 0; continue; }
+      const uint64_t sl = (uint64_t)wave * r.spans_per_chunk + (k - k0);
+      if (r.d_info && (r.d_info[k] & 1u)) { ptr[k - k0] = 0; r.st_f[sl] = 0; continue; }
       const uint64_t eo = r.e_off[k];
-      uint32_t lo = base_idx, hi = r.e_len[k];
+      const uint32_t len = r.e_len[k];
+      uint32_t lo = base_idx, hi = len;
       if (hi < lo) hi = lo;
       while (lo < hi) {
         const uint32_t mid = (lo + hi) >> 1;
         if ((int64_t)r.e_ts[eo + mid] < t0) lo = mid + 1; else hi = mid;
       }
       ptr[k - k0] = lo;
+      // the bracket cache for cursor lo (points lo-1 and lo), filled here
+      // lane-parallel so the first tile needs no per-span loads
+      const uint32_t j = lo;
+      uint2 x = make_uint2(0, UINT32_MAX);
+      longlong2 y = make_longlong2(0, 0);
+      uint32_t f = 4u;
+      double rv = 0.0;
+      if (j >= 1 && j <= len) {
+        x.x = r.e_ts[eo + j - 1];
+        y.x = r.e_val[eo + j - 1];
+        if (r.e_flt[eo + j - 1]) f |= 1u;
+      }
+      if (j < len) {
+        x.y = r.e_ts[eo + j];
+        y.y = r.e_val[eo + j];
+        if (r.e_flt[eo + j]) f |= 2u;
+      }
+      if (RATE && j >= 1 && j <= len) {
+        const double yc = to_double(y.x, (f & 1u) != 0);
+        if (j >= 2) {
+          const int64_t xp = r.e_ts[eo + j - 2];
+          const double yp = to_double(r.e_val[eo + j - 2], r.e_flt[eo + j - 2] != 0);
+          rv = (yc - yp) / (double)((int64_t)x.x - xp);
+        } else {
+          rv = yc / (double)(int64_t)x.x;  // Q5: prev = (0, 0)
+        }
+      }
+      r.st_x[sl] = x;
+      r.st_y[sl] = y;
+      r.st_rv[sl] = rv;
+      r.st_f[sl] = f;
     }
   }
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
@@ -348,6 +381,15 @@ __global__ void __launch_bounds__(256) k_reduce(ReduceArgs r) {
     const int64_t t_last = (int64_t)r.grid[g0 + nvalid - 1];
     Acc acc;
     acc_init(acc);
+    // dual mode: t before the latest float-first point is on the double path
+    // whatever the spans hold (F*, SpanGroup.java:632-645); once every lane's
+    // t is known to be double, no long lerp of this tile is ever read
+    if (MODE == MODE_DUAL && gv && (uint64_t)tl + 1 < r.fstar) acc.flag |= 1u;
+    auto need_long = [&](bool fa, bool fb) {
+      if (MODE == MODE_INT) return true;
+      if (MODE != MODE_DUAL || fa || fb) return false;
+      return ballot(gv && !(acc.flag & 1u)) != 0;
+    };
     // Spans in order, 64 at a time: their E offsets/lengths come in with one
     // load per lane. A span whose E holds exactly this tile's grid points
     // (E[g0 .. g0+n) == G[g0 .. g0+n): aligned series) needs no bracket
@@ -415,7 +457,7 @@ __global__ void __launch_bounds__(256) k_reduce(ReduceArgs r) {
         double yd = 0.0;
         // (dual: a float in the bracket puts t on the double path; the long
         // lerp of this span is then never read)
-        if (MODE == MODE_INT || (MODE == MODE_DUAL && !fc && !fn)) yi = lerp_long(tl, xc, vc, xn, vn);
+        if (need_long(fc, fn)) yi = lerp_long(tl, xc, vc, xn, vn);
         if (MODE != MODE_INT)
           yd = lerp_double(tl, xc, to_double(vc, MODE == MODE_DBL || fc), xn,
                            to_double(vn, MODE == MODE_DBL || fn));
@@ -436,10 +478,16 @@ __global__ void __launch_bounds__(256) k_reduce(ReduceArgs r) {
       if (MODE == MODE_DUAL && (fc || fn)) acc.flag |= 1u;
       int64_t yi = 0;
       double yd = 0.0;
-      if (MODE == MODE_INT || (MODE == MODE_DUAL && !fc && !fn)) yi = lerp_long(tl, (int64_t)x.x, y.x, (int64_t)x.y, y.y);
+#if defined(EXP_NOCACHED)
+      return;
+#elif defined(EXP_NOLERP)
+      yi = y.x; yd = (double)y.y;
+#else
+      if (need_long(fc, fn)) yi = lerp_long(tl, (int64_t)x.x, y.x, (int64_t)x.y, y.y);
       if (MODE != MODE_INT)
         yd = lerp_double(tl, (int64_t)x.x, to_double(y.x, MODE == MODE_DBL || fc), (int64_t)x.y,
                          to_double(y.y, MODE == MODE_DBL || fn));
+#endif
       acc_push<AGG, MODE>(acc, yi, yd);
     };
     // A direct span (k_direct.hip) at lane g: E index e = g - ga; its value
@@ -506,8 +554,8 @@ __global__ void __launch_bounds__(256) k_reduce(ReduceArgs r) {
         f_l = r.st_f[sl];
         if (f_l & 4u) {
           x_l = r.st_x[sl];
+          y_l = r.st_y[sl];
           if (RATE) rv_l = r.st_rv[sl];
-          else y_l = r.st_y[sl];
         }
       }
       bool dirty_l = false;
@@ -529,7 +577,19 @@ __global__ void __launch_bounds__(256) k_reduce(ReduceArgs r) {
         almask = ballot(al);
       }
       // spans with no point in this tile take the cache
-      const uint64_t cmask = ballot(el && !((almask >> lane) & 1) && (f_l & 4u) && (j_l >= len_l || (int64_t)x_l.y > t_last));
+      const bool cl_ok = el && !((almask >> lane) & 1) && (f_l & 4u);
+      const uint64_t cmask = ballot(cl_ok && (j_l >= len_l || (int64_t)x_l.y > t_last));
+      // spans with exactly one point (j) in this tile: point j+1 loaded here,
+      // lane-parallel, so the span needs no load of its own
+      uint32_t x2_l = UINT32_MAX, f2_l = 0;
+      int64_t y2_l = 0;
+      const bool sc = cl_ok && j_l < len_l && (int64_t)x_l.y <= t_last;
+      if (sc && j_l + 1 < len_l) {
+        x2_l = r.e_ts[eo_l + j_l + 1];
+        y2_l = r.e_val[eo_l + j_l + 1];
+        f2_l = r.e_flt[eo_l + j_l + 1];
+      }
+      const uint64_t smask = ballot(sc && (int64_t)x2_l > t_last);
       const uint32_t nb = min((uint32_t)WAVE, k1 - kb);
       for (uint32_t i = 0; i < nb;) {
         if ((dsingle >> i) & 1) {
@@ -570,6 +630,62 @@ __global__ void __launch_bounds__(256) k_reduce(ReduceArgs r) {
           // cursor past the tile; cache stale (refilled by the general path)
           if ((uint32_t)lane >= i && (uint32_t)lane < i + run) { j_l = (uint32_t)(g0 + nvalid); f_l = 0; dirty_l = true; }
           i += run;
+          continue;
+        }
+        if ((smask >> i) & 1) {
+          // one point (x_n = point j) inside the tile: lanes before it keep the
+          // cached bracket (j-1, j), the lane on it takes y_j, lanes after it
+          // bracket (j, j+1) (SpanGroup.java:702-784)
+          const uint32_t j = readlane_u32(j_l, (int)i), len = readlane_u32(len_l, (int)i);
+          const uint32_t f = readlane_u32(f_l, (int)i), f2 = readlane_u32(f2_l, (int)i);
+          const int64_t xc = (int64_t)readlane_u32(x_l.x, (int)i), xn = (int64_t)readlane_u32(x_l.y, (int)i);
+          const int64_t x2 = (int64_t)readlane_u32(x2_l, (int)i);
+          const int64_t yc = (int64_t)readlane_u64((uint64_t)y_l.x, (int)i), yn = (int64_t)readlane_u64((uint64_t)y_l.y, (int)i);
+          const int64_t y2 = (int64_t)readlane_u64((uint64_t)y2_l, (int)i);
+          const bool fc = (f & 1u) != 0, fn = (f & 2u) != 0, ff = f2 != 0;
+          const bool more = j + 1 < len;  // point j+1 exists (past the tile)
+          double rvn = 0.0;                // rate value at point j (j >= 1 in rate mode)
+          if (RATE) rvn = (to_double(yn, fn) - to_double(yc, fc)) / (double)(xn - xc);
+          if (gv) {
+            if (RATE) {
+              const double rvc = __longlong_as_double((long long)readlane_u64((uint64_t)__double_as_longlong(rv_l), (int)i));
+              if (tl < xn) acc_push<AGG, MODE>(acc, 0, rvc);
+              else if (more || tl == xn) acc_push<AGG, MODE>(acc, 0, rvn);  // else past the last point
+            } else if (tl < xn) {
+              if (j == 0) {  // not started: the next slot holds e_0
+                if (MODE == MODE_DUAL && fn) acc.flag |= 1u;
+              } else {
+                if (MODE == MODE_DUAL && (fc || fn)) acc.flag |= 1u;
+                int64_t yi = 0;
+                double yd = 0.0;
+                if (need_long(fc, fn)) yi = lerp_long(tl, xc, yc, xn, yn);
+                if (MODE != MODE_INT)
+                  yd = lerp_double(tl, xc, to_double(yc, MODE == MODE_DBL || fc), xn, to_double(yn, MODE == MODE_DBL || fn));
+                acc_push<AGG, MODE>(acc, yi, yd);
+              }
+            } else if (tl == xn) {
+              if (MODE == MODE_DUAL && (fn || (more && ff))) acc.flag |= 1u;
+              acc_push<AGG, MODE>(acc, yn, MODE == MODE_INT ? 0.0 : to_double(yn, MODE == MODE_DBL || fn));
+            } else if (more) {
+              if (MODE == MODE_DUAL && (fn || ff)) acc.flag |= 1u;
+              int64_t yi = 0;
+              double yd = 0.0;
+              if (need_long(fn, ff)) yi = lerp_long(tl, xn, yn, x2, y2);
+              if (MODE != MODE_INT)
+                yd = lerp_double(tl, xn, to_double(yn, MODE == MODE_DBL || fn), x2, to_double(y2, MODE == MODE_DBL || ff));
+              acc_push<AGG, MODE>(acc, yi, yd);
+            }
+          }
+          // the cursor moves past point j
+          if (lane == (int)i) {
+            j_l = j + 1;
+            x_l = make_uint2((uint32_t)xn, (uint32_t)x2);
+            y_l = make_longlong2(yn, y2);
+            f_l = 4u | (fn ? 1u : 0u) | (ff ? 2u : 0u);
+            rv_l = rvn;
+            dirty_l = true;
+          }
+          i++;
           continue;
         }
         if ((cmask >> i) & 1) {
@@ -623,8 +739,8 @@ __global__ void __launch_bounds__(256) k_reduce(ReduceArgs r) {
         r.st_f[sl] = f_l;
         if (f_l & 4u) {
           r.st_x[sl] = x_l;
+          r.st_y[sl] = y_l;
           if (RATE) r.st_rv[sl] = rv_l;
-          else r.st_y[sl] = y_l;
         }
       }
     }
