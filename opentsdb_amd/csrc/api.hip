@@ -745,6 +745,7 @@ static int spangroup_run(tsdbhip_ctx* ctx, const tsdbhip_sg_desc* d, tsdbhip_sg_
       r.row_ncells = row_ncells; r.row_val_off = row_val_off; r.val = val;
       r.chunk_e = nullptr;
       r.fstar = fstar;
+      r.exact = exact ? 1 : 0;
       if (direct) {
         uint32_t* ce = scratch<uint32_t>(ctx, "chunk_e", n_chunks, true);
         if (n_kept)

@@ -63,6 +63,7 @@ struct ReduceArgs {
   uint32_t* p_dhas;     // double min/max: a non-NaN value was seen
   const uint32_t* chunk_e;  // [n_chunks] chunk holds an E (non-direct) span
   uint64_t fstar;           // F* (FinalArgs.fstar): t + 1 < F* is a double t
+  int32_t exact;            // TSDBHIP_EXACT_ORDER: IEEE division in the double lerp
   // direct spans (k_direct.hip; d_info null: none): values read from the
   // reference's value bytes at grid rank - d_ga
   const uint32_t* d_info;
@@ -467,7 +468,8 @@ __global__ void __launch_bounds__(256) k_reduce(ReduceArgs r) {
     };
     // A span with no point in this tile (its next point j lies past t_last):
     // every lane's bracket is (j-1, j), all from the cache.
-    auto cached = [&](uint32_t j, uint32_t len, uint2 x, longlong2 y, double rv, uint32_t f) {
+    auto cached = [&](uint32_t j, uint32_t len, uint2 x, longlong2 y, double rv, uint32_t f, double y0d, double dyd,
+                      double rinv) {
       if (!gv || j >= len) return;  // expired (all points consumed before this tile)
       if (RATE) {  // cur = j-1 (j >= 1), constant over the tile; active: tl <= last
         if (len >= 2) acc_push<AGG, MODE>(acc, 0, rv);
@@ -478,16 +480,14 @@ __global__ void __launch_bounds__(256) k_reduce(ReduceArgs r) {
       if (MODE == MODE_DUAL && (fc || fn)) acc.flag |= 1u;
       int64_t yi = 0;
       double yd = 0.0;
-#if defined(EXP_NOCACHED)
-      return;
-#elif defined(EXP_NOLERP)
-      yi = y.x; yd = (double)y.y;
-#else
       if (need_long(fc, fn)) yi = lerp_long(tl, (int64_t)x.x, y.x, (int64_t)x.y, y.y);
-      if (MODE != MODE_INT)
-        yd = lerp_double(tl, (int64_t)x.x, to_double(y.x, MODE == MODE_DBL || fc), (int64_t)x.y,
-                         to_double(y.y, MODE == MODE_DBL || fn));
-#endif
+      if (MODE != MODE_INT) {
+        // y0 + ((double)(t - x0) * (y1 - y0)) / (double)(x1 - x0), with y0 and
+        // y1 - y0 converted once per batch; outside TSDBHIP_EXACT_ORDER the
+        // division is a product with the batch-computed reciprocal (<= 1 ulp)
+        const double num = (double)(uint32_t)(tl - (int64_t)x.x) * dyd;
+        yd = r.exact ? y0d + num / (double)(uint32_t)(x.y - x.x) : y0d + num * rinv;
+      }
       acc_push<AGG, MODE>(acc, yi, yd);
     };
     // A direct span (k_direct.hip) at lane g: E index e = g - ga; its value
@@ -559,6 +559,14 @@ __global__ void __launch_bounds__(256) k_reduce(ReduceArgs r) {
         }
       }
       bool dirty_l = false;
+      // per-span doubles of the cached bracket (lane = span): y0, y1 - y0,
+      // 1 / (x1 - x0)
+      double y0d_l = 0.0, dyd_l = 0.0, rinv_l = 0.0;
+      if (!RATE && MODE != MODE_INT && el && (f_l & 4u) && x_l.y > x_l.x) {
+        y0d_l = to_double(y_l.x, MODE == MODE_DBL || (f_l & 1u));
+        dyd_l = to_double(y_l.y, MODE == MODE_DBL || (f_l & 2u)) - y0d_l;
+        rinv_l = 1.0 / (double)(x_l.y - x_l.x);
+      }
       const uint64_t dmask = ballot(dl);
       uint32_t dga_l = 0, dn_l = 0, dx0_l = 0, dstep_l = 0;
       uint64_t dvo_l = 0;
@@ -695,7 +703,14 @@ __global__ void __launch_bounds__(256) k_reduce(ReduceArgs r) {
           if (RATE) rv = __longlong_as_double((long long)readlane_u64((uint64_t)__double_as_longlong(rv_l), (int)i));
           else y = make_longlong2((long long)readlane_u64((uint64_t)y_l.x, (int)i),
                                   (long long)readlane_u64((uint64_t)y_l.y, (int)i));
-          cached(readlane_u32(j_l, (int)i), readlane_u32(len_l, (int)i), x, y, rv, readlane_u32(f_l, (int)i));
+          double y0d = 0.0, dyd = 0.0, rinv = 0.0;
+          if (!RATE && MODE != MODE_INT) {
+            y0d = __longlong_as_double((long long)readlane_u64((uint64_t)__double_as_longlong(y0d_l), (int)i));
+            dyd = __longlong_as_double((long long)readlane_u64((uint64_t)__double_as_longlong(dyd_l), (int)i));
+            rinv = __longlong_as_double((long long)readlane_u64((uint64_t)__double_as_longlong(rinv_l), (int)i));
+          }
+          cached(readlane_u32(j_l, (int)i), readlane_u32(len_l, (int)i), x, y, rv, readlane_u32(f_l, (int)i), y0d,
+                 dyd, rinv);
           i++;
           continue;
         }
