@@ -104,10 +104,11 @@ def pmc_traffic(config, kernel, world):
     if world != 1 or not os.path.exists(path):
         return None, None
     ks = json.load(open(path)).get("kernels", {})
-    for name, e in ks.items():
-        if name.split("<")[0] == kernel and e.get("hbm_bytes_per_launch"):
-            return e["hbm_bytes_per_launch"], os.path.relpath(path, ROOT)
-    return None, None
+    # every instantiation of the kernel launches once per step (e.g. the
+    # integer and float k_ds_spans), and the timed region covers them all
+    tot = sum(e["hbm_bytes_per_launch"] for name, e in ks.items()
+              if name.split("<")[0] == kernel and e.get("hbm_bytes_per_launch"))
+    return (tot, os.path.relpath(path, ROOT)) if tot else (None, None)
 
 
 def dist_setup(n_gpus):
