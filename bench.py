@@ -35,9 +35,9 @@ from opentsdb_amd._lib import Context, lib  # noqa: E402
 METRIC = "input data points/sec aggregated (node) + % HBM roofline, 1/2/4/8 MI355X"
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: 8.0 TB/s spec
 
-def _cfg(n_series, n_points, step, kind, agg, dsi=0, dsa=0, rate=False, gen="device", desc=""):
+def _cfg(n_series, n_points, step, kind, agg, dsi=0, dsa=0, rate=False, gen="device", desc="", groups=1):
     return dict(n_series=n_series, n_points=n_points, step=step, kind=kind, agg=agg, dsi=dsi, dsa=dsa,
-                rate=rate, gen=gen, desc=desc)
+                rate=rate, gen=gen, desc=desc, groups=groups)
 
 
 I64, F32 = _abi.SYN_INT64_COUNTER, _abi.SYN_FLOAT32
@@ -58,6 +58,14 @@ CONFIGS = {
                     "1% float cells), ~10M-point union grid, sum"),
     "c4i": _cfg(1000, 11500, 0, -1, SUM, gen="jitter_int",
                 desc="C4-int: the C4 timestamps with all-int series (the int64 lerp path), sum"),
+    # GROUP BY: the C3* spans as the SpanGroup[] of
+    # TsdbQuery.groupByAndAggregate, all groups in one tsdbhip_spangroup_run_batch
+    "c3s_gb100": _cfg(1_000_000, 3600, 1, I64, SUM, 60, AVG, groups=100,
+                      desc="C3* GROUP BY host=* (100 groups x 10k series), sum + 1m-avg downsample"),
+    "c3s_gb10k": _cfg(1_000_000, 3600, 1, I64, SUM, 60, AVG, groups=10_000,
+                      desc="C3* GROUP BY host=* (10k groups x 100 series), sum + 1m-avg downsample"),
+    "c3_gb100": _cfg(1_000_000, 3600, 1, I64, SUM, groups=100,
+                     desc="C3 GROUP BY host=* (100 groups x 10k series), sum, no downsample"),
     # secondary path (configs[4]): row compaction, see bench_c5
     "c5": _cfg(1_000_000, 0, 0, 0, 0, gen="rows",
                desc="C5: row compaction, 1M rows / ~48M raw cells (1..99 per row, mixed widths, legacy floats, "
@@ -337,6 +345,58 @@ def max_over_ranks(dist, x):
     return float(t.item())
 
 
+def h2d_leg(ctx, L, cfg, n_spans, steps=3):
+    """PCIe-inclusive rate — reported beside the line, never its `value`: the
+    same SpanGroup shape with its row bytes in pinned host memory (registered
+    with tsdbhip_host_register, as the JNI bridge registers its
+    DirectByteBuffers), so every call stages them H2D before
+    the kernels run. A bounded sample of the workload (n_spans series)."""
+    d = _abi.SgDesc()
+    p = _abi.SynthParams(seed=3, n_spans=n_spans, n_points=cfg["n_points"], t0=synth.T0, step=cfg["step"],
+                         kind=cfg["kind"], span0=0)
+    ctx.check(L.tsdbhip_synth_generate(ctx.handle, C.byref(p), C.byref(d)))
+    S, R = int(d.n_spans), int(d.n_rows)
+    arrs = [np.empty(S + 1, np.uint64), np.empty(R, np.uint32), np.empty(R, np.uint32), np.empty(R, np.uint64),
+            np.empty(R, np.uint64), np.empty(R, np.uint32), np.empty(int(d.qual_nbytes), np.uint8),
+            np.empty(int(d.val_nbytes), np.uint8)]
+    ctx.check(L.tsdbhip_desc_download(ctx.handle, C.byref(d), *[a.ctypes.data_as(C.c_void_p) for a in arrs]))
+    L.tsdbhip_synth_free(ctx.handle, C.byref(d))
+    reg = [a for a in arrs if a.nbytes]
+    for a in reg:
+        ctx.check(L.tsdbhip_host_register(ctx.handle, a.ctypes.data_as(C.c_void_p), a.nbytes))
+    try:
+        h = _abi.SgDesc()
+        h.n_spans, h.n_rows = S, R
+        h.span_row_start = _abi.ptr(arrs[0], C.c_uint64)
+        h.row_base = _abi.ptr(arrs[1], C.c_uint32)
+        h.row_ncells = _abi.ptr(arrs[2], C.c_uint32)
+        h.row_qual_off = _abi.ptr(arrs[3], C.c_uint64)
+        h.row_val_off = _abi.ptr(arrs[4], C.c_uint64)
+        h.row_val_len = _abi.ptr(arrs[5], C.c_uint32)
+        h.qual_bytes, h.qual_nbytes = _abi.ptr(arrs[6], C.c_uint8), arrs[6].nbytes
+        h.val_bytes, h.val_nbytes = _abi.ptr(arrs[7], C.c_uint8), arrs[7].nbytes
+        h.flags = 0
+        h.start_time, h.end_time = 0, (1 << 32) - 1
+        h.agg, h.rate, h.ds_interval, h.ds_agg = cfg["agg"], int(cfg["rate"]), cfg["dsi"], cfg["dsa"]
+        cap = max(1, cfg["n_points"] * max(cfg["step"], 1))
+        ts, isi, bits = np.zeros(cap, np.int64), np.zeros(cap, np.uint8), np.zeros(cap, np.int64)
+        out = _abi.SgOut(capacity=cap, ts=_abi.ptr(ts, C.c_int64), is_int=_abi.ptr(isi, C.c_uint8),
+                         bits=_abi.ptr(bits, C.c_int64))
+        ctx.check(L.tsdbhip_spangroup_run(ctx.handle, C.byref(h), C.byref(out)))  # warm-up
+        t0 = time.perf_counter()
+        for _ in range(steps):  # each call returns after its D2H of the results
+            ctx.check(L.tsdbhip_spangroup_run(ctx.handle, C.byref(h), C.byref(out)))
+        dt = (time.perf_counter() - t0) / steps
+    finally:
+        for a in reg:
+            L.tsdbhip_host_unregister(ctx.handle, a.ctypes.data_as(C.c_void_p))
+    nbytes = sum(a.nbytes for a in arrs)
+    return {"value": int(out.n_input_points) / dt, "unit": "input points/s", "ms_per_step": dt * 1e3,
+            "h2d_bytes_per_step": nbytes, "effective_GBs": nbytes / dt / 1e9, "steps": steps,
+            "sample": f"{S} series of the same workload, desc arrays in registered pinned host memory "
+                      "(staged H2D inside every call)"}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -347,6 +407,9 @@ def main():
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--exact", action="store_true", help="TSDBHIP_EXACT_ORDER")
+    ap.add_argument("--groups", type=int, default=0, help="GROUP BY: split the series into this many SpanGroups "
+                    "(tsdbhip_spangroup_run_batch)")
+    ap.add_argument("--no-h2d", action="store_true", help="skip the PCIe-inclusive (host-resident) leg")
     ap.add_argument("--c5-mix", default="c5", choices=["c5", "plain", "nocomplex"],
                     help="C5 row mix (diagnostics; the C5 line is 'c5')")
     ap.add_argument("--dry-run", action="store_true",
@@ -363,7 +426,18 @@ def main():
     if args.series:
         n_series = args.series
         cfg = dict(cfg, n_series=n_series)
-    shards = shard_ranges(n_series, world)
+    if args.groups:
+        cfg = dict(cfg, groups=args.groups)
+    G = cfg["groups"]
+    if G > 1:
+        # GROUP BY: groups are independent SpanGroups, so ranks take whole
+        # groups (contiguous, group order kept) and exchange nothing
+        gb = [n_series * g // G for g in range(G + 1)]
+        granks = shard_ranges(G, world)
+        shards = [(gb[a], gb[b]) for a, b in granks]
+        g_lo, g_hi = granks[rank]
+    else:
+        shards = shard_ranges(n_series, world)
     lo, hi = shards[rank]
 
     def barrier():
@@ -422,7 +496,7 @@ def main():
     d.start_time = 0
     d.end_time = (1 << 32) - 1
     d.agg, d.rate, d.ds_interval, d.ds_agg = agg, int(rate), dsi, dsa
-    if world > 1:
+    if world > 1 and G == 1:
         d.flags |= _abi.SHARDED
     if args.exact:
         d.flags |= _abi.EXACT_ORDER
@@ -438,6 +512,23 @@ def main():
 
     def step_once():
         ctx.check(L.tsdbhip_spangroup_run(ctx.handle, C.byref(d), C.byref(out)))
+
+    if G > 1:
+        Gl = g_hi - g_lo
+        gss = np.array([gb[g] - lo for g in range(g_lo, g_hi + 1)], np.uint32)
+        gcap = cap
+        g_ts = np.zeros(Gl * gcap, np.int64)
+        g_isi = np.zeros(Gl * gcap, np.uint8)
+        g_bits = np.zeros(Gl * gcap, np.int64)
+        outs = (_abi.SgOut * Gl)()
+        for g in range(Gl):
+            outs[g].capacity = gcap
+            outs[g].ts = _abi.ptr(g_ts[g * gcap:], C.c_int64)
+            outs[g].is_int = _abi.ptr(g_isi[g * gcap:], C.c_uint8)
+            outs[g].bits = _abi.ptr(g_bits[g * gcap:], C.c_int64)
+
+        def step_once():
+            ctx.check(L.tsdbhip_spangroup_run_batch(ctx.handle, C.byref(d), Gl, _abi.ptr(gss, C.c_uint32), outs))
 
     hot_ms, total_ms, hot_kernel = [], [], [0]
 
@@ -463,6 +554,13 @@ def main():
             best = gbs if best is None else max(best, gbs)
         probe[name] = best
     n_input = int(out.n_input_points)  # global (allreduced when sharded)
+    if G > 1:  # groups sharded: each rank's own points, summed over ranks
+        n_input = sum(int(outs[g].n_input_points) for g in range(Gl))
+        if dist is not None:
+            import torch as _t
+            t = _t.tensor([n_input], dtype=_t.float64)
+            dist.all_reduce(t)
+            n_input = int(t.item())
     ms_step = elapsed / args.steps * 1e3
     value = n_input / (elapsed / args.steps)
 
@@ -501,8 +599,10 @@ def main():
                 "rate": bool(rate),
                 "aggregator": ["sum", "min", "max", "avg", "dev"][agg],
                 "downsample": f"{dsi}s-{['sum', 'min', 'max', 'avg', 'dev'][dsa]}" if dsi else "none",
-                "parallelism": f"series-sharded x{world} (RCCL exchange of per-t partials)" if world > 1
+                "parallelism": (f"groups-sharded x{world} (independent SpanGroups, no exchange)" if G > 1
+                                else f"series-sharded x{world} (RCCL exchange of per-t partials)") if world > 1
                                else "single GPU",
+                "groups": G,
                 "shards": shards,
             },
             "roofline": {
@@ -523,6 +623,11 @@ def main():
                 "frac_of_read_stream": achieved / probe["read_stream"] if probe else None,
             },
         }
+        if not args.no_h2d and world == 1 and cfg["gen"] == "device" and G == 1:
+            try:
+                res["h2d"] = h2d_leg(ctx, L, cfg, min(n_series, 100_000))
+            except Exception as e:  # diagnostics only; never costs the line
+                res["h2d"] = {"error": repr(e)}
         if not args.no_cpu and world == 1:
             res["cpu_baseline"] = cpu_baseline(args.config, args.cpu_seconds)
         print(json.dumps(res), flush=True)

@@ -18,6 +18,9 @@
  *       Row assembly follows Span.addRow / RowSeq.addRow (Span.java:87-132,
  *       RowSeq.java:92-172), i.e. what TsdbQuery.findSpans does with each
  *       compacted KeyValue (TsdbQuery.java:240-285).
+ *   tsdbhip_spangroup_run_batch — the SpanGroup[] of a GROUP BY query
+ *       (TsdbQuery.groupByAndAggregate, TsdbQuery.java:294-363), all groups in
+ *       one call.
  *   tsdbhip_compact_rows   — CompactionQueue.compact(row, compacted[])
  *       (CompactionQueue.java:243-435, 450-743) for a batch of rows.
  *   tsdbhip_host_register / unregister — pinning of the JNI DirectByteBuffers
@@ -254,6 +257,24 @@ int tsdbhip_host_unregister(tsdbhip_ctx* ctx, void* p);
 int tsdbhip_spangroup_run(tsdbhip_ctx* ctx, const tsdbhip_sg_desc* desc,
                           tsdbhip_sg_out* out);
 int tsdbhip_last_timing(tsdbhip_ctx* ctx, tsdbhip_timing* t);
+
+/* ---- group-by batching ------------------------------------------------- */
+/*
+ * Every SpanGroup of one query's GROUP BY in one call — the array
+ * TsdbQuery.groupByAndAggregate returns (TsdbQuery.java:294-363): the groups
+ * share start/end/rate/aggregator/downsampler (one SpanGroup ctor call per
+ * group with the query's arguments, TsdbQuery.java:346-348). `desc` holds the
+ * spans of all groups, group g's spans being [group_span_start[g],
+ * group_span_start[g+1]) in TreeMap order within the group, groups in the
+ * ByteMap order of their tag-value keys; group_span_start is a host array of
+ * n_groups+1 entries with [0] = 0 and [n_groups] = desc->n_spans. outs[g]
+ * receives group g's points exactly as tsdbhip_spangroup_run on that group
+ * alone would (same err_code / err_index per group). Returns TSDBHIP_OK, or
+ * the first failing group's code (every outs[g].err_code is set). Not with
+ * TSDBHIP_SHARDED. Per-call timings: tsdbhip_last_timing.
+ */
+int tsdbhip_spangroup_run_batch(tsdbhip_ctx* ctx, const tsdbhip_sg_desc* desc, uint32_t n_groups,
+                                const uint32_t* group_span_start, tsdbhip_sg_out* outs);
 
 /* ---- secondary path ---------------------------------------------------- */
 int tsdbhip_compact_rows(tsdbhip_ctx* ctx, const tsdbhip_rows_desc* desc,

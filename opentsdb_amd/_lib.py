@@ -22,7 +22,7 @@ EXPORTS = [
     "tsdbhip_host_register", "tsdbhip_host_unregister", "tsdbhip_spangroup_run",
     "tsdbhip_last_timing", "tsdbhip_compact_rows", "tsdbhip_comm_unique_id",
     "tsdbhip_comm_init", "tsdbhip_synth_generate", "tsdbhip_synth_free",
-    "tsdbhip_desc_download", "tsdbhip_bw_probe",
+    "tsdbhip_desc_download", "tsdbhip_bw_probe", "tsdbhip_spangroup_run_batch",
 ]
 
 
@@ -63,6 +63,9 @@ def lib():
     L.tsdbhip_host_unregister.argtypes = [C.c_void_p, C.c_void_p]
     L.tsdbhip_spangroup_run.argtypes = [C.c_void_p, P(_abi.SgDesc), P(_abi.SgOut)]
     L.tsdbhip_spangroup_run.restype = C.c_int
+    L.tsdbhip_spangroup_run_batch.argtypes = [C.c_void_p, P(_abi.SgDesc), C.c_uint32, P(C.c_uint32),
+                                              P(_abi.SgOut)]
+    L.tsdbhip_spangroup_run_batch.restype = C.c_int
     L.tsdbhip_last_timing.argtypes = [C.c_void_p, P(_abi.Timing)]
     L.tsdbhip_compact_rows.argtypes = [C.c_void_p, P(_abi.RowsDesc), P(_abi.RowsOut)]
     L.tsdbhip_compact_rows.restype = C.c_int

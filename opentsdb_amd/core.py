@@ -9,6 +9,9 @@ Mirrors (names, argument meaning, error behaviour):
     longValue/doubleValue(i))     src/core/SpanGroup.java:46-254
   DataPoint                       src/core/DataPoint.java:20-56
   IllegalDataException            src/core/IllegalDataException.java
+  group_by_and_aggregate          TsdbQuery.groupByAndAggregate (TsdbQuery.java:294-363),
+                                  SpanCmp (TsdbQuery.java:594-621),
+                                  Tags.getValueId (Tags.java:213-227)
 
 The whole SpanGroup is evaluated by libtsdbhip on the GPU on first access
 (tsdbhip_spangroup_run); iteration then replays the reference's lazy
@@ -157,6 +160,49 @@ def run_spanset(ctx, spanset: SpanSet, start, end, agg, rate=False, ds_interval=
     return rc, ts[:n], isi[:n], bits[:n], int(out.n_input_points), int(out.err_index)
 
 
+def run_spanset_batch(ctx, spanset: SpanSet, group_span_start, start, end, agg, rate=False, ds_interval=0,
+                      ds_agg=0, exact=False, capacities=None, device_desc=None):
+    """Low-level: one tsdbhip_spangroup_run_batch over the groups
+    [gss[g], gss[g+1]) of spanset. Returns (code, [per-group tuples as
+    run_spanset returns them])."""
+    gss = np.ascontiguousarray(group_span_start, np.uint32)
+    G = len(gss) - 1
+    desc = _abi.SgDesc()
+    if device_desc is not None:
+        C.pointer(desc)[0] = device_desc
+    else:
+        spanset.fill_desc(desc)
+        desc.flags = 0
+    desc.start_time, desc.end_time = int(start), int(end)
+    desc.rate, desc.agg, desc.ds_agg = int(bool(rate)), int(agg), int(ds_agg)
+    desc.ds_interval = int(ds_interval)
+    if exact:
+        desc.flags |= _abi.EXACT_ORDER
+    if capacities is None:
+        cells = np.concatenate([[0], np.cumsum(spanset.row_ncells.astype(np.int64))])
+        srs = spanset.span_row_start.astype(np.int64)
+        cum = cells[srs]  # cells before span s
+        capacities = np.maximum(1, cum[gss[1:].astype(np.int64)] - cum[gss[:-1].astype(np.int64)])
+    outs = (_abi.SgOut * max(G, 1))()
+    bufs = []
+    for g in range(G):
+        cap = int(capacities[g])
+        ts, isi, bits = np.zeros(cap, np.int64), np.zeros(cap, np.uint8), np.zeros(cap, np.int64)
+        bufs.append((ts, isi, bits))
+        outs[g].capacity = cap
+        outs[g].ts = _abi.ptr(ts, C.c_int64)
+        outs[g].is_int = _abi.ptr(isi, C.c_uint8)
+        outs[g].bits = _abi.ptr(bits, C.c_int64)
+    rc = ctx._lib.tsdbhip_spangroup_run_batch(ctx.handle, C.byref(desc), G, _abi.ptr(gss, C.c_uint32), outs)
+    res = []
+    for g in range(G):
+        n = int(outs[g].n_out)
+        ts, isi, bits = bufs[g]
+        res.append((int(outs[g].err_code), ts[:n], isi[:n], bits[:n], int(outs[g].n_input_points),
+                    int(outs[g].err_index)))
+    return rc, res
+
+
 class SpanGroup:
     """net.opentsdb.core.SpanGroup over libtsdbhip (SpanGroup.java:104-254)."""
 
@@ -240,3 +286,80 @@ class SpanGroup:
 
     def doubleValue(self, i):
         return self._get(i).doubleValue()
+
+
+# ---------------------------------------------------------------- GROUP BY ----
+def span_cmp_key(row_key, metric_width=3):
+    """Sort key equivalent to TsdbQuery.SpanCmp (TsdbQuery.java:594-621):
+    metric id, then the tags, skipping the 4-byte base time; unsigned bytes,
+    a shorter key first on a common prefix (Python bytes order)."""
+    return bytes(row_key[:metric_width]) + bytes(row_key[metric_width + 4:])
+
+
+def get_value_id(row_key, tag_id, metric_width=3, name_width=3, value_width=3):
+    """Tags.getValueId (Tags.java:213-227): the value id of tag `tag_id` in
+    the row key, or None."""
+    pos = metric_width + 4
+    while pos < len(row_key):
+        if bytes(row_key[pos:pos + name_width]) == bytes(tag_id):
+            pos += name_width
+            return bytes(row_key[pos:pos + value_width])
+        pos += name_width + value_width
+    return None
+
+
+def plan_groups(row_keys, group_bys, metric_width=3, name_width=3, value_width=3):
+    """The grouping of TsdbQuery.groupByAndAggregate (TsdbQuery.java:294-363)
+    as a plan: row_keys are the spans' row keys (any order, one per span).
+    Returns (group_keys, order, group_span_start): the span indices in batch
+    order (ByteMap order of the group keys, then SpanCmp order within a
+    group) and the group boundaries. Spans without every group_by tag are
+    dropped, as the reference does (with its log line)."""
+    idx = sorted(range(len(row_keys)), key=lambda i: span_cmp_key(row_keys[i], metric_width))
+    if group_bys is None:
+        return [b""], idx, [0, len(idx)]
+    tag_ids = sorted(bytes(t) for t in group_bys)  # group_bys is sorted by id
+    groups = {}
+    for i in idx:
+        parts = []
+        for t in tag_ids:
+            v = get_value_id(row_keys[i], t, metric_width, name_width, value_width)
+            if v is None:
+                parts = None
+                break
+            parts.append(v)
+        if parts is None:
+            continue  # "WTF? Dropping span for row ..." (TsdbQuery.java:339-344)
+        groups.setdefault(b"".join(parts), []).append(i)
+    keys = sorted(groups)  # ByteMap: unsigned lexicographic
+    order, gss = [], [0]
+    for k in keys:
+        order.extend(groups[k])
+        gss.append(len(order))
+    return keys, order, gss
+
+
+def group_by_and_aggregate(spans, group_bys, start_time, end_time, rate, aggregator, interval=0,
+                           downsampler=None, ctx=None, metric_width=3, name_width=3, value_width=3):
+    """TsdbQuery.groupByAndAggregate over libtsdbhip: `spans` maps row key
+    bytes -> Span (findSpans' TreeMap), `group_bys` the tag-name ids to group
+    by (None: one group). Returns the SpanGroups in the reference's order,
+    all evaluated by one tsdbhip_spangroup_run_batch; each raises its own
+    exception lazily while iterated, like the reference's."""
+    keys = list(spans)
+    if not keys:
+        return []
+    gkeys, order, gss = plan_groups(keys, group_bys, metric_width, name_width, value_width)
+    groups = [SpanGroup(None, start_time, end_time, [spans[keys[i]] for i in order[gss[g]:gss[g + 1]]], rate,
+                        aggregator, interval, downsampler, ctx) for g in range(len(gkeys))]
+    if not groups:
+        return []
+    ss = pack_spans([spans[keys[i]].rows for i in order])
+    ds = downsampler is not None and interval > 0
+    c = groups[0]._context()
+    _, res = run_spanset_batch(c, ss, gss, start_time, end_time, aggregator.code, rate,
+                               interval if ds else 0, downsampler.code if ds else 0)
+    for grp, r in zip(groups, res):
+        grp._ctx = c
+        grp._result = r
+    return groups

@@ -34,6 +34,7 @@
 #include "k_ds_chunks.hip"
 #include "k_compact.hip"
 #include "k_direct.hip"
+#include "k_group.hip"
 
 using namespace tsdb;
 
@@ -57,6 +58,8 @@ struct tsdbhip_ctx {
   std::string err;
   std::map<std::string, Buf> bufs;
   void* host_small = nullptr;  // pinned readback area
+  void* host_big = nullptr;    // grow-only pinned staging (group-by batches)
+  size_t host_big_n = 0;
   hipEvent_t ev[10] = {};  // [8],[9] bracket the dominant kernel
   bool time_reduce = false;  // the dominant kernel is k_reduce (direct path)
   uint32_t hot_kernel = 0;
@@ -179,6 +182,7 @@ extern "C" void tsdbhip_close(tsdbhip_ctx* ctx) {
   for (auto& e : ctx->ev)
     if (e) hipEventDestroy(e);
   if (ctx->host_small) hipHostFree(ctx->host_small);
+  if (ctx->host_big) hipHostFree(ctx->host_big);
   if (ctx->stream) hipStreamDestroy(ctx->stream);
   delete ctx;
 }
@@ -397,6 +401,35 @@ static void dispatch_final(tsdbhip_ctx* ctx, int agg, int mode, bool rate, const
     case 3: return final_mode<3>(ctx, mode, rate, r, f);
     default: return final_mode<4>(ctx, mode, rate, r, f);
   }
+}
+
+// k_reduce launch geometry: (tile group, span chunk) per wave.
+struct ReduceGeom {
+  uint32_t spc, n_chunks, tpw, ntg;
+  uint64_t n_waves;
+};
+static ReduceGeom reduce_geom(uint64_t T, uint32_t n_kept, bool one_chunk) {
+  ReduceGeom g;
+  const uint64_t n_tiles = (T + 63) / 64;
+  const uint64_t target = 16384;  // waves in flight over 256 CUs
+  if (one_chunk || n_kept == 0) {
+    g.n_chunks = 1;
+    g.spc = std::max<uint32_t>(n_kept, 1);
+  } else {
+    // chunks of ~256 spans (fewer partials for the combine), but at
+    // least ~2048 waves when the group is small
+    uint64_t want = std::max<uint64_t>(1, target / n_tiles);
+    const uint64_t by_size = std::max<uint64_t>((n_kept + 255) / 256, (2048 + n_tiles - 1) / n_tiles);
+    want = std::min<uint64_t>(want, by_size);
+    want = std::min<uint64_t>(want, std::max<uint32_t>(1, n_kept / 16));
+    g.n_chunks = (uint32_t)std::max<uint64_t>(1, want);
+    g.spc = (n_kept + g.n_chunks - 1) / g.n_chunks;
+    g.n_chunks = (n_kept + g.spc - 1) / g.spc;
+  }
+  g.tpw = (uint32_t)std::max<uint64_t>(1, (n_tiles * g.n_chunks + target - 1) / target);
+  g.ntg = (uint32_t)((n_tiles + g.tpw - 1) / g.tpw);
+  g.n_waves = (uint64_t)g.ntg * g.n_chunks;
+  return g;
 }
 
 static float ev_ms(hipEvent_t a, hipEvent_t b) {
@@ -715,26 +748,9 @@ static int spangroup_run(tsdbhip_ctx* ctx, const tsdbhip_sg_desc* d, tsdbhip_sg_
     const int mode = rate ? MODE_DBL : (!anyf ? MODE_INT : (!anyi ? MODE_DBL : MODE_DUAL));
     ctx->time_reduce = direct;
     auto run_reduce = [&](bool one_chunk, bool finalize) {
-      const uint64_t n_tiles = (T + 63) / 64;
-      const uint64_t target = 16384;  // waves in flight over 256 CUs
-      uint32_t spc, n_chunks, tpw, ntg;
-      if (one_chunk || n_kept == 0) {
-        n_chunks = 1;
-        spc = std::max<uint32_t>(n_kept, 1);
-      } else {
-        // chunks of ~256 spans (fewer partials for the combine), but at
-        // least ~2048 waves when the group is small
-        uint64_t want = std::max<uint64_t>(1, target / n_tiles);
-        const uint64_t by_size = std::max<uint64_t>((n_kept + 255) / 256, (2048 + n_tiles - 1) / n_tiles);
-        want = std::min<uint64_t>(want, by_size);
-        want = std::min<uint64_t>(want, std::max<uint32_t>(1, n_kept / 16));
-        n_chunks = (uint32_t)std::max<uint64_t>(1, want);
-        spc = (n_kept + n_chunks - 1) / n_chunks;
-        n_chunks = (n_kept + spc - 1) / spc;
-      }
-      tpw = (uint32_t)std::max<uint64_t>(1, (n_tiles * n_chunks + target - 1) / target);
-      ntg = (uint32_t)((n_tiles + tpw - 1) / tpw);
-      const uint64_t n_waves = (uint64_t)ntg * n_chunks;
+      const ReduceGeom rg = reduce_geom(T, n_kept, one_chunk);
+      const uint32_t spc = rg.spc, n_chunks = rg.n_chunks, tpw = rg.tpw, ntg = rg.ntg;
+      const uint64_t n_waves = rg.n_waves;
       ReduceArgs r;
       r.e_off = eoff; r.e_len = e_len; r.e_ts = e_ts; r.e_val = e_val; r.e_flt = e_flt; r.n_kept = n_kept;
       r.grid = gridv; r.T = T; r.bitmap = bitmap; r.word_rank = word_rank; r.lo = lo;
@@ -926,6 +942,8 @@ extern "C" int tsdbhip_spangroup_run(tsdbhip_ctx* ctx, const tsdbhip_sg_desc* de
     return f.code;
   }
 }
+
+#include "batch.hip"
 
 // ------------------------------------------------- synthetic inputs ------
 // Device buffers of a generated desc are owned by ctx under keys derived from

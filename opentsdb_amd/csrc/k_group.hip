@@ -1,0 +1,223 @@
+// k_group.hip — group-by batching: the SpanGroups
+// TsdbQuery.groupByAndAggregate builds for one query (TsdbQuery.java:294-363)
+// evaluated in one call. Spans of group g are the contiguous span range
+// [gss[g], gss[g+1]) (groups in ByteMap order, spans in TreeMap order within a
+// group). Per-span work (assembly, decode, downsampling) runs once over every
+// span; the union grid is segmented: group g owns bitmap words
+// [wbase[g], wbase[g] + nw[g] + 1) over its own [lo[g], hi[g]] (the last word
+// is a zero pad, whose rank is T_g), and its grid points are
+// grid[goff[g], goff[g] + T_g).
+#pragma once
+#include "dev_common.h"
+
+namespace tsdb {
+
+// Per-group results of the segmented passes (one 64-B slot per group).
+struct GroupDev {
+  unsigned long long fstar;   // F* of the group (max float-first ts + 1, 0: none)
+  unsigned long long nan_t;   // first NaN/Inf output index (finalize)
+  unsigned long long bad_at;  // lazy illegal-cell index << 4 | code
+  uint64_t goff;              // first grid index of the group
+  uint64_t T;                 // |G_g|
+  uint32_t gfl;               // bit0: some E point is a float, bit1: some is an int
+  uint32_t ambiguous;         // finalize: int dev near an integer after a Chan merge
+  uint64_t pad[2];
+};
+
+__global__ void k_group_init(GroupDev* gd, uint32_t n_groups) {
+  const uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
+  if (g >= n_groups) return;
+  GroupDev z = {};
+  z.nan_t = ~0ull;
+  z.bad_at = ~0ull;
+  gd[g] = z;
+}
+
+// Per-group span statistics after assembly (SpanGroup.java:135-141 keep rule
+// applied per span by k_assemble).
+struct GroupStat {
+  uint64_t k0;       // first kept index of the group
+  uint64_t nk;       // kept spans
+  uint64_t n_input;  // SpanGroup.aggregatedSize() (SpanGroup.java:206-212)
+  int64_t first;     // min first ts of the kept spans
+  int64_t last;      // max last ts of the kept spans
+};
+
+// Block per group (grid-stride): kept-span group ids and the group's stats.
+__global__ void __launch_bounds__(256) k_group_stats(const uint32_t* gss, uint32_t n_groups, uint32_t n_spans,
+                                                     uint32_t n_kept, const uint8_t* sp_kept, const uint64_t* kidx,
+                                                     const uint32_t* sp_ncells, const int64_t* sp_first,
+                                                     const int64_t* sp_last, uint32_t* kgrp, GroupStat* stat) {
+  __shared__ uint64_t sh_c[4], sh_n[4];
+  __shared__ int64_t sh_f[4], sh_l[4];
+  for (uint32_t g = blockIdx.x; g < n_groups; g += gridDim.x) {
+    const uint32_t s0 = gss[g], s1 = gss[g + 1];
+    uint64_t cnt = 0, nk = 0;
+    int64_t f = INT64_MAX, l = INT64_MIN;
+    for (uint32_t s = s0 + threadIdx.x; s < s1; s += blockDim.x) {
+      if (!sp_kept[s]) continue;
+      kgrp[kidx[s]] = g;
+      nk++;
+      cnt += sp_ncells[s];
+      f = min(f, sp_first[s]);
+      l = max(l, sp_last[s]);
+    }
+    auto add = [](uint64_t x, uint64_t y) { return x + y; };
+    cnt = block_reduce_256(cnt, add, sh_c);
+    nk = block_reduce_256(nk, add, sh_n);
+    f = block_reduce_256(f, [](int64_t x, int64_t y) { return min(x, y); }, sh_f);
+    l = block_reduce_256(l, [](int64_t x, int64_t y) { return max(x, y); }, sh_l);
+    if (threadIdx.x == 0) {
+      GroupStat st;
+      st.k0 = s0 < n_spans ? kidx[s0] : n_kept;
+      st.nk = nk;
+      st.n_input = cnt;
+      st.first = f;
+      st.last = l;
+      stat[g] = st;
+    }
+    __syncthreads();
+  }
+}
+
+// Wave per kept span, after decode: E_EMPTY_SPAN (SpanGroup.java:452-455),
+// the group's F* and (flags) whether the group's E holds floats / ints —
+// what k_span_summary and the decode kernels' global flags give one group.
+__global__ void __launch_bounds__(256) k_group_summary(const uint64_t* e_off, const uint32_t* e_len,
+                                                       const uint32_t* e_ts, const uint8_t* e_flt, uint32_t n_kept,
+                                                       int32_t rate, int32_t flags, const uint32_t* kgrp,
+                                                       GroupDev* gd, int32_t* err) {
+  const int lane = lane_id();
+  const uint32_t wave = (blockIdx.x * blockDim.x + threadIdx.x) / WAVE;
+  const uint32_t nwaves = gridDim.x * blockDim.x / WAVE;
+  for (uint32_t k = wave; k < n_kept; k += nwaves) {
+    const uint32_t len = e_len[k];
+    const uint64_t eo = e_off[k];
+    GroupDev* g = &gd[kgrp[k]];
+    if (len == 0) {
+      if (lane == 0) atomicMin(err, -3 /*E_EMPTY_SPAN*/);
+      continue;
+    }
+    if (lane == 0 && !rate && e_flt[eo]) {
+      const unsigned long long fs = (unsigned long long)e_ts[eo] + 1;  // +1: 0 = none
+      if (g->fstar < fs) atomicMax(&g->fstar, fs);
+    }
+    if (!flags) continue;
+    bool f = false, i = false;
+    for (uint32_t j = lane; j < len; j += WAVE) {
+      const bool x = e_flt[eo + j] != 0;
+      f |= x;
+      i |= !x;
+    }
+    const uint32_t bits = (ballot(f) ? 1u : 0u) | (ballot(i) ? 2u : 0u);
+    if (lane == 0 && (g->gfl & bits) != bits) atomicOr(&g->gfl, bits);
+  }
+}
+
+// Geometry of the segmented bitmap, per group (device copies of host math).
+struct GroupGrid {
+  const int64_t* lo;      // [G]
+  const int64_t* hi;      // [G] (lo > hi: empty grid)
+  const uint64_t* wbase;  // [G] first word
+  const uint32_t* nw;     // [G] words (without the pad word)
+  const uint32_t* wgrp;   // [W] group of each word
+};
+
+// Block per group: the word -> group map.
+__global__ void __launch_bounds__(256) k_group_words(GroupGrid q, uint32_t n_groups, uint32_t* wgrp) {
+  for (uint32_t g = blockIdx.x; g < n_groups; g += gridDim.x) {
+    const uint64_t b = q.wbase[g];
+    const uint32_t n = q.nw[g] + 1;
+    for (uint32_t w = threadIdx.x; w < n; w += blockDim.x) wgrp[b + w] = g;
+  }
+}
+
+// k_grid_mark over every kept span, each into its group's bitmap.
+__global__ void __launch_bounds__(256) k_grid_mark_seg(const uint64_t* e_off, const uint32_t* e_len,
+                                                       const uint32_t* e_ts, uint32_t n_kept, int32_t rate,
+                                                       const uint32_t* kgrp, GroupGrid q, uint32_t* bitmap) {
+  const int lane = lane_id();
+  const uint32_t wave = (blockIdx.x * blockDim.x + threadIdx.x) / WAVE;
+  const uint32_t nwaves = gridDim.x * blockDim.x / WAVE;
+  for (uint32_t k = wave; k < n_kept; k += nwaves) {
+    const uint32_t g = kgrp[k];
+    const int64_t lo = q.lo[g], hi = q.hi[g];
+    if (lo > hi) continue;
+    uint32_t* bm = bitmap + q.wbase[g];
+    const uint64_t eo = e_off[k];
+    const uint32_t len = e_len[k];
+    for (uint32_t i0 = rate ? 1 : 0; i0 < len; i0 += WAVE) {
+      const uint32_t i = i0 + lane;
+      if (i >= len) break;
+      const int64_t t = e_ts[eo + i];
+      if (t > hi) break;  // sorted: the rest are beyond end
+      if (t < lo) continue;
+      const uint64_t b = (uint64_t)(t - lo);
+      const uint32_t bit = 1u << (b & 31);
+      uint32_t* w = &bm[b >> 5];
+      if (!(*w & bit)) atomicOr(w, bit);
+    }
+  }
+}
+
+// k_grid_emit over the concatenated bitmaps: global ranks, grid points from
+// each word's own group origin.
+__global__ void __launch_bounds__(256) k_grid_emit_seg(uint32_t* bitmap, uint32_t* word_rank,
+                                                       const uint32_t* block_sum, uint64_t nwords, GroupGrid q,
+                                                       uint32_t* grid) {
+  const uint64_t w = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+  if (w >= nwords) return;
+  const uint32_t r = word_rank[w] + block_sum[w >> 10];
+  word_rank[w] = r;
+  const uint32_t g = q.wgrp[w];
+  const int64_t base = q.lo[g] + (int64_t)((w - q.wbase[g]) * 32);
+  uint32_t bits = bitmap[w];
+  uint32_t i = r;
+  while (bits) {
+    const int b = __builtin_ctz(bits);
+    grid[i++] = (uint32_t)(base + b);
+    bits &= bits - 1;
+  }
+}
+
+// Thread per group: grid offset and size from the global word ranks.
+__global__ void k_group_T(GroupGrid q, uint32_t n_groups, const uint32_t* word_rank, GroupDev* gd) {
+  const uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
+  if (g >= n_groups) return;
+  const uint64_t b = q.wbase[g];
+  const uint32_t r0 = word_rank[b], r1 = word_rank[b + q.nw[g]];  // pad word: rank after the group
+  gd[g].goff = r0;
+  gd[g].T = r1 - r0;
+}
+
+// Word ranks relative to the group (what grid_rank expects per group).
+__global__ void __launch_bounds__(256) k_group_rebase(GroupGrid q, uint64_t nwords, const GroupDev* gd,
+                                                      uint32_t* word_rank) {
+  const uint64_t w = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+  if (w >= nwords) return;
+  word_rank[w] -= (uint32_t)gd[q.wgrp[w]].goff;
+}
+
+// k_bad_index per kept span against its group's grid.
+__global__ void k_bad_index_seg(const int64_t* e_bad, const uint64_t* e_off, const uint32_t* e_ts,
+                                uint32_t n_kept, int32_t rate, const uint32_t* kgrp, GroupGrid q,
+                                const uint32_t* bitmap, const uint32_t* word_rank, GroupDev* gd) {
+  const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
+  if (k >= n_kept) return;
+  const int64_t b = e_bad[k];
+  if (b < 0) return;
+  const uint32_t g = kgrp[k];
+  const uint64_t idx = (uint64_t)(b >> 4), code = (uint64_t)(b & 15);
+  uint64_t at;
+  if (idx == 0 || (rate && idx == 1)) {
+    at = 0;
+  } else {
+    const int64_t tp = e_ts[e_off[k] + idx - 1];
+    if (tp > q.hi[g]) return;  // never consumed
+    const uint64_t wb = q.wbase[g];
+    at = gd[g].T == 0 ? 0 : grid_rank(bitmap + wb, word_rank + wb, q.lo[g], tp);
+  }
+  atomicMin(&gd[g].bad_at, (unsigned long long)((at << 4) | code));
+}
+
+}  // namespace tsdb

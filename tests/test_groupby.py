@@ -1,0 +1,204 @@
+"""Group-by batching: tsdbhip_spangroup_run_batch
+evaluates every SpanGroup of TsdbQuery.groupByAndAggregate
+(TsdbQuery.java:294-363) in one call. Each group must equal the oracle on
+that group alone — the same bar as a lone SpanGroup: integer results
+bit-exact, doubles within 1e-9 relative (bit-exact with EXACT_ORDER), and
+per-group error codes / lazy error indices.
+
+The grouping plan itself (SpanCmp order, Tags.getValueId, ByteMap order,
+dropped spans) is host logic and runs on CPU."""
+import numpy as np
+import pytest
+
+from helpers import I, F, M, T0, U32MAX, assert_same
+import oracle
+from opentsdb_amd import _abi, core, packing, synth
+
+AGGS = [0, 1, 2, 3, 4]
+
+
+# ------------------------------------------------------------- CPU: plan ----
+def key(metric, ts, *tags):
+    """row key: metric(3) | base_time(4) | (tagk(3) tagv(3))*"""
+    b = metric.to_bytes(3, "big") + ts.to_bytes(4, "big")
+    for k, v in tags:
+        b += k.to_bytes(3, "big") + v.to_bytes(3, "big")
+    return b
+
+
+def test_plan_groups_orders_like_bytemap_and_spancmp():
+    host, dc = 1, 2
+    keys = [
+        key(7, 3600, (dc, 2), (host, 9)),
+        key(7, 0, (dc, 1), (host, 0x800000)),  # unsigned compare: 0x80.. after 0x00..
+        key(7, 7200, (dc, 1), (host, 3)),
+        key(7, 0, (dc, 2), (host, 1)),
+        key(7, 0, (dc, 1)),                     # no host tag: dropped when grouping by host
+    ]
+    gk, order, gss = core.plan_groups(keys, [host.to_bytes(3, "big")])
+    assert gk == [(1).to_bytes(3, "big"), (3).to_bytes(3, "big"), (9).to_bytes(3, "big"),
+                  (0x800000).to_bytes(3, "big")]
+    assert order == [3, 2, 0, 1] and gss == [0, 1, 2, 3, 4]
+    # group by dc: SpanCmp order within a group ignores the base time
+    gk, order, gss = core.plan_groups(keys, [dc.to_bytes(3, "big")])
+    assert gk == [(1).to_bytes(3, "big"), (2).to_bytes(3, "big")]
+    assert order == [4, 2, 1, 3, 0] and gss == [0, 3, 5]
+    # group_bys sorted by id: (dc, host) keys regardless of the order given
+    gk2, order2, gss2 = core.plan_groups(keys, [host.to_bytes(3, "big"), dc.to_bytes(3, "big")])
+    gk3, order3, gss3 = core.plan_groups(keys, [dc.to_bytes(3, "big"), host.to_bytes(3, "big")])
+    assert (gk2, order2, gss2) == (gk3, order3, gss3)
+    assert gk2[0] == (1).to_bytes(3, "big") + (2).to_bytes(3, "big")  # host id 1 < dc id 2
+    # no GROUP BY: one group of every span in SpanCmp order
+    gk, order, gss = core.plan_groups(keys, None)
+    assert gk == [b""] and gss == [0, 5] and order == [4, 2, 1, 3, 0]
+
+
+def test_get_value_id():
+    k = key(1, 0, (5, 6), (7, 8))
+    assert core.get_value_id(k, (7).to_bytes(3, "big")) == (8).to_bytes(3, "big")
+    assert core.get_value_id(k, (6).to_bytes(3, "big")) is None
+
+
+def test_span_cmp_shorter_prefix_first():
+    a, b = key(1, 0, (1, 1)), key(1, 99, (1, 1), (2, 2))
+    assert core.span_cmp_key(a) < core.span_cmp_key(b)
+
+
+# ------------------------------------------------------------ GPU parity ----
+def groups_mixed():
+    """Groups that take different paths: int only, float only, int+float
+    (dual), one span, all spans outside the window, no spans, a Q3 float
+    starting late, a rate-style counter."""
+    T = T0
+    return [
+        [I([(T + 100, 10), (T + 110, 20)]), I([(T + 105, 100), (T + 115, 200)])],
+        [F([(T + 10 * i, 1.5 * i) for i in range(30)]), F([(T + 7 + 13 * i, 0.25 * i) for i in range(20)])],
+        [I([(T + 100, 1), (T + 110, 2)]), F([(T + 200, 1.5), (T + 210, 2.5)]),
+         M([(T + 105, 3), (T + 150, 4.5), (T + 400, 7)])],
+        [I([(T + 3 * i, i * i) for i in range(50)])],
+        [I([(T + 5_000_000 + i, i) for i in range(5)])],
+        [],
+        [I([(T + 100, 0), (T + 103, -10)]), I([(T + 101, 5)])],
+        [I([(T + i * 10, 1000 + 37 * i) for i in range(40)]), I([(T + 5 + i * 10, 50 + 3 * i) for i in range(40)])],
+    ]
+
+
+def pack_groups(groups):
+    spans, gss = [], [0]
+    for g in groups:
+        spans.extend(g)
+        gss.append(len(spans))
+    return packing.pack_spans(spans), gss
+
+
+def check_batch(ctx, ss, gss, start=0, end=U32MAX, agg=0, rate=False, ds_interval=0, ds_agg=0, exact=False):
+    rc, res = core.run_spanset_batch(ctx, ss, gss, start, end, agg, rate, ds_interval, ds_agg, exact=exact)
+    first = 0
+    for g in range(len(gss) - 1):
+        sub = ss.shard(gss[g], gss[g + 1])
+        o = oracle.spangroup(sub, start, end, agg, rate, ds_interval, ds_agg)
+        assert_same(res[g], o, exact_double=exact)
+        if o.code and not first:
+            first = o.code
+    assert rc == first
+    return res
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("agg", AGGS)
+@pytest.mark.parametrize("rate", [False, True])
+@pytest.mark.parametrize("ds", [(0, 0), (60, 3), (30, 0)])
+def test_batch_mixed_groups(ctx, agg, rate, ds):
+    ss, gss = pack_groups(groups_mixed())
+    check_batch(ctx, ss, gss, agg=agg, rate=rate, ds_interval=ds[0], ds_agg=ds[1])
+    check_batch(ctx, ss, gss, agg=agg, rate=rate, ds_interval=ds[0], ds_agg=ds[1], exact=True)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("agg", AGGS)
+def test_batch_window(ctx, agg):
+    ss, gss = pack_groups(groups_mixed())
+    check_batch(ctx, ss, gss, start=T0 + 104, end=T0 + 160, agg=agg)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("kind", [_abi.SYN_INT64_COUNTER, _abi.SYN_FLOAT32])
+@pytest.mark.parametrize("agg", AGGS)
+@pytest.mark.parametrize("ds", [(0, 0), (60, 3), (60, 0)])
+def test_batch_regular_uneven_groups(ctx, kind, agg, ds):
+    """Wide hourly rows (streaming decode / k_ds_spans) in groups of 1..40 spans."""
+    ss = synth.regular(120, 700, kind, seed=11, step=10)
+    rng = np.random.default_rng(5)
+    cuts = sorted(set(rng.integers(1, 120, 9).tolist()))
+    gss = [0] + cuts + [120]
+    check_batch(ctx, ss, gss, agg=agg, ds_interval=ds[0], ds_agg=ds[1])
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("agg", [0, 3, 4])
+@pytest.mark.parametrize("float_frac", [0.0, 0.5, 1.0])
+def test_batch_jittered(ctx, agg, float_frac):
+    """C4-like: jittered sparse series, groups of different int/float mixes
+    (per-group reduce mode), wide per-group bitmaps."""
+    ss = synth.jittered(60, 80, seed=9, span_range=400_000, max_gap=700, float_frac=float_frac)
+    gss = [0, 1, 7, 20, 21, 45, 60]
+    check_batch(ctx, ss, gss, agg=agg)
+    check_batch(ctx, ss, gss, agg=agg, exact=True)
+
+
+@pytest.mark.gpu
+def test_batch_lazy_errors_per_group(ctx):
+    """An illegal cell in one group and a NaN in another: each group reports
+    its own code and error index; the other groups are unaffected."""
+    T = T0
+    bad = packing.KeyValue(T, bytes([0x00, 0x02, 0x00, 0x12]), bytes([1, 2, 3, 4, 5, 6, 0]))
+    groups = [
+        [I([(T + i, i) for i in range(5)])],
+        [I([(T + i, i) for i in range(5)]), [bad]],
+        [F([(T + 1, float("inf")), (T + 2, 1.0)]), F([(T + 1, 1.0), (T + 2, 1.0)])],
+        [I([(T + i, 2 * i) for i in range(9)])],
+    ]
+    ss, gss = pack_groups(groups)
+    res = check_batch(ctx, ss, gss)
+    assert [r[0] for r in res] == [0, _abi.E_ILLEGAL_DATA, _abi.E_NAN_INF, 0]
+
+
+@pytest.mark.gpu
+def test_batch_group_construction_error_falls_back(ctx):
+    """A span without rows (AssertionError at SpanGroup construction) in one
+    group: that group reports E_EMPTY_SPAN, the others their points."""
+    T = T0
+    groups = [[I([(T + i, i) for i in range(5)])], [I([(T + 1, 1), (T + 2, 2)])], [I([(T + 3, 3), (T + 4, 4)])]]
+    spans = [s for g in groups for s in g]
+    ss = packing.pack_spans(spans)
+    # give group 1 a second span with no rows
+    srs = ss.span_row_start.tolist()
+    srs.insert(2, srs[2])
+    ss.span_row_start = np.array(srs, np.uint64)
+    gss = [0, 1, 3, 4]
+    res = check_batch(ctx, ss, gss)
+    assert [r[0] for r in res] == [0, _abi.E_EMPTY_SPAN, 0]
+
+
+@pytest.mark.gpu
+def test_group_by_and_aggregate_mirror(ctx):
+    """The host mirror end to end: spans keyed by row key, GROUP BY host."""
+    T = T0
+    host = (1).to_bytes(3, "big")
+    spans, expect = {}, {}
+    rng = np.random.default_rng(3)
+    for h in range(5):
+        for s in range(1 + h):
+            k = key(9, T, (1, 0x10 + h), (2, s))
+            pts = [(T + 10 * i + s, int(rng.integers(-50, 50))) for i in range(30)]
+            spans[k] = core.Span(I(pts))
+            expect.setdefault(h, []).append((k, I(pts)))
+    groups = core.group_by_and_aggregate(spans, [host], 0, U32MAX, False, core.Aggregators.SUM, ctx=ctx)
+    assert len(groups) == 5
+    for h, grp in enumerate(groups):
+        rows = [r for _, r in sorted(expect[h], key=lambda kv: core.span_cmp_key(kv[0]))]
+        o = oracle.spangroup(packing.pack_spans(rows), 0, U32MAX, 0)
+        got = list(grp)
+        assert [p.timestamp() for p in got] == list(o.ts)
+        assert [p.longValue() for p in got] == list(o.bits)
+        assert grp.aggregatedSize() == o.n_input_points
