@@ -408,10 +408,12 @@ struct ReduceGeom {
   uint32_t spc, n_chunks, tpw, ntg;
   uint64_t n_waves;
 };
-static ReduceGeom reduce_geom(uint64_t T, uint32_t n_kept, bool one_chunk) {
+// target: waves in flight over 256 CUs (a group batch splits it over its
+// groups); min_waves: floor for small groups
+static ReduceGeom reduce_geom(uint64_t T, uint32_t n_kept, bool one_chunk, uint64_t target = 16384,
+                              uint64_t min_waves = 2048) {
   ReduceGeom g;
   const uint64_t n_tiles = (T + 63) / 64;
-  const uint64_t target = 16384;  // waves in flight over 256 CUs
   if (one_chunk || n_kept == 0) {
     g.n_chunks = 1;
     g.spc = std::max<uint32_t>(n_kept, 1);
@@ -419,7 +421,7 @@ static ReduceGeom reduce_geom(uint64_t T, uint32_t n_kept, bool one_chunk) {
     // chunks of ~256 spans (fewer partials for the combine), but at
     // least ~2048 waves when the group is small
     uint64_t want = std::max<uint64_t>(1, target / n_tiles);
-    const uint64_t by_size = std::max<uint64_t>((n_kept + 255) / 256, (2048 + n_tiles - 1) / n_tiles);
+    const uint64_t by_size = std::max<uint64_t>((n_kept + 255) / 256, (min_waves + n_tiles - 1) / n_tiles);
     want = std::min<uint64_t>(want, by_size);
     want = std::min<uint64_t>(want, std::max<uint32_t>(1, n_kept / 16));
     g.n_chunks = (uint32_t)std::max<uint64_t>(1, want);

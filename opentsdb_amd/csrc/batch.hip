@@ -8,7 +8,8 @@
 //   k_group_summary                 E_EMPTY_SPAN, F*_g, int/float flags per group
 //   k_grid_mark_seg .. k_group_rebase  segmented union grids (one bitmap per group,
 //                                   concatenated; pad word per group)          [sync 3]
-//   k_reduce + k_finalize_*         per group, grid and E pointers offset
+//   k_reduce_seg + k_finalize_seg   all groups of one reduce mode per launch (wave ->
+//                                   group, tile group, span chunk)
 //   k_bad_index_seg                 lazy error index per group                  [sync 4]
 //
 // Any error the reference raises at group construction (E_EMPTY_SPAN,
@@ -27,6 +28,28 @@ static void* host_buf(tsdbhip_ctx* ctx, size_t bytes) {
   }
   return ctx->host_big;
 }
+
+template <int AGG, int MODE, bool RATE>
+static void launch_seg(tsdbhip_ctx* ctx, const ReduceArgs& r0, const FinalArgs& f0, const SegReduce& sr,
+                       uint64_t waves, const SegGroup* sg, const uint64_t* goff, uint32_t G, uint64_t T_all,
+                       GroupDev* gd) {
+  if (waves)
+    hipLaunchKernelGGL((k_reduce_seg<AGG, MODE, RATE>), dim3((unsigned)((waves + 3) / 4)), dim3(256), 0,
+                       ctx->stream, r0, sr);
+  if (T_all)
+    hipLaunchKernelGGL((k_finalize_seg<AGG, MODE, RATE>), dim3(grid_for(T_all, 256)), dim3(256), 0, ctx->stream,
+                       r0, f0, sg, goff, G, T_all, gd);
+}
+
+struct LaunchSeg {
+  template <int AGG, typename... A>
+  static void run(tsdbhip_ctx* ctx, int mode, bool rate, A&&... a) {
+    if (rate) return launch_seg<AGG, MODE_DBL, true>(ctx, a...);
+    if (mode == MODE_INT) return launch_seg<AGG, MODE_INT, false>(ctx, a...);
+    if (mode == MODE_DBL) return launch_seg<AGG, MODE_DBL, false>(ctx, a...);
+    launch_seg<AGG, MODE_DUAL, false>(ctx, a...);
+  }
+};
 
 template <typename T>
 static T* upload(tsdbhip_ctx* ctx, const char* name, const std::vector<T>& v) {
@@ -304,7 +327,8 @@ static int spangroup_run_batch(tsdbhip_ctx* ctx, const tsdbhip_sg_desc* d, uint3
   if (h.err) return batch_one_by_one(ctx, dd, G, gss, outs);
   tm.n_grid = T_all;
 
-  // ---- reduce, one launch pair per group (grid / E / bitmap views offset) ----
+  // ---- reduce: one k_reduce_seg + k_finalize_seg per reduce mode present,
+  // each wave mapped to (group, tile group, span chunk) ----
   int64_t* out_ts = scratch<int64_t>(ctx, "out_ts", T_all);
   uint8_t* out_isint = scratch<uint8_t>(ctx, "out_isint", T_all);
   int64_t* out_bits = scratch<int64_t>(ctx, "out_bits", T_all);
@@ -314,51 +338,92 @@ static int spangroup_run_batch(tsdbhip_ctx* ctx, const tsdbhip_sg_desc* d, uint3
     const bool i = anyf && anyi ? (gh[g].gfl & 2u) != 0 : anyi;
     return !f ? (int)MODE_INT : (!i ? (int)MODE_DBL : (int)MODE_DUAL);
   };
-  // scratch sized for the largest group once (reused in stream order)
-  uint64_t max_cur = 1, max_part = 1;
+  std::vector<SegGroup> sgv(G);
+  std::vector<uint64_t> goffv(G);
+  std::vector<uint32_t> glist[3];
+  std::vector<uint64_t> wstart[3];
+  for (auto& w : wstart) w.push_back(0);
+  uint64_t poff = 0, coff = 0;
   for (uint32_t g = 0; g < G; g++) {
-    if (!gh[g].T) continue;
-    const ReduceGeom rg = reduce_geom(gh[g].T, (uint32_t)gs[g].nk, exact);
-    max_cur = std::max<uint64_t>(max_cur, rg.n_waves * rg.spc);
-    max_part = std::max<uint64_t>(max_part, (uint64_t)rg.n_chunks * gh[g].T);
+    SegGroup& x = sgv[g];
+    std::memset(&x, 0, sizeof x);
+    x.k0 = gs[g].k0;
+    x.nk = (uint32_t)gs[g].nk;
+    x.goff = gh[g].goff;
+    x.T = gh[g].T;
+    x.wbase = gwb[g];
+    x.lo = glo[g];
+    x.fstar = gh[g].fstar;
+    x.mode = (uint32_t)mode_of(g);
+    goffv[g] = x.goff;
+    if (!x.T) continue;
+    // the batch shares the single-group wave budget in proportion to spans
+    const double share = n_kept ? (double)x.nk / n_kept : 1.0;
+    const ReduceGeom rg = reduce_geom(x.T, x.nk, exact, std::max<uint64_t>(64, (uint64_t)(16384 * share)),
+                                      std::max<uint64_t>(16, (uint64_t)(2048 * share)));
+    x.spc = rg.spc; x.n_chunks = rg.n_chunks; x.tpw = rg.tpw; x.ntg = rg.ntg;
+    x.poff = poff;
+    poff += (uint64_t)rg.n_chunks * x.T;
+    x.coff = coff;
+    coff += rg.n_waves * rg.spc;
+    glist[x.mode].push_back(g);
+    wstart[x.mode].push_back(wstart[x.mode].back() + rg.n_waves);
   }
   ReduceArgs r0;
   std::memset(&r0, 0, sizeof r0);
-  r0.e_ts = e_ts; r0.e_val = e_val; r0.e_flt = e_flt; r0.exact = exact ? 1 : 0;
-  r0.ptr = scratch<uint32_t>(ctx, "cursor", max_cur);
-  r0.st_x = scratch<uint2>(ctx, "st_x", max_cur);
-  r0.st_y = scratch<longlong2>(ctx, "st_y", max_cur);
-  r0.st_rv = scratch<double>(ctx, "st_rv", max_cur);
-  r0.st_f = scratch<uint32_t>(ctx, "st_f", max_cur);
-  r0.p_cnt = scratch<uint32_t>(ctx, "p_cnt", max_part);
-  r0.p_flag = scratch<uint8_t>(ctx, "p_flag", max_part);
-  r0.p_i = scratch<int64_t>(ctx, "p_i", max_part);
-  r0.p_d = scratch<double>(ctx, "p_d", max_part);
-  r0.p_dhas = scratch<uint32_t>(ctx, "p_dhas", max_part);
-  if (agg == TSDBHIP_AGG_DEV) {
-    r0.p_wim = scratch<double>(ctx, "p_wim", max_part);
-    r0.p_wiv = scratch<double>(ctx, "p_wiv", max_part);
-    r0.p_wdm = scratch<double>(ctx, "p_wdm", max_part);
-    r0.p_wdv = scratch<double>(ctx, "p_wdv", max_part);
+  r0.e_off = eoff; r0.e_len = e_len; r0.e_ts = e_ts; r0.e_val = e_val; r0.e_flt = e_flt; r0.kept = kept;
+  r0.grid = gridv; r0.bitmap = bitmap; r0.word_rank = word_rank; r0.exact = exact ? 1 : 0;
+  auto alloc_reduce = [&](ReduceArgs& r, uint64_t ncur, uint64_t npart) {
+    r.ptr = scratch<uint32_t>(ctx, "cursor", ncur);
+    r.st_x = scratch<uint2>(ctx, "st_x", ncur);
+    r.st_y = scratch<longlong2>(ctx, "st_y", ncur);
+    r.st_rv = scratch<double>(ctx, "st_rv", ncur);
+    r.st_f = scratch<uint32_t>(ctx, "st_f", ncur);
+    r.p_cnt = scratch<uint32_t>(ctx, "p_cnt", npart);
+    r.p_flag = scratch<uint8_t>(ctx, "p_flag", npart);
+    r.p_i = scratch<int64_t>(ctx, "p_i", npart);
+    r.p_d = scratch<double>(ctx, "p_d", npart);
+    r.p_dhas = scratch<uint32_t>(ctx, "p_dhas", npart);
+    if (agg == TSDBHIP_AGG_DEV) {
+      r.p_wim = scratch<double>(ctx, "p_wim", npart);
+      r.p_wiv = scratch<double>(ctx, "p_wiv", npart);
+      r.p_wdm = scratch<double>(ctx, "p_wdm", npart);
+      r.p_wdv = scratch<double>(ctx, "p_wdv", npart);
+    }
+  };
+  alloc_reduce(r0, std::max<uint64_t>(coff, 1), std::max<uint64_t>(poff, 1));
+  FinalArgs f0;
+  std::memset(&f0, 0, sizeof f0);
+  f0.grid = gridv; f0.rate = rate; f0.out_ts = out_ts; f0.out_isint = out_isint; f0.out_bits = out_bits;
+  const SegGroup* sg_d = upload(ctx, "b_seg", sgv);
+  const uint64_t* goff_d = upload(ctx, "b_goff", goffv);
+  for (int m = 0; m < 3; m++) {
+    if (glist[m].empty()) continue;
+    SegReduce sr;
+    sr.sg = sg_d;
+    sr.glist = upload(ctx, m == 0 ? "b_gl0" : m == 1 ? "b_gl1" : "b_gl2", glist[m]);
+    sr.wv_start = upload(ctx, m == 0 ? "b_ws0" : m == 1 ? "b_ws1" : "b_ws2", wstart[m]);
+    sr.n = (uint32_t)glist[m].size();
+    launch_agg<LaunchSeg>(agg, ctx, m, rate, r0, f0, sr, wstart[m].back(), sg_d, goff_d, G, T_all, gd);
   }
-  auto reduce_group = [&](uint32_t g, bool one_chunk) {
+  // ambiguous-int-dev reruns: one group, one chunk (k_reduce + k_finalize_seq)
+  auto reduce_group = [&](uint32_t g) {
     const uint64_t T = gh[g].T, go = gh[g].goff, k0 = gs[g].k0;
     const uint32_t nk = (uint32_t)gs[g].nk;
-    const ReduceGeom rg = reduce_geom(T, nk, one_chunk);
+    const ReduceGeom rg = reduce_geom(T, nk, true);
     ReduceArgs r = r0;
+    alloc_reduce(r, rg.n_waves * rg.spc, (uint64_t)rg.n_chunks * T);
     r.e_off = eoff + k0; r.e_len = e_len + k0; r.n_kept = nk; r.kept = kept + k0;
     r.grid = gridv + go; r.T = T; r.bitmap = bitmap + gwb[g]; r.word_rank = word_rank + gwb[g]; r.lo = glo[g];
     r.spans_per_chunk = rg.spc; r.n_chunks = rg.n_chunks; r.tiles_per_wave = rg.tpw; r.n_tile_groups = rg.ntg;
     r.fstar = gh[g].fstar;
-    FinalArgs f;
-    f.T = T; f.n_chunks = rg.n_chunks; f.grid = gridv + go; f.fstar = gh[g].fstar; f.rate = rate;
+    FinalArgs f = f0;
+    f.T = T; f.n_chunks = rg.n_chunks; f.grid = gridv + go; f.fstar = gh[g].fstar;
     f.out_ts = out_ts + go; f.out_isint = out_isint + go; f.out_bits = out_bits + go;
     f.nan_t = &gd[g].nan_t;
     f.ambiguous = &gd[g].ambiguous;
-    dispatch_reduce(ctx, agg, mode_of(g), rate, (unsigned)((rg.n_waves + 3) / 4), r, f, rg.n_chunks >= 64, true);
+    dispatch_reduce(ctx, agg, mode_of(g), rate, (unsigned)((rg.n_waves + 3) / 4), r, f, false, true);
   };
-  for (uint32_t g = 0; g < G; g++)
-    if (gh[g].T) reduce_group(g, exact);
   if (n_kept)
     hipLaunchKernelGGL(k_bad_index_seg, dim3(grid_for(n_kept, 256)), dim3(256), 0, st, e_bad, eoff, e_ts, n_kept,
                        (int32_t)rate, kgrp, q, bitmap, word_rank, gd);
@@ -375,7 +440,7 @@ static int spangroup_run_batch(tsdbhip_ctx* ctx, const tsdbhip_sg_desc* d, uint3
       std::memcpy(ctx->host_small, &z, sizeof z);
       HIPCHK(hipMemcpyAsync(&gd[g], ctx->host_small, sizeof z, hipMemcpyHostToDevice, st));
       HIPCHK(hipStreamSynchronize(st));
-      reduce_group(g, true);
+      reduce_group(g);
     }
     if (any) read_groups();
   }

@@ -9,6 +9,8 @@
 // grid[goff[g], goff[g] + T_g).
 #pragma once
 #include "dev_common.h"
+#include "k_grid.hip"
+#include "k_reduce.hip"
 
 namespace tsdb {
 
@@ -218,6 +220,115 @@ __global__ void k_bad_index_seg(const int64_t* e_bad, const uint64_t* e_off, con
     at = gd[g].T == 0 ? 0 : grid_rank(bitmap + wb, word_rank + wb, q.lo[g], tp);
   }
   atomicMin(&gd[g].bad_at, (unsigned long long)((at << 4) | code));
+}
+
+// ---- one reduce launch for many groups ------------------------------------
+// Per-group view of the shared E / grid / partial buffers (host-computed
+// after the segmented grid is known).
+struct SegGroup {
+  uint64_t k0;       // first kept index
+  uint64_t goff;     // first grid index (output offset)
+  uint64_t T;        // |G_g|
+  uint64_t wbase;    // first bitmap word
+  int64_t lo;        // bitmap origin
+  uint64_t fstar;    // F*_g
+  uint64_t poff;     // partials offset ([n_chunks][T] block of the group)
+  uint64_t coff;     // cursor / bracket-cache offset
+  uint32_t nk, spc, n_chunks, tpw, ntg, mode;
+};
+
+struct SegReduce {
+  const SegGroup* sg;
+  const uint32_t* glist;     // groups of this launch (one reduce mode)
+  const uint64_t* wv_start;  // [n+1] first wave of each listed group
+  uint32_t n;
+};
+
+DEVI void seg_view(ReduceArgs& r, const SegGroup& G) {
+  r.e_off += G.k0;
+  r.e_len += G.k0;
+  r.kept += G.k0;
+  r.n_kept = G.nk;
+  r.grid += G.goff;
+  r.T = G.T;
+  r.bitmap += G.wbase;
+  r.word_rank += G.wbase;
+  r.lo = G.lo;
+  r.spans_per_chunk = G.spc;
+  r.n_chunks = G.n_chunks;
+  r.tiles_per_wave = G.tpw;
+  r.n_tile_groups = G.ntg;
+  r.fstar = G.fstar;
+  r.ptr += G.coff;
+  r.st_x += G.coff;
+  r.st_y += G.coff;
+  r.st_rv += G.coff;
+  r.st_f += G.coff;
+  r.p_cnt += G.poff;
+  r.p_flag += G.poff;
+  r.p_i += G.poff;
+  r.p_d += G.poff;
+  r.p_dhas += G.poff;
+  if (r.p_wim) {
+    r.p_wim += G.poff;
+    r.p_wiv += G.poff;
+    r.p_wdm += G.poff;
+    r.p_wdv += G.poff;
+  }
+}
+
+// k_reduce over the groups of one mode: wave -> group by a (scalar) binary
+// search of the launch's wave offsets, then the single-group wave body.
+template <int AGG, int MODE, bool RATE>
+__global__ void __launch_bounds__(256) k_reduce_seg(ReduceArgs r0, SegReduce s) {
+  const uint64_t wave = __builtin_amdgcn_readfirstlane((blockIdx.x * blockDim.x + threadIdx.x) / WAVE);
+  if (wave >= s.wv_start[s.n]) return;
+  uint32_t lo = 0, hi = s.n;  // wv_start[lo] <= wave < wv_start[hi]
+  while (hi - lo > 1) {
+    const uint32_t mid = (lo + hi) >> 1;
+    if (s.wv_start[mid] <= wave) lo = mid; else hi = mid;
+  }
+  const SegGroup G = s.sg[s.glist[lo]];
+  ReduceArgs r = r0;
+  seg_view(r, G);
+  reduce_wave<AGG, MODE, RATE, false>(r, (uint32_t)(wave - s.wv_start[lo]));
+}
+
+// k_finalize_seq over every grid point of the groups of one mode.
+template <int AGG, int MODE, bool RATE>
+__global__ void __launch_bounds__(256) k_finalize_seg(ReduceArgs r0, FinalArgs f0, const SegGroup* sg,
+                                                      const uint64_t* goff, uint32_t n_groups, uint64_t T_all,
+                                                      GroupDev* gd) {
+  const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= T_all) return;
+  uint32_t lo = 0, hi = n_groups;  // last group with goff <= t (empty groups share the next offset)
+  while (hi - lo > 1) {
+    const uint32_t mid = (lo + hi) >> 1;
+    if (goff[mid] <= t) lo = mid; else hi = mid;
+  }
+  const SegGroup G = sg[lo];
+  if (G.mode != (uint32_t)MODE || t - G.goff >= G.T) return;
+  ReduceArgs r = r0;
+  seg_view(r, G);
+  FinalArgs f = f0;
+  f.T = G.T;
+  f.n_chunks = G.n_chunks;
+  f.grid += G.goff;
+  f.fstar = G.fstar;
+  f.out_ts += G.goff;
+  f.out_isint += G.goff;
+  f.out_bits += G.goff;
+  f.nan_t = &gd[lo].nan_t;
+  f.ambiguous = &gd[lo].ambiguous;
+  const uint64_t g = t - G.goff;
+  Acc a;
+  acc_load<AGG, MODE>(r, g, a);
+  for (uint32_t c = 1; c < f.n_chunks; c++) {
+    Acc b;
+    acc_load<AGG, MODE>(r, (uint64_t)c * f.T + g, b);
+    acc_merge<AGG, MODE>(a, b);
+  }
+  finalize_one<AGG, MODE, RATE>(f, g, a);
 }
 
 }  // namespace tsdb

@@ -294,10 +294,11 @@ DEVI void direct_run(const ReduceArgs& r, Acc& acc, uint32_t run, uint32_t i, ui
 // DONLY: the instantiation for span chunks holding direct spans only (no E
 // span state, fewer registers); with direct spans present both are launched
 // and each takes the chunks r.chunk_e marks as its own.
+// reduce_wave: the work of one wave (tile group x span chunk) of a group;
+// k_reduce runs one group, k_reduce_seg (k_group.hip) many groups per launch.
 template <int AGG, int MODE, bool RATE, bool DONLY>
-__global__ void __launch_bounds__(256) k_reduce(ReduceArgs r) {
+DEVI void reduce_wave(const ReduceArgs& r, const uint32_t wave) {
   const int lane = lane_id();
-  const uint32_t wave = (blockIdx.x * blockDim.x + threadIdx.x) / WAVE;
   const uint32_t n_waves = r.n_chunks * r.n_tile_groups;
   if (wave >= n_waves) return;
   const uint32_t chunk = wave % r.n_chunks;
@@ -764,6 +765,11 @@ __global__ void __launch_bounds__(256) k_reduce(ReduceArgs r) {
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
   }
+}
+
+template <int AGG, int MODE, bool RATE, bool DONLY>
+__global__ void __launch_bounds__(256) k_reduce(ReduceArgs r) {
+  reduce_wave<AGG, MODE, RATE, DONLY>(r, (blockIdx.x * blockDim.x + threadIdx.x) / WAVE);
 }
 
 __global__ void k_chunk_flags(const uint32_t* d_info, uint32_t n_kept, uint32_t spc, uint32_t* chunk_e) {
