@@ -33,8 +33,11 @@ template <int AGG, int MODE, bool RATE>
 static void launch_seg(tsdbhip_ctx* ctx, const ReduceArgs& r0, const FinalArgs& f0, const SegReduce& sr,
                        uint64_t waves, const SegGroup* sg, const uint64_t* goff, uint32_t G, uint64_t T_all,
                        GroupDev* gd) {
+  if (waves && r0.d_info)  // span chunks without E spans (k_reduce's DONLY instantiation)
+    hipLaunchKernelGGL((k_reduce_seg<AGG, MODE, RATE, true>), dim3((unsigned)((waves + 3) / 4)), dim3(256), 0,
+                       ctx->stream, r0, sr);
   if (waves)
-    hipLaunchKernelGGL((k_reduce_seg<AGG, MODE, RATE>), dim3((unsigned)((waves + 3) / 4)), dim3(256), 0,
+    hipLaunchKernelGGL((k_reduce_seg<AGG, MODE, RATE, false>), dim3((unsigned)((waves + 3) / 4)), dim3(256), 0,
                        ctx->stream, r0, sr);
   if (T_all)
     hipLaunchKernelGGL((k_finalize_seg<AGG, MODE, RATE>), dim3(grid_for(T_all, 256)), dim3(256), 0, ctx->stream,
@@ -246,8 +249,11 @@ static int spangroup_run_batch(tsdbhip_ctx* ctx, const tsdbhip_sg_desc* d, uint3
   da.end = d->end_time; da.interval = interval; da.ds_agg = ds_agg; da.rate = rate; da.err = &sm->err;
   da.gflags = sm->gflags; da.range = sm->range; da.fstar = &sm->fstar;
   HIPCHK(hipEventRecord(ctx->ev[1], st));
+  bool direct = false;  // k_direct_scan took the no-downsampling path
+  DirectArgs dg = {};
   if (n_kept) {
     const unsigned blocks = grid_for(n_kept, 4, 65536);
+    const char* force = getenv("TSDBHIP_DECODE");  // "fast": no direct path (tests)
     const bool fast = R > 0 && h.n_input / R >= 64;  // wide (hourly compacted) rows
     da.fb_list = scratch<uint32_t>(ctx, "fb_list", n_kept);
     da.fb_count = scratch<uint32_t>(ctx, "fb_count", 1, true);
@@ -263,8 +269,36 @@ static int spangroup_run_batch(tsdbhip_ctx* ctx, const tsdbhip_sg_desc* d, uint3
       else launch_agg<LaunchGeneralDs>(ds_agg, ctx, blocks, da);
       HIPCHK(hipEventRecord(ctx->ev[9], st));
     } else if (interval == 0) {
-      hipLaunchKernelGGL((k_decode_fast<0, false>), dim3(blocks), dim3(256), 0, st, da, row_ncells, row_val_len);
-      HIPCHK(hipEventRecord(ctx->ev[9], st));
+      DecodeArgs fa = da;
+      direct = !(force && !strcmp(force, "fast"));
+      if (direct) {
+        // regular-cadence spans on consecutive grid ranks of their group skip E
+        // (k_direct.hip); the scan only proves the cadence here, the group
+        // grids are marked after decode (k_direct_mark_seg)
+        dg.info = scratch<uint32_t>(ctx, "d_info", n_kept);
+        dg.n = scratch<uint32_t>(ctx, "d_n", n_kept);
+        dg.x0 = scratch<uint32_t>(ctx, "d_x0", n_kept);
+        dg.step = scratch<uint32_t>(ctx, "d_step", n_kept);
+        dg.voff = scratch<uint64_t>(ctx, "d_voff", n_kept);
+        dg.c0 = scratch<uint32_t>(ctx, "d_c0", n_kept);
+        dg.r0 = scratch<uint64_t>(ctx, "d_r0", n_kept);
+        dg.ga = scratch<uint32_t>(ctx, "d_ga", n_kept);
+        dg.row_cpre = scratch<uint32_t>(ctx, "row_cpre", R);
+        dg.list = scratch<uint32_t>(ctx, "d_list", n_kept);
+        dg.list_count = scratch<uint32_t>(ctx, "d_list_count", 1, true);
+        dg.bitmap = nullptr;
+        dg.lo = 0;
+        dg.hi = -1;
+        dg.rate = rate;
+        ctx->hot_kernel = TSDBHIP_HOT_REDUCE_DIRECT;  // timed around the reduce launches
+        hipLaunchKernelGGL(k_direct_scan, dim3(grid_for(n_kept, 4 * DIRB, 1u << 20)), dim3(256), 0, st, da, dg,
+                           row_ncells, row_val_len);
+        fa.span_list = dg.list;
+        fa.span_count = dg.list_count;
+      }
+      const unsigned lblocks = fa.span_list ? std::min(blocks, 1024u) : blocks;
+      hipLaunchKernelGGL((k_decode_fast<0, false>), dim3(lblocks), dim3(256), 0, st, fa, row_ncells, row_val_len);
+      if (!direct) HIPCHK(hipEventRecord(ctx->ev[9], st));
       hipLaunchKernelGGL(k_decode_nods, dim3(std::min(blocks, 1024u)), dim3(256), 0, st, ga);
     } else {
       DecodeArgs fa = da;
@@ -288,10 +322,8 @@ static int spangroup_run_batch(tsdbhip_ctx* ctx, const tsdbhip_sg_desc* d, uint3
   // ---- per-group summary and segmented union grids ----
   GroupDev* gd = scratch<GroupDev>(ctx, "b_gd", G);
   hipLaunchKernelGGL(k_group_init, dim3(grid_for(G, 256)), dim3(256), 0, st, gd, G);
-  if (n_kept)
-    hipLaunchKernelGGL(k_group_summary, dim3(grid_for(n_kept, 4, 65536)), dim3(256), 0, st, eoff, e_len, e_ts,
-                       e_flt, n_kept, (int32_t)rate, (int32_t)(!rate && anyf && anyi), kgrp, gd, &sm->err);
   HIPCHK(hipEventRecord(ctx->ev[3], st));
+  const uint32_t* d_info = direct ? dg.info : nullptr;
   uint32_t* bitmap = scratch<uint32_t>(ctx, "bitmap", W, true);
   uint32_t* word_rank = scratch<uint32_t>(ctx, "word_rank", W);
   const uint64_t nb = (W + 1023) / 1024;
@@ -300,7 +332,10 @@ static int spangroup_run_batch(tsdbhip_ctx* ctx, const tsdbhip_sg_desc* d, uint3
                      G, wgrp);
   if (n_kept)
     hipLaunchKernelGGL(k_grid_mark_seg, dim3(grid_for(n_kept, 4, 65536)), dim3(256), 0, st, eoff, e_len, e_ts,
-                       n_kept, (int32_t)rate, kgrp, q, bitmap);
+                       n_kept, (int32_t)rate, kgrp, q, bitmap, d_info);
+  if (direct && n_kept)
+    hipLaunchKernelGGL(k_direct_mark_seg, dim3(grid_for(n_kept, 4 * WAVE, 16384)), dim3(256), 0, st, dg, n_kept,
+                       kgrp, q, bitmap);
   GridArgs ga;
   std::memset(&ga, 0, sizeof ga);
   ga.bitmap = bitmap; ga.nwords = W; ga.word_rank = word_rank; ga.block_sum = bsum; ga.total = &sm->T;
@@ -314,6 +349,27 @@ static int spangroup_run_batch(tsdbhip_ctx* ctx, const tsdbhip_sg_desc* d, uint3
   hipLaunchKernelGGL(k_group_T, dim3(grid_for(G, 256)), dim3(256), 0, st, q, G, (const uint32_t*)word_rank, gd);
   hipLaunchKernelGGL(k_group_rebase, dim3(grid_for(W, 256)), dim3(256), 0, st, q, W, (const GroupDev*)gd,
                      word_rank);
+  if (direct && n_kept) {
+    // candidates whose points are not consecutive ranks of their group grid
+    // need E (their grid points are already marked)
+    HIPCHK(hipMemsetAsync(dg.list_count, 0, 4, st));
+    HIPCHK(hipMemsetAsync(da.fb_count, 0, 4, st));
+    hipLaunchKernelGGL(k_direct_verify_seg, dim3(grid_for(n_kept, 256)), dim3(256), 0, st, dg, n_kept, kgrp, q,
+                       (const uint32_t*)bitmap, (const uint32_t*)word_rank);
+    DecodeArgs fa = da;
+    fa.span_list = dg.list;
+    fa.span_count = dg.list_count;
+    const unsigned vb = std::min(grid_for(n_kept, 4, 65536), 1024u);
+    hipLaunchKernelGGL((k_decode_fast<0, false>), dim3(vb), dim3(256), 0, st, fa, row_ncells, row_val_len);
+    DecodeArgs gfa = da;
+    gfa.use_fb = 1;
+    hipLaunchKernelGGL(k_decode_nods, dim3(vb), dim3(256), 0, st, gfa);
+  }
+  // E_EMPTY_SPAN, F*_g and the group's int/float flags, over final E / direct spans
+  if (n_kept)
+    hipLaunchKernelGGL(k_group_summary, dim3(grid_for(n_kept, 4, 65536)), dim3(256), 0, st, eoff, e_len, e_ts,
+                       e_flt, n_kept, (int32_t)rate, (int32_t)(!rate && anyf && anyi), kgrp, d_info,
+                       (const uint32_t*)dg.x0, gd, &sm->err);
   HIPCHK(hipEventRecord(ctx->ev[4], st));
   std::vector<GroupDev> gh(G);
   auto read_groups = [&]() {
@@ -343,7 +399,8 @@ static int spangroup_run_batch(tsdbhip_ctx* ctx, const tsdbhip_sg_desc* d, uint3
   std::vector<uint32_t> glist[3];
   std::vector<uint64_t> wstart[3];
   for (auto& w : wstart) w.push_back(0);
-  uint64_t poff = 0, coff = 0;
+  uint64_t poff = 0, coff = 0, choff = 0;
+  std::vector<uint64_t> choffv(G, 0);
   for (uint32_t g = 0; g < G; g++) {
     SegGroup& x = sgv[g];
     std::memset(&x, 0, sizeof x);
@@ -366,6 +423,9 @@ static int spangroup_run_batch(tsdbhip_ctx* ctx, const tsdbhip_sg_desc* d, uint3
     poff += (uint64_t)rg.n_chunks * x.T;
     x.coff = coff;
     coff += rg.n_waves * rg.spc;
+    x.choff = choff;
+    choffv[g] = choff;
+    choff += rg.n_chunks;
     glist[x.mode].push_back(g);
     wstart[x.mode].push_back(wstart[x.mode].back() + rg.n_waves);
   }
@@ -397,6 +457,19 @@ static int spangroup_run_batch(tsdbhip_ctx* ctx, const tsdbhip_sg_desc* d, uint3
   f0.grid = gridv; f0.rate = rate; f0.out_ts = out_ts; f0.out_isint = out_isint; f0.out_bits = out_bits;
   const SegGroup* sg_d = upload(ctx, "b_seg", sgv);
   const uint64_t* goff_d = upload(ctx, "b_goff", goffv);
+  if (direct) {
+    r0.d_info = dg.info; r0.d_n = dg.n; r0.d_ga = dg.ga; r0.d_voff = dg.voff; r0.d_x0 = dg.x0;
+    r0.d_step = dg.step; r0.d_c0 = dg.c0; r0.d_r0 = dg.r0; r0.row_cpre = dg.row_cpre;
+    r0.span_row_start = span_row_start; r0.row_ncells = row_ncells; r0.row_val_off = dd.row_val_off;
+    r0.val = dd.val_bytes;
+    uint32_t* ce = scratch<uint32_t>(ctx, "chunk_e", std::max<uint64_t>(choff, 1), true);
+    const uint64_t* choff_d = upload(ctx, "b_choff", choffv);
+    if (n_kept)
+      hipLaunchKernelGGL(k_chunk_flags_seg, dim3(grid_for(n_kept, 256)), dim3(256), 0, st, (const uint32_t*)dg.info,
+                         n_kept, (const uint32_t*)kgrp, sg_d, choff_d, ce);
+    r0.chunk_e = ce;
+    HIPCHK(hipEventRecord(ctx->ev[8], st));
+  }
   for (int m = 0; m < 3; m++) {
     if (glist[m].empty()) continue;
     SegReduce sr;
@@ -406,6 +479,7 @@ static int spangroup_run_batch(tsdbhip_ctx* ctx, const tsdbhip_sg_desc* d, uint3
     sr.n = (uint32_t)glist[m].size();
     launch_agg<LaunchSeg>(agg, ctx, m, rate, r0, f0, sr, wstart[m].back(), sg_d, goff_d, G, T_all, gd);
   }
+  if (direct) HIPCHK(hipEventRecord(ctx->ev[9], st));  // (finalize included: small next to the reduce)
   // ambiguous-int-dev reruns: one group, one chunk (k_reduce + k_finalize_seq)
   auto reduce_group = [&](uint32_t g) {
     const uint64_t T = gh[g].T, go = gh[g].goff, k0 = gs[g].k0;
@@ -417,6 +491,13 @@ static int spangroup_run_batch(tsdbhip_ctx* ctx, const tsdbhip_sg_desc* d, uint3
     r.grid = gridv + go; r.T = T; r.bitmap = bitmap + gwb[g]; r.word_rank = word_rank + gwb[g]; r.lo = glo[g];
     r.spans_per_chunk = rg.spc; r.n_chunks = rg.n_chunks; r.tiles_per_wave = rg.tpw; r.n_tile_groups = rg.ntg;
     r.fstar = gh[g].fstar;
+    if (r.d_info) {  // one chunk, taken by the E instantiation (mixed chunks are its own)
+      r.d_info += k0; r.d_n += k0; r.d_ga += k0; r.d_voff += k0; r.d_x0 += k0; r.d_step += k0;
+      r.d_c0 += k0; r.d_r0 += k0;
+      uint32_t* one = scratch<uint32_t>(ctx, "chunk_e1", 1);
+      HIPCHK(hipMemsetAsync(one, 0xff, 4, st));
+      r.chunk_e = one;
+    }
     FinalArgs f = f0;
     f.T = T; f.n_chunks = rg.n_chunks; f.grid = gridv + go; f.fstar = gh[g].fstar;
     f.out_ts = out_ts + go; f.out_isint = out_isint + go; f.out_bits = out_bits + go;

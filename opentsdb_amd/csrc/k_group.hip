@@ -11,6 +11,7 @@
 #include "dev_common.h"
 #include "k_grid.hip"
 #include "k_reduce.hip"
+#include "k_direct.hip"
 
 namespace tsdb {
 
@@ -85,9 +86,12 @@ __global__ void __launch_bounds__(256) k_group_stats(const uint32_t* gss, uint32
 // Wave per kept span, after decode: E_EMPTY_SPAN (SpanGroup.java:452-455),
 // the group's F* and (flags) whether the group's E holds floats / ints —
 // what k_span_summary and the decode kernels' global flags give one group.
+// Direct spans (d_info & DIR_ON, k_direct.hip) hold no E: one cell type,
+// first point x0.
 __global__ void __launch_bounds__(256) k_group_summary(const uint64_t* e_off, const uint32_t* e_len,
                                                        const uint32_t* e_ts, const uint8_t* e_flt, uint32_t n_kept,
                                                        int32_t rate, int32_t flags, const uint32_t* kgrp,
+                                                       const uint32_t* d_info, const uint32_t* d_x0,
                                                        GroupDev* gd, int32_t* err) {
   const int lane = lane_id();
   const uint32_t wave = (blockIdx.x * blockDim.x + threadIdx.x) / WAVE;
@@ -96,6 +100,19 @@ __global__ void __launch_bounds__(256) k_group_summary(const uint64_t* e_off, co
     const uint32_t len = e_len[k];
     const uint64_t eo = e_off[k];
     GroupDev* g = &gd[kgrp[k]];
+    const uint32_t info = d_info ? d_info[k] : 0u;
+    if (info & DIR_ON) {
+      if (lane == 0) {
+        const bool f = (info & DIR_FLT) != 0;
+        if (f && !rate) {
+          const unsigned long long fs = (unsigned long long)d_x0[k] + 1;
+          if (g->fstar < fs) atomicMax(&g->fstar, fs);
+        }
+        const uint32_t bits = f ? 1u : 2u;
+        if (flags && (g->gfl & bits) != bits) atomicOr(&g->gfl, bits);
+      }
+      continue;
+    }
     if (len == 0) {
       if (lane == 0) atomicMin(err, -3 /*E_EMPTY_SPAN*/);
       continue;
@@ -135,13 +152,16 @@ __global__ void __launch_bounds__(256) k_group_words(GroupGrid q, uint32_t n_gro
 }
 
 // k_grid_mark over every kept span, each into its group's bitmap.
+// (direct candidates, which hold no E, are marked by k_direct_mark_seg)
 __global__ void __launch_bounds__(256) k_grid_mark_seg(const uint64_t* e_off, const uint32_t* e_len,
                                                        const uint32_t* e_ts, uint32_t n_kept, int32_t rate,
-                                                       const uint32_t* kgrp, GroupGrid q, uint32_t* bitmap) {
+                                                       const uint32_t* kgrp, GroupGrid q, uint32_t* bitmap,
+                                                       const uint32_t* d_info) {
   const int lane = lane_id();
   const uint32_t wave = (blockIdx.x * blockDim.x + threadIdx.x) / WAVE;
   const uint32_t nwaves = gridDim.x * blockDim.x / WAVE;
   for (uint32_t k = wave; k < n_kept; k += nwaves) {
+    if (d_info && (d_info[k] & DIR_ON)) continue;
     const uint32_t g = kgrp[k];
     const int64_t lo = q.lo[g], hi = q.hi[g];
     if (lo > hi) continue;
@@ -234,6 +254,7 @@ struct SegGroup {
   uint64_t fstar;    // F*_g
   uint64_t poff;     // partials offset ([n_chunks][T] block of the group)
   uint64_t coff;     // cursor / bracket-cache offset
+  uint64_t choff;    // chunk offset (chunk_e)
   uint32_t nk, spc, n_chunks, tpw, ntg, mode;
 };
 
@@ -259,6 +280,17 @@ DEVI void seg_view(ReduceArgs& r, const SegGroup& G) {
   r.tiles_per_wave = G.tpw;
   r.n_tile_groups = G.ntg;
   r.fstar = G.fstar;
+  if (r.d_info) {
+    r.d_info += G.k0;
+    r.d_n += G.k0;
+    r.d_ga += G.k0;
+    r.d_voff += G.k0;
+    r.d_x0 += G.k0;
+    r.d_step += G.k0;
+    r.d_c0 += G.k0;
+    r.d_r0 += G.k0;
+    r.chunk_e += G.choff;
+  }
   r.ptr += G.coff;
   r.st_x += G.coff;
   r.st_y += G.coff;
@@ -279,7 +311,7 @@ DEVI void seg_view(ReduceArgs& r, const SegGroup& G) {
 
 // k_reduce over the groups of one mode: wave -> group by a (scalar) binary
 // search of the launch's wave offsets, then the single-group wave body.
-template <int AGG, int MODE, bool RATE>
+template <int AGG, int MODE, bool RATE, bool DONLY>
 __global__ void __launch_bounds__(256) k_reduce_seg(ReduceArgs r0, SegReduce s) {
   const uint64_t wave = __builtin_amdgcn_readfirstlane((blockIdx.x * blockDim.x + threadIdx.x) / WAVE);
   if (wave >= s.wv_start[s.n]) return;
@@ -291,7 +323,7 @@ __global__ void __launch_bounds__(256) k_reduce_seg(ReduceArgs r0, SegReduce s) 
   const SegGroup G = s.sg[s.glist[lo]];
   ReduceArgs r = r0;
   seg_view(r, G);
-  reduce_wave<AGG, MODE, RATE, false>(r, (uint32_t)(wave - s.wv_start[lo]));
+  reduce_wave<AGG, MODE, RATE, DONLY>(r, (uint32_t)(wave - s.wv_start[lo]));
 }
 
 // k_finalize_seq over every grid point of the groups of one mode.
@@ -329,6 +361,99 @@ __global__ void __launch_bounds__(256) k_finalize_seg(ReduceArgs r0, FinalArgs f
     acc_merge<AGG, MODE>(a, b);
   }
   finalize_one<AGG, MODE, RATE>(f, g, a);
+}
+
+// ---- the direct no-downsampling path per group (k_direct.hip) -------------
+// Marks each direct candidate's points {x0 + i*step} in its group's bitmap:
+// wave per 64 candidates, runs of the same (group, pattern) marked once.
+__global__ void __launch_bounds__(256) k_direct_mark_seg(DirectArgs dg, uint32_t n_kept, const uint32_t* kgrp,
+                                                         GroupGrid q, uint32_t* bitmap) {
+  const int lane = lane_id();
+  const uint32_t wave = (blockIdx.x * blockDim.x + threadIdx.x) / WAVE;
+  const uint32_t nwaves = gridDim.x * blockDim.x / WAVE;
+  uint32_t m_g = ~0u, m_step = 0, m_np = 0;
+  int64_t m_xf = -1;
+  for (uint32_t kb = ufl(wave) * WAVE; kb < n_kept; kb += nwaves * WAVE) {
+    const uint32_t k = kb + lane;
+    uint32_t info = 0, x0 = 0, step = 0, ne = 0, g = 0;
+    if (k < n_kept) {
+      info = dg.info[k];
+      if (info & DIR_ON) {
+        x0 = dg.x0[k];
+        step = dg.step[k];
+        ne = dg.n[k];
+        g = kgrp[k];
+      }
+    }
+    uint64_t todo = ballot((info & DIR_ON) != 0);
+    while (todo) {
+      const int j = __builtin_ctzll(todo);
+      todo &= todo - 1;
+      const uint32_t gj = readlane_u32(g, j), sj = readlane_u32(step, j), nj = readlane_u32(ne, j);
+      const int64_t xj = (int64_t)readlane_u32(x0, j);
+      const int64_t xf = dg.rate ? xj + sj : xj;
+      const uint32_t np = dg.rate ? nj - 1 : nj;
+      if (np == 0 || (gj == m_g && xf == m_xf && sj == m_step && np == m_np)) continue;
+      DirectArgs v = dg;
+      v.bitmap = bitmap + q.wbase[gj];
+      v.lo = q.lo[gj];
+      direct_mark(v, xf, sj, np);
+      m_g = gj;
+      m_xf = xf;
+      m_step = sj;
+      m_np = np;
+    }
+  }
+}
+
+// k_direct_verify against each candidate's group grid (word ranks rebased).
+__global__ void __launch_bounds__(256) k_direct_verify_seg(DirectArgs dg, uint32_t n_kept, const uint32_t* kgrp,
+                                                           GroupGrid q, const uint32_t* bitmap,
+                                                           const uint32_t* word_rank) {
+  const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
+  bool fail = false;
+  if (k < n_kept) {
+    const uint32_t info = dg.info[k];
+    if (info & DIR_ON) {
+      const uint32_t ne = dg.n[k], step = dg.step[k];
+      const int64_t x0 = dg.x0[k];
+      const int64_t xf = dg.rate ? x0 + step : x0;
+      const uint32_t np = dg.rate ? ne - 1 : ne;
+      if (np == 0) {
+        dg.ga[k] = 0;
+      } else {
+        const uint32_t g = kgrp[k];
+        const uint64_t wb = q.wbase[g];
+        const int64_t xl = x0 + (int64_t)(ne - 1) * step;
+        const uint32_t ra = grid_rank(bitmap + wb, word_rank + wb, q.lo[g], xf);
+        const uint32_t rl = grid_rank(bitmap + wb, word_rank + wb, q.lo[g], xl);
+        dg.ga[k] = ra;
+        if (rl - ra != np - 1) {
+          fail = true;
+          dg.info[k] = 0;
+        }
+      }
+    }
+  }
+  const uint64_t m = ballot(fail);
+  if (m) {
+    const int lane = lane_id();
+    uint32_t base = 0;
+    if (lane == __builtin_ctzll(m)) base = atomicAdd(dg.list_count, (uint32_t)__popcll(m));
+    base = __shfl(base, __builtin_ctzll(m));
+    if (fail) dg.list[base + __popcll(m & lanemask_lt(lane))] = k;
+  }
+}
+
+// k_chunk_flags per group: chunk c of group g holds an E span.
+__global__ void k_chunk_flags_seg(const uint32_t* d_info, uint32_t n_kept, const uint32_t* kgrp,
+                                  const SegGroup* sg, const uint64_t* choff, uint32_t* chunk_e) {
+  const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
+  if (k >= n_kept || (d_info[k] & DIR_ON)) return;
+  const uint32_t g = kgrp[k];
+  const SegGroup G = sg[g];
+  if (!G.T) return;
+  chunk_e[choff[g] + (k - G.k0) / G.spc] = 1u;
 }
 
 }  // namespace tsdb

@@ -202,3 +202,39 @@ def test_group_by_and_aggregate_mirror(ctx):
         assert [p.timestamp() for p in got] == list(o.ts)
         assert [p.longValue() for p in got] == list(o.bits)
         assert grp.aggregatedSize() == o.n_input_points
+
+
+def regular_pts(t0, n, step, seed, float_=False):
+    rng = np.random.default_rng(seed)
+    if float_:
+        return [(t0 + i * step, float(np.float32(100 + rng.standard_normal()))) for i in range(n)]
+    v = np.cumsum(rng.integers(0, 1000, n))
+    return [(t0 + i * step, int(v[i])) for i in range(n)]
+
+
+def groups_direct():
+    """Wide hourly rows (the direct no-downsampling path): groups whose spans
+    stay direct (same cadence), fall back to E after the per-group grid check
+    (a phase-shifted or coarser span), float direct spans, and a late start."""
+    T = T0
+    A = [I(regular_pts(T, 900, 10, s)) for s in range(6)]
+    B = [I(regular_pts(T, 900, 10, 10 + s)) for s in range(4)] + [I(regular_pts(T + 5, 900, 10, 20))]
+    C = [F(regular_pts(T, 700, 10, 30 + s, True)) for s in range(3)]
+    D = [I(regular_pts(T, 900, 10, 40)), I(regular_pts(T, 450, 20, 41)), I(regular_pts(T, 900, 10, 42))]
+    E = [I(regular_pts(T + 3000, 500, 10, 50)), I(regular_pts(T, 900, 10, 51))]
+    return [A, B, C, D, E, A[:1]]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("agg", AGGS)
+@pytest.mark.parametrize("rate", [False, True])
+@pytest.mark.parametrize("decode", ["auto", "fast"])
+def test_batch_direct_groups(ctx, agg, rate, decode, monkeypatch):
+    if decode == "fast":
+        monkeypatch.setenv("TSDBHIP_DECODE", "fast")  # the E path for every span
+    else:
+        monkeypatch.delenv("TSDBHIP_DECODE", raising=False)
+    ss, gss = pack_groups(groups_direct())
+    check_batch(ctx, ss, gss, agg=agg, rate=rate)
+    check_batch(ctx, ss, gss, agg=agg, rate=rate, start=T0 + 1234, end=T0 + 7000)
+    check_batch(ctx, ss, gss, agg=agg, rate=rate, exact=True)
