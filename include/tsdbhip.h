@@ -21,6 +21,8 @@
  *   tsdbhip_spangroup_run_batch — the SpanGroup[] of a GROUP BY query
  *       (TsdbQuery.groupByAndAggregate, TsdbQuery.java:294-363), all groups in
  *       one call.
+ *   tsdbhip_format_points  — the text GraphHandler.respondAsciiQuery,
+ *       Plot.dumpToFiles and CliQuery print for each DataPoint.
  *   tsdbhip_compact_rows   — CompactionQueue.compact(row, compacted[])
  *       (CompactionQueue.java:243-435, 450-743) for a batch of rows.
  *   tsdbhip_host_register / unregister — pinning of the JNI DirectByteBuffers
@@ -275,6 +277,28 @@ int tsdbhip_last_timing(tsdbhip_ctx* ctx, tsdbhip_timing* t);
  */
 int tsdbhip_spangroup_run_batch(tsdbhip_ctx* ctx, const tsdbhip_sg_desc* desc, uint32_t n_groups,
                                 const uint32_t* group_span_start, tsdbhip_sg_out* outs);
+
+/* ---- output formatting (host cores, no GPU) ----------------------------- */
+/*
+ * Writes the text the reference's consumers print for n points of one
+ * SpanGroup (tsdbhip_sg_out arrays) into buf:
+ *   TSDBHIP_FMT_ASCII   "<metric> <ts> <value><tags>\n"   GraphHandler.respondAsciiQuery
+ *                        (GraphHandler.java:785-808); tags = " k=v k2=v2" as the
+ *                        caller built it from getTags()
+ *   TSDBHIP_FMT_GNUPLOT "<ts + utc_offset> <value>\n"     Plot.dumpToFiles (Plot.java:190-204)
+ *   TSDBHIP_FMT_CLI     "<metric> <ts> <value> <tags>\n"  CliQuery (CliQuery.java:161-170);
+ *                        tags = getTags().toString(), doubles as String.format("%f")
+ * Longs as Long.toString, doubles as Double.toString (JDK 19+ shortest
+ * digits). Returns the bytes written, TSDBHIP_E_CAPACITY if cap is too small
+ * (nothing written), TSDBHIP_E_NAN_INF for a NaN/Infinity in ASCII/GNUPLOT
+ * (the reference's IllegalStateException), TSDBHIP_E_INVALID_ARG.
+ */
+#define TSDBHIP_FMT_ASCII   0
+#define TSDBHIP_FMT_GNUPLOT 1
+#define TSDBHIP_FMT_CLI     2
+int64_t tsdbhip_format_points(int32_t mode, const char* metric, const char* tags, int64_t utc_offset,
+                              const int64_t* ts, const uint8_t* is_int, const int64_t* bits, uint64_t n,
+                              char* buf, uint64_t cap);
 
 /* ---- secondary path ---------------------------------------------------- */
 int tsdbhip_compact_rows(tsdbhip_ctx* ctx, const tsdbhip_rows_desc* desc,

@@ -23,6 +23,7 @@ EXPORTS = [
     "tsdbhip_last_timing", "tsdbhip_compact_rows", "tsdbhip_comm_unique_id",
     "tsdbhip_comm_init", "tsdbhip_synth_generate", "tsdbhip_synth_free",
     "tsdbhip_desc_download", "tsdbhip_bw_probe", "tsdbhip_spangroup_run_batch",
+    "tsdbhip_format_points",
 ]
 
 
@@ -66,6 +67,9 @@ def lib():
     L.tsdbhip_spangroup_run_batch.argtypes = [C.c_void_p, P(_abi.SgDesc), C.c_uint32, P(C.c_uint32),
                                               P(_abi.SgOut)]
     L.tsdbhip_spangroup_run_batch.restype = C.c_int
+    L.tsdbhip_format_points.argtypes = [C.c_int32, C.c_char_p, C.c_char_p, C.c_int64, P(C.c_int64),
+                                        P(C.c_uint8), P(C.c_int64), C.c_uint64, C.c_char_p, C.c_uint64]
+    L.tsdbhip_format_points.restype = C.c_int64
     L.tsdbhip_last_timing.argtypes = [C.c_void_p, P(_abi.Timing)]
     L.tsdbhip_compact_rows.argtypes = [C.c_void_p, P(_abi.RowsDesc), P(_abi.RowsOut)]
     L.tsdbhip_compact_rows.restype = C.c_int

@@ -363,3 +363,29 @@ def group_by_and_aggregate(spans, group_bys, start_time, end_time, rate, aggrega
         grp._ctx = c
         grp._result = r
     return groups
+
+
+# ------------------------------------------------------------ output text ----
+FMT_ASCII, FMT_GNUPLOT, FMT_CLI = 0, 1, 2
+
+
+def format_points(mode, ts, is_int, bits, metric="", tags="", utc_offset=0):
+    """tsdbhip_format_points: the lines GraphHandler.respondAsciiQuery
+    (GraphHandler.java:785-808), Plot.dumpToFiles (Plot.java:190-204) or
+    CliQuery (CliQuery.java:161-170) print for these points. Raises
+    IllegalStateException on a NaN/Infinity where the reference does."""
+    from ._lib import lib
+    L = lib()
+    ts = np.ascontiguousarray(ts, np.int64)
+    isi = np.ascontiguousarray(is_int, np.uint8)
+    bits = np.ascontiguousarray(bits, np.int64)
+    n = len(ts)
+    cap = max(64, n * (len(metric) + len(tags) + 64))
+    buf = C.create_string_buffer(cap)
+    rc = L.tsdbhip_format_points(mode, metric.encode(), tags.encode(), int(utc_offset), _abi.ptr(ts, C.c_int64),
+                                 _abi.ptr(isi, C.c_uint8), _abi.ptr(bits, C.c_int64), n, buf, cap)
+    if rc == _abi.E_NAN_INF:
+        raise IllegalStateException("NaN or Infinity")
+    if rc < 0:
+        raise TsdbHipError(int(rc), "tsdbhip_format_points")
+    return buf.raw[:rc].decode()

@@ -946,6 +946,7 @@ extern "C" int tsdbhip_spangroup_run(tsdbhip_ctx* ctx, const tsdbhip_sg_desc* de
 }
 
 #include "batch.hip"
+#include "fmt.hip"
 
 // ------------------------------------------------- synthetic inputs ------
 // Device buffers of a generated desc are owned by ctx under keys derived from

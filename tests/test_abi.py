@@ -14,7 +14,7 @@ HEADER = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))
 
 def declared_functions():
     src = open(HEADER).read()
-    return sorted(set(re.findall(r"^\s*(?:int|void|const char\*)\s+(tsdbhip_\w+)\s*\(", src, re.M)))
+    return sorted(set(re.findall(r"^\s*(?:int|int64_t|void|const char\*)\s+(tsdbhip_\w+)\s*\(", src, re.M)))
 
 
 def test_header_declares_expected_entry_points():

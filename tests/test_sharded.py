@@ -166,3 +166,20 @@ def test_bench_harness_gloo_world2():
     d = json.loads(lines[0])
     assert d["n_gpus"] == 2 and d["steps"] == 3 and d["value"] > 0
     assert d["config"]["shards"] == [[0, 500000], [500000, 1000000]]
+
+
+def test_bench_harness_groups_world2():
+    """GROUP BY over 2 ranks: whole groups per rank (no exchange), group
+    boundaries respected by the span split."""
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1", MASTER_PORT=str(_free_port()))
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
+           "--master-addr=127.0.0.1", f"--master-port={env['MASTER_PORT']}",
+           os.path.join(ROOT, "bench.py"), "--gpus", "2", "--steps", "2", "--warmup", "1", "--dry-run",
+           "--config", "c3s_gb100", "--groups", "3"]
+    r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=240)
+    assert r.returncode == 0, r.stderr[-2000:]
+    lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, r.stdout
+    import json
+    d = json.loads(lines[0])
+    assert d["config"]["shards"] == [[0, 333333], [333333, 1000000]]
