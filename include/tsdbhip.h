@@ -332,7 +332,10 @@ int tsdbhip_desc_download(tsdbhip_ctx* ctx, const tsdbhip_sg_desc* ddesc,
 /* Bandwidth probe over a device-resident desc (TSDBHIP_DESC_DEVICE):
  * mode 0 streams its qualifier + value rows with the geometry of the
  * downsampling kernel (one wave per span, 16-B loads), mode 1 copies its
- * value bytes device-to-device. *ms = kernel time, *bytes = bytes moved.
+ * value bytes device-to-device, mode 2 is a flat grid-stride read of the
+ * value bytes, mode 3 is mode 0 with two chunks in flight per wave and the
+ * next span's metadata loaded ahead (width 8, single-row spans).
+ * *ms = kernel time, *bytes = bytes moved.
  * `width` = value bytes per cell (4 or 8). Not part of the reference API:
  * it reports the achievable bandwidth beside the 8 TB/s peak. */
 int tsdbhip_bw_probe(tsdbhip_ctx* ctx, const tsdbhip_sg_desc* desc, int32_t mode, uint32_t width,

@@ -1195,6 +1195,16 @@ extern "C" int tsdbhip_bw_probe(tsdbhip_ctx* ctx, const tsdbhip_sg_desc* d, int3
                          d->row_ncells, d->row_qual_off, d->row_val_off, d->qual_bytes, d->val_bytes, d->n_spans,
                          width, sink);
       *bytes = d->qual_nbytes + d->val_nbytes;
+    } else if (mode == 2) {
+      const uint64_t n16 = d->val_nbytes / 16;
+      hipLaunchKernelGGL(k_probe_flat, dim3(grid_for(n16, 1024, 1u << 16)), dim3(256), 0, st,
+                         (const uint4*)d->val_bytes, n16, sink);
+      *bytes = n16 * 16;
+    } else if (mode == 3) {
+      hipLaunchKernelGGL(k_probe_read2, dim3(grid_for(d->n_spans, 4, 1u << 20)), dim3(256), 0, st,
+                         d->span_row_start, d->row_ncells, d->row_qual_off, d->row_val_off, d->qual_bytes,
+                         d->val_bytes, d->n_spans, sink);
+      *bytes = d->qual_nbytes + d->val_nbytes;
     } else {
       const uint64_t n16 = d->val_nbytes / 16;
       uint4* dst = scratch<uint4>(ctx, "probe_dst", n16);
