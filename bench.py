@@ -531,13 +531,15 @@ def main():
         def step_once():
             ctx.check(L.tsdbhip_spangroup_run_batch(ctx.handle, C.byref(d), Gl, _abi.ptr(gss, C.c_uint32), outs))
 
-    hot_ms, total_ms, hot_kernel = [], [], [0]
+    hot_ms, total_ms, hot_kernel, red_ms, emitted = [], [], [0], [], [0, 0]
 
     def record():
         tm = ctx.timing()
         hot_ms.append(tm.hot_ms)
         total_ms.append(tm.total_ms)
+        red_ms.append(tm.reduce_ms)
         hot_kernel[0] = tm.hot_kernel
+        emitted[0], emitted[1] = int(tm.n_emitted), int(tm.n_grid)
 
     elapsed = max_over_ranks(dist, timed_loop(step_once, torch.cuda.synchronize, barrier, args.steps,
                                               args.warmup, record))
@@ -576,6 +578,13 @@ def main():
         else:
             nc = ss.row_ncells.astype(np.int64)
             hot_bytes = int((ss.row_val_len.astype(np.int64) - (nc > 1)).sum())
+    reduce_ms = float(np.mean(red_ms))
+    if G == 1 and kname != "k_reduce" and reduce_ms > 2 * hot:
+        # the cross-span reducer dominates (C4: VALU-bound lerps): roofline on
+        # it, with its algorithmic bytes = the E points it reads (u32 ts, i64
+        # bits, u8 flag) + the output it writes (T x 17 B)
+        kname, hot = "k_reduce", reduce_ms
+        hot_bytes = emitted[0] * 13 + emitted[1] * 17
     achieved = hot_bytes / (hot * 1e-3) / 1e9
     traffic, traffic_src = pmc_traffic(args.config, kname, world)
     if rank == 0:

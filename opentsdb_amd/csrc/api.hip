@@ -260,6 +260,18 @@ static const T* stage(tsdbhip_ctx* ctx, const char* name, const T* src, size_t c
   return d;
 }
 
+// grow-only pinned host staging
+static void* host_buf(tsdbhip_ctx* ctx, size_t bytes) {
+  if (ctx->host_big_n < bytes) {
+    if (ctx->host_big) HIPCHK(hipHostFree(ctx->host_big));
+    ctx->host_big = nullptr;
+    size_t n = std::max(bytes, ctx->host_big_n + ctx->host_big_n / 4);
+    HIPCHK(hipHostMalloc(&ctx->host_big, n, hipHostMallocDefault));
+    ctx->host_big_n = n;
+  }
+  return ctx->host_big;
+}
+
 static void readback(tsdbhip_ctx* ctx, void* host, const void* dev, size_t bytes) {
   HIPCHK(hipMemcpyAsync(ctx->host_small, dev, bytes, hipMemcpyDeviceToHost, ctx->stream));
   HIPCHK(hipStreamSynchronize(ctx->stream));
@@ -803,6 +815,10 @@ static int spangroup_run(tsdbhip_ctx* ctx, const tsdbhip_sg_desc* d, tsdbhip_sg_
     if (!sharded) {
       run_reduce(exact, true);
       HIPCHK(hipEventRecord(ctx->ev[5], st));
+      // lazy error index for illegal cells (independent of a re-run below)
+      if (n_kept)
+        hipLaunchKernelGGL(k_bad_index, dim3(grid_for(n_kept, 256)), dim3(256), 0, st, e_bad, eoff, e_ts, n_kept,
+                           (int32_t)rate, hi, bitmap, word_rank, lo, T, &sm->bad_at);
       readback(ctx, &h, sm, sizeof h);  // sync 4
       if (h.ambiguous && !exact) {
         Small z = h;
@@ -863,14 +879,13 @@ static int spangroup_run(tsdbhip_ctx* ctx, const tsdbhip_sg_desc* d, tsdbhip_sg_
       all.n_chunks = (uint32_t)nr;
       dispatch_final(ctx, agg, mode, rate, all, fin);
       HIPCHK(hipEventRecord(ctx->ev[5], st));
+      // lazy error index for illegal cells
+      if (n_kept)
+        hipLaunchKernelGGL(k_bad_index, dim3(grid_for(n_kept, 256)), dim3(256), 0, st, e_bad, eoff, e_ts, n_kept,
+                           (int32_t)rate, hi, bitmap, word_rank, lo, T, &sm->bad_at);
       readback(ctx, &h, sm, sizeof h);
       tm.exchange_ms = ev_ms(ctx->ev[6], ctx->ev[7]);
     }
-    // lazy error index for illegal cells
-    if (n_kept)
-      hipLaunchKernelGGL(k_bad_index, dim3(grid_for(n_kept, 256)), dim3(256), 0, st, e_bad, eoff, e_ts, n_kept,
-                         (int32_t)rate, hi, bitmap, word_rank, lo, T, &sm->bad_at);
-    readback(ctx, &h, sm, sizeof h);
   } else {
     HIPCHK(hipEventRecord(ctx->ev[5], st));
     if (n_kept)
@@ -905,7 +920,18 @@ static int spangroup_run(tsdbhip_ctx* ctx, const tsdbhip_sg_desc* d, tsdbhip_sg_
     out->err_code = TSDBHIP_E_CAPACITY;
     return TSDBHIP_E_CAPACITY;
   }
-  if (n_ok) {
+  if (n_ok && n_ok * 17 <= (256u << 10)) {
+    // small results: three async copies into pinned staging, one sync (a
+    // copy into pageable memory would synchronise once per array)
+    uint8_t* hb = (uint8_t*)host_buf(ctx, n_ok * 17);
+    HIPCHK(hipMemcpyAsync(hb, scratch<int64_t>(ctx, "out_ts", T), n_ok * 8, hipMemcpyDeviceToHost, st));
+    HIPCHK(hipMemcpyAsync(hb + 8 * n_ok, scratch<int64_t>(ctx, "out_bits", T), n_ok * 8, hipMemcpyDeviceToHost, st));
+    HIPCHK(hipMemcpyAsync(hb + 16 * n_ok, scratch<uint8_t>(ctx, "out_isint", T), n_ok, hipMemcpyDeviceToHost, st));
+    HIPCHK(hipStreamSynchronize(st));
+    std::memcpy(out->ts, hb, n_ok * 8);
+    std::memcpy(out->bits, hb + 8 * n_ok, n_ok * 8);
+    std::memcpy(out->is_int, hb + 16 * n_ok, n_ok);
+  } else if (n_ok) {
     HIPCHK(hipMemcpyAsync(out->ts, scratch<int64_t>(ctx, "out_ts", T), n_ok * 8, hipMemcpyDeviceToHost, st));
     HIPCHK(hipMemcpyAsync(out->is_int, scratch<uint8_t>(ctx, "out_isint", T), n_ok, hipMemcpyDeviceToHost, st));
     HIPCHK(hipMemcpyAsync(out->bits, scratch<int64_t>(ctx, "out_bits", T), n_ok * 8, hipMemcpyDeviceToHost, st));

@@ -18,16 +18,6 @@
 // a lone SpanGroup would; so does a set of group grids too large for one
 // segmented bitmap (sparse groups over a very wide time range).
 
-static void* host_buf(tsdbhip_ctx* ctx, size_t bytes) {
-  if (ctx->host_big_n < bytes) {
-    if (ctx->host_big) HIPCHK(hipHostFree(ctx->host_big));
-    ctx->host_big = nullptr;
-    size_t n = std::max(bytes, ctx->host_big_n + ctx->host_big_n / 4);
-    HIPCHK(hipHostMalloc(&ctx->host_big, n, hipHostMallocDefault));
-    ctx->host_big_n = n;
-  }
-  return ctx->host_big;
-}
 
 template <int AGG, int MODE, bool RATE>
 static void launch_seg(tsdbhip_ctx* ctx, const ReduceArgs& r0, const FinalArgs& f0, const SegReduce& sr,
