@@ -552,31 +552,31 @@ static int spangroup_run(tsdbhip_ctx* ctx, const tsdbhip_sg_desc* d, tsdbhip_sg_
     hipLaunchKernelGGL(k_kept_scatter, dim3(grid_for(S, 256, 1024)), dim3(256), 0, st, sp_kept, kidx, eoff_s,
                        sp_ncells, S, kept, eoff, &sm->n_input, sp_first, sp_last, sm->bound);
   }
+  if (sharded) {
+    // every rank needs the same bitmap geometry and the same error: the kept
+    // spans' bounds (min first, max last; ranks without kept spans hold the
+    // neutral ~0 / 0) and the error code (most negative) are reduced in place,
+    // so the one readback below returns the agreed values
+    NCCLCHK(ncclGroupStart());
+    NCCLCHK(ncclAllReduce(&sm->bound[0], &sm->bound[0], 1, ncclUint64, ncclMin, ctx->comm, st));
+    NCCLCHK(ncclAllReduce(&sm->bound[1], &sm->bound[1], 1, ncclUint64, ncclMax, ctx->comm, st));
+    NCCLCHK(ncclAllReduce(&sm->err, &sm->err, 1, ncclInt32, ncclMin, ctx->comm, st));
+    NCCLCHK(ncclGroupEnd());
+  }
   Small h;
   readback(ctx, &h, sm, sizeof h);  // sync 1
-  if (h.err && !sharded) throw Fail{h.err};  // (sharded: after the bounds exchange, on every rank)
+  if (h.err) throw Fail{h.err};
   const uint32_t n_kept = (uint32_t)h.n_kept;
   out->n_input_points = h.n_input;
   uint64_t n_input_global = h.n_input;
 
   // ---- union-grid bitmap range: every E point lies in [first, last] of its
-  // span and in [start, ...]; G keeps those <= end (SURVEY.md §8a closed form)
+  // span and in [start, ...]; G keeps those <= end (SURVEY.md §8a closed form).
+  // A kept span has first <= end and last >= start, so [lo, hi] is non-empty
+  // whenever some (rank's) span is kept.
   int64_t lo = std::max<int64_t>(d->start_time, h.bound[0] == ~0ull ? INT64_MAX : (int64_t)h.bound[0]);
   int64_t hi = std::min<int64_t>(d->end_time, (int64_t)h.bound[1]);
   if (h.bound[0] == ~0ull) hi = -1;
-  if (sharded) {  // every rank needs the same bitmap geometry (and the same error)
-    unsigned long long* x = scratch<unsigned long long>(ctx, "xchg_bound", 4);
-    unsigned long long hv[4] = {lo <= hi ? (unsigned long long)lo : ~0ull, lo <= hi ? (unsigned long long)hi : 0ull,
-                                (unsigned long long)(int64_t)(-h.err), 0};
-    std::memcpy(ctx->host_small, hv, sizeof hv);
-    HIPCHK(hipMemcpyAsync(x, ctx->host_small, sizeof hv, hipMemcpyHostToDevice, st));
-    NCCLCHK(ncclAllReduce(x, x, 1, ncclUint64, ncclMin, ctx->comm, st));
-    NCCLCHK(ncclAllReduce(x + 1, x + 1, 2, ncclUint64, ncclMax, ctx->comm, st));
-    readback(ctx, hv, x, sizeof hv);
-    if (hv[2]) throw Fail{-(int)hv[2]};
-    lo = hv[0] == ~0ull ? 1 : (int64_t)hv[0];
-    hi = hv[0] == ~0ull ? 0 : (int64_t)hv[1];
-  }
   const bool empty_grid = lo > hi;
   const uint64_t nwords = empty_grid ? 0 : (uint64_t)(hi - lo + 1 + 31) / 32;
   uint32_t* bitmap = empty_grid ? nullptr : scratch<uint32_t>(ctx, "bitmap", nwords, true);
@@ -683,28 +683,24 @@ static int spangroup_run(tsdbhip_ctx* ctx, const tsdbhip_sg_desc* d, tsdbhip_sg_
   HIPCHK(hipEventRecord(ctx->ev[2], st));
   if (n_kept)
     hipLaunchKernelGGL(k_span_summary, dim3(grid_for(n_kept, 256, 1024)), dim3(256), 0, st, da, mark_list, mark_count);
+  if (sharded) {
+    // agree on the int/float flags, F*, the error and the input count across
+    // ranks, in place, ahead of the one readback
+    NCCLCHK(ncclGroupStart());
+    NCCLCHK(ncclAllReduce(sm->gflags, sm->gflags, 2, ncclUint32, ncclMax, ctx->comm, st));
+    NCCLCHK(ncclAllReduce(&sm->fstar, &sm->fstar, 1, ncclUint64, ncclMax, ctx->comm, st));
+    NCCLCHK(ncclAllReduce(&sm->err, &sm->err, 1, ncclInt32, ncclMin, ctx->comm, st));
+    NCCLCHK(ncclAllReduce(&sm->n_input, &sm->n_input, 1, ncclUint64, ncclSum, ctx->comm, st));
+    NCCLCHK(ncclGroupEnd());
+  }
   readback(ctx, &h, sm, sizeof h);  // sync 2
-  if (h.err && !sharded) throw Fail{h.err};
+  if (h.err) throw Fail{h.err};
 
   // ---- union grid ----
   bool anyf = h.gflags[0] != 0, anyi = h.gflags[1] != 0;
   uint64_t fstar = h.fstar;
   if (sharded) {
-    // agree on flags, F* and the input count across ranks
-    unsigned long long* x = scratch<unsigned long long>(ctx, "xchg_small", 8);
-    unsigned long long hv[8] = {(unsigned long long)fstar, (unsigned long long)anyf, (unsigned long long)anyi,
-                                (unsigned long long)(int64_t)(-h.err), h.n_input, 0, 0, 0};
-    std::memcpy(ctx->host_small, hv, sizeof hv);
-    HIPCHK(hipMemcpyAsync(x, ctx->host_small, sizeof hv, hipMemcpyHostToDevice, st));
-    NCCLCHK(ncclAllReduce(x, x, 4, ncclUint64, ncclMax, ctx->comm, st));
-    NCCLCHK(ncclAllReduce(x + 4, x + 4, 1, ncclUint64, ncclSum, ctx->comm, st));
-    readback(ctx, hv, x, sizeof hv);
-    if (hv[3]) throw Fail{-(int)hv[3]};
-    hv[3] = hv[4];
-    fstar = hv[0];
-    anyf = hv[1] != 0;
-    anyi = hv[2] != 0;
-    n_input_global = hv[3];
+    n_input_global = h.n_input;
     out->n_input_points = n_input_global;
   }
   uint64_t T = 0;
