@@ -5,10 +5,10 @@
 //   k_assemble        Span.addRow / RowSeq.addRow rules, S7 keep rule, E caps
 //   scans             kept-span list, E offsets                     [sync 1]
 //   k_decode_*        RowSeq decode (+ greedy downsampling) -> E_s   (HBM-bound)
-//   k_span_summary    grid range, F*                                [sync 2]
-//   k_grid_*          union grid G as bitmap + ranks                 [sync 3]
+//   k_span_summary    grid range, F*
+//   k_grid_*          union grid G as bitmap + ranks                 [sync 2]
 //   k_reduce          per (tile, span chunk) lerp/rate + aggregation
-//   k_finalize_*      chunk combine, int/double select, NaN check   [sync 4]
+//   k_finalize_*      chunk combine, int/double select, NaN check   [sync 3]
 // With TSDBHIP_SHARDED the grid bitmap and the per-t partials are exchanged
 // over RCCL (allgather, then a rank-ordered combine on every rank).
 #include <hip/hip_runtime.h>
@@ -311,12 +311,13 @@ struct LaunchFastDs {
 struct LaunchChunks {
   template <int AGG>
   static void run(tsdbhip_ctx* ctx, const DecodeArgs& da, DecodeArgs& fa, const uint32_t* ncells,
-                  const uint32_t* vlen, SpanDsArgs g) {
+                  const uint32_t* vlen, SpanDsArgs g, uint32_t* zeroed2 = nullptr) {
     if (AGG == 4) return;  // dev: Welford is order-dependent, serial kernels only
     hipStream_t st = ctx->stream;
     const uint32_t n_kept = da.n_kept;
     g.list = scratch<uint32_t>(ctx, "ck_list", n_kept);
-    g.list_count = scratch<uint32_t>(ctx, "ck_list_count", 1, true);
+    // (zeroed2: two list counters already zero on the device, no memsets)
+    g.list_count = zeroed2 ? zeroed2 : scratch<uint32_t>(ctx, "ck_list_count", 1, true);
     g.in_list = nullptr;
     g.in_count = nullptr;
     // integer spans over every kept span, then float spans over the ones left
@@ -324,7 +325,7 @@ struct LaunchChunks {
     gf.in_list = g.list;
     gf.in_count = g.list_count;
     gf.list = scratch<uint32_t>(ctx, "ck_list2", n_kept);
-    gf.list_count = scratch<uint32_t>(ctx, "ck_list2_count", 1, true);
+    gf.list_count = zeroed2 ? zeroed2 + 1 : scratch<uint32_t>(ctx, "ck_list2_count", 1, true);
     HIPCHK(hipEventRecord(ctx->ev[8], st));
     hipLaunchKernelGGL((k_ds_spans<AGG, false>), dim3(grid_for(n_kept, 4, 1u << 20)), dim3(256), 0, st, da, g,
                        ncells, vlen);
@@ -497,6 +498,9 @@ static int spangroup_run(tsdbhip_ctx* ctx, const tsdbhip_sg_desc* d, tsdbhip_sg_
     uint64_t e_total;
     uint64_t T;
     unsigned long long bound[2];  // [min first ts, max last ts] of the kept spans
+    uint32_t cnt[6];  // list counters, zeroed by the init copy below (no memsets):
+                      // [0] assembly queue, [1] decode fallback, [2] direct list,
+                      // [3] [4] k_ds_spans int / float leftovers
   };
   Small* sm = scratch<Small>(ctx, "small", 1);
   {
@@ -534,7 +538,7 @@ static int spangroup_run(tsdbhip_ctx* ctx, const tsdbhip_sg_desc* d, tsdbhip_sg_
     a.sp_q1_shift = sp_q1s; a.sp_ovf_cell = sp_ovf; a.err = &sm->err;
     if (S) {  // thread per span, then a wave per span for the ones it queued
       uint32_t* alist = scratch<uint32_t>(ctx, "asm_list", S);
-      uint32_t* acount = scratch<uint32_t>(ctx, "asm_count", 1, true);
+      uint32_t* acount = &sm->cnt[0];
       hipLaunchKernelGGL(k_assemble_fast, dim3(grid_for(S, 256)), dim3(256), 0, st, a, alist, acount);
       hipLaunchKernelGGL(k_assemble, dim3(grid_for(S, 4, 4096)), dim3(256), 0, st, a, (const uint32_t*)alist,
                          (const uint32_t*)acount);
@@ -615,7 +619,7 @@ static int spangroup_run(tsdbhip_ctx* ctx, const tsdbhip_sg_desc* d, tsdbhip_sg_
     if (force && !strcmp(force, "chunks")) { fast = chunks = true; direct = false; }
     if (force && !strcmp(force, "direct")) { fast = chunks = true; direct = interval == 0 && bitmap != nullptr; }
     da.fb_list = scratch<uint32_t>(ctx, "fb_list", n_kept);
-    da.fb_count = scratch<uint32_t>(ctx, "fb_count", 1, true);
+    da.fb_count = &sm->cnt[1];
     da.use_fb = 0;
     da.span_list = nullptr;
     da.span_count = nullptr;
@@ -641,7 +645,7 @@ static int spangroup_run(tsdbhip_ctx* ctx, const tsdbhip_sg_desc* d, tsdbhip_sg_
         dg.ga = scratch<uint32_t>(ctx, "d_ga", n_kept);
         dg.row_cpre = scratch<uint32_t>(ctx, "row_cpre", R);
         dg.list = scratch<uint32_t>(ctx, "d_list", n_kept);
-        dg.list_count = scratch<uint32_t>(ctx, "d_list_count", 1, true);
+        dg.list_count = &sm->cnt[2];
         dg.bitmap = bitmap;
         dg.lo = lo;
         dg.hi = hi;
@@ -666,7 +670,7 @@ static int spangroup_run(tsdbhip_ctx* ctx, const tsdbhip_sg_desc* d, tsdbhip_sg_
         g.lo = lo;
         g.hi = hi;
         g.rate = rate;
-        launch_agg<LaunchChunks>(ds_agg, ctx, da, fa, row_ncells, row_val_len, g);
+        launch_agg<LaunchChunks>(ds_agg, ctx, da, fa, row_ncells, row_val_len, g, &sm->cnt[3]);
         chunk_marked = bitmap != nullptr && fa.span_list != nullptr;
       }
       if (chunk_marked) {
@@ -693,16 +697,18 @@ static int spangroup_run(tsdbhip_ctx* ctx, const tsdbhip_sg_desc* d, tsdbhip_sg_
     NCCLCHK(ncclAllReduce(&sm->n_input, &sm->n_input, 1, ncclUint64, ncclSum, ctx->comm, st));
     NCCLCHK(ncclGroupEnd());
   }
-  readback(ctx, &h, sm, sizeof h);  // sync 2
-  if (h.err) throw Fail{h.err};
+  // (no readback here: the flags, F*, errors and input count come back with
+  // |G| below. A decode error leaves every e_len <= its capacity, so the grid
+  // kernels stay inside E before the error is thrown.)
+  auto after_sync2 = [&]() {
+    if (h.err) throw Fail{h.err};
+    if (sharded) {
+      n_input_global = h.n_input;
+      out->n_input_points = n_input_global;
+    }
+  };
 
   // ---- union grid ----
-  bool anyf = h.gflags[0] != 0, anyi = h.gflags[1] != 0;
-  uint64_t fstar = h.fstar;
-  if (sharded) {
-    n_input_global = h.n_input;
-    out->n_input_points = n_input_global;
-  }
   uint64_t T = 0;
   uint32_t* word_rank = nullptr;
   uint32_t* gridv = nullptr;
@@ -728,7 +734,9 @@ static int spangroup_run(tsdbhip_ctx* ctx, const tsdbhip_sg_desc* d, tsdbhip_sg_
     }
     hipLaunchKernelGGL(k_grid_popc, dim3((unsigned)nb), dim3(256), 0, st, ga);
     hipLaunchKernelGGL(k_grid_scan_blocks, dim3(1), dim3(256), 0, st, ga, (uint32_t)nb);
-    readback(ctx, &T, &sm->T, 8);  // sync 3
+    readback(ctx, &h, sm, sizeof h);  // sync 2: |G|, flags, F*, errors
+    after_sync2();
+    T = h.T;
     gridv = scratch<uint32_t>(ctx, "grid", T);
     ga.grid = gridv;
     hipLaunchKernelGGL(k_grid_emit, dim3(grid_for(nwords, 256)), dim3(256), 0, st, ga);
@@ -749,7 +757,12 @@ static int spangroup_run(tsdbhip_ctx* ctx, const tsdbhip_sg_desc* d, tsdbhip_sg_
       gfa.use_fb = 1;
       hipLaunchKernelGGL(k_decode_nods, dim3(std::min(grid_for(n_kept, 4, 65536), 1024u)), dim3(256), 0, st, gfa);
     }
+  } else {
+    readback(ctx, &h, sm, sizeof h);  // sync 2 (no grid)
+    after_sync2();
   }
+  const bool anyf = h.gflags[0] != 0, anyi = h.gflags[1] != 0;
+  const uint64_t fstar = h.fstar;
   HIPCHK(hipEventRecord(ctx->ev[4], st));
   tm.n_grid = T;
 
@@ -815,7 +828,7 @@ static int spangroup_run(tsdbhip_ctx* ctx, const tsdbhip_sg_desc* d, tsdbhip_sg_
       if (n_kept)
         hipLaunchKernelGGL(k_bad_index, dim3(grid_for(n_kept, 256)), dim3(256), 0, st, e_bad, eoff, e_ts, n_kept,
                            (int32_t)rate, hi, bitmap, word_rank, lo, T, &sm->bad_at);
-      readback(ctx, &h, sm, sizeof h);  // sync 4
+      readback(ctx, &h, sm, sizeof h);  // sync 3
       if (h.ambiguous && !exact) {
         Small z = h;
         z.ambiguous = 0;
