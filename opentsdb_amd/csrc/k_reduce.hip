@@ -330,6 +330,10 @@ DEVI void reduce_wave(const ReduceArgs& r, const uint32_t wave) {
       const uint32_t len = r.e_len[k];
       uint32_t lo = base_idx, hi = len;
       if (hi < lo) hi = lo;
+      // a span that starts at/after the wave's first grid point (every span
+      // of a single-tile grid: C3*) has its cursor at base_idx: one load
+      // instead of a dependent binary search
+      if (lo < hi && (int64_t)r.e_ts[eo + lo] >= t0) hi = lo;
       while (lo < hi) {
         const uint32_t mid = (lo + hi) >> 1;
         if ((int64_t)r.e_ts[eo + mid] < t0) lo = mid + 1; else hi = mid;
@@ -624,15 +628,16 @@ DEVI void reduce_wave(const ReduceArgs& r, const uint32_t wave) {
         }
         if (ALIGNED_OK && ((almask >> i) & 1)) {
           const uint64_t m = almask >> i;  // bit 0: span kb + i
-          const uint32_t run = min(8u, ~m == 0 ? 64u : (uint32_t)__builtin_ctzll(~m));
-          int64_t v[8];
+          constexpr uint32_t AR = 8;  // aligned spans whose values are in flight together (16: 3 waves/SIMD)
+          const uint32_t run = min(AR, ~m == 0 ? 64u : (uint32_t)__builtin_ctzll(~m));
+          int64_t v[AR];
 #pragma unroll
-          for (uint32_t u = 0; u < 8; u++) {
+          for (uint32_t u = 0; u < AR; u++) {
             const uint64_t eo_u = readlane_u64(eo_l, (int)min(i + u, 63u));
             v[u] = (u < run && gv) ? r.e_val[eo_u + g0 + lane] : 0;
           }
 #pragma unroll
-          for (uint32_t u = 0; u < 8; u++) {
+          for (uint32_t u = 0; u < AR; u++) {
             if (u >= run) break;
             if (gv) acc_push<AGG, MODE>(acc, v[u], MODE == MODE_INT ? 0.0 : to_double(v[u], true));
           }
