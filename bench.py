@@ -220,6 +220,17 @@ def cpu_baseline_c5(batch, seconds=10.0):
                       f"CompactionQueue.compact; no JVM in the image)"}
 
 
+_JSON_OUT = None
+
+
+def emit(res):
+    """The one JSON line, on the process's original stdout. main() points fd 1
+    at stderr first, so banners native libraries print to stdout (RCCL's
+    version block at communicator init) cannot land beside the line."""
+    out = _JSON_OUT or sys.stdout
+    print(json.dumps(res), file=out, flush=True)
+
+
 def bench_c5(args):
     """C5 (configs[4]): tsdbhip_compact_rows over 1M HBM-resident rows."""
     import torch
@@ -309,7 +320,7 @@ def bench_c5(args):
     }
     if not args.no_cpu:
         res["cpu_baseline"] = cpu_baseline_c5(b, args.cpu_seconds)
-    print(json.dumps(res), flush=True)
+    emit(res)
     ctx.close()
 
 
@@ -413,10 +424,18 @@ def main():
                     "registered pinned memory, 100k-series sample; reported beside the line, never its value)")
     ap.add_argument("--c5-mix", default="c5", choices=["c5", "plain", "nocomplex"],
                     help="C5 row mix (diagnostics; the C5 line is 'c5')")
+    ap.add_argument("--rehearse-shards", type=int, default=0,
+                    help="diagnostic at N=1: run rank 0's shard of an N-way series split through the sharded "
+                         "path on a 1-rank RCCL communicator (per-rank work and exchange code of an N-GPU run; "
+                         "the line says so and its value is that one shard's rate)")
     ap.add_argument("--dry-run", action="store_true",
                     help="harness check without a GPU: the multi-rank timing/barrier/report path with a "
                          "no-op step (its value is meaningless and says so)")
     args = ap.parse_args()
+    global _JSON_OUT
+    sys.stdout.flush()
+    _JSON_OUT = os.fdopen(os.dup(1), "w")
+    os.dup2(2, 1)
     if args.config == "c5":
         return bench_c5(args)
 
@@ -439,6 +458,9 @@ def main():
         g_lo, g_hi = granks[rank]
     else:
         shards = shard_ranges(n_series, world)
+    rehearse = args.rehearse_shards if (world == 1 and G == 1 and args.rehearse_shards > 1) else 0
+    if rehearse:
+        shards = shard_ranges(n_series, rehearse)
     lo, hi = shards[rank]
 
     def barrier():
@@ -449,10 +471,10 @@ def main():
         elapsed = max_over_ranks(dist, timed_loop(lambda: time.sleep(0.001), lambda: None, barrier,
                                                    args.steps, args.warmup))
         if rank == 0:
-            print(json.dumps({"metric": METRIC, "value": n_series * n_points / (elapsed / args.steps),
+            emit({"metric": METRIC, "value": n_series * n_points / (elapsed / args.steps),
                               "unit": "input points/s", "n_gpus": world, "steps": args.steps,
                               "warmup": args.warmup, "ms_per_step": elapsed / args.steps * 1e3,
-                              "dry_run": True, "config": {"workload": desc_txt, "shards": shards}}), flush=True)
+                              "dry_run": True, "config": {"workload": desc_txt, "shards": shards}})
         if dist is not None:
             dist.destroy_process_group()
         return
@@ -465,6 +487,8 @@ def main():
         uid = [Context.unique_id() if rank == 0 else None]
         dist.broadcast_object_list(uid, src=0)
         ctx.comm_init(world, rank, uid[0])
+    elif rehearse:
+        ctx.comm_init(1, 0, Context.unique_id())
 
     d = _abi.SgDesc()
     keep = []
@@ -497,7 +521,7 @@ def main():
     d.start_time = 0
     d.end_time = (1 << 32) - 1
     d.agg, d.rate, d.ds_interval, d.ds_agg = agg, int(rate), dsi, dsa
-    if world > 1 and G == 1:
+    if (world > 1 or rehearse) and G == 1:
         d.flags |= _abi.SHARDED
     if args.exact:
         d.flags |= _abi.EXACT_ORDER
@@ -633,14 +657,18 @@ def main():
                 "frac_of_read_stream": achieved / probe["read_stream"] if probe else None,
             },
         }
+        if rehearse:
+            res["rehearsal"] = {"shards": rehearse, "note": f"shard 0 of {rehearse} on a 1-rank RCCL "
+                                "communicator; value = this shard's points/s, not a node figure"}
+            res["config"]["parallelism"] = f"rehearsal: 1 of {rehearse} series shards"
         if args.h2d and world == 1 and cfg["gen"] == "device" and G == 1:
             try:
                 res["h2d"] = h2d_leg(ctx, L, cfg, min(n_series, 100_000))
             except Exception as e:  # diagnostics only; never costs the line
                 res["h2d"] = {"error": repr(e)}
-        if not args.no_cpu and world == 1:
+        if not args.no_cpu and world == 1 and not rehearse:
             res["cpu_baseline"] = cpu_baseline(args.config, args.cpu_seconds)
-        print(json.dumps(res), flush=True)
+        emit(res)
     if cfg["gen"] == "device":
         L.tsdbhip_synth_free(ctx.handle, C.byref(d))
     ctx.close()

@@ -376,8 +376,12 @@ static void dispatch_reduce(tsdbhip_ctx* ctx, int agg, int mode, bool rate, unsi
 template <int AGG, int MODE>
 static void launch_combine(tsdbhip_ctx* ctx, const ReduceArgs& src, const ReduceArgs& dst, uint64_t T,
                            uint32_t n_chunks) {
-  hipLaunchKernelGGL((k_combine_chunks<AGG, MODE>), dim3(grid_for(T, 256)), dim3(256), 0, ctx->stream, src,
-                     dst, T, n_chunks);
+  if (n_chunks >= 64)  // (as the finalize: serial chunk loops are latency-bound)
+    hipLaunchKernelGGL((k_combine_par<AGG, MODE>), dim3((unsigned)T), dim3(256), 0, ctx->stream, src, dst, T,
+                       n_chunks);
+  else
+    hipLaunchKernelGGL((k_combine_chunks<AGG, MODE>), dim3(grid_for(T, 256)), dim3(256), 0, ctx->stream, src,
+                       dst, T, n_chunks);
 }
 template <int AGG>
 static void combine_mode(tsdbhip_ctx* ctx, int mode, const ReduceArgs& s, const ReduceArgs& d, uint64_t T,

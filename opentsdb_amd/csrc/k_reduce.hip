@@ -888,4 +888,35 @@ __global__ void __launch_bounds__(256) k_combine_chunks(ReduceArgs src, ReduceAr
   }
   acc_store<AGG, MODE>(dst, g, a);
 }
+
+// The same combine for many chunks (a shard's ~2048 partials per t at small
+// T): one block per t, contiguous chunk ranges per thread, then the
+// order-preserving tree of k_finalize_par, stored to dst slot g.
+template <int AGG, int MODE>
+__global__ void __launch_bounds__(256) k_combine_par(ReduceArgs src, ReduceArgs dst, uint64_t T,
+                                                     uint32_t n_chunks) {
+  __shared__ Acc s_acc[256];
+  const uint64_t g = blockIdx.x;
+  const uint32_t t = threadIdx.x;
+  const uint32_t per = (n_chunks + 255) / 256;
+  const uint32_t c0 = t * per, c1 = min(n_chunks, c0 + per);
+  Acc a;
+  acc_init(a);
+  for (uint32_t c = c0; c < c1; c++) {
+    Acc b;
+    acc_load<AGG, MODE>(src, (uint64_t)c * T + g, b);
+    acc_merge<AGG, MODE>(a, b);
+  }
+  s_acc[t] = a;
+  __syncthreads();
+  for (uint32_t d = 1; d < 256; d <<= 1) {
+    if ((t % (2 * d)) == 0) {
+      Acc x = s_acc[t];
+      acc_merge<AGG, MODE>(x, s_acc[t + d]);
+      s_acc[t] = x;
+    }
+    __syncthreads();
+  }
+  if (t == 0) acc_store<AGG, MODE>(dst, g, s_acc[0]);
+}
 }  // namespace tsdb
