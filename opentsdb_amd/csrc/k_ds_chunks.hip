@@ -110,6 +110,18 @@ struct BkLds {
   int64_t v[BKB];     // value sum / min / max
 };
 
+// Scalar (SMEM) load of read-only metadata at a wave-uniform address: the
+// span prologue's dependent chain (kept -> span rows -> row fields) then waits
+// on lgkmcnt through the scalar cache instead of one vmcnt(0) round trip per
+// level. Only for arrays no kernel in flight writes.
+template <class T>
+DEVI T sld(const T* p) { return *(const __attribute__((address_space(4))) T*)p; }
+// the byte at p through the aligned dword holding it
+DEVI uint32_t sld_u8(const uint8_t* p) {
+  const uintptr_t u = (uintptr_t)p;
+  return (sld((const uint32_t*)(u & ~(uintptr_t)3)) >> (8 * (u & 3))) & 0xFFu;
+}
+
 // wave-uniform copies (SGPR) of values every lane holds alike
 DEVI uint32_t ufl(uint32_t x) { return (uint32_t)__builtin_amdgcn_readfirstlane((int)x); }
 DEVI uint64_t ufl64(uint64_t x) { return ((uint64_t)ufl((uint32_t)(x >> 32)) << 32) | (uint64_t)ufl((uint32_t)x); }
@@ -422,34 +434,38 @@ __global__ void __launch_bounds__(256) k_ds_spans(DecodeArgs a, SpanDsArgs g, co
   const uint32_t nwaves = gridDim.x * blockDim.x / WAVE;
   bool any_i = false, any_f = false;
   int64_t fs = 0;  // F*: latest first bucket ts of a float span, + 1
-  const uint32_t n_in = g.in_list ? *g.in_count : a.n_kept;
+  const uint32_t n_in = g.in_list ? sld(g.in_count) : a.n_kept;
   for (uint32_t w = ufl(wave); w < n_in; w += nwaves) {
-    const uint32_t k = g.in_list ? ufl(g.in_list[w]) : w;
-    const uint32_t s = ufl(a.kept[k]);
-    const uint64_t r0 = ufl64(a.span_row_start[s]), r1 = ufl64(a.span_row_start[s + 1]);
-    const uint32_t n = ufl(a.sp_ncells[s]);
-    bool ok = a.sp_q1[s] < 0 && a.sp_ovf_cell[s] < 0 && n > 0 && r1 > r0 && a.interval > 0;
-    for (uint64_t rb = r0; ok && rb < r1; rb += WAVE) {  // (uniform loop: keeps `ok` scalar)
-      const uint64_t r = rb + lane;
-      ok = ballot(r < r1 && (a.row_ok[r] == 0 || ncells[r] == 0)) == 0;
+    const uint32_t k = g.in_list ? sld(&g.in_list[w]) : w;
+    const uint32_t s = sld(&a.kept[k]);
+    const uint64_t r0 = sld(&a.span_row_start[s]), r1 = sld(&a.span_row_start[s + 1]);
+    const uint32_t n = sld(&a.sp_ncells[s]);
+    bool ok = sld(&a.sp_q1[s]) < 0 && sld(&a.sp_ovf_cell[s]) < 0 && n > 0 && r1 > r0 && a.interval > 0;
+    if (ok && r1 - r0 == 1) {  // (one row: the usual hourly span)
+      ok = sld_u8(&a.row_ok[r0]) != 0 && sld(&ncells[r0]) != 0;
+    } else {
+      for (uint64_t rb = r0; ok && rb < r1; rb += WAVE) {  // (uniform loop: keeps `ok` scalar)
+        const uint64_t r = rb + lane;
+        ok = ballot(r < r1 && (a.row_ok[r] == 0 || ncells[r] == 0)) == 0;
+      }
     }
     // value width of the span's rows (all must match and be aligned)
     uint32_t W = 0;
     if (ok) {
-      const uint32_t nc = ncells[r0], vl = vlen[r0];
+      const uint32_t nc = sld(&ncells[r0]), vl = sld(&vlen[r0]);
       const uint32_t vb = nc > 1 ? vl - 1 : vl;
       W = vb == (vb / nc) * nc ? vb / nc : 0;
       ok = W == 8 || W == 4;
     }
-    const uint64_t eo = ufl64(a.e_off[k]);
-    const uint32_t cap = ufl((uint32_t)a.sp_cap[s]);
+    const uint64_t eo = sld(&a.e_off[k]);
+    const uint32_t cap = (uint32_t)sld(&a.sp_cap[s]);
     DsState st = {};
     uint32_t cell = 0;
     for (uint64_t r = r0; ok && r < r1; r++) {
-      const uint32_t nc = ufl(ncells[r]);
-      const uint32_t vl = ufl(vlen[r]);
-      const uint64_t qoff = ufl64(a.row_qual_off[r]), voff = ufl64(a.row_val_off[r]);
-      const uint32_t rbase = ufl(a.row_base[r]);
+      const uint32_t nc = sld(&ncells[r]);
+      const uint32_t vl = sld(&vlen[r]);
+      const uint64_t qoff = sld(&a.row_qual_off[r]), voff = sld(&a.row_val_off[r]);
+      const uint32_t rbase = sld(&a.row_base[r]);
       const uint32_t vb = nc > 1 ? vl - 1 : vl;
       if (!(vb == W * nc && (qoff & 7) == 0 && (voff & 15) == 0)) {
         ok = false;
