@@ -183,3 +183,18 @@ def test_bench_harness_groups_world2():
     import json
     d = json.loads(lines[0])
     assert d["config"]["shards"] == [[0, 333333], [333333, 1000000]]
+
+
+def test_bench_rehearsal_split_and_single_line():
+    """--rehearse-shards N at N=1 takes rank 0's 1/N shard, and the process's
+    stdout holds the JSON line alone (native banners go to stderr)."""
+    cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--steps", "2", "--warmup", "1", "--dry-run",
+           "--rehearse-shards", "8"]
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=240)
+    assert r.returncode == 0, r.stderr[-2000:]
+    lines = r.stdout.splitlines()
+    assert len(lines) == 1, r.stdout
+    import json
+    d = json.loads(lines[0])
+    assert d["n_gpus"] == 1 and len(d["config"]["shards"]) == 8
+    assert d["config"]["shards"][0] == [0, 125000]
