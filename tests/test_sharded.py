@@ -65,6 +65,26 @@ def test_sharded_c3s_shape(sctx, agg):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("agg", [0, 1, 2, 3, 4])
+def test_sharded_many_chunks_combine(sctx, agg):
+    """>= 64 reduce chunks per rank (2048 spans, T = 10 buckets): the rank's
+    chunk partials go through k_combine_par (block per t, ordered tree)."""
+    ss = synth.regular(2048, 600, _abi.SYN_INT64_COUNTER, seed=11, step=1)
+    g, o = run_sharded(sctx, ss, agg=agg, ds_interval=60, ds_agg=3)
+    assert_same(g, o)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("agg", [0, 2, 3])
+@pytest.mark.parametrize("rate", [False, True])
+def test_sharded_many_chunks_direct(sctx, agg, rate):
+    """the direct path with >= 64 chunks per rank (1100 spans, T = 200)"""
+    ss = synth.regular(1100, 200, _abi.SYN_INT64_COUNTER, seed=12, step=1)
+    g, o = run_sharded(sctx, ss, agg=agg, rate=rate)
+    assert_same(g, o)
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("seed", [1, 2])
 @pytest.mark.parametrize("agg", [0, 2, 4])
 def test_sharded_jittered_mixed(sctx, seed, agg):
