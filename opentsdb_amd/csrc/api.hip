@@ -346,7 +346,10 @@ static void launch_reduce(tsdbhip_ctx* ctx, unsigned blocks, const ReduceArgs& r
   hipLaunchKernelGGL((k_reduce<AGG, MODE, RATE, false>), dim3(blocks), dim3(256), 0, ctx->stream, r);
   if (ctx->time_reduce) HIPCHK(hipEventRecord(ctx->ev[9], ctx->stream));
   if (!finalize) return;
-  if (par)
+  if (par && f.T >= 1024)  // (large T: coalesced columns)
+    hipLaunchKernelGGL((k_chunks_cols<AGG, MODE, RATE, true>), dim3((unsigned)((f.T + 63) / 64)), dim3(64 * COLW), 0,
+                       ctx->stream, r, r, f, f.T, f.n_chunks);
+  else if (par)
     hipLaunchKernelGGL((k_finalize_par<AGG, MODE, RATE>), dim3((unsigned)f.T), dim3(256), 0, ctx->stream, r, f);
   else
     hipLaunchKernelGGL((k_finalize_seq<AGG, MODE, RATE>), dim3(grid_for(f.T, 256)), dim3(256), 0, ctx->stream,
@@ -376,7 +379,11 @@ static void dispatch_reduce(tsdbhip_ctx* ctx, int agg, int mode, bool rate, unsi
 template <int AGG, int MODE>
 static void launch_combine(tsdbhip_ctx* ctx, const ReduceArgs& src, const ReduceArgs& dst, uint64_t T,
                            uint32_t n_chunks) {
-  if (n_chunks >= 64)  // (as the finalize: serial chunk loops are latency-bound)
+  if (n_chunks >= 64 && T >= 1024) {  // (large T: coalesced columns)
+    FinalArgs nf = {};
+    hipLaunchKernelGGL((k_chunks_cols<AGG, MODE, false, false>), dim3((unsigned)((T + 63) / 64)), dim3(64 * COLW), 0,
+                       ctx->stream, src, dst, nf, T, n_chunks);
+  } else if (n_chunks >= 64)  // (as the finalize: serial chunk loops are latency-bound)
     hipLaunchKernelGGL((k_combine_par<AGG, MODE>), dim3((unsigned)T), dim3(256), 0, ctx->stream, src, dst, T,
                        n_chunks);
   else

@@ -870,6 +870,38 @@ __global__ void __launch_bounds__(256) k_finalize_par(ReduceArgs r, FinalArgs f)
   if (t == 0) finalize_one<AGG, MODE, RATE>(f, g, s_acc[0]);
 }
 
+// Many chunks at large T (C3: ~290 chunks x 3600 t): a block of 16 waves per
+// 64 consecutive t, so every partial load is a coalesced row segment; wave w
+// merges chunk range w in order, then the 16 wave results merge in order.
+// FINAL: finalize into the output; else store to dst slot t (rank combine).
+constexpr uint32_t COLW = 16;
+template <int AGG, int MODE, bool RATE, bool FINAL>
+__global__ void __launch_bounds__(64 * COLW) k_chunks_cols(ReduceArgs r, ReduceArgs dst, FinalArgs f, uint64_t T,
+                                                        uint32_t n_chunks) {
+  __shared__ Acc s_acc[COLW][WAVE];
+  const int lane = lane_id();
+  const uint32_t w = threadIdx.x / WAVE;
+  const uint64_t g = (uint64_t)blockIdx.x * WAVE + lane;
+  const uint32_t per = (n_chunks + COLW - 1) / COLW;
+  const uint32_t c0 = min(n_chunks, w * per), c1 = min(n_chunks, c0 + per);
+  Acc a;
+  acc_init(a);
+  if (g < T) {
+    for (uint32_t c = c0; c < c1; c++) {
+      Acc b;
+      acc_load<AGG, MODE>(r, (uint64_t)c * T + g, b);
+      acc_merge<AGG, MODE>(a, b);
+    }
+  }
+  s_acc[w][lane] = a;
+  __syncthreads();
+  if (w == 0 && g < T) {
+    for (uint32_t v = 1; v < COLW; v++) acc_merge<AGG, MODE>(a, s_acc[v][lane]);
+    if (FINAL) finalize_one<AGG, MODE, RATE>(f, g, a);
+    else acc_store<AGG, MODE>(dst, g, a);
+  }
+}
+
 }  // namespace tsdb
 
 namespace tsdb {

@@ -85,6 +85,19 @@ def test_sharded_many_chunks_direct(sctx, agg, rate):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("agg", [0, 1, 3, 4])
+@pytest.mark.parametrize("rate", [False, True])
+@pytest.mark.parametrize("sharded", [False, True])
+def test_many_chunks_large_t(sctx, agg, rate, sharded):
+    """>= 64 chunks at T >= 1024 (1100 spans x 1200 points): the coalesced
+    column merge (k_chunks_cols) as the finalize and as the rank combine"""
+    ss = synth.regular(1100, 1200, _abi.SYN_INT64_COUNTER, seed=13, step=1)
+    g = core.run_spanset(sctx, ss, 0, U32MAX, agg, sharded=sharded, rate=rate)
+    o = oracle.spangroup(ss, 0, U32MAX, agg, rate, 0, 0)
+    assert_same(g, o)
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("seed", [1, 2])
 @pytest.mark.parametrize("agg", [0, 2, 4])
 def test_sharded_jittered_mixed(sctx, seed, agg):
