@@ -185,7 +185,9 @@ DEVI bool ds_row(const DecodeArgs& a, const SpanDsArgs& g, DsState& st, uint64_t
   RawW<W> A, B;
   auto issue = [&](uint32_t c0, RawW<W>& x) {
     const uint32_t c = c0 + 8u * lane;
+    __builtin_amdgcn_s_setprio(2);  // the chunk's loads ahead of other waves' VALU
     load_raw<W>(a, qoff, voff, c < nc ? c : clamp_c, x);
+    __builtin_amdgcn_s_setprio(0);
   };
   issue(0, A);
   issue(DCH, B);
