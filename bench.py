@@ -264,12 +264,14 @@ def bench_c5(args):
     qcap, vcap = b.qual_extent + 64, b.val_extent + R + 64
     o = {k: torch.zeros(n, dtype=dt, device=dev) for k, n, dt in
          [("st", R, torch.uint8), ("qo", R, torch.int64), ("ql", R, torch.int32), ("vo", R, torch.int64),
-          ("vl", R, torch.int32), ("q", qcap, torch.uint8), ("v", vcap, torch.uint8)]}
+          ("vl", R, torch.int32), ("q", qcap, torch.uint8), ("v", vcap, torch.uint8), ("w", R, torch.uint8),
+          ("k", R, torch.int32)]}
     P = lambda t, ct: C.cast(C.c_void_p(t.data_ptr()), C.POINTER(ct))  # noqa: E731
     out = _abi.RowsOut(qual_capacity=qcap, val_capacity=vcap, row_status=P(o["st"], C.c_uint8),
                        row_qual_off=P(o["qo"], C.c_uint64), row_qual_len=P(o["ql"], C.c_uint32),
                        row_val_off=P(o["vo"], C.c_uint64), row_val_len=P(o["vl"], C.c_uint32),
-                       qual_bytes=P(o["q"], C.c_uint8), val_bytes=P(o["v"], C.c_uint8))
+                       qual_bytes=P(o["q"], C.c_uint8), val_bytes=P(o["v"], C.c_uint8),
+                       row_write=P(o["w"], C.c_uint8), row_keep_kv=P(o["k"], C.c_int32))
 
     def step_once():
         ctx.check(L.tsdbhip_compact_rows(ctx.handle, C.byref(d), C.byref(out)))

@@ -49,7 +49,7 @@
 extern "C" {
 #endif
 
-#define TSDBHIP_ABI_VERSION 2
+#define TSDBHIP_ABI_VERSION 3
 
 /* ---- return codes ---------------------------------------------------- */
 #define TSDBHIP_OK               0
@@ -228,6 +228,24 @@ typedef struct tsdbhip_rows_out {
   uint64_t  val_used;        /* out: value extent written                   */
   uint64_t  n_complex;       /* out: rows that reached complexCompact
                                 (status COMPLEX, ERROR or OOB)             */
+  /* The write/delete decision of compact() (CompactionQueue.java:276,
+   * 355-404, 419-434) for a row whose base time is old enough to be written
+   * back (the caller applies the cut-off of :408-413 and
+   * TSDB.enable_compactions). Both arrays are optional (NULL: not produced).
+   *   row_write[r]   1: tsdb.put(key, compacted qualifier, compacted value)
+   *                  (TRIVIAL rows, and COMPLEX rows unless a KV of the row
+   *                  already holds exactly the compacted qualifier AND
+   *                  value, :388-396); 0 otherwise.
+   *   row_keep_kv[r] index, relative to row_kv_start[r], of the KV that
+   *                  holds the compacted qualifier (:364-400) and must NOT
+   *                  be deleted; -1 if none.
+   * The delete set of a TRIVIAL/COMPLEX row (tsdb.delete, :421-434) is every
+   * KV of the row whose qualifier length is even and non-zero (junk KVs were
+   * dropped from the list, :301-306), except row_keep_kv. SINGLE / NONE /
+   * ERROR / OOB rows: no put, no delete (:245-269 return before any write;
+   * an exception aborts the row). */
+  uint8_t*  row_write;       /* [n_rows] or NULL                             */
+  int32_t*  row_keep_kv;     /* [n_rows] or NULL                             */
 } tsdbhip_rows_out;
 
 /* ---- synthetic, HBM-resident inputs (bench / tests) -------------------- */

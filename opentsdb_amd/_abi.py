@@ -6,7 +6,7 @@ and the test harness.
 """
 import ctypes as C
 
-ABI_VERSION = 2
+ABI_VERSION = 3
 
 OK = 0
 E_ILLEGAL_DATA = -1
@@ -139,6 +139,8 @@ class RowsOut(C.Structure):
         ("qual_used", C.c_uint64),
         ("val_used", C.c_uint64),
         ("n_complex", C.c_uint64),
+        ("row_write", P8),
+        ("row_keep_kv", C.POINTER(C.c_int32)),
     ]
 
 

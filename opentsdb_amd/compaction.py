@@ -20,6 +20,9 @@ import numpy as np
 
 from . import _abi
 
+NONE, SINGLE, TRIVIAL, COMPLEX, ERROR, OOB = (_abi.ROW_NONE, _abi.ROW_SINGLE, _abi.ROW_TRIVIAL, _abi.ROW_COMPLEX,
+                                             _abi.ROW_ERROR, _abi.ROW_OOB)
+
 
 @dataclass
 class RowBatch:
@@ -106,6 +109,8 @@ class RowsResult:
     val_len: np.ndarray   # uint32
     qual: np.ndarray      # uint8 (rows placed per tsdbhip.h; gaps undefined)
     val: np.ndarray
+    write: np.ndarray = None    # uint8 [n_rows]: tsdb.put of the compacted cell
+    keep_kv: np.ndarray = None  # int32 [n_rows]: KV (index in the row) not to delete, -1 none
     n_complex: int = 0
 
     def row(self, r):
@@ -116,6 +121,17 @@ class RowsResult:
 
     def rows(self):
         return [self.row(r) for r in range(len(self.status))]
+
+    def decision(self, r, kv_qual_lens):
+        """-> (put?, sorted KV indices to delete) of row r, the flush-path
+        writes of CompactionQueue.compact (CompactionQueue.java:419-434) for a
+        row old enough to be written back; kv_qual_lens = the row's KV
+        qualifier lengths."""
+        if int(self.status[r]) not in (TRIVIAL, COMPLEX):
+            return False, []
+        keep = int(self.keep_kv[r])
+        dele = [i for i, ql in enumerate(kv_qual_lens) if ql and ql % 2 == 0 and i != keep]
+        return bool(self.write[r]), dele
 
     @staticmethod
     def _packed(buf, off, ln):
@@ -141,7 +157,8 @@ def out_buffers(batch: RowBatch):
     vcap = batch.val_extent + n + 64
     res = RowsResult(np.zeros(max(n, 1), np.uint8), np.zeros(max(n, 1), np.uint64),
                      np.zeros(max(n, 1), np.uint32), np.zeros(max(n, 1), np.uint64),
-                     np.zeros(max(n, 1), np.uint32), np.zeros(qcap, np.uint8), np.zeros(vcap, np.uint8))
+                     np.zeros(max(n, 1), np.uint32), np.zeros(qcap, np.uint8), np.zeros(vcap, np.uint8),
+                     np.full(max(n, 1), 0xEE, np.uint8), np.full(max(n, 1), -7, np.int32))
     out = _abi.RowsOut(qual_capacity=qcap, val_capacity=vcap,
                        row_status=_abi.ptr(res.status, C.c_uint8),
                        row_qual_off=_abi.ptr(res.qual_off, C.c_uint64),
@@ -149,12 +166,14 @@ def out_buffers(batch: RowBatch):
                        row_val_off=_abi.ptr(res.val_off, C.c_uint64),
                        row_val_len=_abi.ptr(res.val_len, C.c_uint32),
                        qual_bytes=_abi.ptr(res.qual, C.c_uint8),
-                       val_bytes=_abi.ptr(res.val, C.c_uint8))
+                       val_bytes=_abi.ptr(res.val, C.c_uint8),
+                       row_write=_abi.ptr(res.write, C.c_uint8),
+                       row_keep_kv=_abi.ptr(res.keep_kv, C.c_int32))
     return res, out
 
 
 def _trim(res, n):
-    for f in ("status", "qual_off", "qual_len", "val_off", "val_len"):
+    for f in ("status", "qual_off", "qual_len", "val_off", "val_len", "write", "keep_kv"):
         setattr(res, f, getattr(res, f)[:n])
     return res
 

@@ -1112,8 +1112,9 @@ extern "C" int tsdbhip_compact_rows(tsdbhip_ctx* ctx, const tsdbhip_rows_desc* d
   if (R == 0) return TSDBHIP_OK;
   if (!d->row_kv_start || !d->row_qual_off || !d->row_val_off || (d->n_kvs && (!d->kv_qual_len || !d->kv_val_len)) ||
       !d->qual_bytes || !d->val_bytes || !out->row_status || !out->row_qual_off || !out->row_qual_len ||
-      !out->row_val_off || !out->row_val_len || !out->qual_bytes || !out->val_bytes || R >= (1ull << 32)) {
-    set_error(ctx, "tsdbhip_compact_rows: null array or too many rows");
+      !out->row_val_off || !out->row_val_len || !out->qual_bytes || !out->val_bytes || R >= (1ull << 32) ||
+      (!out->row_write != !out->row_keep_kv)) {
+    set_error(ctx, "tsdbhip_compact_rows: null array, row_write without row_keep_kv, or too many rows");
     return TSDBHIP_E_INVALID_ARG;
   }
   try {
@@ -1158,7 +1159,11 @@ extern "C" int tsdbhip_compact_rows(tsdbhip_ctx* ctx, const tsdbhip_rows_desc* d
     a.val_nbytes = d->val_nbytes;
     a.qcap = out->qual_capacity;
     a.vcap = out->val_capacity;
+    a.out_write = nullptr;
+    a.out_keep = nullptr;
     if (dev) {
+      a.out_write = out->row_write;
+      a.out_keep = out->row_keep_kv;
       a.status = out->row_status;
       a.out_qoff = out->row_qual_off;
       a.out_qlen = out->row_qual_len;
@@ -1176,6 +1181,10 @@ extern "C" int tsdbhip_compact_rows(tsdbhip_ctx* ctx, const tsdbhip_rows_desc* d
       a.ov = scratch<uint8_t>(ctx, "c_ov", vext + R);
       a.qcap = qext;
       a.vcap = vext + R;
+      if (out->row_write || out->row_keep_kv) {  // both, or neither
+        a.out_write = scratch<uint8_t>(ctx, "c_ow", R);
+        a.out_keep = scratch<int32_t>(ctx, "c_ok", R);
+      }
     }
     a.counters = scratch<uint32_t>(ctx, "c_cnt", 4, true);
     a.list_lds = scratch<uint32_t>(ctx, "c_llds", R);
@@ -1188,6 +1197,7 @@ extern "C" int tsdbhip_compact_rows(tsdbhip_ctx* ctx, const tsdbhip_rows_desc* d
     HIPCHK(hipEventRecord(ctx->ev[9], ctx->stream));
     hipLaunchKernelGGL(k_compact_complex<true>, dim3(1024), dim3(256), 0, ctx->stream, a);
     hipLaunchKernelGGL(k_compact_complex<false>, dim3(256), dim3(256), 0, ctx->stream, a);
+    if (a.out_write) hipLaunchKernelGGL(k_compact_dups, dim3(grid_for(R, 4 * WAVE, 4096)), dim3(256), 0, ctx->stream, a);
     HIPCHK(hipGetLastError());
     HIPCHK(hipEventRecord(ctx->ev[1], ctx->stream));
     uint32_t cnt[4];
@@ -1204,6 +1214,10 @@ extern "C" int tsdbhip_compact_rows(tsdbhip_ctx* ctx, const tsdbhip_rows_desc* d
       HIPCHK(hipMemcpyAsync(out->row_val_len, a.out_vlen, 4 * R, hipMemcpyDeviceToHost, ctx->stream));
       if (qext) HIPCHK(hipMemcpyAsync(out->qual_bytes, a.oq, qext, hipMemcpyDeviceToHost, ctx->stream));
       HIPCHK(hipMemcpyAsync(out->val_bytes, a.ov, vext + R, hipMemcpyDeviceToHost, ctx->stream));
+      if (a.out_write) {
+        HIPCHK(hipMemcpyAsync(out->row_write, a.out_write, R, hipMemcpyDeviceToHost, ctx->stream));
+        HIPCHK(hipMemcpyAsync(out->row_keep_kv, a.out_keep, 4 * R, hipMemcpyDeviceToHost, ctx->stream));
+      }
       HIPCHK(hipStreamSynchronize(ctx->stream));
     }
     tsdbhip_timing t = {};

@@ -53,6 +53,8 @@ struct CompactArgs {
   uint32_t* out_vlen;
   uint8_t* oq;
   uint8_t* ov;
+  uint8_t* out_write;   // optional (null): tsdb.put decision per row
+  int32_t* out_keep;    // optional: KV of the row not to delete, -1 none
   uint32_t* counters;   // [0] complex rows in LDS list, [1] in big list, [2] bad-argument flag,
                         // [3] complex rows finished in-wave by k_compact_tiles
   uint32_t* list_lds;   // complex rows with <= CQ_LDS_CELLS cells
@@ -89,10 +91,17 @@ DEVI RowHdr cq_row(const CompactArgs& a, uint64_t r) {
   return h;
 }
 
+// Row results. Write-back decision: every TRIVIAL row is put (:276; its
+// compacted qualifier is longer than any of its KVs'), COMPLEX rows are put
+// unless k_compact_dups finds the compacted cell already in the row.
 DEVI void cq_finish(const CompactArgs& a, uint64_t r, uint8_t st, uint32_t qlen, uint32_t vlen) {
   a.status[r] = st;
   a.out_qlen[r] = qlen;
   a.out_vlen[r] = vlen;
+  if (a.out_write) {
+    a.out_write[r] = (st == CQ_TRIVIAL || st == CQ_COMPLEX) ? 1 : 0;
+    a.out_keep[r] = -1;
+  }
 }
 
 // Wave copy of n bytes, lanes striding (coalesced on both sides).
@@ -916,5 +925,109 @@ __global__ void __launch_bounds__(256) k_compact_tiles(CompactArgs a) {
   }
   __syncthreads();
   if (tid == 0 && L.n_complex) atomicAdd(&a.counters[3], L.n_complex);
+}
+
+// ===========================================================================
+// k_compact_dups: the write/delete decision of complexCompact rows
+// (CompactionQueue.java:355-404). `longest` is the row's first KV as handed
+// in, replaced by each later non-2-byte, even, non-empty qualifier strictly
+// longer than it (:283-312); if the compacted qualifier is not longer than
+// longest's, the KV holding exactly the compacted qualifier — longest itself
+// if it matches, else the first such KV in row order (:369-387) — is kept
+// out of the delete set, and nothing is written when its value is the
+// compacted value too (:388-399). One wave per row, only for COMPLEX rows
+// (found by a ballot over 64 rows' statuses); reads the row's KV lengths and
+// the candidate qualifiers again, and the compacted bytes just written.
+// ===========================================================================
+DEVI bool cq_wave_equal(const uint8_t* x, const uint8_t* y, uint32_t n, int lane) {
+  bool ne = false;
+  for (uint32_t j = lane; j < n; j += WAVE) ne |= x[j] != y[j];
+  return ballot(ne) == 0;
+}
+
+DEVI void cq_dup_row(const CompactArgs& a, uint64_t r, int lane) {
+  const uint64_t kb = a.row_kv_start[r], nk = a.row_kv_start[r + 1] - kb;
+  const uint64_t qs = a.row_qual_off[r], vs = a.row_val_off[r];
+  const uint32_t cql = a.out_qlen[r], cvl = a.out_vlen[r];
+  const uint8_t* cq = a.oq + a.out_qoff[r];
+  const uint8_t* cv = a.ov + a.out_voff[r];
+  // ---- longest (:283-312) ----
+  uint32_t lbest = a.kv_qual_len[kb];
+  uint64_t li = 0, lq = qs, lv = vs;
+  uint32_t lvl = a.kv_val_len[kb];
+  uint64_t qcar = 0, vcar = 0;
+  for (uint64_t base = 0; base < nk; base += WAVE) {
+    const uint64_t i = base + lane;
+    const bool act = i < nk;
+    const uint32_t ql = act ? a.kv_qual_len[kb + i] : 0u, vl = act ? a.kv_val_len[kb + i] : 0u;
+    const uint32_t qi = wave_incl_scan_u32_dpp(ql), vi = wave_incl_scan_u32_dpp(vl);
+    const uint64_t qpos = qs + qcar + (qi - ql), vpos = vs + vcar + (vi - vl);
+    qcar += readlane_u32(qi, 63);
+    vcar += readlane_u32(vi, 63);
+    const bool multi = act && ql != 2 && ql != 0 && (ql & 1) == 0;
+    uint32_t mx = multi ? ql : 0u;
+#pragma unroll
+    for (int m = 1; m < WAVE; m <<= 1) mx = max(mx, (uint32_t)__shfl_xor((int)mx, m));
+    if (mx > lbest) {  // first KV of this chunk at the new maximum
+      const int fl = __ffsll((long long)ballot(multi && ql == mx)) - 1;
+      lbest = mx;
+      li = base + fl;
+      lq = readlane_u64(qpos, fl);
+      lv = readlane_u64(vpos, fl);
+      lvl = readlane_u32(vl, fl);
+    }
+  }
+  if (cql > lbest) return;  // :366 — cannot overwrite an existing cell
+  // ---- the KV holding the compacted qualifier (:369-387) ----
+  int64_t dup = -1;
+  uint64_t dvpos = 0;
+  uint32_t dvl = 0;
+  if (lbest == cql && cq_wave_equal(a.qual + lq, cq, cql, lane)) {
+    dup = (int64_t)li;
+    dvpos = lv;
+    dvl = lvl;
+  } else {
+    qcar = vcar = 0;
+    for (uint64_t base = 0; base < nk && dup < 0; base += WAVE) {
+      const uint64_t i = base + lane;
+      const bool act = i < nk;
+      const uint32_t ql = act ? a.kv_qual_len[kb + i] : 0u, vl = act ? a.kv_val_len[kb + i] : 0u;
+      const uint32_t qi = wave_incl_scan_u32_dpp(ql), vi = wave_incl_scan_u32_dpp(vl);
+      const uint64_t qpos = qs + qcar + (qi - ql), vpos = vs + vcar + (vi - vl);
+      qcar += readlane_u32(qi, 63);
+      vcar += readlane_u32(vi, 63);
+      uint64_t cand = ballot(act && ql == cql);
+      while (cand) {
+        const int l = __ffsll((long long)cand) - 1;
+        cand &= cand - 1;
+        if (cq_wave_equal(a.qual + readlane_u64(qpos, l), cq, cql, lane)) {
+          dup = (int64_t)(base + l);
+          dvpos = readlane_u64(vpos, l);
+          dvl = readlane_u32(vl, l);
+          break;
+        }
+      }
+    }
+  }
+  if (dup < 0) return;
+  const bool same = dvl == cvl && cq_wave_equal(a.val + dvpos, cv, cvl, lane);  // :391
+  if (lane == 0) {
+    if (same) a.out_write[r] = 0;
+    a.out_keep[r] = (int32_t)dup;  // :399
+  }
+}
+
+__global__ void __launch_bounds__(256) k_compact_dups(CompactArgs a) {
+  const int lane = lane_id();
+  const uint64_t nw = (uint64_t)gridDim.x * 4;
+  for (uint64_t g = (uint64_t)blockIdx.x * 4 + threadIdx.x / WAVE; g * WAVE < a.n_rows; g += nw) {
+    const uint64_t r = g * WAVE + lane;
+    uint64_t m = ballot(r < a.n_rows && a.status[r] == CQ_COMPLEX);
+    while (m) {
+      const int l = __ffsll((long long)m) - 1;
+      m &= m - 1;
+      cq_dup_row(a, g * WAVE + l, lane);
+    }
+  }
 }
 }  // namespace tsdb

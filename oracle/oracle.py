@@ -33,6 +33,10 @@ def lib():
         L.oracle_agg_double.argtypes = [C.c_int, C.POINTER(C.c_double), C.c_size_t, C.POINTER(C.c_double)]
         L.oracle_compact_rows.argtypes = [C.POINTER(_abi.RowsDesc), C.POINTER(_abi.RowsOut)]
         L.oracle_compact_rows.restype = C.c_int
+        L.oracle_regular_sharded.argtypes = [C.c_uint64, C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint32,
+                                             C.c_uint32, C.c_int64, C.c_int64, C.c_int, C.c_int, C.c_int32,
+                                             C.c_int, C.c_uint32, C.c_int, C.POINTER(_abi.SgOut)]
+        L.oracle_regular_sharded.restype = C.c_int
         _LIB = L
     return _LIB
 
@@ -75,6 +79,25 @@ def spangroup(spanset, start, end, agg, rate=False, ds_interval=0, ds_agg=0, cap
     n = int(out.n_out)
     return Result(code, ts[:n].copy(), isi[:n].copy(), bits[:n].copy(),
                   int(out.n_input_points), int(out.err_index))
+
+
+def regular_sharded(n_spans, n_points, kind, seed, step, start, end, agg, rate=False, ds_interval=0, ds_agg=0,
+                    t0=None, shard_spans=2000, threads=None, capacity=None):
+    """The synthetic regular SpanGroup of synth.regular / tsdbhip_synth_generate
+    at full size, generated and iterated shard by shard on host threads and
+    combined in shard order (oracle.cc: oracle_regular_sharded; sum / min /
+    max on aligned grids only)."""
+    from opentsdb_amd import synth
+    t0 = synth.T0 if t0 is None else t0
+    cap = int(capacity or max(1, n_points if not ds_interval else n_points * step // ds_interval + 2))
+    ts, isi, bits = np.zeros(cap, np.int64), np.zeros(cap, np.uint8), np.zeros(cap, np.int64)
+    out = _abi.SgOut(capacity=cap, ts=_abi.ptr(ts, C.c_int64), is_int=_abi.ptr(isi, C.c_uint8),
+                     bits=_abi.ptr(bits, C.c_int64))
+    threads = threads or max(1, min(16, os.cpu_count() or 1))
+    code = lib().oracle_regular_sharded(seed, n_spans, n_points, t0, step, kind, int(start), int(end), agg,
+                                        int(bool(rate)), ds_interval, ds_agg, shard_spans, threads, C.byref(out))
+    n = int(out.n_out)
+    return Result(code, ts[:n].copy(), isi[:n].copy(), bits[:n].copy(), int(out.n_input_points), -1)
 
 
 def agg_long(agg, values):

@@ -2,7 +2,8 @@
 (src/core/CompactionQueue.java:243-743) — a second, independent restatement
 used only to cross-check oracle/oracle.cc on random rows. Returns
 (status, qualifier bytes, value bytes) with the row status codes of
-include/tsdbhip.h.
+include/tsdbhip.h; `decide` adds the flush path's write/delete decision
+(:276, :355-404, :419-434) as (put?, KV index kept from the delete, or -1).
 """
 NONE, SINGLE, TRIVIAL, COMPLEX, ERROR, OOB = 0, 1, 2, 3, 4, 5
 
@@ -114,3 +115,27 @@ def _compact(row):
             vs.append(fv)
         return TRIVIAL, b"".join(qs), b"".join(vs) + b"\0"
     return _complex(kept)
+
+
+def decide(row):
+    """-> (status, qualifier, value, put, keep): compact() plus the flush
+    path's writes for a row old enough to be written back. The KVs deleted
+    are the row's even, non-empty qualifiers except index `keep`."""
+    st, q, v = compact(row)
+    if st == TRIVIAL:
+        return st, q, v, True, -1   # the compacted qualifier is longer than any KV's
+    if st != COMPLEX:
+        return st, q, v, False, -1  # no put, no delete (returned early or threw)
+    # `longest` (:283-312): row[0] as handed in, then every later valid
+    # non-2-byte qualifier strictly longer than the current one
+    li, ll = 0, len(row[0][0])
+    for i, (kq, _) in enumerate(row):
+        if len(kq) != 2 and len(kq) % 2 == 0 and kq and len(kq) > ll:
+            li, ll = i, len(kq)
+    if len(q) > ll:
+        return st, q, v, True, -1
+    dup = li if row[li][0] == q else next(
+        (i for i, (kq, _) in enumerate(row) if kq and len(kq) % 2 == 0 and kq == q), -1)
+    if dup < 0:
+        return st, q, v, True, -1
+    return st, q, v, row[dup][1] != v, dup

@@ -5,7 +5,8 @@ Nothing here is computed by the oracle or the GPU path. The expected values
 are the reference's own test vectors and hand-derived known answers:
   * TestAggregators.java:68-109 (dev on 0..9999, {3,3,3}, {1,2});
   * TestCompactionQueue.java:77-299 (the ten byte-exact compaction vectors,
-    KEY-independent: compacted[0]'s qualifier/value bytes);
+    KEY-independent: compacted[0]'s qualifier/value bytes, and the put /
+    delete calls each test verifies);
   * KA-1..KA-8 of SURVEY.md §8(c), traced by hand through
     SpanGroup.java:435-784 / Span.java:377-511 (KA-3/KA-6 re-derived here
     with absolute timestamps: the rate quirk Q5 divides by x0 itself).
@@ -61,29 +62,39 @@ def spangroups():
 
 
 def compaction():
+    # "put": whether tsdb.put(KEY, qual, val) is verified once (times(1)) or
+    # never; "delete": the KVs (indices into "kvs") of the verified
+    # tsdb.delete(KEY, new byte[][] {...}) call, [] for never() — both read
+    # off the test's verify() lines (TestCompactionQueue.java:84-86, 98-100,
+    # 116-119, 138-141, 162-165, 201-203, 227-230, 262-265, 294-298); an
+    # expected exception (:168) means neither.
     q1, q2, q3 = "0007", "0027", "0017"
     return [
-        {"name": "emptyRow", "kvs": [], "status": "none"},
-        {"name": "oneCellRow", "kvs": [["0003", L(42)]], "status": "single", "qual": "0003", "val": L(42)},
+        {"name": "emptyRow", "kvs": [], "status": "none", "put": False, "delete": []},
+        {"name": "oneCellRow", "kvs": [["0003", L(42)]], "status": "single", "qual": "0003", "val": L(42),
+         "put": False, "delete": []},
         {"name": "twoCellRow", "kvs": [["0007", L(4)], ["0017", L(5)]], "status": "trivial",
-         "qual": "00070017", "val": L(4) + L(5) + "00"},
+         "qual": "00070017", "val": L(4) + L(5) + "00", "put": True, "delete": [0, 1]},
         {"name": "fixQualifierFlags", "kvs": [["0003", L(4)], ["0017", L(5)]], "status": "trivial",
-         "qual": "00070017", "val": L(4) + L(5) + "00"},
+         "qual": "00070017", "val": L(4) + L(5) + "00", "put": True, "delete": [0, 1]},
         {"name": "fixFloatingPoint", "kvs": [["0007", L(4)], ["001b", L(fbits(4.2))]], "status": "trivial",
-         "qual": "0007001b", "val": L(4) + I4(fbits(4.2)) + "00"},
-        {"name": "overlappingDataPoints", "kvs": [["0007", L(4)], ["0003", I4(4)]], "status": "error"},
+         "qual": "0007001b", "val": L(4) + I4(fbits(4.2)) + "00", "put": True, "delete": [0, 1]},
+        {"name": "overlappingDataPoints", "kvs": [["0007", L(4)], ["0003", I4(4)]], "status": "error",
+         "put": False, "delete": []},
         {"name": "failedCompactNoop", "kvs": [[q1, L(4)], [q3, L(5)], [q1 + q3, L(4) + L(5) + "00"]],
-         "status": "complex", "qual": q1 + q3, "val": L(4) + L(5) + "00"},
+         "status": "complex", "qual": q1 + q3, "val": L(4) + L(5) + "00", "put": False, "delete": [0, 1]},
         {"name": "secondCompact", "kvs": [[q1 + q2, L(4) + L(5) + "00"], [q3, L(6)]], "status": "complex",
-         "qual": q1 + q3 + q2, "val": L(4) + L(6) + L(5) + "00"},
+         "qual": q1 + q3 + q2, "val": L(4) + L(6) + L(5) + "00", "put": True, "delete": [0, 1]},
         {"name": "doubleFailedCompactNoop",
          "kvs": [[q1, L(4)], [q1 + q3 + q2, L(4) + L(6) + L(5) + "00"], [q1 + q2, L(4) + L(5) + "00"],
                  [q3, L(6)], [q2, L(5)]],
-         "status": "complex", "qual": q1 + q3 + q2, "val": L(4) + L(6) + L(5) + "00"},
+         "status": "complex", "qual": q1 + q3 + q2, "val": L(4) + L(6) + L(5) + "00", "put": False,
+         "delete": [0, 2, 3, 4]},
         {"name": "weirdOverlappingCompactedCells",
          "kvs": [[q1, L(4)], [q1 + q2, L(4) + L(5) + "00"], [q1 + q3, L(4) + L(6) + "00"], [q3, L(6)],
                  [q2, L(5)]],
-         "status": "complex", "qual": q1 + q3 + q2, "val": L(4) + L(6) + L(5) + "00"},
+         "status": "complex", "qual": q1 + q3 + q2, "val": L(4) + L(6) + L(5) + "00", "put": True,
+         "delete": [0, 1, 2, 3, 4]},
     ]
 
 

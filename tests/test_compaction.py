@@ -94,6 +94,30 @@ def test_oracle_edge_rows(name):
     row = EDGE[name]
     res = oracle.compact_rows(compaction.pack_rows([row]))
     assert res.row(0) == cfc.compact(row)
+    st, q, v, put, keep = cfc.decide(row)
+    assert (bool(res.write[0]), int(res.keep_kv[0])) == (put, keep)
+
+
+def test_oracle_decision_cases():
+    """The write/delete decision (CompactionQueue.java:364-400) on rows
+    built to reach each branch: the dup found as `longest`, found by the
+    loop (a 2-byte KV equal to a deduplicated 1-cell compaction: same
+    qualifier, value without the meta byte, so put but keep the cell), a junk row[0]
+    longer than every valid qualifier (:283 takes it before :302 drops it)."""
+    c12 = compacted([(1, 7, L(1)), (2, 7, L(2))])
+    one = compacted([(3, 0, b"\x01"), (3, 0, b"\x01")])  # dedupes to the single cell (3, 0)
+    rows = {
+        "dup is longest, same value": ([(Q(1, 7), L(1)), c12, (Q(2, 7), L(2))], False, 1),
+        "dup by loop, different value": ([(Q(3, 0), b"\x01"), one], True, 0),
+        "junk row0 longest": ([(b"\x00\x01\x02\x03\x04", b"j"), c12, (Q(1, 7), L(1))], False, 1),
+        "no dup": ([(Q(1, 7), L(1)), compacted([(2, 7, L(2)), (3, 7, L(3))])], True, -1),
+    }
+    b = compaction.pack_rows([r for r, _, _ in rows.values()])
+    res = oracle.compact_rows(b)
+    for i, (name, (row, put, keep)) in enumerate(rows.items()):
+        assert res.row(i)[0] == cfc.COMPLEX, name
+        assert (bool(res.write[i]), int(res.keep_kv[i])) == (put, keep), name
+        assert cfc.decide(row)[3:] == (put, keep), name
 
 
 def test_oracle_edge_statuses():
@@ -121,7 +145,9 @@ def test_oracle_random_batch_vs_restatement():
     res = oracle.compact_rows(b)
     rows = batch_rows(b)
     for r in range(b.n_rows):
-        assert res.row(r) == cfc.compact(rows[r]), r
+        st, q, v, put, keep = cfc.decide(rows[r])
+        assert res.row(r) == (st, q, v), r
+        assert (bool(res.write[r]), int(res.keep_kv[r])) == (put, keep), r
     st = np.bincount(res.status, minlength=6)
     assert st[cfc.TRIVIAL] and st[cfc.COMPLEX] and st[cfc.ERROR] and st[cfc.SINGLE]
 
@@ -169,6 +195,8 @@ def assert_same(g, o):
     assert np.array_equal(g.packed_qual(), o.packed_qual())
     assert np.array_equal(g.packed_val(), o.packed_val())
     assert g.n_complex == o.n_complex
+    assert np.array_equal(g.write, o.write), "row_write"
+    assert np.array_equal(g.keep_kv, o.keep_kv), "row_keep_kv"
 
 
 @pytest.mark.gpu
@@ -187,6 +215,7 @@ def test_gpu_compaction_golden(ctx):
         assert st == status[c["status"]], c["name"]
         if "qual" in c:
             assert q.hex() == c["qual"] and v.hex() == c["val"], c["name"]
+        assert g.decision(r, [len(k) for k, _ in rows[r]]) == (c["put"], c["delete"]), c["name"]
 
 
 @pytest.mark.gpu

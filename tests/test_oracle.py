@@ -79,6 +79,9 @@ def test_oracle_compaction_vectors(case):
     assert st == STATUS[case["status"]]
     if "qual" in case:
         assert q.hex() == case["qual"] and v.hex() == case["val"]
+    # the put / delete calls the test verifies (write-back of an old row)
+    put, dele = res.decision(0, [len(k) for k, _ in rows[0]])
+    assert put == case["put"] and dele == case["delete"]
 
 
 def _random_group(rng, n_spans, mixed, minimal):
