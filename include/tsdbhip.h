@@ -265,7 +265,30 @@ typedef struct tsdbhip_synth_params {
 } tsdbhip_synth_params;
 
 /* ---- context ----------------------------------------------------------- */
+/*
+ * A context owns a pool of per-call slots (HIP stream, HBM scratch, pinned
+ * staging): every entry point is re-entrant, and calls from several host
+ * threads on one context run concurrently, each on its own slot (the
+ * reference's Netty workers and gnuplot pool threads call SpanGroup
+ * concurrently, GraphHandler.java:182,285). tsdbhip_last_error is the calling
+ * thread's last message; tsdbhip_last_timing the calling thread's last call
+ * on that context.
+ */
 int         tsdbhip_open(int32_t device, tsdbhip_ctx** out);
+/*
+ * One context over several GPUs of this process (the JVM's, TsdbQuery.java:
+ * 301-307): tsdbhip_spangroup_run splits each SpanGroup into contiguous span
+ * ranges (span order kept, balanced by points for host descs), runs rank r on
+ * devices[r] from a host thread of its own, and exchanges grid and partials
+ * over RCCL (ncclCommInitAll) when the devices are distinct; when a device
+ * repeats, the ranks sharing it exchange through device copies (several
+ * shards on one GPU: same results, used to run the N-rank exchange on one
+ * GPU). tsdbhip_open_mask: the devices of the set bits of gpu_mask.
+ * Compaction, group-by batches, synthetic inputs and probes of a
+ * multi-device context run on its first device. */
+int         tsdbhip_open_devices(const int32_t* devices, uint32_t n, tsdbhip_ctx** out);
+int         tsdbhip_open_mask(uint32_t gpu_mask, tsdbhip_ctx** out);
+int         tsdbhip_ranks(tsdbhip_ctx* ctx);  /* shards per SpanGroup (1: one device) */
 void        tsdbhip_close(tsdbhip_ctx* ctx);
 const char* tsdbhip_last_error(tsdbhip_ctx* ctx);
 int         tsdbhip_abi_version(void);

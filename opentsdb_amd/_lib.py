@@ -23,7 +23,7 @@ EXPORTS = [
     "tsdbhip_last_timing", "tsdbhip_compact_rows", "tsdbhip_comm_unique_id",
     "tsdbhip_comm_init", "tsdbhip_synth_generate", "tsdbhip_synth_free",
     "tsdbhip_desc_download", "tsdbhip_bw_probe", "tsdbhip_spangroup_run_batch",
-    "tsdbhip_format_points",
+    "tsdbhip_format_points", "tsdbhip_open_devices", "tsdbhip_open_mask", "tsdbhip_ranks",
 ]
 
 
@@ -55,6 +55,12 @@ def lib():
     P = C.POINTER
     L.tsdbhip_open.argtypes = [C.c_int32, P(C.c_void_p)]
     L.tsdbhip_open.restype = C.c_int
+    L.tsdbhip_open_devices.argtypes = [P(C.c_int32), C.c_uint32, P(C.c_void_p)]
+    L.tsdbhip_open_devices.restype = C.c_int
+    L.tsdbhip_open_mask.argtypes = [C.c_uint32, P(C.c_void_p)]
+    L.tsdbhip_open_mask.restype = C.c_int
+    L.tsdbhip_ranks.argtypes = [C.c_void_p]
+    L.tsdbhip_ranks.restype = C.c_int
     L.tsdbhip_close.argtypes = [C.c_void_p]
     L.tsdbhip_close.restype = None
     L.tsdbhip_last_error.argtypes = [C.c_void_p]
@@ -88,15 +94,23 @@ def lib():
 
 
 class Context:
-    """One tsdbhip_ctx: a GPU, its stream and its HBM scratch."""
+    """One tsdbhip_ctx: a GPU (or, with `devices`, one shard per listed GPU of
+    this process, a device may repeat), its pool of per-call streams and HBM
+    scratch."""
 
-    def __init__(self, device=0):
+    def __init__(self, device=0, devices=None):
         self._lib = lib()
         self._h = C.c_void_p()
-        rc = self._lib.tsdbhip_open(int(device), C.byref(self._h))
+        if devices is not None:
+            arr = (C.c_int32 * len(devices))(*[int(d) for d in devices])
+            rc = self._lib.tsdbhip_open_devices(arr, len(devices), C.byref(self._h))
+            device = int(devices[0])
+        else:
+            rc = self._lib.tsdbhip_open(int(device), C.byref(self._h))
         if rc:
             raise TsdbHipError(rc, self._lib.tsdbhip_last_error(None).decode())
         self.device = device
+        self.ranks = self._lib.tsdbhip_ranks(self._h)
 
     @property
     def handle(self):

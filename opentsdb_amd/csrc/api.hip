@@ -19,8 +19,10 @@
 #include <cstdio>
 #include <cstring>
 #include <map>
+#include <memory>
 #include <mutex>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "../../include/tsdbhip.h"
@@ -51,33 +53,54 @@ struct Fail {
 
 }  // namespace
 
-struct tsdbhip_ctx {
+// Per-call resources. A call takes a free slot of its context (or a new
+// one), so calls from several host threads on one context run concurrently,
+// each on its own stream with its own scratch (the reference's Netty workers
+// and gnuplot pool call SpanGroup concurrently, GraphHandler.java:182,285).
+struct Xchg;
+struct Slot {
   int device = 0;
   hipStream_t stream = nullptr;
-  std::mutex mu;
-  std::string err;
-  std::map<std::string, Buf> bufs;
-  void* host_small = nullptr;  // pinned readback area
-  void* host_big = nullptr;    // grow-only pinned staging (group-by batches)
+  std::map<std::string, Buf> bufs;  // grow-only named scratch (HBM)
+  void* host_small = nullptr;       // pinned readback area
+  void* host_big = nullptr;         // grow-only pinned staging (group-by batches)
   size_t host_big_n = 0;
   hipEvent_t ev[10] = {};  // [8],[9] bracket the dominant kernel
   bool time_reduce = false;  // the dominant kernel is k_reduce (direct path)
   uint32_t hot_kernel = 0;
   tsdbhip_timing timing = {};
+  Xchg* x = nullptr;  // the exchange of a sharded call (its rank / nranks)
+  bool want_output = true;  // false: a non-zero rank of an in-process sharded call
+};
+
+struct Multi;
+struct tsdbhip_ctx {
+  int device = 0;
+  std::mutex mu;                   // slot pool, owned buffers, last timing
+  std::vector<Slot*> slots, free_slots;
+  std::map<std::string, Buf> owned;  // tsdbhip_synth_generate datasets
+  tsdbhip_timing last = {};
+  // one process per GPU (tsdbhip_comm_init): sharded calls serialise on the
+  // communicator (every rank must issue its collectives in the same order)
+  std::mutex comm_mu;
   ncclComm_t comm = nullptr;
-  int nranks = 1, rank = 0;
+  Xchg* rccl = nullptr;
+  // one process, several GPUs / shards (tsdbhip_open_devices): member
+  // contexts, one per rank
+  Multi* multi = nullptr;
 };
 
 static thread_local std::string g_thread_err;
+static thread_local const tsdbhip_ctx* g_last_ctx = nullptr;  // this thread's last call
+static thread_local tsdbhip_timing g_last_timing = {};
 
-static void set_error(tsdbhip_ctx* c, const char* fmt, ...) {
+static void set_error(const void*, const char* fmt, ...) {
   char buf[512];
   va_list ap;
   va_start(ap, fmt);
   vsnprintf(buf, sizeof buf, fmt, ap);
   va_end(ap);
   g_thread_err = buf;
-  if (c) c->err = buf;
 }
 
 #define HIPCHK(x)                                                                  \
@@ -102,7 +125,7 @@ static void set_error(tsdbhip_ctx* c, const char* fmt, ...) {
 
 // grow-only named scratch
 template <typename T>
-static T* scratch(tsdbhip_ctx* ctx, const char* name, size_t count, bool zero = false) {
+static T* scratch(Slot* ctx, const char* name, size_t count, bool zero = false) {
   size_t bytes = std::max<size_t>(count * sizeof(T), 16) + 64;
   Buf& b = ctx->bufs[name];
   if (b.n < bytes) {
@@ -123,7 +146,9 @@ static unsigned grid_for(uint64_t work, unsigned per_block, unsigned cap = 1u <<
   return (unsigned)g;
 }
 
-static void dscan_u64(tsdbhip_ctx* ctx, const uint64_t* in, uint64_t* out, uint64_t n, uint64_t* d_total,
+#include "xchg.hip"
+
+static void dscan_u64(Slot* ctx, const uint64_t* in, uint64_t* out, uint64_t n, uint64_t* d_total,
                       const char* tag) {
   const uint64_t nb = (n + 1023) / 1024;
   std::string key = std::string("scan_blocks_") + tag;
@@ -137,17 +162,101 @@ static void dscan_u64(tsdbhip_ctx* ctx, const uint64_t* in, uint64_t* out, uint6
   hipLaunchKernelGGL(k_scan_add_u64, dim3(grid_for(n, 256)), dim3(256), 0, ctx->stream, out, n, bs);
 }
 
+// ------------------------------------------------------------ slot pool ----
+static void slot_free(Slot* s) {
+  if (!s) return;
+  hipSetDevice(s->device);
+  if (s->stream) hipStreamSynchronize(s->stream);
+  for (auto& kv : s->bufs)
+    if (kv.second.p) hipFree(kv.second.p);
+  for (auto& e : s->ev)
+    if (e) hipEventDestroy(e);
+  if (s->host_small) hipHostFree(s->host_small);
+  if (s->host_big) hipHostFree(s->host_big);
+  if (s->stream) hipStreamDestroy(s->stream);
+  delete s;
+}
+
+static Slot* slot_new(int device) {
+  Slot* ctx = new Slot();
+  ctx->device = device;
+  try {
+    HIPCHK(hipSetDevice(device));
+    HIPCHK(hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking));
+    HIPCHK(hipHostMalloc(&ctx->host_small, 4096, hipHostMallocDefault));
+    for (auto& e : ctx->ev) HIPCHK(hipEventCreate(&e));
+  } catch (Fail&) {
+    slot_free(ctx);
+    throw;
+  }
+  return ctx;
+}
+
+static constexpr size_t MAX_SLOTS = 64;  // concurrent calls per context
+
+// A slot held for the duration of one call.
+struct Lease {
+  tsdbhip_ctx* c;
+  Slot* s = nullptr;
+  explicit Lease(tsdbhip_ctx* c_) : c(c_) {
+    {
+      std::lock_guard<std::mutex> lk(c->mu);
+      if (!c->free_slots.empty()) {
+        s = c->free_slots.back();
+        c->free_slots.pop_back();
+      } else if (c->slots.size() >= MAX_SLOTS) {
+        set_error(c, "more than %zu concurrent calls on one context", MAX_SLOTS);
+        throw Fail{TSDBHIP_E_INVALID_ARG};
+      }
+    }
+    if (!s) {
+      s = slot_new(c->device);
+      std::lock_guard<std::mutex> lk(c->mu);
+      c->slots.push_back(s);
+    }
+    s->x = nullptr;
+    s->want_output = true;
+    Slot* ctx = s;
+    HIPCHK(hipSetDevice(c->device));
+  }
+  ~Lease() {
+    s->x = nullptr;
+    g_last_ctx = c;
+    g_last_timing = s->timing;
+    std::lock_guard<std::mutex> lk(c->mu);
+    c->last = s->timing;
+    c->free_slots.push_back(s);
+  }
+};
+
+// ---------------------------------------------- in-process multi-device ----
+// tsdbhip_open_devices: rank r is member context r (device devs[r]); a
+// SpanGroup is split into contiguous span ranges, one per rank, run by one
+// host thread each through the sharded path.
+struct Multi {
+  int n = 0;
+  std::vector<int> devs;
+  std::vector<tsdbhip_ctx*> members;
+  std::vector<std::unique_ptr<Xchg>> xs;
+  std::vector<ncclComm_t> comms;
+  LocalGroup local;
+  bool rccl = false;
+  std::mutex call_mu;  // one sharded call at a time (collectives in lockstep)
+  // per rank > 0: result buffers of its (unused) copy of the output
+  std::vector<std::vector<int64_t>> ts, bits;
+  std::vector<std::vector<uint8_t>> isint;
+};
+
+// plain context of a call: a multi-device context's non-sharded work
+// (inputs, compaction, probes) runs on its first member
+static tsdbhip_ctx* plain_of(tsdbhip_ctx* c) { return c->multi ? c->multi->members[0] : c; }
+
 // ----------------------------------------------------------------------------
 extern "C" int tsdbhip_abi_version(void) { return TSDBHIP_ABI_VERSION; }
 
-extern "C" const char* tsdbhip_last_error(tsdbhip_ctx* ctx) {
-  return ctx ? ctx->err.c_str() : g_thread_err.c_str();
-}
+extern "C" const char* tsdbhip_last_error(tsdbhip_ctx*) { return g_thread_err.c_str(); }
 
-extern "C" int tsdbhip_open(int32_t device, tsdbhip_ctx** out) {
-  tsdbhip_ctx* ctx = nullptr;
-  if (!out) return TSDBHIP_E_INVALID_ARG;
-  *out = nullptr;
+static int ctx_open(int32_t device, tsdbhip_ctx** out) {
   int n = 0;
   if (hipGetDeviceCount(&n) != hipSuccess || n <= 0) {
     set_error(nullptr, "no HIP device available");
@@ -157,41 +266,147 @@ extern "C" int tsdbhip_open(int32_t device, tsdbhip_ctx** out) {
     set_error(nullptr, "device %d out of range (%d devices)", device, n);
     return TSDBHIP_E_INVALID_ARG;
   }
-  ctx = new tsdbhip_ctx();
-  ctx->device = device;
+  tsdbhip_ctx* c = new tsdbhip_ctx();
+  c->device = device;
   try {
-    HIPCHK(hipSetDevice(device));
-    HIPCHK(hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking));
-    HIPCHK(hipHostMalloc(&ctx->host_small, 4096, hipHostMallocDefault));
-    for (auto& e : ctx->ev) HIPCHK(hipEventCreate(&e));
+    Slot* s = slot_new(device);  // the first slot (and a check that the device works)
+    c->slots.push_back(s);
+    c->free_slots.push_back(s);
   } catch (Fail& f) {
-    delete ctx;
+    delete c;
     return f.code;
   }
-  *out = ctx;
+  *out = c;
   return TSDBHIP_OK;
+}
+
+extern "C" int tsdbhip_open(int32_t device, tsdbhip_ctx** out) {
+  if (!out) return TSDBHIP_E_INVALID_ARG;
+  *out = nullptr;
+  return ctx_open(device, out);
 }
 
 extern "C" void tsdbhip_close(tsdbhip_ctx* ctx) {
   if (!ctx) return;
+  if (ctx->multi) {
+    Multi* m = ctx->multi;
+    for (int r = 0; r < m->n; r++) {
+      hipSetDevice(m->devs[r]);
+      if (r < (int)m->local.ready.size() && m->local.ready[r]) hipEventDestroy(m->local.ready[r]);
+      if (r < (int)m->local.done.size() && m->local.done[r]) hipEventDestroy(m->local.done[r]);
+    }
+    for (ncclComm_t cm : m->comms)
+      if (cm) ncclCommDestroy(cm);
+    for (tsdbhip_ctx* mc : m->members) tsdbhip_close(mc);
+    delete m;
+    delete ctx;
+    return;
+  }
   hipSetDevice(ctx->device);
-  if (ctx->stream) hipStreamSynchronize(ctx->stream);
-  if (ctx->comm) ncclCommDestroy(ctx->comm);
-  for (auto& kv : ctx->bufs)
+  for (Slot* s : ctx->slots) slot_free(s);
+  for (auto& kv : ctx->owned)
     if (kv.second.p) hipFree(kv.second.p);
-  for (auto& e : ctx->ev)
-    if (e) hipEventDestroy(e);
-  if (ctx->host_small) hipHostFree(ctx->host_small);
-  if (ctx->host_big) hipHostFree(ctx->host_big);
-  if (ctx->stream) hipStreamDestroy(ctx->stream);
+  if (ctx->comm) ncclCommDestroy(ctx->comm);
+  delete ctx->rccl;
   delete ctx;
+}
+
+// One context over several devices; devs may repeat (several shards on one
+// GPU exchange through device copies, LocalXchg); distinct devices exchange
+// over RCCL (one communicator per device, ncclCommInitAll) unless
+// TSDBHIP_XCHG=local.
+extern "C" int tsdbhip_open_devices(const int32_t* devs, uint32_t n, tsdbhip_ctx** out) {
+  if (!out || !devs || n == 0 || n > 64) return TSDBHIP_E_INVALID_ARG;
+  *out = nullptr;
+  if (n == 1) return ctx_open(devs[0], out);
+  tsdbhip_ctx* ctx = new tsdbhip_ctx();
+  Multi* m = new Multi();
+  ctx->multi = m;
+  ctx->device = devs[0];
+  m->n = (int)n;
+  m->devs.assign(devs, devs + n);
+  int rc = TSDBHIP_OK;
+  for (uint32_t r = 0; r < n && !rc; r++) {
+    tsdbhip_ctx* mc = nullptr;
+    rc = ctx_open(devs[r], &mc);
+    if (!rc) m->members.push_back(mc);
+  }
+  bool distinct = true;
+  for (uint32_t a = 0; a < n; a++)
+    for (uint32_t b = a + 1; b < n; b++) distinct = distinct && devs[a] != devs[b];
+  const char* xe = getenv("TSDBHIP_XCHG");
+  m->rccl = distinct && !(xe && !strcmp(xe, "local"));
+  try {
+    if (rc) throw Fail{rc};
+    if (m->rccl) {
+      m->comms.assign(n, nullptr);
+      std::vector<int> dl(devs, devs + n);
+      NCCLCHK(ncclCommInitAll(m->comms.data(), (int)n, dl.data()));
+      for (uint32_t r = 0; r < n; r++) {
+        RcclXchg* x = new RcclXchg();
+        x->comm = m->comms[r];
+        x->nranks = (int)n;
+        x->rank = (int)r;
+        m->xs.emplace_back(x);
+      }
+    } else {
+      LocalGroup& G = m->local;
+      G.n = (int)n;
+      G.dev = m->devs;
+      G.ptr.assign(n, nullptr);
+      G.ready.assign(n, nullptr);
+      G.done.assign(n, nullptr);
+      for (uint32_t r = 0; r < n; r++) {
+        HIPCHK(hipSetDevice(devs[r]));
+        HIPCHK(hipEventCreateWithFlags(&G.ready[r], hipEventDisableTiming));
+        HIPCHK(hipEventCreateWithFlags(&G.done[r], hipEventDisableTiming));
+        if (!distinct) continue;
+        for (uint32_t q = 0; q < n; q++) {  // peer copies between distinct devices
+          int can = 0;
+          if (devs[q] != devs[r] && hipDeviceCanAccessPeer(&can, devs[r], devs[q]) == hipSuccess && can)
+            (void)hipDeviceEnablePeerAccess(devs[q], 0);
+        }
+      }
+      (void)hipGetLastError();  // (peer access already enabled is not an error here)
+      for (uint32_t r = 0; r < n; r++) {
+        LocalXchg* x = new LocalXchg();
+        x->G = &G;
+        x->nranks = (int)n;
+        x->rank = (int)r;
+        m->xs.emplace_back(x);
+      }
+    }
+  } catch (Fail& f) {
+    tsdbhip_close(ctx);
+    return f.code;
+  }
+  m->ts.resize(n);
+  m->bits.resize(n);
+  m->isint.resize(n);
+  *out = ctx;
+  return TSDBHIP_OK;
+}
+
+extern "C" int tsdbhip_open_mask(uint32_t gpu_mask, tsdbhip_ctx** out) {
+  int32_t devs[32];
+  uint32_t n = 0;
+  for (int d = 0; d < 32; d++)
+    if (gpu_mask & (1u << d)) devs[n++] = d;
+  if (!n) return TSDBHIP_E_INVALID_ARG;
+  return tsdbhip_open_devices(devs, n, out);
+}
+
+extern "C" int tsdbhip_ranks(tsdbhip_ctx* ctx) {
+  if (!ctx) return TSDBHIP_E_INVALID_ARG;
+  return ctx->multi ? ctx->multi->n : 1;
 }
 
 extern "C" int tsdbhip_host_register(tsdbhip_ctx* ctx, void* p, size_t n) {
   if (!ctx || !p || !n) return TSDBHIP_E_INVALID_ARG;
   try {
     HIPCHK(hipSetDevice(ctx->device));
-    HIPCHK(hipHostRegister(p, n, hipHostRegisterDefault));
+    // (portable: pinned for every device of a multi-device context)
+    HIPCHK(hipHostRegister(p, n, ctx->multi ? hipHostRegisterPortable : hipHostRegisterDefault));
   } catch (Fail& f) {
     return f.code;
   }
@@ -209,9 +424,15 @@ extern "C" int tsdbhip_host_unregister(tsdbhip_ctx* ctx, void* p) {
   return TSDBHIP_OK;
 }
 
+// The timings of this thread's last call on ctx (else of the ctx's last call).
 extern "C" int tsdbhip_last_timing(tsdbhip_ctx* ctx, tsdbhip_timing* t) {
   if (!ctx || !t) return TSDBHIP_E_INVALID_ARG;
-  *t = ctx->timing;
+  if (g_last_ctx == ctx) {
+    *t = g_last_timing;
+    return TSDBHIP_OK;
+  }
+  std::lock_guard<std::mutex> lk(ctx->mu);
+  *t = ctx->last;
   return TSDBHIP_OK;
 }
 
@@ -231,7 +452,8 @@ extern "C" int tsdbhip_comm_unique_id(uint8_t out[TSDBHIP_UNIQUE_ID_BYTES]) {
 
 extern "C" int tsdbhip_comm_init(tsdbhip_ctx* ctx, int32_t nranks, int32_t rank,
                                  const uint8_t id[TSDBHIP_UNIQUE_ID_BYTES]) {
-  if (!ctx || nranks < 1 || rank < 0 || rank >= nranks) return TSDBHIP_E_INVALID_ARG;
+  if (!ctx || ctx->multi || nranks < 1 || rank < 0 || rank >= nranks) return TSDBHIP_E_INVALID_ARG;
+  std::lock_guard<std::mutex> lk(ctx->comm_mu);
   try {
     HIPCHK(hipSetDevice(ctx->device));
     ncclUniqueId uid;
@@ -241,8 +463,12 @@ extern "C" int tsdbhip_comm_init(tsdbhip_ctx* ctx, int32_t nranks, int32_t rank,
       ctx->comm = nullptr;
     }
     NCCLCHK(ncclCommInitRank(&ctx->comm, nranks, uid, rank));
-    ctx->nranks = nranks;
-    ctx->rank = rank;
+    delete ctx->rccl;
+    RcclXchg* x = new RcclXchg();
+    x->comm = ctx->comm;
+    x->nranks = nranks;
+    x->rank = rank;
+    ctx->rccl = x;
   } catch (Fail& f) {
     return f.code;
   }
@@ -251,7 +477,7 @@ extern "C" int tsdbhip_comm_init(tsdbhip_ctx* ctx, int32_t nranks, int32_t rank,
 
 // ------------------------------------------------------------- helpers ----
 template <typename T>
-static const T* stage(tsdbhip_ctx* ctx, const char* name, const T* src, size_t count, bool on_device,
+static const T* stage(Slot* ctx, const char* name, const T* src, size_t count, bool on_device,
                       size_t pad = 0) {
   if (on_device) return src;
   T* d = scratch<T>(ctx, name, count + pad);
@@ -261,7 +487,7 @@ static const T* stage(tsdbhip_ctx* ctx, const char* name, const T* src, size_t c
 }
 
 // grow-only pinned host staging
-static void* host_buf(tsdbhip_ctx* ctx, size_t bytes) {
+static void* host_buf(Slot* ctx, size_t bytes) {
   if (ctx->host_big_n < bytes) {
     if (ctx->host_big) HIPCHK(hipHostFree(ctx->host_big));
     ctx->host_big = nullptr;
@@ -272,7 +498,7 @@ static void* host_buf(tsdbhip_ctx* ctx, size_t bytes) {
   return ctx->host_big;
 }
 
-static void readback(tsdbhip_ctx* ctx, void* host, const void* dev, size_t bytes) {
+static void readback(Slot* ctx, void* host, const void* dev, size_t bytes) {
   HIPCHK(hipMemcpyAsync(ctx->host_small, dev, bytes, hipMemcpyDeviceToHost, ctx->stream));
   HIPCHK(hipStreamSynchronize(ctx->stream));
   std::memcpy(host, ctx->host_small, bytes);
@@ -292,14 +518,14 @@ static void launch_agg(int agg, A&&... args) {
 
 struct LaunchGeneralDs {
   template <int AGG>
-  static void run(tsdbhip_ctx* ctx, unsigned blocks, const DecodeArgs& a) {
+  static void run(Slot* ctx, unsigned blocks, const DecodeArgs& a) {
     hipLaunchKernelGGL(k_decode_ds<AGG>, dim3(blocks), dim3(256), 0, ctx->stream, a);
   }
 };
 
 struct LaunchFastDs {
   template <int AGG>
-  static void run(tsdbhip_ctx* ctx, unsigned blocks, const DecodeArgs& a, const uint32_t* ncells,
+  static void run(Slot* ctx, unsigned blocks, const DecodeArgs& a, const uint32_t* ncells,
                   const uint32_t* vlen) {
     hipLaunchKernelGGL((k_decode_fast<AGG, true>), dim3(blocks), dim3(256), 0, ctx->stream, a, ncells, vlen);
   }
@@ -310,7 +536,7 @@ struct LaunchFastDs {
 // k_decode_fast.
 struct LaunchChunks {
   template <int AGG>
-  static void run(tsdbhip_ctx* ctx, const DecodeArgs& da, DecodeArgs& fa, const uint32_t* ncells,
+  static void run(Slot* ctx, const DecodeArgs& da, DecodeArgs& fa, const uint32_t* ncells,
                   const uint32_t* vlen, SpanDsArgs g, uint32_t* zeroed2 = nullptr) {
     if (AGG == 4) return;  // dev: Welford is order-dependent, serial kernels only
     hipStream_t st = ctx->stream;
@@ -339,7 +565,7 @@ struct LaunchChunks {
 };
 
 template <int AGG, int MODE, bool RATE>
-static void launch_reduce(tsdbhip_ctx* ctx, unsigned blocks, const ReduceArgs& r, const FinalArgs& f,
+static void launch_reduce(Slot* ctx, unsigned blocks, const ReduceArgs& r, const FinalArgs& f,
                           bool par, bool finalize) {
   if (ctx->time_reduce) HIPCHK(hipEventRecord(ctx->ev[8], ctx->stream));
   if (r.d_info) hipLaunchKernelGGL((k_reduce<AGG, MODE, RATE, true>), dim3(blocks), dim3(256), 0, ctx->stream, r);
@@ -357,7 +583,7 @@ static void launch_reduce(tsdbhip_ctx* ctx, unsigned blocks, const ReduceArgs& r
 }
 
 template <int AGG>
-static void dispatch_mode(tsdbhip_ctx* ctx, int mode, bool rate, unsigned blocks, const ReduceArgs& r,
+static void dispatch_mode(Slot* ctx, int mode, bool rate, unsigned blocks, const ReduceArgs& r,
                           const FinalArgs& f, bool par, bool fin) {
   if (rate) return launch_reduce<AGG, MODE_DBL, true>(ctx, blocks, r, f, par, fin);
   if (mode == MODE_INT) return launch_reduce<AGG, MODE_INT, false>(ctx, blocks, r, f, par, fin);
@@ -365,7 +591,7 @@ static void dispatch_mode(tsdbhip_ctx* ctx, int mode, bool rate, unsigned blocks
   return launch_reduce<AGG, MODE_DUAL, false>(ctx, blocks, r, f, par, fin);
 }
 
-static void dispatch_reduce(tsdbhip_ctx* ctx, int agg, int mode, bool rate, unsigned blocks,
+static void dispatch_reduce(Slot* ctx, int agg, int mode, bool rate, unsigned blocks,
                             const ReduceArgs& r, const FinalArgs& f, bool par, bool fin) {
   switch (agg) {
     case 0: return dispatch_mode<0>(ctx, mode, rate, blocks, r, f, par, fin);
@@ -377,7 +603,7 @@ static void dispatch_reduce(tsdbhip_ctx* ctx, int agg, int mode, bool rate, unsi
 }
 
 template <int AGG, int MODE>
-static void launch_combine(tsdbhip_ctx* ctx, const ReduceArgs& src, const ReduceArgs& dst, uint64_t T,
+static void launch_combine(Slot* ctx, const ReduceArgs& src, const ReduceArgs& dst, uint64_t T,
                            uint32_t n_chunks) {
   if (n_chunks >= 64 && T >= 1024) {  // (large T: coalesced columns)
     FinalArgs nf = {};
@@ -391,13 +617,13 @@ static void launch_combine(tsdbhip_ctx* ctx, const ReduceArgs& src, const Reduce
                        dst, T, n_chunks);
 }
 template <int AGG>
-static void combine_mode(tsdbhip_ctx* ctx, int mode, const ReduceArgs& s, const ReduceArgs& d, uint64_t T,
+static void combine_mode(Slot* ctx, int mode, const ReduceArgs& s, const ReduceArgs& d, uint64_t T,
                          uint32_t n) {
   if (mode == MODE_INT) return launch_combine<AGG, MODE_INT>(ctx, s, d, T, n);
   if (mode == MODE_DBL) return launch_combine<AGG, MODE_DBL>(ctx, s, d, T, n);
   return launch_combine<AGG, MODE_DUAL>(ctx, s, d, T, n);
 }
-static void dispatch_combine(tsdbhip_ctx* ctx, int agg, int mode, const ReduceArgs& s, const ReduceArgs& d,
+static void dispatch_combine(Slot* ctx, int agg, int mode, const ReduceArgs& s, const ReduceArgs& d,
                              uint64_t T, uint32_t n) {
   switch (agg) {
     case 0: return combine_mode<0>(ctx, mode, s, d, T, n);
@@ -409,14 +635,14 @@ static void dispatch_combine(tsdbhip_ctx* ctx, int agg, int mode, const ReduceAr
 }
 
 template <int AGG>
-static void final_mode(tsdbhip_ctx* ctx, int mode, bool rate, const ReduceArgs& r, const FinalArgs& f) {
+static void final_mode(Slot* ctx, int mode, bool rate, const ReduceArgs& r, const FinalArgs& f) {
   const dim3 g(grid_for(f.T, 256)), b(256);
   if (rate) hipLaunchKernelGGL((k_finalize_seq<AGG, MODE_DBL, true>), g, b, 0, ctx->stream, r, f);
   else if (mode == MODE_INT) hipLaunchKernelGGL((k_finalize_seq<AGG, MODE_INT, false>), g, b, 0, ctx->stream, r, f);
   else if (mode == MODE_DBL) hipLaunchKernelGGL((k_finalize_seq<AGG, MODE_DBL, false>), g, b, 0, ctx->stream, r, f);
   else hipLaunchKernelGGL((k_finalize_seq<AGG, MODE_DUAL, false>), g, b, 0, ctx->stream, r, f);
 }
-static void dispatch_final(tsdbhip_ctx* ctx, int agg, int mode, bool rate, const ReduceArgs& r,
+static void dispatch_final(Slot* ctx, int agg, int mode, bool rate, const ReduceArgs& r,
                            const FinalArgs& f) {
   switch (agg) {
     case 0: return final_mode<0>(ctx, mode, rate, r, f);
@@ -465,11 +691,12 @@ static float ev_ms(hipEvent_t a, hipEvent_t b) {
 }
 
 // ------------------------------------------------------- the hot path ----
-static int spangroup_run(tsdbhip_ctx* ctx, const tsdbhip_sg_desc* d, tsdbhip_sg_out* out) {
+static int spangroup_run(Slot* ctx, const tsdbhip_sg_desc* d, tsdbhip_sg_out* out) {
   const bool dev = (d->flags & TSDBHIP_DESC_DEVICE) != 0;
   const bool exact = (d->flags & TSDBHIP_EXACT_ORDER) != 0;
   // (a 1-rank communicator runs the same exchange code: tests use it)
-  const bool sharded = (d->flags & TSDBHIP_SHARDED) != 0 && ctx->comm && ctx->nranks >= 1;
+  Xchg* X = (d->flags & TSDBHIP_SHARDED) ? ctx->x : nullptr;
+  const bool sharded = X != nullptr;
   const uint32_t S = d->n_spans;
   const uint64_t R = d->n_rows;
   const bool rate = d->rate != 0;
@@ -499,7 +726,7 @@ static int spangroup_run(tsdbhip_ctx* ctx, const tsdbhip_sg_desc* d, tsdbhip_sg_
   struct Small {
     int32_t err;
     uint32_t gflags[2];
-    uint32_t ambiguous;
+    uint32_t reserved;
     unsigned long long range[2];
     unsigned long long fstar;
     unsigned long long n_input;
@@ -572,11 +799,11 @@ static int spangroup_run(tsdbhip_ctx* ctx, const tsdbhip_sg_desc* d, tsdbhip_sg_
     // spans' bounds (min first, max last; ranks without kept spans hold the
     // neutral ~0 / 0) and the error code (most negative) are reduced in place,
     // so the one readback below returns the agreed values
-    NCCLCHK(ncclGroupStart());
-    NCCLCHK(ncclAllReduce(&sm->bound[0], &sm->bound[0], 1, ncclUint64, ncclMin, ctx->comm, st));
-    NCCLCHK(ncclAllReduce(&sm->bound[1], &sm->bound[1], 1, ncclUint64, ncclMax, ctx->comm, st));
-    NCCLCHK(ncclAllReduce(&sm->err, &sm->err, 1, ncclInt32, ncclMin, ctx->comm, st));
-    NCCLCHK(ncclGroupEnd());
+    X->group_start(ctx);
+    X->allreduce(ctx, &sm->bound[0], 1, X_U64, X_MIN);
+    X->allreduce(ctx, &sm->bound[1], 1, X_U64, X_MAX);
+    X->allreduce(ctx, &sm->err, 1, X_I32, X_MIN);
+    X->group_end(ctx);
   }
   Small h;
   readback(ctx, &h, sm, sizeof h);  // sync 1
@@ -701,12 +928,12 @@ static int spangroup_run(tsdbhip_ctx* ctx, const tsdbhip_sg_desc* d, tsdbhip_sg_
   if (sharded) {
     // agree on the int/float flags, F*, the error and the input count across
     // ranks, in place, ahead of the one readback
-    NCCLCHK(ncclGroupStart());
-    NCCLCHK(ncclAllReduce(sm->gflags, sm->gflags, 2, ncclUint32, ncclMax, ctx->comm, st));
-    NCCLCHK(ncclAllReduce(&sm->fstar, &sm->fstar, 1, ncclUint64, ncclMax, ctx->comm, st));
-    NCCLCHK(ncclAllReduce(&sm->err, &sm->err, 1, ncclInt32, ncclMin, ctx->comm, st));
-    NCCLCHK(ncclAllReduce(&sm->n_input, &sm->n_input, 1, ncclUint64, ncclSum, ctx->comm, st));
-    NCCLCHK(ncclGroupEnd());
+    X->group_start(ctx);
+    X->allreduce(ctx, sm->gflags, 2, X_U32, X_MAX);
+    X->allreduce(ctx, &sm->fstar, 1, X_U64, X_MAX);
+    X->allreduce(ctx, &sm->err, 1, X_I32, X_MIN);
+    X->allreduce(ctx, &sm->n_input, 1, X_U64, X_SUM);
+    X->group_end(ctx);
   }
   // (no readback here: the flags, F*, errors and input count come back with
   // |G| below. A decode error leaves every e_len <= its capacity, so the grid
@@ -738,9 +965,9 @@ static int spangroup_run(tsdbhip_ctx* ctx, const tsdbhip_sg_desc* d, tsdbhip_sg_
       hipLaunchKernelGGL(k_grid_mark, dim3(mark_list ? std::min(grid_for(n_kept, 4, 65536), 1024u) : grid_for(n_kept, 4, 65536)),
                          dim3(256), 0, st, ga);
     if (sharded) {
-      uint32_t* all = scratch<uint32_t>(ctx, "bitmap_all", nwords * ctx->nranks);
-      NCCLCHK(ncclAllGather(bitmap, all, nwords, ncclUint32, ctx->comm, st));
-      hipLaunchKernelGGL(k_bitmap_or, dim3(grid_for(nwords, 256)), dim3(256), 0, st, all, (uint32_t)ctx->nranks,
+      uint32_t* all = scratch<uint32_t>(ctx, "bitmap_all", nwords * X->nranks);
+      X->allgather(ctx, bitmap, all, nwords * 4);
+      hipLaunchKernelGGL(k_bitmap_or, dim3(grid_for(nwords, 256)), dim3(256), 0, st, all, (uint32_t)X->nranks,
                          nwords, bitmap);
     }
     hipLaunchKernelGGL(k_grid_popc, dim3((unsigned)nb), dim3(256), 0, st, ga);
@@ -781,11 +1008,59 @@ static int spangroup_run(tsdbhip_ctx* ctx, const tsdbhip_sg_desc* d, tsdbhip_sg_
   if (T > 0) {
     const int mode = rate ? MODE_DBL : (!anyf ? MODE_INT : (!anyi ? MODE_DBL : MODE_DUAL));
     ctx->time_reduce = direct;
-    auto run_reduce = [&](bool one_chunk, bool finalize) {
-      const ReduceGeom rg = reduce_geom(T, n_kept, one_chunk);
+    // integer dev is reduced in one span-ordered pass (and, sharded, in rank
+    // order): the reference's sequential Welford before the (long)
+    // truncation (Aggregators.java:196-217) admits no merge of partial
+    // states; EXACT_ORDER does the same for every aggregator
+    const bool seq = exact || (agg == TSDBHIP_AGG_DEV && mode != MODE_DBL);
+    FinalArgs fin;
+    std::memset(&fin, 0, sizeof fin);
+    fin.T = T; fin.n_chunks = 1; fin.grid = gridv; fin.fstar = fstar; fin.rate = rate;
+    fin.out_ts = scratch<int64_t>(ctx, "out_ts", T);
+    fin.out_isint = scratch<uint8_t>(ctx, "out_isint", T);
+    fin.out_bits = scratch<int64_t>(ctx, "out_bits", T);
+    fin.nan_t = &sm->nan_t;
+    // per-t partial fields ([n][T] layout) under scratch names prefix + field
+    auto partials = [&](ReduceArgs& r, const char* pre, uint64_t np) {
+      auto nm = [&](const char* f) { return std::string(pre) + f; };
+      r.p_cnt = scratch<uint32_t>(ctx, nm("cnt").c_str(), np);
+      r.p_flag = scratch<uint8_t>(ctx, nm("flag").c_str(), np);
+      r.p_i = scratch<int64_t>(ctx, nm("i").c_str(), np);
+      r.p_d = scratch<double>(ctx, nm("d").c_str(), np);
+      r.p_dhas = scratch<uint32_t>(ctx, nm("dhas").c_str(), np);
+      r.p_wim = r.p_wiv = r.p_wdm = r.p_wdv = nullptr;
+      if (agg == TSDBHIP_AGG_DEV) {
+        r.p_wim = scratch<double>(ctx, nm("wim").c_str(), np);
+        r.p_wiv = scratch<double>(ctx, nm("wiv").c_str(), np);
+        r.p_wdm = scratch<double>(ctx, nm("wdm").c_str(), np);
+        r.p_wdv = scratch<double>(ctx, nm("wdv").c_str(), np);
+      }
+    };
+    // the fields acc_store writes for (agg, mode), at slot offset `off`
+    struct Fld { void* p; size_t esz; XType t; XOp op; };
+    auto fields = [&](const ReduceArgs& r, uint64_t off) {
+      std::vector<Fld> v;
+      v.push_back({r.p_cnt + off, 4, X_U32, X_SUM});
+      if (mode == MODE_DUAL || agg == 1 || agg == 2) v.push_back({r.p_flag + off, 1, X_U8, X_MAX});
+      if (mode != MODE_DBL && agg != 4)
+        v.push_back({r.p_i + off, 8, agg == 1 ? X_I64 : agg == 2 ? X_I64 : X_U64,
+                     agg == 1 ? X_MIN : agg == 2 ? X_MAX : X_SUM});
+      if (mode != MODE_INT && agg != 4) v.push_back({r.p_d + off, 8, X_F64, X_SUM});
+      if (mode != MODE_INT && (agg == 1 || agg == 2)) v.push_back({r.p_dhas + off, 4, X_U32, X_MAX});
+      if (agg == 4) {
+        if (mode != MODE_DBL) { v.push_back({r.p_wim + off, 8, X_F64, X_SUM}); v.push_back({r.p_wiv + off, 8, X_F64, X_SUM}); }
+        if (mode != MODE_INT) { v.push_back({r.p_wdm + off, 8, X_F64, X_SUM}); v.push_back({r.p_wdv + off, 8, X_F64, X_SUM}); }
+      }
+      return v;
+    };
+    // one reduce launch over this rank's kept spans; `init`: the per-t state
+    // to continue from (one chunk)
+    auto run_reduce = [&](bool one_chunk, bool finalize, const ReduceArgs* init) {
+      const ReduceGeom rg = reduce_geom(T, n_kept, one_chunk || init);
       const uint32_t spc = rg.spc, n_chunks = rg.n_chunks, tpw = rg.tpw, ntg = rg.ntg;
       const uint64_t n_waves = rg.n_waves;
       ReduceArgs r;
+      std::memset(&r, 0, sizeof r);
       r.e_off = eoff; r.e_len = e_len; r.e_ts = e_ts; r.e_val = e_val; r.e_flt = e_flt; r.n_kept = n_kept;
       r.grid = gridv; r.T = T; r.bitmap = bitmap; r.word_rank = word_rank; r.lo = lo;
       r.spans_per_chunk = spc; r.n_chunks = n_chunks; r.tiles_per_wave = tpw; r.n_tile_groups = ntg;
@@ -796,6 +1071,11 @@ static int spangroup_run(tsdbhip_ctx* ctx, const tsdbhip_sg_desc* d, tsdbhip_sg_
       r.chunk_e = nullptr;
       r.fstar = fstar;
       r.exact = exact ? 1 : 0;
+      if (init) {
+        r.i_cnt = init->p_cnt; r.i_flag = init->p_flag; r.i_i = init->p_i; r.i_d = init->p_d;
+        r.i_dhas = init->p_dhas; r.i_wim = init->p_wim; r.i_wiv = init->p_wiv; r.i_wdm = init->p_wdm;
+        r.i_wdv = init->p_wdv;
+      }
       if (direct) {
         uint32_t* ce = scratch<uint32_t>(ctx, "chunk_e", n_chunks, true);
         if (n_kept)
@@ -807,102 +1087,91 @@ static int spangroup_run(tsdbhip_ctx* ctx, const tsdbhip_sg_desc* d, tsdbhip_sg_
       r.st_y = scratch<longlong2>(ctx, "st_y", n_waves * spc);
       r.st_rv = scratch<double>(ctx, "st_rv", n_waves * spc);
       r.st_f = scratch<uint32_t>(ctx, "st_f", n_waves * spc);
-      const uint64_t np = (uint64_t)n_chunks * T;
-      r.p_cnt = scratch<uint32_t>(ctx, "p_cnt", np);
-      r.p_flag = scratch<uint8_t>(ctx, "p_flag", np);
-      r.p_i = scratch<int64_t>(ctx, "p_i", np);
-      r.p_d = scratch<double>(ctx, "p_d", np);
-      r.p_dhas = scratch<uint32_t>(ctx, "p_dhas", np);
-      if (agg == TSDBHIP_AGG_DEV) {
-        r.p_wim = scratch<double>(ctx, "p_wim", np);
-        r.p_wiv = scratch<double>(ctx, "p_wiv", np);
-        r.p_wdm = scratch<double>(ctx, "p_wdm", np);
-        r.p_wdv = scratch<double>(ctx, "p_wdv", np);
-      } else {
-        r.p_wim = r.p_wiv = r.p_wdm = r.p_wdv = nullptr;
-      }
-      FinalArgs f;
-      f.T = T; f.n_chunks = n_chunks; f.grid = gridv; f.fstar = fstar; f.rate = rate;
-      f.out_ts = scratch<int64_t>(ctx, "out_ts", T);
-      f.out_isint = scratch<uint8_t>(ctx, "out_isint", T);
-      f.out_bits = scratch<int64_t>(ctx, "out_bits", T);
-      f.nan_t = &sm->nan_t;
-      f.ambiguous = &sm->ambiguous;
+      partials(r, "p_", (uint64_t)n_chunks * T);
+      FinalArgs f = fin;
+      f.n_chunks = n_chunks;
       const unsigned blocks = (unsigned)((n_waves + 3) / 4);
       dispatch_reduce(ctx, agg, mode, rate, blocks, r, f, n_chunks >= 64, finalize);
-      return std::make_pair(r, f);
+      return r;
     };
     if (!sharded) {
-      run_reduce(exact, true);
+      run_reduce(seq, true, nullptr);
       HIPCHK(hipEventRecord(ctx->ev[5], st));
-      // lazy error index for illegal cells (independent of a re-run below)
-      if (n_kept)
+      if (n_kept)  // lazy error index for illegal cells
         hipLaunchKernelGGL(k_bad_index, dim3(grid_for(n_kept, 256)), dim3(256), 0, st, e_bad, eoff, e_ts, n_kept,
                            (int32_t)rate, hi, bitmap, word_rank, lo, T, &sm->bad_at);
       readback(ctx, &h, sm, sizeof h);  // sync 3
-      if (h.ambiguous && !exact) {
-        Small z = h;
-        z.ambiguous = 0;
-        z.nan_t = ~0ull;
-        std::memcpy(ctx->host_small, &z, sizeof z);
-        HIPCHK(hipMemcpyAsync(sm, ctx->host_small, sizeof z, hipMemcpyHostToDevice, st));
-        run_reduce(true, true);
-        HIPCHK(hipEventRecord(ctx->ev[5], st));
-        readback(ctx, &h, sm, sizeof h);
-      }
     } else {
-      // local partials (chunks combined in order into this rank's slot), one
-      // RCCL allgather per field, then a rank-ordered combine on every rank.
-      auto rf = run_reduce(exact, false);
-      ReduceArgs loc = rf.first;
-      FinalArgs fin = rf.second;
-      const int nr = ctx->nranks;
-      ReduceArgs all = loc;
-      all.p_cnt = scratch<uint32_t>(ctx, "x_cnt", (uint64_t)nr * T);
-      all.p_flag = scratch<uint8_t>(ctx, "x_flag", (uint64_t)nr * T);
-      all.p_i = scratch<int64_t>(ctx, "x_i", (uint64_t)nr * T);
-      all.p_d = scratch<double>(ctx, "x_d", (uint64_t)nr * T);
-      all.p_dhas = scratch<uint32_t>(ctx, "x_dhas", (uint64_t)nr * T);
-      if (agg == TSDBHIP_AGG_DEV) {
-        all.p_wim = scratch<double>(ctx, "x_wim", (uint64_t)nr * T);
-        all.p_wiv = scratch<double>(ctx, "x_wiv", (uint64_t)nr * T);
-        all.p_wdm = scratch<double>(ctx, "x_wdm", (uint64_t)nr * T);
-        all.p_wdv = scratch<double>(ctx, "x_wdv", (uint64_t)nr * T);
-      }
-      ReduceArgs mine = all;
-      const uint64_t off = (uint64_t)ctx->rank * T;
-      mine.p_cnt += off; mine.p_flag += off; mine.p_i += off; mine.p_d += off; mine.p_dhas += off;
-      if (agg == TSDBHIP_AGG_DEV) { mine.p_wim += off; mine.p_wiv += off; mine.p_wdm += off; mine.p_wdv += off; }
-      dispatch_combine(ctx, agg, mode, loc, mine, T, loc.n_chunks);
-      HIPCHK(hipEventRecord(ctx->ev[6], st));
-      NCCLCHK(ncclGroupStart());
-      NCCLCHK(ncclAllGather(mine.p_cnt, all.p_cnt, T, ncclUint32, ctx->comm, st));
-      NCCLCHK(ncclAllGather(mine.p_flag, all.p_flag, T, ncclUint8, ctx->comm, st));
-      if (agg != TSDBHIP_AGG_DEV) {
-        if (mode != MODE_DBL) NCCLCHK(ncclAllGather(mine.p_i, all.p_i, T, ncclInt64, ctx->comm, st));
-        if (mode != MODE_INT) NCCLCHK(ncclAllGather(mine.p_d, all.p_d, T, ncclFloat64, ctx->comm, st));
-        if (mode != MODE_INT && (agg == 1 || agg == 2))
-          NCCLCHK(ncclAllGather(mine.p_dhas, all.p_dhas, T, ncclUint32, ctx->comm, st));
+      const int nr = X->nranks, rk = X->rank;
+      ReduceArgs src;  // per-t partials the finalize merges ([n_src][T])
+      uint32_t n_src = 1;
+      if (seq) {
+        // span order across ranks: rank 0 reduces its spans in one chunk;
+        // rank r continues from rank r-1's per-t state, which reaches it by
+        // broadcast; the last broadcast gives every rank the final state
+        ReduceArgs S;
+        std::memset(&S, 0, sizeof S);
+        partials(S, "s_", T);
+        HIPCHK(hipEventRecord(ctx->ev[6], st));
+        for (int step = 0; step < nr; step++) {
+          ReduceArgs P = S;  // (non-roots: the send side of the broadcast is unused)
+          if (rk == step) P = run_reduce(true, false, step ? &S : nullptr);
+          const std::vector<Fld> fp = fields(P, 0), fs = fields(S, 0);
+          X->group_start(ctx);
+          for (size_t i = 0; i < fp.size(); i++) X->broadcast(ctx, fp[i].p, fs[i].p, T * fp[i].esz, step);
+          X->group_end(ctx);
+        }
+        HIPCHK(hipEventRecord(ctx->ev[7], st));
+        src = S;
       } else {
-        if (mode != MODE_DBL) {
-          NCCLCHK(ncclAllGather(mine.p_wim, all.p_wim, T, ncclFloat64, ctx->comm, st));
-          NCCLCHK(ncclAllGather(mine.p_wiv, all.p_wiv, T, ncclFloat64, ctx->comm, st));
-        }
-        if (mode != MODE_INT) {
-          NCCLCHK(ncclAllGather(mine.p_wdm, all.p_wdm, T, ncclFloat64, ctx->comm, st));
-          NCCLCHK(ncclAllGather(mine.p_wdv, all.p_wdv, T, ncclFloat64, ctx->comm, st));
+        // this rank's chunks combined in order into one slot per t
+        ReduceArgs loc = run_reduce(false, false, nullptr);
+        if (mode == MODE_INT && agg != TSDBHIP_AGG_DEV) {
+          // exact integer partials: one allreduce per field (wrapping u64
+          // sum, i64 min / max, count sum), no ordering needed
+          ReduceArgs mine = loc;
+          partials(mine, "m_", T);
+          dispatch_combine(ctx, agg, mode, loc, mine, T, loc.n_chunks);
+          if (agg == TSDBHIP_AGG_MIN || agg == TSDBHIP_AGG_MAX)
+            hipLaunchKernelGGL(k_neutral_minmax, dim3(grid_for(T, 256)), dim3(256), 0, st, mine.p_cnt, mine.p_i, T,
+                               agg == TSDBHIP_AGG_MIN ? INT64_MAX : INT64_MIN);
+          HIPCHK(hipEventRecord(ctx->ev[6], st));
+          X->group_start(ctx);
+          for (const Fld& f : fields(mine, 0)) X->allreduce(ctx, f.p, T, f.t, f.op);
+          X->group_end(ctx);
+          HIPCHK(hipEventRecord(ctx->ev[7], st));
+          src = mine;
+        } else {
+          // doubles (sums / Welford states depend on the order): every
+          // rank's slot gathered, merged in rank order on every rank
+          ReduceArgs all = loc;
+          partials(all, "x_", (uint64_t)nr * T);
+          ReduceArgs mine = all;
+          const uint64_t off = (uint64_t)rk * T;
+          mine.p_cnt += off; mine.p_flag += off; mine.p_i += off; mine.p_d += off; mine.p_dhas += off;
+          if (agg == TSDBHIP_AGG_DEV) { mine.p_wim += off; mine.p_wiv += off; mine.p_wdm += off; mine.p_wdv += off; }
+          dispatch_combine(ctx, agg, mode, loc, mine, T, loc.n_chunks);
+          HIPCHK(hipEventRecord(ctx->ev[6], st));
+          const std::vector<Fld> fm = fields(mine, 0), fa = fields(all, 0);
+          X->group_start(ctx);
+          for (size_t i = 0; i < fm.size(); i++) X->allgather(ctx, fm[i].p, fa[i].p, T * fm[i].esz);
+          X->group_end(ctx);
+          HIPCHK(hipEventRecord(ctx->ev[7], st));
+          src = all;
+          n_src = (uint32_t)nr;
         }
       }
-      NCCLCHK(ncclGroupEnd());
-      HIPCHK(hipEventRecord(ctx->ev[7], st));
-      fin.n_chunks = (uint32_t)nr;
-      all.n_chunks = (uint32_t)nr;
-      dispatch_final(ctx, agg, mode, rate, all, fin);
+      FinalArgs f = fin;
+      f.n_chunks = n_src;
+      src.n_chunks = n_src;
+      dispatch_final(ctx, agg, mode, rate, src, f);
       HIPCHK(hipEventRecord(ctx->ev[5], st));
-      // lazy error index for illegal cells
+      // lazy error index for illegal cells: a grid rank of the global grid,
+      // the smallest over the ranks
       if (n_kept)
         hipLaunchKernelGGL(k_bad_index, dim3(grid_for(n_kept, 256)), dim3(256), 0, st, e_bad, eoff, e_ts, n_kept,
                            (int32_t)rate, hi, bitmap, word_rank, lo, T, &sm->bad_at);
+      X->allreduce(ctx, &sm->bad_at, 1, X_U64, X_MIN);
       readback(ctx, &h, sm, sizeof h);
       tm.exchange_ms = ev_ms(ctx->ev[6], ctx->ev[7]);
     }
@@ -911,6 +1180,7 @@ static int spangroup_run(tsdbhip_ctx* ctx, const tsdbhip_sg_desc* d, tsdbhip_sg_
     if (n_kept)
       hipLaunchKernelGGL(k_bad_index, dim3(grid_for(n_kept, 256)), dim3(256), 0, st, e_bad, eoff, e_ts, n_kept,
                          (int32_t)rate, hi, bitmap, word_rank, lo, T, &sm->bad_at);
+    if (sharded) X->allreduce(ctx, &sm->bad_at, 1, X_U64, X_MIN);
     readback(ctx, &h, sm, sizeof h);
   }
   HIPCHK(hipStreamSynchronize(st));
@@ -936,11 +1206,13 @@ static int spangroup_run(tsdbhip_ctx* ctx, const tsdbhip_sg_desc* d, tsdbhip_sg_
     code = TSDBHIP_E_NAN_INF;
   }
   if (err_at >= 0) n_ok = (uint64_t)err_at;
-  if (n_ok > out->capacity) {
+  if (n_ok > out->capacity && ctx->want_output) {
     out->err_code = TSDBHIP_E_CAPACITY;
     return TSDBHIP_E_CAPACITY;
   }
-  if (n_ok && n_ok * 17 <= (256u << 10)) {
+  if (!ctx->want_output) {
+    // (a non-zero rank of an in-process sharded call: rank 0 returns the output)
+  } else if (n_ok && n_ok * 17 <= (256u << 10)) {
     // small results: three async copies into pinned staging, one sync (a
     // copy into pageable memory would synchronise once per array)
     uint8_t* hb = (uint8_t*)host_buf(ctx, n_ok * 17);
@@ -966,6 +1238,183 @@ static int spangroup_run(tsdbhip_ctx* ctx, const tsdbhip_sg_desc* d, tsdbhip_sg_
   return code;
 }
 
+// One call on a plain context: a slot of its pool; x = the exchange of a
+// sharded call (null: unsharded).
+static int run_plain(tsdbhip_ctx* c, const tsdbhip_sg_desc* desc, tsdbhip_sg_out* out, Xchg* x, bool want_output) {
+  try {
+    Lease L(c);
+    Slot* ctx = L.s;
+    ctx->x = x;
+    ctx->want_output = want_output;
+    try {
+      int rc = spangroup_run(ctx, desc, out);
+      if (rc) set_error(ctx, "spangroup_run: error %d at output %lld", rc, (long long)out->err_index);
+      return rc;
+    } catch (Fail& f) {
+      out->err_code = f.code;
+      if (f.code != TSDBHIP_E_HIP && f.code != TSDBHIP_E_RCCL) {
+        out->err_index = 0;
+        set_error(ctx, "spangroup_run: error %d", f.code);
+      }
+      hipStreamSynchronize(ctx->stream);
+      return f.code;
+    }
+  } catch (Fail& f) {  // (no slot)
+    out->err_code = f.code;
+    return f.code;
+  }
+}
+
+// ---- in-process sharding (tsdbhip_open_devices) ----
+// Rank r of a multi-device context takes the contiguous span range
+// [b[r], b[r+1]) of the group (span order kept), balanced by
+// cell count for host descs and by span count for device descs, as a desc of
+// its own (rows and bytes rebased to the shard).
+struct ShardDesc {
+  tsdbhip_sg_desc d;
+  std::vector<uint64_t> srs, qoff, voff;  // host descs: the rebased arrays
+};
+
+static void plan_shards(tsdbhip_ctx* mc, const tsdbhip_sg_desc* desc, std::vector<ShardDesc>& sh) {
+  Multi* m = mc->multi;
+  Slot* ctx = nullptr;  // (for set_error in the checks)
+  const int n = m->n;
+  const uint32_t S = desc->n_spans;
+  sh.assign(n, ShardDesc());
+  std::vector<uint32_t> b(n + 1);
+  const bool dev = (desc->flags & TSDBHIP_DESC_DEVICE) != 0;
+  std::vector<uint64_t> srs_h;
+  const uint64_t* srs = desc->span_row_start;
+  if (dev) {  // the span -> row index, read once
+    srs_h.resize((size_t)S + 1);
+    HIPCHK(hipMemcpy(srs_h.data(), desc->span_row_start, 8ull * (S + 1), hipMemcpyDeviceToHost));
+    srs = srs_h.data();
+    for (int r = 0; r <= n; r++) b[r] = (uint32_t)((uint64_t)S * r / n);
+  } else {  // balanced by points
+    std::vector<uint64_t> pre((size_t)S + 1, 0);
+    for (uint32_t s = 0; s < S; s++) {
+      uint64_t c = 0;
+      for (uint64_t r = srs[s]; r < srs[s + 1]; r++) c += desc->row_ncells[r];
+      pre[s + 1] = pre[s] + c;
+    }
+    b[0] = 0;
+    b[n] = S;
+    for (int r = 1; r < n; r++) {
+      const uint64_t want = pre[S] * r / n;
+      b[r] = (uint32_t)(std::lower_bound(pre.begin(), pre.end(), want) - pre.begin());
+      b[r] = std::max(b[r - 1], std::min(b[r], S));
+    }
+  }
+  for (int r = 0; r < n; r++) {
+    ShardDesc& x = sh[r];
+    const uint32_t s0 = b[r], s1 = b[r + 1];
+    const uint64_t r0 = srs[s0], r1 = srs[s1];
+    x.d = *desc;
+    x.d.n_spans = s1 - s0;
+    x.d.n_rows = r1 - r0;
+    x.srs.resize((size_t)(s1 - s0) + 1);
+    for (uint32_t s = s0; s <= s1; s++) x.srs[s - s0] = srs[s] - r0;
+    x.d.row_base = desc->row_base + r0;
+    x.d.row_ncells = desc->row_ncells + r0;
+    x.d.row_val_len = desc->row_val_len + r0;
+    if (dev) {
+      // (row offsets stay absolute into the shared byte arrays; only the
+      // span -> row index moves, uploaded to rank r's device)
+      std::string key = "shard_srs";
+      tsdbhip_ctx* c = m->members[r];
+      Buf& bb = c->owned[key];
+      const size_t bytes = 8 * x.srs.size() + 64;
+      if (bb.n < bytes) {
+        HIPCHK(hipSetDevice(c->device));
+        if (bb.p) HIPCHK(hipFree(bb.p));
+        bb.p = nullptr;
+        HIPCHK(hipMalloc(&bb.p, bytes));
+        bb.n = bytes;
+      }
+      HIPCHK(hipMemcpy(bb.p, x.srs.data(), 8 * x.srs.size(), hipMemcpyHostToDevice));
+      x.d.span_row_start = (const uint64_t*)bb.p;
+      x.d.row_qual_off = desc->row_qual_off + r0;
+      x.d.row_val_off = desc->row_val_off + r0;
+      continue;
+    }
+    // host desc: the shard's byte ranges only (16-B aligned starts keep the
+    // packer's row alignment), offsets rebased
+    uint64_t qmin = ~0ull, qmax = 0, vmin = ~0ull, vmax = 0;
+    for (uint64_t rr = r0; rr < r1; rr++) {
+      qmin = std::min<uint64_t>(qmin, desc->row_qual_off[rr]);
+      qmax = std::max<uint64_t>(qmax, desc->row_qual_off[rr] + 2ull * desc->row_ncells[rr]);
+      vmin = std::min<uint64_t>(vmin, desc->row_val_off[rr]);
+      vmax = std::max<uint64_t>(vmax, desc->row_val_off[rr] + desc->row_val_len[rr]);
+    }
+    if (r1 == r0) qmin = qmax = vmin = vmax = 0;
+    qmin &= ~15ull;
+    vmin &= ~15ull;
+    x.qoff.resize(r1 - r0);
+    x.voff.resize(r1 - r0);
+    for (uint64_t rr = r0; rr < r1; rr++) {
+      x.qoff[rr - r0] = desc->row_qual_off[rr] - qmin;
+      x.voff[rr - r0] = desc->row_val_off[rr] - vmin;
+    }
+    x.d.span_row_start = x.srs.data();
+    x.d.row_qual_off = x.qoff.data();
+    x.d.row_val_off = x.voff.data();
+    x.d.qual_bytes = desc->qual_bytes + qmin;
+    x.d.qual_nbytes = std::min<uint64_t>(desc->qual_nbytes, std::max<uint64_t>(qmax, qmin + 16)) - qmin;
+    x.d.val_bytes = desc->val_bytes + vmin;
+    x.d.val_nbytes = std::min<uint64_t>(desc->val_nbytes, std::max<uint64_t>(vmax, vmin + 16)) - vmin;
+  }
+}
+
+static int multi_run(tsdbhip_ctx* mc, const tsdbhip_sg_desc* desc, tsdbhip_sg_out* out) {
+  Multi* m = mc->multi;
+  std::lock_guard<std::mutex> lk(m->call_mu);
+  const int n = m->n;
+  std::vector<ShardDesc> sh;
+  try {
+    plan_shards(mc, desc, sh);
+  } catch (Fail& f) {
+    out->err_code = f.code;
+    return f.code;
+  }
+  std::vector<tsdbhip_sg_out> outs(n);
+  std::vector<int> rcs(n, 0);
+  std::vector<std::string> errs(n);
+  for (int r = 0; r < n; r++) {
+    sh[r].d.flags |= TSDBHIP_SHARDED;
+    outs[r] = tsdbhip_sg_out();
+  }
+  outs[0] = *out;
+  auto rank_main = [&](int r) {
+    rcs[r] = run_plain(m->members[r], &sh[r].d, &outs[r], m->xs[r].get(), r == 0);
+    if (rcs[r]) {
+      errs[r] = g_thread_err;
+      if (!m->rccl) m->local.abort();  // peers waiting at a barrier give up
+    }
+  };
+  std::vector<std::thread> th;
+  for (int r = 1; r < n; r++) th.emplace_back(rank_main, r);
+  rank_main(0);
+  for (auto& t : th) t.join();
+  if (!m->rccl) m->local.reset();
+  *out = outs[0];
+  g_last_ctx = mc;
+  g_last_timing = mc->multi->members[0]->last;
+  {
+    std::lock_guard<std::mutex> l2(mc->mu);
+    mc->last = g_last_timing;
+  }
+  int rc = rcs[0];
+  int first = -1;
+  for (int r = 0; r < n; r++)
+    if (rcs[r] && first < 0) first = r;
+  if (!rc && first >= 0) rc = rcs[first];
+  if (first >= 0) {
+    g_thread_err = "rank " + std::to_string(first) + ": " + errs[first];
+    if (rc != rcs[0]) out->err_code = rc;
+  }
+  return rc;
+}
+
 extern "C" int tsdbhip_spangroup_run(tsdbhip_ctx* ctx, const tsdbhip_sg_desc* desc, tsdbhip_sg_out* out) {
   if (!ctx || !desc || !out) return TSDBHIP_E_INVALID_ARG;
   if (desc->agg > 4 || (desc->ds_interval > 0 && desc->ds_agg > 4) || desc->ds_interval < 0 ||
@@ -974,21 +1423,12 @@ extern "C" int tsdbhip_spangroup_run(tsdbhip_ctx* ctx, const tsdbhip_sg_desc* de
     out->err_code = TSDBHIP_E_INVALID_ARG;
     return TSDBHIP_E_INVALID_ARG;
   }
-  std::lock_guard<std::mutex> lock(ctx->mu);
-  try {
-    HIPCHK(hipSetDevice(ctx->device));
-    int rc = spangroup_run(ctx, desc, out);
-    if (rc) set_error(ctx, "spangroup_run: error %d at output %lld", rc, (long long)out->err_index);
-    return rc;
-  } catch (Fail& f) {
-    out->err_code = f.code;
-    if (f.code != TSDBHIP_E_HIP && f.code != TSDBHIP_E_RCCL) {
-      out->err_index = 0;
-      set_error(ctx, "spangroup_run: error %d", f.code);
-    }
-    hipStreamSynchronize(ctx->stream);
-    return f.code;
+  if (ctx->multi) return multi_run(ctx, desc, out);
+  if ((desc->flags & TSDBHIP_SHARDED) && ctx->rccl) {
+    std::lock_guard<std::mutex> lk(ctx->comm_mu);  // collectives in the same order on every rank
+    return run_plain(ctx, desc, out, ctx->rccl, true);
   }
+  return run_plain(ctx, desc, out, nullptr, true);
 }
 
 #include "batch.hip"
@@ -1003,13 +1443,15 @@ static std::string synth_key(const tsdbhip_sg_desc* d, const char* f) {
   return b;
 }
 
-extern "C" int tsdbhip_synth_generate(tsdbhip_ctx* ctx, const tsdbhip_synth_params* p, tsdbhip_sg_desc* d) {
-  if (!ctx || !p || !d || p->n_spans == 0 || p->n_points == 0 || p->step == 0 || 3600 % p->step ||
+
+extern "C" int tsdbhip_synth_generate(tsdbhip_ctx* c, const tsdbhip_synth_params* p, tsdbhip_sg_desc* d) {
+  if (!c || !p || !d || p->n_spans == 0 || p->n_points == 0 || p->step == 0 || 3600 % p->step ||
       p->t0 % 3600 || p->kind > 2)
     return TSDBHIP_E_INVALID_ARG;
-  std::lock_guard<std::mutex> lock(ctx->mu);
+  c = plain_of(c);
   try {
-    HIPCHK(hipSetDevice(ctx->device));
+    Lease L(c);
+    Slot* ctx = L.s;
     SynthArgs a;
     a.seed = p->seed; a.n_spans = p->n_spans; a.n_points = p->n_points; a.t0 = p->t0; a.step = p->step;
     a.kind = p->kind;
@@ -1023,13 +1465,24 @@ extern "C" int tsdbhip_synth_generate(tsdbhip_ctx* ctx, const tsdbhip_synth_para
     const uint64_t n_rows = (uint64_t)p->n_spans * a.rps;
     auto al = [&](const char* f, size_t bytes) -> void* {
       std::string k = synth_key(d, f);
-      Buf& b = ctx->bufs[k];
-      if (b.p) HIPCHK(hipFree(b.p));
-      b.p = nullptr;
-      HIPCHK(hipMalloc(&b.p, bytes + 64));
-      b.n = bytes + 64;
-      HIPCHK(hipMemsetAsync(b.p, 0, bytes + 64, ctx->stream));
-      return b.p;
+      void* q = nullptr;
+      {
+        std::lock_guard<std::mutex> lk(c->mu);
+        auto it = c->owned.find(k);
+        if (it != c->owned.end()) {
+          q = it->second.p;
+          c->owned.erase(it);
+        }
+      }
+      if (q) HIPCHK(hipFree(q));
+      q = nullptr;
+      HIPCHK(hipMalloc(&q, bytes + 64));
+      {
+        std::lock_guard<std::mutex> lk(c->mu);
+        c->owned[k] = Buf{q, bytes + 64};
+      }
+      HIPCHK(hipMemsetAsync(q, 0, bytes + 64, ctx->stream));
+      return q;
     };
     a.span_row_start = (uint64_t*)al("srs", 8ull * (p->n_spans + 1));
     a.row_base = (uint32_t*)al("base", 4ull * n_rows);
@@ -1063,28 +1516,30 @@ extern "C" int tsdbhip_synth_generate(tsdbhip_ctx* ctx, const tsdbhip_synth_para
   return TSDBHIP_OK;
 }
 
-extern "C" int tsdbhip_synth_free(tsdbhip_ctx* ctx, tsdbhip_sg_desc* d) {
-  if (!ctx || !d) return TSDBHIP_E_INVALID_ARG;
-  std::lock_guard<std::mutex> lock(ctx->mu);
-  hipSetDevice(ctx->device);
-  hipStreamSynchronize(ctx->stream);
+extern "C" int tsdbhip_synth_free(tsdbhip_ctx* c, tsdbhip_sg_desc* d) {
+  if (!c || !d) return TSDBHIP_E_INVALID_ARG;
+  c = plain_of(c);
+  hipSetDevice(c->device);
+  hipDeviceSynchronize();  // (no call may still read the dataset)
+  std::lock_guard<std::mutex> lock(c->mu);
   for (const char* f : {"srs", "base", "ncells", "qoff", "voff", "vlen", "qual", "val"}) {
-    auto it = ctx->bufs.find(synth_key(d, f));
-    if (it != ctx->bufs.end()) {
+    auto it = c->owned.find(synth_key(d, f));
+    if (it != c->owned.end()) {
       if (it->second.p) hipFree(it->second.p);
-      ctx->bufs.erase(it);
+      c->owned.erase(it);
     }
   }
   return TSDBHIP_OK;
 }
 
-extern "C" int tsdbhip_desc_download(tsdbhip_ctx* ctx, const tsdbhip_sg_desc* d, uint64_t* srs, uint32_t* base,
+extern "C" int tsdbhip_desc_download(tsdbhip_ctx* c, const tsdbhip_sg_desc* d, uint64_t* srs, uint32_t* base,
                                      uint32_t* ncells, uint64_t* qoff, uint64_t* voff, uint32_t* vlen,
                                      uint8_t* qual, uint8_t* val) {
-  if (!ctx || !d || !(d->flags & TSDBHIP_DESC_DEVICE)) return TSDBHIP_E_INVALID_ARG;
-  std::lock_guard<std::mutex> lock(ctx->mu);
+  if (!c || !d || !(d->flags & TSDBHIP_DESC_DEVICE)) return TSDBHIP_E_INVALID_ARG;
+  c = plain_of(c);
   try {
-    HIPCHK(hipSetDevice(ctx->device));
+    Lease L(c);
+    Slot* ctx = L.s;
     const uint64_t R = d->n_rows;
     HIPCHK(hipMemcpy(srs, d->span_row_start, 8ull * (d->n_spans + 1), hipMemcpyDeviceToHost));
     HIPCHK(hipMemcpy(base, d->row_base, 4 * R, hipMemcpyDeviceToHost));
@@ -1104,9 +1559,18 @@ extern "C" int tsdbhip_desc_download(tsdbhip_ctx* ctx, const tsdbhip_sg_desc* d,
 // CompactionQueue.compact (CompactionQueue.java:243-743) for a batch of rows:
 // k_compact_tiles (16-row LDS tiles, wave per row) then k_compact_complex for the rows holding a
 // compacted cell (LDS cell table, or global scratch for very long rows).
-extern "C" int tsdbhip_compact_rows(tsdbhip_ctx* ctx, const tsdbhip_rows_desc* d, tsdbhip_rows_out* out) {
-  if (!ctx || !d || !out) return TSDBHIP_E_INVALID_ARG;
-  std::lock_guard<std::mutex> lock(ctx->mu);
+static int compact_rows(Slot* ctx, const tsdbhip_rows_desc* d, tsdbhip_rows_out* out);
+extern "C" int tsdbhip_compact_rows(tsdbhip_ctx* c, const tsdbhip_rows_desc* d, tsdbhip_rows_out* out) {
+  if (!c || !d || !out) return TSDBHIP_E_INVALID_ARG;
+  try {
+    Lease L(plain_of(c));
+    return compact_rows(L.s, d, out);
+  } catch (Fail& f) {
+    return f.code;
+  }
+}
+
+static int compact_rows(Slot* ctx, const tsdbhip_rows_desc* d, tsdbhip_rows_out* out) {
   out->qual_used = out->val_used = out->n_complex = 0;
   const uint64_t R = d->n_rows;
   if (R == 0) return TSDBHIP_OK;
@@ -1118,7 +1582,6 @@ extern "C" int tsdbhip_compact_rows(tsdbhip_ctx* ctx, const tsdbhip_rows_desc* d
     return TSDBHIP_E_INVALID_ARG;
   }
   try {
-    HIPCHK(hipSetDevice(ctx->device));
     const bool dev = (d->flags & TSDBHIP_DESC_DEVICE) != 0;
     uint64_t ext[4];  // row_qual_off[0], [R], row_val_off[0], [R]
     if (dev) {
@@ -1240,13 +1703,13 @@ extern "C" int tsdbhip_compact_rows(tsdbhip_ctx* ctx, const tsdbhip_rows_desc* d
 // mode 0: streaming read of a device desc's row bytes with k_ds_spans'
 // geometry; mode 1: device-to-device copy of its value bytes. Returns the
 // kernel time (HIP events) and the bytes it moved.
-extern "C" int tsdbhip_bw_probe(tsdbhip_ctx* ctx, const tsdbhip_sg_desc* d, int32_t mode, uint32_t width,
+extern "C" int tsdbhip_bw_probe(tsdbhip_ctx* c, const tsdbhip_sg_desc* d, int32_t mode, uint32_t width,
                                 float* ms, uint64_t* bytes) {
-  if (!ctx || !d || !ms || !bytes || !(d->flags & TSDBHIP_DESC_DEVICE) || (width != 4 && width != 8))
+  if (!c || !d || !ms || !bytes || !(d->flags & TSDBHIP_DESC_DEVICE) || (width != 4 && width != 8))
     return TSDBHIP_E_INVALID_ARG;
-  std::lock_guard<std::mutex> lock(ctx->mu);
   try {
-    HIPCHK(hipSetDevice(ctx->device));
+    Lease L(plain_of(c));
+    Slot* ctx = L.s;
     hipStream_t st = ctx->stream;
     uint32_t* sink = scratch<uint32_t>(ctx, "probe_sink", 1);
     HIPCHK(hipEventRecord(ctx->ev[0], st));

@@ -20,7 +20,7 @@
 
 
 template <int AGG, int MODE, bool RATE>
-static void launch_seg(tsdbhip_ctx* ctx, const ReduceArgs& r0, const FinalArgs& f0, const SegReduce& sr,
+static void launch_seg(Slot* ctx, const ReduceArgs& r0, const FinalArgs& f0, const SegReduce& sr,
                        uint64_t waves, const SegGroup* sg, const uint64_t* goff, uint32_t G, uint64_t T_all,
                        GroupDev* gd) {
   if (waves && r0.d_info)  // span chunks without E spans (k_reduce's DONLY instantiation)
@@ -36,7 +36,7 @@ static void launch_seg(tsdbhip_ctx* ctx, const ReduceArgs& r0, const FinalArgs& 
 
 struct LaunchSeg {
   template <int AGG, typename... A>
-  static void run(tsdbhip_ctx* ctx, int mode, bool rate, A&&... a) {
+  static void run(Slot* ctx, int mode, bool rate, A&&... a) {
     if (rate) return launch_seg<AGG, MODE_DBL, true>(ctx, a...);
     if (mode == MODE_INT) return launch_seg<AGG, MODE_INT, false>(ctx, a...);
     if (mode == MODE_DBL) return launch_seg<AGG, MODE_DBL, false>(ctx, a...);
@@ -45,7 +45,7 @@ struct LaunchSeg {
 };
 
 template <typename T>
-static T* upload(tsdbhip_ctx* ctx, const char* name, const std::vector<T>& v) {
+static T* upload(Slot* ctx, const char* name, const std::vector<T>& v) {
   T* d = scratch<T>(ctx, name, v.size());
   if (v.empty()) return d;
   void* h = host_buf(ctx, v.size() * sizeof(T));
@@ -57,7 +57,7 @@ static T* upload(tsdbhip_ctx* ctx, const char* name, const std::vector<T>& v) {
 
 // One group through the single-group path, with the error mapping of the
 // tsdbhip_spangroup_run wrapper (HIP/RCCL failures propagate).
-static int run_group_alone(tsdbhip_ctx* ctx, const tsdbhip_sg_desc* sub, tsdbhip_sg_out* out) {
+static int run_group_alone(Slot* ctx, const tsdbhip_sg_desc* sub, tsdbhip_sg_out* out) {
   try {
     return spangroup_run(ctx, sub, out);
   } catch (Fail& f) {
@@ -70,7 +70,7 @@ static int run_group_alone(tsdbhip_ctx* ctx, const tsdbhip_sg_desc* sub, tsdbhip
 }
 
 // Groups one by one over the already staged (device) inputs.
-static int batch_one_by_one(tsdbhip_ctx* ctx, const tsdbhip_sg_desc& dd, uint32_t G, const uint32_t* gss,
+static int batch_one_by_one(Slot* ctx, const tsdbhip_sg_desc& dd, uint32_t G, const uint32_t* gss,
                             tsdbhip_sg_out* outs) {
   int first = TSDBHIP_OK;
   for (uint32_t g = 0; g < G; g++) {
@@ -83,7 +83,7 @@ static int batch_one_by_one(tsdbhip_ctx* ctx, const tsdbhip_sg_desc& dd, uint32_
   return first;
 }
 
-static int spangroup_run_batch(tsdbhip_ctx* ctx, const tsdbhip_sg_desc* d, uint32_t G, const uint32_t* gss,
+static int spangroup_run_batch(Slot* ctx, const tsdbhip_sg_desc* d, uint32_t G, const uint32_t* gss,
                                tsdbhip_sg_out* outs) {
   const bool dev = (d->flags & TSDBHIP_DESC_DEVICE) != 0;
   const bool exact = (d->flags & TSDBHIP_EXACT_ORDER) != 0;
@@ -406,7 +406,10 @@ static int spangroup_run_batch(tsdbhip_ctx* ctx, const tsdbhip_sg_desc* d, uint3
     if (!x.T) continue;
     // the batch shares the single-group wave budget in proportion to spans
     const double share = n_kept ? (double)x.nk / n_kept : 1.0;
-    const ReduceGeom rg = reduce_geom(x.T, x.nk, exact, std::max<uint64_t>(64, (uint64_t)(16384 * share)),
+    // integer dev in one span-ordered pass: the reference's sequential
+    // Welford, bit-exact after the (long) truncation (Aggregators.java:196-217)
+    const bool seq = exact || (agg == TSDBHIP_AGG_DEV && x.mode != MODE_DBL);
+    const ReduceGeom rg = reduce_geom(x.T, x.nk, seq, std::max<uint64_t>(64, (uint64_t)(16384 * share)),
                                       std::max<uint64_t>(16, (uint64_t)(2048 * share)));
     x.spc = rg.spc; x.n_chunks = rg.n_chunks; x.tpw = rg.tpw; x.ntg = rg.ntg;
     x.poff = poff;
@@ -470,51 +473,11 @@ static int spangroup_run_batch(tsdbhip_ctx* ctx, const tsdbhip_sg_desc* d, uint3
     launch_agg<LaunchSeg>(agg, ctx, m, rate, r0, f0, sr, wstart[m].back(), sg_d, goff_d, G, T_all, gd);
   }
   if (direct) HIPCHK(hipEventRecord(ctx->ev[9], st));  // (finalize included: small next to the reduce)
-  // ambiguous-int-dev reruns: one group, one chunk (k_reduce + k_finalize_seq)
-  auto reduce_group = [&](uint32_t g) {
-    const uint64_t T = gh[g].T, go = gh[g].goff, k0 = gs[g].k0;
-    const uint32_t nk = (uint32_t)gs[g].nk;
-    const ReduceGeom rg = reduce_geom(T, nk, true);
-    ReduceArgs r = r0;
-    alloc_reduce(r, rg.n_waves * rg.spc, (uint64_t)rg.n_chunks * T);
-    r.e_off = eoff + k0; r.e_len = e_len + k0; r.n_kept = nk; r.kept = kept + k0;
-    r.grid = gridv + go; r.T = T; r.bitmap = bitmap + gwb[g]; r.word_rank = word_rank + gwb[g]; r.lo = glo[g];
-    r.spans_per_chunk = rg.spc; r.n_chunks = rg.n_chunks; r.tiles_per_wave = rg.tpw; r.n_tile_groups = rg.ntg;
-    r.fstar = gh[g].fstar;
-    if (r.d_info) {  // one chunk, taken by the E instantiation (mixed chunks are its own)
-      r.d_info += k0; r.d_n += k0; r.d_ga += k0; r.d_voff += k0; r.d_x0 += k0; r.d_step += k0;
-      r.d_c0 += k0; r.d_r0 += k0;
-      uint32_t* one = scratch<uint32_t>(ctx, "chunk_e1", 1);
-      HIPCHK(hipMemsetAsync(one, 0xff, 4, st));
-      r.chunk_e = one;
-    }
-    FinalArgs f = f0;
-    f.T = T; f.n_chunks = rg.n_chunks; f.grid = gridv + go; f.fstar = gh[g].fstar;
-    f.out_ts = out_ts + go; f.out_isint = out_isint + go; f.out_bits = out_bits + go;
-    f.nan_t = &gd[g].nan_t;
-    f.ambiguous = &gd[g].ambiguous;
-    dispatch_reduce(ctx, agg, mode_of(g), rate, (unsigned)((rg.n_waves + 3) / 4), r, f, false, true);
-  };
   if (n_kept)
     hipLaunchKernelGGL(k_bad_index_seg, dim3(grid_for(n_kept, 256)), dim3(256), 0, st, e_bad, eoff, e_ts, n_kept,
                        (int32_t)rate, kgrp, q, bitmap, word_rank, gd);
   HIPCHK(hipEventRecord(ctx->ev[5], st));
   read_groups();  // sync 4
-  if (!exact) {  // int dev close to an integer after a Chan merge: the group in span order
-    bool any = false;
-    for (uint32_t g = 0; g < G; g++) {
-      if (!gh[g].ambiguous) continue;
-      any = true;
-      GroupDev z = gh[g];
-      z.ambiguous = 0;
-      z.nan_t = ~0ull;
-      std::memcpy(ctx->host_small, &z, sizeof z);
-      HIPCHK(hipMemcpyAsync(&gd[g], ctx->host_small, sizeof z, hipMemcpyHostToDevice, st));
-      HIPCHK(hipStreamSynchronize(st));
-      reduce_group(g);
-    }
-    if (any) read_groups();
-  }
   HIPCHK(hipStreamSynchronize(st));
   tm.decode_ms = ev_ms(ctx->ev[1], ctx->ev[2]);
   if (ctx->hot_kernel) tm.hot_ms = ev_ms(ctx->ev[8], ctx->ev[9]);
@@ -572,30 +535,35 @@ static int spangroup_run_batch(tsdbhip_ctx* ctx, const tsdbhip_sg_desc* d, uint3
   return first;
 }
 
-extern "C" int tsdbhip_spangroup_run_batch(tsdbhip_ctx* ctx, const tsdbhip_sg_desc* desc, uint32_t n_groups,
+extern "C" int tsdbhip_spangroup_run_batch(tsdbhip_ctx* c, const tsdbhip_sg_desc* desc, uint32_t n_groups,
                                            const uint32_t* group_span_start, tsdbhip_sg_out* outs) {
-  if (!ctx || !desc || !outs || !group_span_start || n_groups == 0) return TSDBHIP_E_INVALID_ARG;
+  if (!c || !desc || !outs || !group_span_start || n_groups == 0) return TSDBHIP_E_INVALID_ARG;
   if (desc->agg > 4 || (desc->ds_interval > 0 && desc->ds_agg > 4) || desc->ds_interval < 0 ||
       desc->start_time < 0 || desc->end_time < 0 || (desc->flags & TSDBHIP_SHARDED) ||
       group_span_start[0] != 0 || group_span_start[n_groups] != desc->n_spans) {
-    set_error(ctx, "invalid SpanGroup batch arguments");
+    set_error(c, "invalid SpanGroup batch arguments");
     return TSDBHIP_E_INVALID_ARG;
   }
   for (uint32_t g = 0; g < n_groups; g++)
     if (group_span_start[g + 1] < group_span_start[g]) {
-      set_error(ctx, "group_span_start not non-decreasing at group %u", g);
+      set_error(c, "group_span_start not non-decreasing at group %u", g);
       return TSDBHIP_E_INVALID_ARG;
     }
-  std::lock_guard<std::mutex> lock(ctx->mu);
   try {
-    HIPCHK(hipSetDevice(ctx->device));
-    const int rc = spangroup_run_batch(ctx, desc, n_groups, group_span_start, outs);
-    if (rc) set_error(ctx, "spangroup_run_batch: first failing group error %d", rc);
-    return rc;
+    Lease L(plain_of(c));
+    Slot* ctx = L.s;
+    try {
+      const int rc = spangroup_run_batch(ctx, desc, n_groups, group_span_start, outs);
+      if (rc) set_error(ctx, "spangroup_run_batch: first failing group error %d", rc);
+      return rc;
+    } catch (Fail& f) {
+      for (uint32_t g = 0; g < n_groups; g++) outs[g].err_code = f.code;
+      set_error(ctx, "spangroup_run_batch: error %d", f.code);
+      hipStreamSynchronize(ctx->stream);
+      return f.code;
+    }
   } catch (Fail& f) {
     for (uint32_t g = 0; g < n_groups; g++) outs[g].err_code = f.code;
-    set_error(ctx, "spangroup_run_batch: error %d", f.code);
-    hipStreamSynchronize(ctx->stream);
     return f.code;
   }
 }

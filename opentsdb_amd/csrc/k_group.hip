@@ -23,7 +23,7 @@ struct GroupDev {
   uint64_t goff;              // first grid index of the group
   uint64_t T;                 // |G_g|
   uint32_t gfl;               // bit0: some E point is a float, bit1: some is an int
-  uint32_t ambiguous;         // finalize: int dev near an integer after a Chan merge
+  uint32_t reserved;
   uint64_t pad[2];
 };
 
@@ -351,7 +351,6 @@ __global__ void __launch_bounds__(256) k_finalize_seg(ReduceArgs r0, FinalArgs f
   f.out_isint += G.goff;
   f.out_bits += G.goff;
   f.nan_t = &gd[lo].nan_t;
-  f.ambiguous = &gd[lo].ambiguous;
   const uint64_t g = t - G.goff;
   Acc a;
   acc_load<AGG, MODE>(r, g, a);

@@ -61,6 +61,19 @@ struct ReduceArgs {
   double* p_wdm;
   double* p_wdv;
   uint32_t* p_dhas;     // double min/max: a non-NaN value was seen
+  // initial per-t state ([T] slot layout, null: none): the reduction
+  // continues from it (the sequential pass over the ranks of a sharded
+  // group: rank r starts from rank r-1's state, so values are pushed in span
+  // order across ranks)
+  const uint32_t* i_cnt;
+  const uint8_t* i_flag;
+  const int64_t* i_i;
+  const double* i_d;
+  const uint32_t* i_dhas;
+  const double* i_wim;
+  const double* i_wiv;
+  const double* i_wdm;
+  const double* i_wdv;
   const uint32_t* chunk_e;  // [n_chunks] chunk holds an E (non-direct) span
   uint64_t fstar;           // F* (FinalArgs.fstar): t + 1 < F* is a double t
   int32_t exact;            // TSDBHIP_EXACT_ORDER: IEEE division in the double lerp
@@ -179,6 +192,22 @@ DEVI void acc_store(const ReduceArgs& r, uint64_t p, const Acc& a) {
   if (AGG == 4) {
     if (MODE != MODE_DBL) { r.p_wim[p] = a.wi.mean; r.p_wiv[p] = a.wi.var; }
     if (MODE != MODE_INT) { r.p_wdm[p] = a.wd.mean; r.p_wdv[p] = a.wd.var; }
+  }
+}
+
+// the initial state of t (ReduceArgs.i_*), or empty
+template <int AGG, int MODE>
+DEVI void acc_start(const ReduceArgs& r, uint64_t g, Acc& a) {
+  acc_init(a);
+  if (!r.i_cnt) return;
+  a.cnt = r.i_cnt[g];
+  if (MODE == MODE_DUAL || AGG == 1 || AGG == 2) a.flag = r.i_flag[g];
+  if (MODE != MODE_DBL && AGG != 4) a.ia = r.i_i[g];
+  if (MODE != MODE_INT && AGG != 4) a.da = r.i_d[g];
+  if (MODE != MODE_INT && (AGG == 1 || AGG == 2)) a.dhas = r.i_dhas[g];
+  if (AGG == 4) {
+    if (MODE != MODE_DBL) { a.wi.n = a.cnt; a.wi.mean = r.i_wim[g]; a.wi.var = r.i_wiv[g]; }
+    if (MODE != MODE_INT) { a.wd.n = a.cnt; a.wd.mean = r.i_wdm[g]; a.wd.var = r.i_wdv[g]; }
   }
 }
 
@@ -314,7 +343,7 @@ DEVI void reduce_wave(const ReduceArgs& r, const uint32_t wave) {
     // still write empty partials for this chunk's tiles
     for (uint64_t t = tb; t < te; t++) {
       const uint64_t g = t * WAVE + lane;
-      if (g < r.T) { Acc a; acc_init(a); acc_store<AGG, MODE>(r, (uint64_t)chunk * r.T + g, a); }
+      if (g < r.T) { Acc a; acc_start<AGG, MODE>(r, g, a); acc_store<AGG, MODE>(r, (uint64_t)chunk * r.T + g, a); }
     }
     return;
   }
@@ -386,7 +415,8 @@ DEVI void reduce_wave(const ReduceArgs& r, const uint32_t wave) {
     const int64_t t_first = (int64_t)r.grid[g0];
     const int64_t t_last = (int64_t)r.grid[g0 + nvalid - 1];
     Acc acc;
-    acc_init(acc);
+    if (gv) acc_start<AGG, MODE>(r, g, acc);
+    else acc_init(acc);
     // dual mode: t before the latest float-first point is on the double path
     // whatever the spans hold (F*, SpanGroup.java:632-645); once every lane's
     // t is known to be double, no long lerp of this tile is ever read
@@ -793,7 +823,6 @@ struct FinalArgs {
   uint8_t* out_isint;
   int64_t* out_bits;
   unsigned long long* nan_t; // [1] min t index with NaN/Inf double
-  unsigned int* ambiguous;   // [1] int dev near an integer after a Chan merge
 };
 
 template <int AGG, int MODE, bool RATE>
@@ -811,15 +840,10 @@ DEVI void finalize_one(const FinalArgs& f, uint64_t g, const Acc& a) {
     bits = dbits(d);
   } else {
     if (AGG == 3) bits = ldiv(a.ia, (int64_t)(int32_t)a.cnt);
-    else if (AGG == 4) {
-      const double v = wf_result(a.wi);
-      bits = d2l(v);
-      if (f.n_chunks > 1) {
-        const double fr = v - floor(v);
-        const double tol = 1e-7 * (v > 1.0 ? v : 1.0);
-        if (fr < tol || 1.0 - fr < tol) atomicOr(f.ambiguous, 1u);
-      }
-    } else bits = a.ia;
+    // (integer dev: the caller reduces in one span-ordered pass, so this is
+    // the reference's sequential Welford, :196-217)
+    else if (AGG == 4) bits = d2l(wf_result(a.wi));
+    else bits = a.ia;
   }
   f.out_ts[g] = t;
   f.out_isint[g] = isflt ? 0 : 1;

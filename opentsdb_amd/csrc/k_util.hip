@@ -199,6 +199,13 @@ __global__ void k_synth_cells(SynthArgs a) {
 }  // namespace tsdb
 
 namespace tsdb {
+// An empty integer min / max partial (count 0) as the neutral element of the
+// rank allreduce (acc_merge skips empty partials; a reduction cannot).
+__global__ void k_neutral_minmax(const uint32_t* cnt, int64_t* v, uint64_t T, int64_t neutral) {
+  const uint64_t g = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (g < T && cnt[g] == 0) v[g] = neutral;
+}
+
 __global__ void k_bitmap_or(const uint32_t* all, uint32_t nranks, uint64_t nwords, uint32_t* out) {
   const uint64_t w = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (w >= nwords) return;

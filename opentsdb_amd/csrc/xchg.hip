@@ -1,0 +1,191 @@
+// xchg.hip — the exchange step of a series-sharded SpanGroup:
+// the few collectives spangroup_run issues between the ranks that each hold
+// a contiguous range of the group's spans.
+//
+//   RcclXchg   one RCCL communicator (ncclAllReduce / AllGather / Broadcast
+//              over xGMI): one process per GPU (tsdbhip_comm_init), or one
+//              process driving several distinct GPUs (tsdbhip_open_devices,
+//              ncclCommInitAll).
+//   LocalXchg  the ranks are host threads of this process whose devices may
+//              repeat (several shards on one GPU): the same collectives as
+//              device-to-device / peer copies ordered by HIP events, the
+//              threads meeting at a host barrier. This is what runs an N-rank
+//              exchange on a single GPU (tests, oversubscription).
+// Every rank issues the same collectives in the same order; buffers are
+// device memory, operations are stream-ordered on the caller's stream.
+#pragma once
+#include <condition_variable>
+#include <mutex>
+#include <vector>
+
+enum XType { X_U8 = 0, X_I32, X_U32, X_I64, X_U64, X_F64 };
+enum XOp { X_SUM = 0, X_MIN, X_MAX };
+
+static size_t xsize(XType t) {
+  switch (t) {
+    case X_U8: return 1;
+    case X_I32:
+    case X_U32: return 4;
+    default: return 8;
+  }
+}
+
+struct Xchg {
+  int nranks = 1, rank = 0;
+  virtual ~Xchg() {}
+  virtual void group_start(Slot* ctx) {}
+  virtual void group_end(Slot* ctx) {}
+  // in place, element-wise over the ranks
+  virtual void allreduce(Slot* ctx, void* buf, size_t count, XType t, XOp op) = 0;
+  // recv[r * bytes, (r+1) * bytes) = rank r's send
+  virtual void allgather(Slot* ctx, const void* send, void* recv, size_t bytes) = 0;
+  // every rank's recv = root's send (the root's recv too)
+  virtual void broadcast(Slot* ctx, const void* send, void* recv, size_t bytes, int root) = 0;
+};
+
+// ---------------------------------------------------------------- RCCL ----
+static ncclDataType_t nccl_type(XType t) {
+  switch (t) {
+    case X_U8: return ncclUint8;
+    case X_I32: return ncclInt32;
+    case X_U32: return ncclUint32;
+    case X_I64: return ncclInt64;
+    case X_U64: return ncclUint64;
+    default: return ncclFloat64;
+  }
+}
+
+struct RcclXchg : Xchg {
+  ncclComm_t comm = nullptr;
+  void group_start(Slot* ctx) override { NCCLCHK(ncclGroupStart()); }
+  void group_end(Slot* ctx) override { NCCLCHK(ncclGroupEnd()); }
+  void allreduce(Slot* ctx, void* buf, size_t count, XType t, XOp op) override {
+    const ncclRedOp_t o = op == X_SUM ? ncclSum : op == X_MIN ? ncclMin : ncclMax;
+    NCCLCHK(ncclAllReduce(buf, buf, count, nccl_type(t), o, comm, ctx->stream));
+  }
+  void allgather(Slot* ctx, const void* send, void* recv, size_t bytes) override {
+    NCCLCHK(ncclAllGather(send, recv, bytes, ncclUint8, comm, ctx->stream));
+  }
+  void broadcast(Slot* ctx, const void* send, void* recv, size_t bytes, int root) override {
+    NCCLCHK(ncclBroadcast(send, recv, bytes, ncclUint8, root, comm, ctx->stream));
+  }
+};
+
+// ------------------------------------------------------------ in-process ----
+namespace tsdb {
+// out[i] = op over ranks r (in rank order) of all[r * count + i]
+template <typename T, int OP>
+__global__ void k_xreduce(const T* all, uint32_t n, uint64_t count, T* out) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= count) return;
+  T x = all[i];
+  for (uint32_t r = 1; r < n; r++) {
+    const T y = all[(uint64_t)r * count + i];
+    if (OP == X_SUM) x = (T)(x + y);  // (unsigned types: wrapping)
+    else if (OP == X_MIN) x = y < x ? y : x;
+    else x = y > x ? y : x;
+  }
+  out[i] = x;
+}
+}  // namespace tsdb
+
+struct LocalGroup {
+  int n = 0;
+  std::vector<int> dev;
+  std::mutex m;
+  std::condition_variable cv;
+  int arrived = 0;
+  uint64_t gen = 0;
+  bool broken = false;
+  std::vector<const void*> ptr;       // each rank's source buffer of the current op
+  std::vector<hipEvent_t> ready, done;
+
+  // Host barrier of the n rank threads; throws once a rank has failed (its
+  // peers would otherwise wait for it forever).
+  void barrier() {
+    std::unique_lock<std::mutex> lk(m);
+    if (broken) throw Fail{TSDBHIP_E_RCCL};
+    const uint64_t g = gen;
+    if (++arrived == n) {
+      arrived = 0;
+      gen++;
+      cv.notify_all();
+      return;
+    }
+    cv.wait(lk, [&] { return gen != g || broken; });
+    if (gen == g) throw Fail{TSDBHIP_E_RCCL};  // (woken by abort(), not by the last arrival)
+  }
+  void abort() {
+    std::lock_guard<std::mutex> lk(m);
+    broken = true;
+    cv.notify_all();
+  }
+  void reset() {
+    std::lock_guard<std::mutex> lk(m);
+    broken = false;
+    arrived = 0;
+  }
+};
+
+struct LocalXchg : Xchg {
+  LocalGroup* G = nullptr;
+
+  void copy_from(Slot* ctx, void* dst, int q, const void* src, size_t bytes) {
+    if (!bytes) return;
+    if (G->dev[q] == G->dev[rank])
+      HIPCHK(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToDevice, ctx->stream));
+    else
+      HIPCHK(hipMemcpyPeerAsync(dst, G->dev[rank], src, G->dev[q], bytes, ctx->stream));
+  }
+  // publish `src` (ready once this stream reaches here), wait for every rank
+  void publish(Slot* ctx, const void* src) {
+    G->ptr[rank] = src;
+    HIPCHK(hipEventRecord(G->ready[rank], ctx->stream));
+    G->barrier();
+  }
+  // this rank has finished reading the others' buffers; nobody overwrites
+  // its source before every reader is done
+  void retire(Slot* ctx) {
+    HIPCHK(hipEventRecord(G->done[rank], ctx->stream));
+    G->barrier();
+    for (int q = 0; q < nranks; q++)
+      if (q != rank) HIPCHK(hipStreamWaitEvent(ctx->stream, G->done[q], 0));
+  }
+  void allgather(Slot* ctx, const void* send, void* recv, size_t bytes) override {
+    publish(ctx, send);
+    for (int q = 0; q < nranks; q++) {
+      if (q != rank) HIPCHK(hipStreamWaitEvent(ctx->stream, G->ready[q], 0));
+      copy_from(ctx, (char*)recv + (size_t)q * bytes, q, G->ptr[q], bytes);
+    }
+    retire(ctx);
+  }
+  void broadcast(Slot* ctx, const void* send, void* recv, size_t bytes, int root) override {
+    publish(ctx, send);
+    if (rank != root) HIPCHK(hipStreamWaitEvent(ctx->stream, G->ready[root], 0));
+    if (rank != root || send != recv) copy_from(ctx, recv, root, G->ptr[root], bytes);
+    retire(ctx);
+  }
+  void allreduce(Slot* ctx, void* buf, size_t count, XType t, XOp op) override {
+    const size_t bytes = count * xsize(t);
+    uint8_t* all = scratch<uint8_t>(ctx, "x_allreduce", bytes * nranks);
+    allgather(ctx, buf, all, bytes);
+    if (!count) return;
+    const dim3 g(grid_for(count, 256)), b(256);
+    const uint32_t n = (uint32_t)nranks;
+#define XR(T, O) hipLaunchKernelGGL((k_xreduce<T, O>), g, b, 0, ctx->stream, (const T*)all, n, (uint64_t)count, (T*)buf)
+#define XR3(TS, TM)              \
+  if (op == X_SUM) XR(TS, X_SUM); \
+  else if (op == X_MIN) XR(TM, X_MIN); \
+  else XR(TM, X_MAX)
+    switch (t) {
+      case X_U8: XR3(uint8_t, uint8_t); break;
+      case X_I32: XR3(uint32_t, int32_t); break;
+      case X_U32: XR3(uint32_t, uint32_t); break;
+      case X_I64: XR3(uint64_t, int64_t); break;
+      case X_U64: XR3(uint64_t, uint64_t); break;
+      default: XR3(double, double); break;
+    }
+#undef XR3
+#undef XR
+  }
+};

@@ -1,0 +1,212 @@
+"""N-rank series sharding on one GPU (the exchange had only ever
+run on a 1-rank communicator). A context over devices [0] * N splits every
+SpanGroup into N contiguous span ranges, one host thread per rank, and the
+ranks exchange bounds, flags, grid bitmaps and per-t partials through the
+same collectives the RCCL path issues (LocalXchg: device copies ordered by
+HIP events); results are compared with the oracle on the whole group:
+integers (integer dev included: the span-ordered pass continues from rank to
+rank) bit-exact, doubles at 1e-9 relative, or bit-exact with EXACT_ORDER.
+Shards get differing grids (jittered spans), mixed int/float, every
+aggregator, ranks without spans, and errors raised inside a non-zero rank's
+shard. The last test drives one context and per-thread contexts from 8 host
+threads at once (re-entrancy)."""
+import threading
+
+import numpy as np
+import pytest
+
+import oracle
+from helpers import I, F, T0, U32MAX, assert_same
+from opentsdb_amd import _abi, core, packing, synth
+
+AGGS = [0, 1, 2, 3, 4]
+
+
+@pytest.fixture(scope="module", params=[2, 4, 8])
+def mctx(request):
+    from opentsdb_amd._lib import Context
+    c = Context(devices=[0] * request.param)
+    assert c.ranks == request.param
+    yield c
+    c.close()
+
+
+def both(c, ss, start=0, end=U32MAX, agg=0, rate=False, dsi=0, dsa=0, exact=False):
+    g = core.run_spanset(c, ss, start, end, agg, rate, dsi, dsa, exact=exact)
+    o = oracle.spangroup(ss, start, end, agg, rate, dsi, dsa)
+    return g, o
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("agg", AGGS)
+@pytest.mark.parametrize("rate", [False, True])
+def test_regular_downsampled(mctx, agg, rate):
+    ss = synth.regular(40, 2000, _abi.SYN_INT64_COUNTER, seed=7, step=10)
+    g, o = both(mctx, ss, agg=agg, rate=rate, dsi=60, dsa=3)
+    assert_same(g, o)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("agg", AGGS)
+@pytest.mark.parametrize("rate", [False, True])
+def test_regular_direct(mctx, agg, rate):
+    """no downsampling: the direct path's consecutive-rank check against the
+    exchanged grid"""
+    ss = synth.regular(33, 1300, _abi.SYN_INT64_COUNTER, seed=5, step=5)
+    g, o = both(mctx, ss, agg=agg, rate=rate)
+    assert_same(g, o)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("agg", AGGS)
+def test_c3s_shape_many_chunks(mctx, agg):
+    """>= 64 reduce chunks per rank, their in-order combine before the exchange"""
+    ss = synth.regular(2100, 600, _abi.SYN_INT64_COUNTER, seed=11, step=1)
+    g, o = both(mctx, ss, agg=agg, dsi=60, dsa=3)
+    assert_same(g, o)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("seed", [1, 2])
+@pytest.mark.parametrize("agg", AGGS)
+@pytest.mark.parametrize("rate", [False, True])
+def test_jittered_mixed_differing_grids(mctx, seed, agg, rate):
+    """each shard's grid differs (allgather + OR of the bitmaps); mixed
+    int/float series, so the double path and F* travel between ranks"""
+    ss = synth.jittered(13, 70, seed=seed, span_range=400_000, max_gap=700)
+    g, o = both(mctx, ss, agg=agg, rate=rate)
+    assert_same(g, o)
+    g, o = both(mctx, ss, agg=agg, rate=rate, exact=True)
+    assert_same(g, o, exact_double=True)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("seed", [4, 5, 6])
+@pytest.mark.parametrize("agg", AGGS)
+def test_jittered_int_lerp(mctx, seed, agg):
+    """all-integer jittered series: int64 lerp; integer dev bit-exact"""
+    ss = synth.jittered(17, 90, seed=seed, span_range=300_000, max_gap=900, float_frac=0.0, float_cell_frac=0.0)
+    g, o = both(mctx, ss, agg=agg)
+    assert_same(g, o, exact_double=True)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("agg", [0, 3, 4])
+def test_integer_dev_large_values(mctx, agg):
+    """dev over 8-byte counters near 2^40 (C3's values): Chan merges of
+    shard states would differ from the sequential Welford in the last bits,
+    which the (long) cast exposes"""
+    ss = synth.regular(300, 700, _abi.SYN_INT64_COUNTER, seed=3, step=1)
+    g, o = both(mctx, ss, agg=agg)
+    assert_same(g, o, exact_double=True)
+
+
+@pytest.mark.gpu
+def test_fewer_spans_than_ranks(mctx):
+    ss = packing.pack_spans([I([(T0 + 10 * i, i) for i in range(40)]), F([(T0 + 5 + 7 * i, 0.5 * i) for i in range(30)])])
+    for agg in AGGS:
+        g, o = both(mctx, ss, agg=agg)
+        assert_same(g, o)
+    ss = packing.pack_spans([])
+    g, o = both(mctx, ss)
+    assert_same(g, o)
+
+
+@pytest.mark.gpu
+def test_illegal_cell_in_a_later_rank(mctx):
+    """the IllegalDataException's lazy index comes from the rank holding the
+    bad cell (allreduced), every rank agrees on the code"""
+    T = T0
+    bad = packing.KeyValue(T, bytes([0x00, 0x02, 0x00, 0x12]), bytes([1, 2, 3, 4, 5, 6, 0]))  # 3-byte ints
+    spans = [I([(T + i, i) for i in range(5)]) for _ in range(5)] + [[bad]]
+    ss = packing.pack_spans(spans)
+    g, o = both(mctx, ss)
+    assert g[0] == _abi.E_ILLEGAL_DATA
+    assert_same(g, o)
+
+
+@pytest.mark.gpu
+def test_empty_span_and_nan_in_a_later_rank(mctx):
+    T = T0
+    ss = packing.pack_spans([I([(T + 1, 1), (T + 2, 2)])] * 6)
+    ss.span_row_start = np.concatenate([ss.span_row_start, [ss.span_row_start[-1]]]).astype(np.uint64)
+    g, o = both(mctx, ss)
+    assert o.code == _abi.E_EMPTY_SPAN
+    assert_same(g, o)
+    spans = [F([(T + 1, 1.0), (T + 2, 1.0)])] * 5 + [F([(T + 1, float("inf")), (T + 2, 1.0)])]
+    g, o = both(mctx, packing.pack_spans(spans))
+    assert g[0] == _abi.E_NAN_INF
+    assert_same(g, o)
+
+
+@pytest.mark.gpu
+def test_device_desc_sharded(mctx):
+    """device-resident input (tsdbhip_synth_generate) split by span count"""
+    import ctypes as C
+    d = _abi.SgDesc()
+    p = _abi.SynthParams(seed=9, n_spans=150, n_points=900, t0=synth.T0, step=1, kind=_abi.SYN_INT64_COUNTER,
+                         span0=0)
+    mctx.check(mctx._lib.tsdbhip_synth_generate(mctx.handle, C.byref(p), C.byref(d)))
+    try:
+        ss = synth.regular(150, 900, _abi.SYN_INT64_COUNTER, seed=9, step=1)
+        for agg, dsi in ((0, 60), (4, 0), (2, 0)):
+            g = core.run_spanset(mctx, ss, 0, U32MAX, agg, False, dsi, 3 if dsi else 0, device_desc=d)
+            o = oracle.spangroup(ss, 0, U32MAX, agg, False, dsi, 3 if dsi else 0)
+            assert_same(g, o, exact_double=True)
+    finally:
+        mctx._lib.tsdbhip_synth_free(mctx.handle, C.byref(d))
+
+
+# ------------------------------------------------------------ re-entrancy ----
+def _workload(seed):
+    rng = np.random.default_rng(seed)
+    kind = int(rng.integers(0, 3))
+    if kind == 0:
+        ss = synth.regular(int(rng.integers(5, 60)), int(rng.integers(200, 3000)), _abi.SYN_INT64_COUNTER,
+                           seed=seed, step=1)
+        return ss, dict(agg=int(rng.integers(0, 5)), dsi=int(rng.choice([0, 60])), dsa=3, rate=bool(seed % 2))
+    if kind == 1:
+        ss = synth.jittered(int(rng.integers(3, 15)), 60, seed=seed, span_range=300_000, max_gap=900)
+        return ss, dict(agg=int(rng.integers(0, 5)), dsi=0, dsa=0, rate=bool(seed % 3 == 0))
+    ss = synth.regular(int(rng.integers(5, 40)), 1440, _abi.SYN_FLOAT32, seed=seed, step=10)
+    return ss, dict(agg=3, dsi=60, dsa=3, rate=False)
+
+
+@pytest.mark.gpu
+@pytest.mark.timeout(300)
+def test_concurrent_calls_shared_and_private_contexts(ctx):
+    """8 host threads x 6 SpanGroups each, half on one shared context (one
+    slot per concurrent call), half on a context of their own; every result
+    checked against the oracle, and each thread's last_error / last_timing
+    are its own."""
+    from opentsdb_amd._lib import Context
+    work = [[_workload(1000 * t + i) for i in range(6)] for t in range(8)]
+    expected = [[oracle.spangroup(ss, 0, U32MAX, kw["agg"], kw["rate"], kw["dsi"], kw["dsa"]) for ss, kw in w]
+                for w in work]
+    errors = []
+    barrier = threading.Barrier(8)
+
+    def worker(t):
+        try:
+            c = ctx if t % 2 == 0 else Context(0)
+            barrier.wait()
+            for (ss, kw), o in zip(work[t], expected[t]):
+                g = core.run_spanset(c, ss, 0, U32MAX, kw["agg"], kw["rate"], kw["dsi"], kw["dsa"])
+                assert_same(g, o)
+                assert c.timing().total_ms > 0
+            # a failing call reports its own message on this thread
+            bad = packing.pack_spans([I([(T0 + 1, 1)])])
+            bad.span_row_start = np.array([0, 1, 1], np.uint64)
+            assert core.run_spanset(c, bad, 0, U32MAX, 0)[0] == _abi.E_EMPTY_SPAN
+            assert "error -3" in c.last_error()
+            if c is not ctx:
+                c.close()
+        except Exception as e:  # reported below
+            errors.append((t, repr(e)))
+
+    th = [threading.Thread(target=worker, args=(t,)) for t in range(8)]
+    for x in th:
+        x.start()
+    for x in th:
+        x.join()
+    assert not errors, errors
