@@ -410,6 +410,21 @@ def h2d_leg(ctx, L, cfg, n_spans, steps=3):
                       "(staged H2D inside every call)"}
 
 
+def spawn_ranks(n):
+    """`python bench.py --gpus N` without a launcher: run the same command as
+    N ranks of torch.distributed.run on this node (127.0.0.1 rendezvous) as
+    a child process; its rank 0 prints the line."""
+    import socket
+    import subprocess
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr=127.0.0.1", f"--master-port={port}", os.path.abspath(__file__)] + sys.argv[1:]
+    return subprocess.run(cmd).returncode
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -434,6 +449,14 @@ def main():
                     help="harness check without a GPU: the multi-rank timing/barrier/report path with a "
                          "no-op step (its value is meaningless and says so)")
     args = ap.parse_args()
+    world_env = os.environ.get("WORLD_SIZE")
+    if args.gpus > 1 and world_env is None:
+        # one process per GPU: start the N ranks under torch.distributed.run
+        # (before anything here touches a GPU) and exit with their status
+        sys.exit(spawn_ranks(args.gpus))
+    if world_env is not None and int(world_env) != args.gpus:
+        print(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world_env}", file=sys.stderr)
+        sys.exit(2)
     global _JSON_OUT
     sys.stdout.flush()
     _JSON_OUT = os.fdopen(os.dup(1), "w")

@@ -231,3 +231,19 @@ def test_bench_rehearsal_split_and_single_line():
     d = json.loads(lines[0])
     assert d["n_gpus"] == 1 and len(d["config"]["shards"]) == 8
     assert d["config"]["shards"][0] == [0, 125000]
+
+
+def test_bench_spawns_its_ranks_without_a_launcher():
+    """`python bench.py --gpus 2` (no torchrun) starts 2 ranks itself and the
+    line reports n_gpus 2; a WORLD_SIZE that disagrees with --gpus fails."""
+    cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--steps", "2", "--warmup", "1",
+           "--dry-run"]
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=240)
+    assert r.returncode == 0, r.stderr[-2000:]
+    lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, r.stdout
+    import json
+    assert json.loads(lines[0])["n_gpus"] == 2
+    r = subprocess.run(cmd, env=dict(env, WORLD_SIZE="1"), capture_output=True, text=True, timeout=240)
+    assert r.returncode != 0
