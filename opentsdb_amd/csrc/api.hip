@@ -534,27 +534,35 @@ struct LaunchFastDs {
 // Streaming downsampling of regular-cadence integer spans (k_ds_spans, wave
 // per span); leaves the spans it did not take in fa.span_list for
 // k_decode_fast.
+constexpr uint32_t CK_NSEG = 64;
 struct LaunchChunks {
   template <int AGG>
   static void run(Slot* ctx, const DecodeArgs& da, DecodeArgs& fa, const uint32_t* ncells,
-                  const uint32_t* vlen, SpanDsArgs g, uint32_t* zeroed2 = nullptr) {
+                  const uint32_t* vlen, SpanDsArgs g, uint32_t* zeroed2 = nullptr, uint32_t* zeroed_seg = nullptr) {
     if (AGG == 4) return;  // dev: Welford is order-dependent, serial kernels only
     hipStream_t st = ctx->stream;
     const uint32_t n_kept = da.n_kept;
-    g.list = scratch<uint32_t>(ctx, "ck_list", n_kept);
-    // (zeroed2: two list counters already zero on the device, no memsets)
-    g.list_count = zeroed2 ? zeroed2 : scratch<uint32_t>(ctx, "ck_list_count", 1, true);
+    const unsigned iblocks = grid_for(n_kept, 4, 1u << 20);
+    // the integer instantiation's leftovers: 64 segments (block % 64)
+    g.nseg = CK_NSEG;
+    g.seg_cap = 4 * ((iblocks + CK_NSEG - 1) / CK_NSEG);
+    g.list = scratch<uint32_t>(ctx, "ck_list", (uint64_t)g.seg_cap * CK_NSEG);
+    // (zeroed2 / zeroed_seg: list counters already zero on the device, no memsets)
+    g.list_count = zeroed_seg ? zeroed_seg : scratch<uint32_t>(ctx, "ck_seg_count", CK_NSEG, true);
     g.in_list = nullptr;
     g.in_count = nullptr;
+    g.in_nseg = g.in_seg_cap = 0;
     // integer spans over every kept span, then float spans over the ones left
     SpanDsArgs gf = g;
     gf.in_list = g.list;
     gf.in_count = g.list_count;
+    gf.in_nseg = g.nseg;
+    gf.in_seg_cap = g.seg_cap;
+    gf.nseg = gf.seg_cap = 0;
     gf.list = scratch<uint32_t>(ctx, "ck_list2", n_kept);
     gf.list_count = zeroed2 ? zeroed2 + 1 : scratch<uint32_t>(ctx, "ck_list2_count", 1, true);
     HIPCHK(hipEventRecord(ctx->ev[8], st));
-    hipLaunchKernelGGL((k_ds_spans<AGG, false>), dim3(grid_for(n_kept, 4, 1u << 20)), dim3(256), 0, st, da, g,
-                       ncells, vlen);
+    hipLaunchKernelGGL((k_ds_spans<AGG, false>), dim3(iblocks), dim3(256), 0, st, da, g, ncells, vlen);
     hipLaunchKernelGGL((k_ds_spans<AGG, true>), dim3(std::min(grid_for(n_kept, 4, 1u << 20), 1024u)), dim3(256), 0,
                        st, da, gf, ncells, vlen);
     HIPCHK(hipEventRecord(ctx->ev[9], st));
@@ -739,6 +747,7 @@ static int spangroup_run(Slot* ctx, const tsdbhip_sg_desc* d, tsdbhip_sg_out* ou
     uint32_t cnt[6];  // list counters, zeroed by the init copy below (no memsets):
                       // [0] assembly queue, [1] decode fallback, [2] direct list,
                       // [3] [4] k_ds_spans int / float leftovers
+    uint32_t seg[CK_NSEG];  // k_ds_spans integer leftovers, per segment
   };
   Small* sm = scratch<Small>(ctx, "small", 1);
   {
@@ -889,7 +898,10 @@ static int spangroup_run(Slot* ctx, const tsdbhip_sg_desc* d, tsdbhip_sg_out* ou
         dg.hi = hi;
         dg.rate = rate;
         ctx->hot_kernel = TSDBHIP_HOT_REDUCE_DIRECT;  // timed around k_reduce
-        hipLaunchKernelGGL(k_direct_scan, dim3(grid_for(n_kept, 4 * DIRB, 1u << 20)), dim3(256), 0, st, da, dg,
+        // (spans per wave: 32 for big groups; fewer below ~64k spans, so a
+        // small group still spreads over ~2048 waves instead of a handful)
+        dg.batch = std::max<uint32_t>(1, std::min<uint32_t>(DIRB, n_kept / 2048));
+        hipLaunchKernelGGL(k_direct_scan, dim3(grid_for(n_kept, 4 * dg.batch, 1u << 20)), dim3(256), 0, st, da, dg,
                            row_ncells, row_val_len);
         fa.span_list = dg.list;
         fa.span_count = dg.list_count;
@@ -908,7 +920,7 @@ static int spangroup_run(Slot* ctx, const tsdbhip_sg_desc* d, tsdbhip_sg_out* ou
         g.lo = lo;
         g.hi = hi;
         g.rate = rate;
-        launch_agg<LaunchChunks>(ds_agg, ctx, da, fa, row_ncells, row_val_len, g, &sm->cnt[3]);
+        launch_agg<LaunchChunks>(ds_agg, ctx, da, fa, row_ncells, row_val_len, g, &sm->cnt[3], sm->seg);
         chunk_marked = bitmap != nullptr && fa.span_list != nullptr;
       }
       if (chunk_marked) {

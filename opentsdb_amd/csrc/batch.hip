@@ -281,7 +281,10 @@ static int spangroup_run_batch(Slot* ctx, const tsdbhip_sg_desc* d, uint32_t G, 
         dg.hi = -1;
         dg.rate = rate;
         ctx->hot_kernel = TSDBHIP_HOT_REDUCE_DIRECT;  // timed around the reduce launches
-        hipLaunchKernelGGL(k_direct_scan, dim3(grid_for(n_kept, 4 * DIRB, 1u << 20)), dim3(256), 0, st, da, dg,
+        // (spans per wave: 32 for big groups; fewer below ~64k spans, so a
+        // small group still spreads over ~2048 waves instead of a handful)
+        dg.batch = std::max<uint32_t>(1, std::min<uint32_t>(DIRB, n_kept / 2048));
+        hipLaunchKernelGGL(k_direct_scan, dim3(grid_for(n_kept, 4 * dg.batch, 1u << 20)), dim3(256), 0, st, da, dg,
                            row_ncells, row_val_len);
         fa.span_list = dg.list;
         fa.span_count = dg.list_count;

@@ -41,6 +41,8 @@ struct DirectArgs {
   const uint32_t* word_rank;
   int64_t lo, hi;
   int32_t rate;
+  uint32_t batch;      // spans per wave batch (<= DIRB): fewer for small groups, so
+                       // they spread over more waves
 };
 
 // Marks {xf + p*step : 0 <= p < np} (all inside [lo, hi]) in the grid bitmap;
@@ -96,7 +98,7 @@ DEVI uint2 qload(__amdgpu_buffer_rsrc_t rs, uint32_t voff, uint32_t soff) {
   return make_uint2(v[0], v[1]);
 }
 
-#define DIRB 32           // spans per wave batch
+#define DIRB 32           // spans per wave batch (at most)
 #define DIRG 8            // groups of 256 cells per wave iteration (4 cells per lane each)
 #define DIRQ (256 * DIRG)
 
@@ -114,12 +116,13 @@ __global__ void __launch_bounds__(256) k_direct_scan(DecodeArgs a, DirectArgs g,
   // the last marked pattern (regular series repeat it span after span)
   int64_t m_xf = -1;
   uint32_t m_step = 0, m_np = 0;
-  for (uint32_t kb = ufl(wave) * DIRB; kb < a.n_kept; kb += nwaves * DIRB) {
+  const uint32_t B = g.batch;
+  for (uint32_t kb = ufl(wave) * B; kb < a.n_kept; kb += nwaves * B) {
     const uint32_t kl = kb + lane;
     uint32_t s_l = 0, n_l = 0, nc_l = 0, vl_l = 0, base_l = 0;
     uint64_t r0_l = 0, r1_l = 0, qoff_l = 0, voff_l = 0;
     bool ok_l = false;
-    if (lane < DIRB && kl < a.n_kept) {
+    if ((uint32_t)lane < B && kl < a.n_kept) {
       s_l = a.kept[kl];
       r0_l = a.span_row_start[s_l];
       r1_l = a.span_row_start[s_l + 1];
@@ -134,7 +137,7 @@ __global__ void __launch_bounds__(256) k_direct_scan(DecodeArgs a, DirectArgs g,
         ok_l = a.row_ok[r0_l] != 0 && nc_l > 0;
       }
     }
-    const uint32_t nb = min((uint32_t)DIRB, a.n_kept - kb);
+    const uint32_t nb = min(B, a.n_kept - kb);
     const uint64_t okm = ballot(ok_l);
     // qualifier chunks; the next span's first chunk is loaded while the
     // current span's last chunk is processed (`carry`)

@@ -37,9 +37,16 @@ namespace tsdb {
 
 struct SpanDsArgs {
   uint32_t* list;        // spans left to the serial kernels
-  uint32_t* list_count;  // [1]
+  uint32_t* list_count;  // [1], or [nseg]
+  // nseg > 0: `list` is nseg segments of seg_cap entries, block b appending
+  // to segment b % nseg with its own counter (one wave per span appends
+  // once per rejected span: one shared counter would serialise 10k+
+  // same-address atomics when whole groups are rejected, e.g. float spans
+  // passing through the integer instantiation)
+  uint32_t nseg, seg_cap;
   const uint32_t* in_list;   // spans to take (null: every kept span)
-  const uint32_t* in_count;
+  const uint32_t* in_count;  // [1], or [in_nseg]
+  uint32_t in_nseg, in_seg_cap;
   uint32_t* bitmap;      // union-grid bitmap over [lo, hi] (null: no marking)
   int64_t lo, hi;
   int32_t rate;
@@ -436,9 +443,27 @@ __global__ void __launch_bounds__(256) k_ds_spans(DecodeArgs a, SpanDsArgs g, co
   const uint32_t nwaves = gridDim.x * blockDim.x / WAVE;
   bool any_i = false, any_f = false;
   int64_t fs = 0;  // F*: latest first bucket ts of a float span, + 1
-  const uint32_t n_in = g.in_list ? sld(g.in_count) : a.n_kept;
+  // a segmented input list: segment counts lane-parallel, their exclusive
+  // prefix locates item w
+  uint32_t seg_ex = 0;
+  uint32_t n_in = a.n_kept;
+  if (g.in_list && g.in_nseg) {
+    const uint32_t c = (uint32_t)lane < g.in_nseg ? g.in_count[lane] : 0u;
+    const uint32_t inc = wave_incl_scan_u32_dpp(c);
+    seg_ex = inc - c;
+    n_in = readlane_u32(inc, 63);
+  } else if (g.in_list) {
+    n_in = sld(g.in_count);
+  }
   for (uint32_t w = ufl(wave); w < n_in; w += nwaves) {
-    const uint32_t k = g.in_list ? sld(&g.in_list[w]) : w;
+    uint32_t k = w;
+    if (g.in_list && g.in_nseg) {
+      const uint64_t m = ballot((uint32_t)lane < g.in_nseg && seg_ex <= w);
+      const int sg = 63 - __builtin_clzll(m);
+      k = sld(&g.in_list[(uint64_t)sg * g.in_seg_cap + (w - readlane_u32(seg_ex, sg))]);
+    } else if (g.in_list) {
+      k = sld(&g.in_list[w]);
+    }
     const uint32_t s = sld(&a.kept[k]);
     const uint64_t r0 = sld(&a.span_row_start[s]), r1 = sld(&a.span_row_start[s + 1]);
     const uint32_t n = sld(&a.sp_ncells[s]);
@@ -458,6 +483,10 @@ __global__ void __launch_bounds__(256) k_ds_spans(DecodeArgs a, SpanDsArgs g, co
       const uint32_t vb = nc > 1 ? vl - 1 : vl;
       W = vb == (vb / nc) * nc ? vb / nc : 0;
       ok = W == 8 || W == 4;
+      // the first cell's type picks the instantiation: the other one leaves
+      // the span without streaming it (float spans pass through the integer
+      // kernel first)
+      if (ok) ok = ((sld_u8(a.qual + sld(&a.row_qual_off[r0]) + 1) & 8u) != 0) == FLT;
     }
     const uint64_t eo = sld(&a.e_off[k]);
     const uint32_t cap = (uint32_t)sld(&a.sp_cap[s]);
@@ -538,7 +567,12 @@ __global__ void __launch_bounds__(256) k_ds_spans(DecodeArgs a, SpanDsArgs g, co
         }
       }
     } else if (lane == 0) {
-      g.list[atomicAdd(g.list_count, 1u)] = k;
+      if (g.nseg) {
+        const uint32_t sg = blockIdx.x % g.nseg;
+        g.list[(uint64_t)sg * g.seg_cap + atomicAdd(&g.list_count[sg], 1u)] = k;
+      } else {
+        g.list[atomicAdd(g.list_count, 1u)] = k;
+      }
     }
   }
   if (lane == 0) {
