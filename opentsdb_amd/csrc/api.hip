@@ -791,17 +791,18 @@ static int spangroup_run(Slot* ctx, const tsdbhip_sg_desc* d, tsdbhip_sg_out* ou
                          (const uint32_t*)acount);
     }
   }
-  uint64_t* kflag = scratch<uint64_t>(ctx, "kflag", S);
-  uint64_t* kidx = scratch<uint64_t>(ctx, "kidx", S);
-  uint64_t* eoff_s = scratch<uint64_t>(ctx, "eoff_s", S);
   uint32_t* kept = scratch<uint32_t>(ctx, "kept", S);
   uint64_t* eoff = scratch<uint64_t>(ctx, "eoff", S);
-  if (S) {
-    hipLaunchKernelGGL(k_kept_flags, dim3(grid_for(S, 256)), dim3(256), 0, st, sp_kept, kflag, S);
-    dscan_u64(ctx, kflag, kidx, S, &sm->n_kept, "k");
-    dscan_u64(ctx, sp_cap, eoff_s, S, &sm->e_total, "e");
-    hipLaunchKernelGGL(k_kept_scatter, dim3(grid_for(S, 256, 1024)), dim3(256), 0, st, sp_kept, kidx, eoff_s,
-                       sp_ncells, S, kept, eoff, &sm->n_input, sp_first, sp_last, sm->bound);
+  if (S && S <= KC_MAX) {  // kept list, E offsets, counts and bounds: one launch
+    hipLaunchKernelGGL(k_kept_compact, dim3(1), dim3(1024), 0, st, sp_kept, sp_cap, sp_ncells, S, kept, eoff,
+                       &sm->n_input, sp_first, sp_last, sm->bound, &sm->n_kept, &sm->e_total);
+  } else if (S) {  // bigger groups: tile sums, then per-tile offsets + scatter
+    const uint32_t nt = (S + 1023) / 1024;
+    ulonglong2* ts = scratch<ulonglong2>(ctx, "kept_tiles", nt);
+    hipLaunchKernelGGL(k_kept_tiles, dim3(nt), dim3(256), 0, st, sp_kept, sp_cap, S, ts);
+    hipLaunchKernelGGL(k_kept_scatter_tiles, dim3(nt), dim3(256), 0, st, sp_kept, sp_cap, sp_ncells, S,
+                       (const ulonglong2*)ts, kept, eoff, &sm->n_input, sp_first, sp_last, sm->bound, &sm->n_kept,
+                       &sm->e_total);
   }
   if (sharded) {
     // every rank needs the same bitmap geometry and the same error: the kept

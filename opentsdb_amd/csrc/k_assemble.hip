@@ -193,8 +193,10 @@ DEVI void assemble_finish(const AssembleArgs& a, uint32_t s, bool has_rows) {
 // One thread per span: the common case (at most ASM_ROWS rows, each starting
 // after the previous one ended with no RowSeq merge possible, no seek inside
 // the first row) written directly; every other span is queued for the
-// wave-per-span kernel below.
-constexpr uint32_t ASM_ROWS = 64;
+// wave-per-span kernel below. (A thread walks its rows one dependent load
+// chain after the other: spans of many rows — a day of hourly rows — go to
+// the wave kernel, which loads 64 rows at once.)
+constexpr uint32_t ASM_ROWS = 4;
 __global__ void __launch_bounds__(256) k_assemble_fast(AssembleArgs a, uint32_t* list, uint32_t* count) {
   const uint32_t s = blockIdx.x * blockDim.x + threadIdx.x;
   bool defer = false;

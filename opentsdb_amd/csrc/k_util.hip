@@ -99,6 +99,198 @@ __global__ void __launch_bounds__(256) k_kept_scatter(const uint8_t* kept, const
   }
 }
 
+// The same in one launch for groups of up to KC_MAX spans (replaces
+// k_kept_flags + two 3-kernel scans + k_kept_scatter): one 1024-thread block
+// walks the spans 4096 at a time, carrying the two running prefixes. (A
+// multi-block single pass would need a look-back across the XCDs' separate
+// L2s, i.e. device-scope fences per tile: slower than the scan kernels.)
+constexpr uint32_t KC_MAX = 1u << 14;
+__global__ void __launch_bounds__(1024) k_kept_compact(const uint8_t* kept, const uint64_t* cap,
+                                                       const uint32_t* ncells, uint32_t n, uint32_t* kept_list,
+                                                       uint64_t* eoff_k, unsigned long long* n_input,
+                                                       const int64_t* sp_first, const int64_t* sp_last,
+                                                       unsigned long long* bound, uint64_t* n_kept_out,
+                                                       uint64_t* e_total_out) {
+  __shared__ uint64_t s_wk[16], s_we[16];
+  __shared__ uint64_t s_c[16];
+  __shared__ int64_t s_f[16], s_l[16];
+  const int t = threadIdx.x, lane = lane_id(), w = t / WAVE;
+  uint64_t ck = 0, ce = 0;  // carries: kept spans / E capacity before this round
+  uint64_t cnt = 0;
+  int64_t f = INT64_MAX, l = INT64_MIN;
+  for (uint64_t base0 = 0; base0 < n; base0 += 4096) {
+    const uint64_t base = base0 + 4 * t;
+    uint32_t fk[4];
+    uint64_t fe[4], sk = 0, se = 0;
+#pragma unroll
+    for (int i = 0; i < 4; i++) {
+      const uint64_t s = base + i;
+      fk[i] = s < n && kept[s] ? 1u : 0u;
+      fe[i] = s < n ? cap[s] : 0ull;
+      sk += fk[i];
+      se += fe[i];
+    }
+    const uint64_t ik = wave_incl_scan_u64_dpp(sk), ie = wave_incl_scan_u64_dpp(se);
+    if (lane == 63) {
+      s_wk[w] = ik;
+      s_we[w] = ie;
+    }
+    __syncthreads();
+    uint64_t wk = 0, we = 0, tk = 0, te = 0;
+    for (int i = 0; i < 16; i++) {
+      if (i < w) {
+        wk += s_wk[i];
+        we += s_we[i];
+      }
+      tk += s_wk[i];
+      te += s_we[i];
+    }
+    __syncthreads();  // (s_wk reused next round)
+    uint64_t rk = ck + wk + ik - sk, re = ce + we + ie - se;
+#pragma unroll
+    for (int i = 0; i < 4; i++) {
+      const uint64_t s = base + i;
+      if (fk[i]) {
+        kept_list[rk] = (uint32_t)s;
+        eoff_k[rk] = re;
+        cnt += ncells[s];
+        f = min(f, sp_first[s]);
+        l = max(l, sp_last[s]);
+      }
+      rk += fk[i];
+      re += fe[i];
+    }
+    ck += tk;
+    ce += te;
+  }
+  // block totals: aggregatedSize and the kept spans' [min first, max last]
+#pragma unroll
+  for (int m = 1; m < WAVE; m <<= 1) {
+    cnt += shfl_xor_u64(cnt, m);
+    f = min(f, (int64_t)shfl_xor_u64((uint64_t)f, m));
+    l = max(l, (int64_t)shfl_xor_u64((uint64_t)l, m));
+  }
+  if (lane == 0) {
+    s_c[w] = cnt;
+    s_f[w] = f;
+    s_l[w] = l;
+  }
+  __syncthreads();
+  if (t == 0) {
+    for (int i = 1; i < 16; i++) {
+      cnt += s_c[i];
+      f = min(f, s_f[i]);
+      l = max(l, s_l[i]);
+    }
+    *n_kept_out = ck;
+    *e_total_out = ce;
+    if (cnt) {
+      atomicAdd(n_input, (unsigned long long)cnt);
+      atomicMin(&bound[0], (unsigned long long)f);
+      atomicMax(&bound[1], (unsigned long long)l);
+    }
+  }
+}
+
+// Bigger groups in two launches: per tile of 1024 spans its (kept, capacity)
+// sums; then each tile adds up its predecessors' sums itself (at most a few
+// thousand tiles: no serial chain across tiles) and scatters.
+__global__ void __launch_bounds__(256) k_kept_tiles(const uint8_t* kept, const uint64_t* cap, uint32_t n,
+                                                    ulonglong2* tile_sum) {
+  __shared__ uint64_t sh_k[4], sh_e[4];
+  const uint64_t base = (uint64_t)blockIdx.x * 1024 + 4 * threadIdx.x;
+  uint64_t sk = 0, se = 0;
+#pragma unroll
+  for (int i = 0; i < 4; i++) {
+    const uint64_t s = base + i;
+    if (s < n) {
+      sk += kept[s] ? 1u : 0u;
+      se += cap[s];
+    }
+  }
+  sk = block_reduce_256(sk, [](uint64_t x, uint64_t y) { return x + y; }, sh_k);
+  se = block_reduce_256(se, [](uint64_t x, uint64_t y) { return x + y; }, sh_e);
+  if (threadIdx.x == 0) tile_sum[blockIdx.x] = make_ulonglong2(sk, se);
+}
+
+__global__ void __launch_bounds__(256) k_kept_scatter_tiles(const uint8_t* kept, const uint64_t* cap,
+                                                            const uint32_t* ncells, uint32_t n,
+                                                            const ulonglong2* tile_sum, uint32_t* kept_list,
+                                                            uint64_t* eoff_k, unsigned long long* n_input,
+                                                            const int64_t* sp_first, const int64_t* sp_last,
+                                                            unsigned long long* bound, uint64_t* n_kept_out,
+                                                            uint64_t* e_total_out) {
+  __shared__ uint64_t s_wk[4], s_we[4];
+  __shared__ uint64_t sh_c[4];
+  __shared__ int64_t sh_f[4], sh_l[4];
+  const int t = threadIdx.x, lane = lane_id(), w = t / WAVE;
+  const uint32_t tile = blockIdx.x;
+  // this tile's offset: the sum of its predecessors' sums
+  uint64_t pk = 0, pe = 0;
+  for (uint32_t q = t; q < tile; q += 256) {
+    const ulonglong2 v = tile_sum[q];
+    pk += v.x;
+    pe += v.y;
+  }
+  pk = block_reduce_256(pk, [](uint64_t x, uint64_t y) { return x + y; }, sh_c);
+  __syncthreads();
+  pe = block_reduce_256(pe, [](uint64_t x, uint64_t y) { return x + y; }, sh_c);
+  __shared__ uint64_t s_pk, s_pe;
+  if (t == 0) {
+    s_pk = pk;
+    s_pe = pe;
+  }
+  const uint64_t base = (uint64_t)tile * 1024 + 4 * t;
+  uint32_t fk[4];
+  uint64_t fe[4], sk = 0, se = 0;
+#pragma unroll
+  for (int i = 0; i < 4; i++) {
+    const uint64_t s = base + i;
+    fk[i] = s < n && kept[s] ? 1u : 0u;
+    fe[i] = s < n ? cap[s] : 0ull;
+    sk += fk[i];
+    se += fe[i];
+  }
+  const uint64_t ik = wave_incl_scan_u64_dpp(sk), ie = wave_incl_scan_u64_dpp(se);
+  if (lane == 63) {
+    s_wk[w] = ik;
+    s_we[w] = ie;
+  }
+  __syncthreads();
+  uint64_t rk = s_pk + ik - sk, re = s_pe + ie - se;
+  for (int i = 0; i < w; i++) {
+    rk += s_wk[i];
+    re += s_we[i];
+  }
+  if (t == 255 && (uint64_t)tile * 1024 + 1024 >= n) {  // the last tile: totals
+    *n_kept_out = rk + sk;
+    *e_total_out = re + se;
+  }
+  uint64_t cnt = 0;
+  int64_t f = INT64_MAX, l = INT64_MIN;
+#pragma unroll
+  for (int i = 0; i < 4; i++) {
+    const uint64_t s = base + i;
+    if (fk[i]) {
+      kept_list[rk] = (uint32_t)s;
+      eoff_k[rk] = re;
+      cnt += ncells[s];
+      f = min(f, sp_first[s]);
+      l = max(l, sp_last[s]);
+    }
+    rk += fk[i];
+    re += fe[i];
+  }
+  cnt = block_reduce_256(cnt, [](uint64_t x, uint64_t y) { return x + y; }, sh_c);
+  f = block_reduce_256(f, [](int64_t x, int64_t y) { return min(x, y); }, sh_f);
+  l = block_reduce_256(l, [](int64_t x, int64_t y) { return max(x, y); }, sh_l);
+  if (t == 0 && cnt) {
+    atomicAdd(n_input, (unsigned long long)cnt);
+    atomicMin(&bound[0], (unsigned long long)f);
+    atomicMax(&bound[1], (unsigned long long)l);
+  }
+}
+
 // ---- lazy error index (where the reference would throw) ----------------------
 // A bad cell in E point k is read when point k-1 moves into the current slot
 // (SpanGroup.java:583-608), i.e. while emitting ts(e_{k-1}); points 0 (and 1
