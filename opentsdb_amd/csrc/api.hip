@@ -984,7 +984,7 @@ static int spangroup_run(Slot* ctx, const tsdbhip_sg_desc* d, tsdbhip_sg_out* ou
                          nwords, bitmap);
     }
     hipLaunchKernelGGL(k_grid_popc, dim3((unsigned)nb), dim3(256), 0, st, ga);
-    hipLaunchKernelGGL(k_grid_scan_blocks, dim3(1), dim3(256), 0, st, ga, (uint32_t)nb);
+    if (nb > 1) hipLaunchKernelGGL(k_grid_scan_blocks, dim3(1), dim3(256), 0, st, ga, (uint32_t)nb);
     readback(ctx, &h, sm, sizeof h);  // sync 2: |G|, flags, F*, errors
     after_sync2();
     T = h.T;
@@ -1016,6 +1016,11 @@ static int spangroup_run(Slot* ctx, const tsdbhip_sg_desc* d, tsdbhip_sg_out* ou
   const uint64_t fstar = h.fstar;
   HIPCHK(hipEventRecord(ctx->ev[4], st));
   tm.n_grid = T;
+  // lazy error index for illegal cells (every span's E and e_bad are final
+  // here; sharded: a rank of the global grid, reduced with the exchange)
+  if (n_kept)
+    hipLaunchKernelGGL(k_bad_index, dim3(grid_for(n_kept, 256)), dim3(256), 0, st, e_bad, eoff, e_ts, n_kept,
+                       (int32_t)rate, hi, bitmap, word_rank, lo, T, &sm->bad_at);
 
   // ---- reduce ----
   if (T > 0) {
@@ -1110,9 +1115,6 @@ static int spangroup_run(Slot* ctx, const tsdbhip_sg_desc* d, tsdbhip_sg_out* ou
     if (!sharded) {
       run_reduce(seq, true, nullptr);
       HIPCHK(hipEventRecord(ctx->ev[5], st));
-      if (n_kept)  // lazy error index for illegal cells
-        hipLaunchKernelGGL(k_bad_index, dim3(grid_for(n_kept, 256)), dim3(256), 0, st, e_bad, eoff, e_ts, n_kept,
-                           (int32_t)rate, hi, bitmap, word_rank, lo, T, &sm->bad_at);
       readback(ctx, &h, sm, sizeof h);  // sync 3
     } else {
       const int nr = X->nranks, rk = X->rank;
@@ -1132,6 +1134,7 @@ static int spangroup_run(Slot* ctx, const tsdbhip_sg_desc* d, tsdbhip_sg_out* ou
           const std::vector<Fld> fp = fields(P, 0), fs = fields(S, 0);
           X->group_start(ctx);
           for (size_t i = 0; i < fp.size(); i++) X->broadcast(ctx, fp[i].p, fs[i].p, T * fp[i].esz, step);
+          if (step == 0) X->allreduce(ctx, &sm->bad_at, 1, X_U64, X_MIN);
           X->group_end(ctx);
         }
         HIPCHK(hipEventRecord(ctx->ev[7], st));
@@ -1151,6 +1154,7 @@ static int spangroup_run(Slot* ctx, const tsdbhip_sg_desc* d, tsdbhip_sg_out* ou
           HIPCHK(hipEventRecord(ctx->ev[6], st));
           X->group_start(ctx);
           for (const Fld& f : fields(mine, 0)) X->allreduce(ctx, f.p, T, f.t, f.op);
+          X->allreduce(ctx, &sm->bad_at, 1, X_U64, X_MIN);
           X->group_end(ctx);
           HIPCHK(hipEventRecord(ctx->ev[7], st));
           src = mine;
@@ -1168,6 +1172,7 @@ static int spangroup_run(Slot* ctx, const tsdbhip_sg_desc* d, tsdbhip_sg_out* ou
           const std::vector<Fld> fm = fields(mine, 0), fa = fields(all, 0);
           X->group_start(ctx);
           for (size_t i = 0; i < fm.size(); i++) X->allgather(ctx, fm[i].p, fa[i].p, T * fm[i].esz);
+          X->allreduce(ctx, &sm->bad_at, 1, X_U64, X_MIN);
           X->group_end(ctx);
           HIPCHK(hipEventRecord(ctx->ev[7], st));
           src = all;
@@ -1179,20 +1184,11 @@ static int spangroup_run(Slot* ctx, const tsdbhip_sg_desc* d, tsdbhip_sg_out* ou
       src.n_chunks = n_src;
       dispatch_final(ctx, agg, mode, rate, src, f);
       HIPCHK(hipEventRecord(ctx->ev[5], st));
-      // lazy error index for illegal cells: a grid rank of the global grid,
-      // the smallest over the ranks
-      if (n_kept)
-        hipLaunchKernelGGL(k_bad_index, dim3(grid_for(n_kept, 256)), dim3(256), 0, st, e_bad, eoff, e_ts, n_kept,
-                           (int32_t)rate, hi, bitmap, word_rank, lo, T, &sm->bad_at);
-      X->allreduce(ctx, &sm->bad_at, 1, X_U64, X_MIN);
       readback(ctx, &h, sm, sizeof h);
       tm.exchange_ms = ev_ms(ctx->ev[6], ctx->ev[7]);
     }
   } else {
     HIPCHK(hipEventRecord(ctx->ev[5], st));
-    if (n_kept)
-      hipLaunchKernelGGL(k_bad_index, dim3(grid_for(n_kept, 256)), dim3(256), 0, st, e_bad, eoff, e_ts, n_kept,
-                         (int32_t)rate, hi, bitmap, word_rank, lo, T, &sm->bad_at);
     if (sharded) X->allreduce(ctx, &sm->bad_at, 1, X_U64, X_MIN);
     readback(ctx, &h, sm, sizeof h);
   }

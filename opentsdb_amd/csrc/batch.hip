@@ -333,7 +333,7 @@ static int spangroup_run_batch(Slot* ctx, const tsdbhip_sg_desc* d, uint32_t G, 
   std::memset(&ga, 0, sizeof ga);
   ga.bitmap = bitmap; ga.nwords = W; ga.word_rank = word_rank; ga.block_sum = bsum; ga.total = &sm->T;
   hipLaunchKernelGGL(k_grid_popc, dim3((unsigned)nb), dim3(256), 0, st, ga);
-  hipLaunchKernelGGL(k_grid_scan_blocks, dim3(1), dim3(256), 0, st, ga, (uint32_t)nb);
+  if (nb > 1) hipLaunchKernelGGL(k_grid_scan_blocks, dim3(1), dim3(256), 0, st, ga, (uint32_t)nb);
   readback(ctx, &h, sm, sizeof h);  // total |G| over the groups (grid buffer size)
   const uint64_t T_all = h.T;
   uint32_t* gridv = scratch<uint32_t>(ctx, "grid", T_all);

@@ -79,7 +79,13 @@ __global__ void __launch_bounds__(256) k_grid_popc(GridArgs g) {
     if (w < g.nwords) g.word_rank[w] = run;
     run += c[i];
   }
-  if (t == 255) g.block_sum[blockIdx.x] = woff + incl;
+  if (t == 255) {
+    g.block_sum[blockIdx.x] = woff + incl;
+    if (gridDim.x == 1) {  // one block: its offset is 0 and its sum is T (no k_grid_scan_blocks)
+      g.block_sum[0] = 0;
+      g.total[0] = woff + incl;
+    }
+  }
 }
 
 // Single block: exclusive scan of the block sums; writes T.
