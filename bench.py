@@ -114,8 +114,9 @@ def pmc_traffic(config, kernel, world):
     ks = json.load(open(path)).get("kernels", {})
     # every instantiation of the kernel launches once per step (e.g. the
     # integer and float k_ds_spans), and the timed region covers them all
+    names = kernel.split("+")  # (a "+"-joined name: the kernels the timed bracket covers)
     tot = sum(e["hbm_bytes_per_launch"] for name, e in ks.items()
-              if name.split("<")[0] == kernel and e.get("hbm_bytes_per_launch"))
+              if name.split("<")[0] in names and e.get("hbm_bytes_per_launch"))
     return (tot, os.path.relpath(path, ROOT)) if tot else (None, None)
 
 
@@ -279,7 +280,7 @@ def bench_c5(args):
     for _ in range(args.warmup):
         step_once()
     torch.cuda.synchronize()
-    hot, tot, cx = [], [], []
+    hot, tot, cx, cls, rows_k = [], [], [], [], []
     t0 = time.perf_counter()
     for _ in range(args.steps):
         step_once()
@@ -287,6 +288,8 @@ def bench_c5(args):
         hot.append(tm.hot_ms)
         tot.append(tm.total_ms)
         cx.append(tm.reduce_ms)
+        cls.append(tm.decode_ms)
+        rows_k.append(tm.grid_ms)
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
     st = o["st"].cpu().numpy()
@@ -297,13 +300,16 @@ def bench_c5(args):
     row_v = np.diff(b.row_val_off.astype(np.int64))
     n_cx = int(out.n_complex)
     alg_all = int(row_q.sum() + row_v.sum() + ql.sum() + vl.sum())
-    # k_compact_tiles finishes every row except complexCompact rows of > 256
-    # cells (none in C5), which k_compact_complex redoes: all bytes are its.
+    # k_compact_quals + k_compact_vals move every row's qualifier and value
+    # bytes (in and out); classification, the LDS row kernel (non-plain
+    # rows) and the complex kernels are the rest of the call (call_achieved)
     alg_rows = alg_all
     cells = int(b.kv_qual_len.astype(np.int64).sum() // 2)
     hot_ms = float(np.mean(hot))
     achieved = alg_rows / (hot_ms * 1e-3) / 1e9
-    traffic, traffic_src = pmc_traffic("c5", "k_compact_tiles", 1)
+    kname = ("k_compact_tiles" if os.environ.get("TSDBHIP_COMPACT") == "tiles"
+             else "k_compact_quals+k_compact_vals")
+    traffic, traffic_src = pmc_traffic("c5", kname, 1)
     res = {
         "metric": "raw cells/sec compacted (CompactionQueue.compact) + % HBM roofline, 1 MI355X",
         "value": cells / (elapsed / args.steps), "unit": "raw cells/s", "n_gpus": 1, "steps": args.steps,
@@ -313,10 +319,11 @@ def bench_c5(args):
                 f"HBM-resident before timing)",
         "config": {"workload": CONFIGS["c5"]["desc"], "n_rows": R, "n_kvs": b.n_kvs, "raw_cells": cells,
                    "rows_complex": n_cx, "status_counts": np.bincount(st, minlength=6).tolist()},
-        "roofline": {"bound": "hbm", "kernel": "k_compact_tiles", "achieved": achieved, "peak": HBM_PEAK_GBS,
+        "roofline": {"bound": "hbm", "kernel": kname, "achieved": achieved, "peak": HBM_PEAK_GBS,
                      "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                      "traffic_source": traffic_src, "alg_bytes_per_launch": alg_rows, "kernel_ms": hot_ms,
-                     "complex_kernel_ms": float(np.mean(cx)), "step_device_ms": float(np.mean(tot)),
+                     "complex_kernel_ms": float(np.mean(cx)), "classify_kernel_ms": float(np.mean(cls)),
+                     "rows_kernel_ms": float(np.mean(rows_k)), "step_device_ms": float(np.mean(tot)),
                      "call_alg_bytes": alg_all,
                      "call_achieved": alg_all / (float(np.mean(tot)) * 1e-3) / 1e9},
     }

@@ -87,7 +87,7 @@ class SgOut(C.Structure):
 
 
 HOT_NONE, HOT_DS_CHUNKS, HOT_DECODE_FAST, HOT_DECODE_GEN = 0, 1, 2, 3
-HOT_NAMES = {1: "k_ds_spans", 2: "k_decode_fast", 3: "k_decode_general", 4: "k_compact_tiles", 5: "k_reduce"}
+HOT_NAMES = {1: "k_ds_spans", 2: "k_decode_fast", 3: "k_decode_general", 4: "k_compact_quals+k_compact_vals", 5: "k_reduce"}
 
 
 class Timing(C.Structure):

@@ -476,6 +476,8 @@ extern "C" int tsdbhip_comm_init(tsdbhip_ctx* ctx, int32_t nranks, int32_t rank,
 }
 
 // ------------------------------------------------------------- helpers ----
+static int err_code(uint64_t key) { return key == ERR_NONE ? 0 : -(int)(key & 0xFFu); }
+
 template <typename T>
 static const T* stage(Slot* ctx, const char* name, const T* src, size_t count, bool on_device,
                       size_t pad = 0) {
@@ -732,7 +734,7 @@ static int spangroup_run(Slot* ctx, const tsdbhip_sg_desc* d, tsdbhip_sg_out* ou
 
   // ---- small device state ----
   struct Small {
-    int32_t err;
+    unsigned long long err;  // first error (err_raise key), ERR_NONE: none
     uint32_t gflags[2];
     uint32_t reserved;
     unsigned long long range[2];
@@ -752,7 +754,7 @@ static int spangroup_run(Slot* ctx, const tsdbhip_sg_desc* d, tsdbhip_sg_out* ou
   Small* sm = scratch<Small>(ctx, "small", 1);
   {
     Small init = {};
-    init.err = 0;
+    init.err = ERR_NONE;
     init.range[0] = ~0ull;
     init.range[1] = 0;
     init.nan_t = ~0ull;
@@ -812,12 +814,12 @@ static int spangroup_run(Slot* ctx, const tsdbhip_sg_desc* d, tsdbhip_sg_out* ou
     X->group_start(ctx);
     X->allreduce(ctx, &sm->bound[0], 1, X_U64, X_MIN);
     X->allreduce(ctx, &sm->bound[1], 1, X_U64, X_MAX);
-    X->allreduce(ctx, &sm->err, 1, X_I32, X_MIN);
+    X->allreduce(ctx, &sm->err, 1, X_U64, X_MIN);
     X->group_end(ctx);
   }
   Small h;
   readback(ctx, &h, sm, sizeof h);  // sync 1
-  if (h.err) throw Fail{h.err};
+  if (h.err != ERR_NONE) throw Fail{err_code(h.err)};
   const uint32_t n_kept = (uint32_t)h.n_kept;
   out->n_input_points = h.n_input;
   uint64_t n_input_global = h.n_input;
@@ -944,7 +946,7 @@ static int spangroup_run(Slot* ctx, const tsdbhip_sg_desc* d, tsdbhip_sg_out* ou
     X->group_start(ctx);
     X->allreduce(ctx, sm->gflags, 2, X_U32, X_MAX);
     X->allreduce(ctx, &sm->fstar, 1, X_U64, X_MAX);
-    X->allreduce(ctx, &sm->err, 1, X_I32, X_MIN);
+    X->allreduce(ctx, &sm->err, 1, X_U64, X_MIN);
     X->allreduce(ctx, &sm->n_input, 1, X_U64, X_SUM);
     X->group_end(ctx);
   }
@@ -952,7 +954,7 @@ static int spangroup_run(Slot* ctx, const tsdbhip_sg_desc* d, tsdbhip_sg_out* ou
   // |G| below. A decode error leaves every e_len <= its capacity, so the grid
   // kernels stay inside E before the error is thrown.)
   auto after_sync2 = [&]() {
-    if (h.err) throw Fail{h.err};
+    if (h.err != ERR_NONE) throw Fail{err_code(h.err)};
     if (sharded) {
       n_input_global = h.n_input;
       out->n_input_points = n_input_global;
@@ -1617,7 +1619,7 @@ static int compact_rows(Slot* ctx, const tsdbhip_rows_desc* d, tsdbhip_rows_out*
                 (unsigned long long)qext, (unsigned long long)(vext + R));
       return TSDBHIP_E_CAPACITY;
     }
-    CompactArgs a;
+    CompactArgs a = {};
     a.n_rows = R;
     a.n_kvs = d->n_kvs;
     a.row_kv_start = stage(ctx, "c_rks", d->row_kv_start, R + 1, dev);
@@ -1658,15 +1660,37 @@ static int compact_rows(Slot* ctx, const tsdbhip_rows_desc* d, tsdbhip_rows_out*
         a.out_keep = scratch<int32_t>(ctx, "c_ok", R);
       }
     }
-    a.counters = scratch<uint32_t>(ctx, "c_cnt", 4, true);
+    a.counters = scratch<uint32_t>(ctx, "c_cnt", 8, true);
     a.list_lds = scratch<uint32_t>(ctx, "c_llds", R);
     a.list_big = scratch<uint32_t>(ctx, "c_lbig", R);
     a.big_cells = scratch<uint64_t>(ctx, "c_cells", qext / 2 + R + 1);
-    HIPCHK(hipEventRecord(ctx->ev[0], ctx->stream));
-    HIPCHK(hipEventRecord(ctx->ev[8], ctx->stream));
-    hipLaunchKernelGGL(k_compact_tiles, dim3(grid_for(R, CT_ROWS, 1u << 16)), dim3(256), 0, ctx->stream, a);
+    hipStream_t st = ctx->stream;
+    HIPCHK(hipEventRecord(ctx->ev[0], st));
+    const char* cm = getenv("TSDBHIP_COMPACT");
+    if (cm && !strcmp(cm, "tiles")) {  // (every row through the LDS tiles: the A/B reference)
+      HIPCHK(hipEventRecord(ctx->ev[8], st));
+      HIPCHK(hipEventRecord(ctx->ev[4], st));
+      HIPCHK(hipEventRecord(ctx->ev[2], st));
+      hipLaunchKernelGGL(k_compact_tiles, dim3(grid_for(R, CT_ROWS, 1u << 16)), dim3(256), 0, st, a);
+      HIPCHK(hipEventRecord(ctx->ev[9], st));
+      HIPCHK(hipEventRecord(ctx->ev[3], st));
+    } else {
+      // plain rows: qualifiers copied, classified (a row per quarter wave,
+      // flag fix-ups in place, legacy-float holes recorded), values copied
+      // around the holes; the other rows through the LDS row kernel
+      a.tile_bad = scratch<uint8_t>(ctx, "c_tbad", R / CC_ROWS + 1);
+      a.row_holes = scratch<uint2>(ctx, "c_holes", R);
+      HIPCHK(hipEventRecord(ctx->ev[8], st));
+      hipLaunchKernelGGL(k_compact_quals, dim3(grid_for(R, CC_ROWS, 1u << 16)), dim3(256), 0, st, a);
+      HIPCHK(hipEventRecord(ctx->ev[4], st));
+      hipLaunchKernelGGL(k_compact_classify, dim3(grid_for(R, 16, 1u << 16)), dim3(256), 0, st, a);
+      HIPCHK(hipEventRecord(ctx->ev[2], st));
+      hipLaunchKernelGGL(k_compact_vals, dim3(grid_for(R, 16, 1u << 16)), dim3(256), 0, st, a);
+      HIPCHK(hipEventRecord(ctx->ev[9], st));
+      hipLaunchKernelGGL(k_compact_rows, dim3(grid_for(R, CR_RANGE, 1u << 14)), dim3(256), 0, st, a);
+      HIPCHK(hipEventRecord(ctx->ev[3], st));
+    }
     HIPCHK(hipGetLastError());
-    HIPCHK(hipEventRecord(ctx->ev[9], ctx->stream));
     hipLaunchKernelGGL(k_compact_complex<true>, dim3(1024), dim3(256), 0, ctx->stream, a);
     hipLaunchKernelGGL(k_compact_complex<false>, dim3(256), dim3(256), 0, ctx->stream, a);
     if (a.out_write) hipLaunchKernelGGL(k_compact_dups, dim3(grid_for(R, 4 * WAVE, 4096)), dim3(256), 0, ctx->stream, a);
@@ -1694,10 +1718,11 @@ static int compact_rows(Slot* ctx, const tsdbhip_rows_desc* d, tsdbhip_rows_out*
     }
     tsdbhip_timing t = {};
     t.total_ms = ev_ms(ctx->ev[0], ctx->ev[1]);
-    t.hot_ms = ev_ms(ctx->ev[8], ctx->ev[9]);
+    t.hot_ms = ev_ms(ctx->ev[8], ctx->ev[4]) + ev_ms(ctx->ev[2], ctx->ev[9]);  // k_compact_quals + k_compact_vals (tiles: k_compact_tiles)
     t.hot_kernel = TSDBHIP_HOT_COMPACT;
-    t.decode_ms = t.hot_ms;                                 // k_compact_rows
-    t.reduce_ms = ev_ms(ctx->ev[9], ctx->ev[1]);            // k_compact_complex
+    t.decode_ms = ev_ms(ctx->ev[4], ctx->ev[2]);  // k_compact_classify
+    t.grid_ms = ev_ms(ctx->ev[9], ctx->ev[3]);    // k_compact_rows
+    t.reduce_ms = ev_ms(ctx->ev[3], ctx->ev[1]);  // k_compact_complex + k_compact_dups
     ctx->timing = t;
     out->qual_used = qext;
     out->val_used = vext + R;

@@ -120,9 +120,8 @@ static int spangroup_run_batch(Slot* ctx, const tsdbhip_sg_desc* d, uint32_t G, 
   const uint32_t* row_val_len = dd.row_val_len;
 
   struct Small {
-    int32_t err;
+    unsigned long long err;  // err_raise key, ERR_NONE: none
     uint32_t gflags[2];
-    uint32_t pad;
     unsigned long long range[2];
     unsigned long long fstar;
     unsigned long long n_input;
@@ -134,6 +133,7 @@ static int spangroup_run_batch(Slot* ctx, const tsdbhip_sg_desc* d, uint32_t G, 
   Small* sm = scratch<Small>(ctx, "b_small", 1);
   {
     Small init = {};
+    init.err = ERR_NONE;
     init.range[0] = ~0ull;
     init.bound[0] = ~0ull;
     std::memcpy(ctx->host_small, &init, sizeof init);
@@ -183,7 +183,7 @@ static int spangroup_run_batch(Slot* ctx, const tsdbhip_sg_desc* d, uint32_t G, 
   }
   Small h;
   readback(ctx, &h, sm, sizeof h);
-  if (h.err) return batch_one_by_one(ctx, dd, G, gss, outs);
+  if (h.err != ERR_NONE) return batch_one_by_one(ctx, dd, G, gss, outs);
   const uint32_t n_kept = (uint32_t)h.n_kept;
   hipLaunchKernelGGL(k_group_stats, dim3(std::min<uint32_t>(std::max<uint32_t>(G, 1), 65536)), dim3(256), 0, st,
                      gss_d, G, S, n_kept, sp_kept, kidx, sp_ncells, sp_first, sp_last, kgrp, stat);
@@ -309,7 +309,7 @@ static int spangroup_run_batch(Slot* ctx, const tsdbhip_sg_desc* d, uint32_t G, 
   }
   HIPCHK(hipEventRecord(ctx->ev[2], st));
   readback(ctx, &h, sm, sizeof h);  // sync 2: decode errors, global int/float flags
-  if (h.err) return batch_one_by_one(ctx, dd, G, gss, outs);
+  if (h.err != ERR_NONE) return batch_one_by_one(ctx, dd, G, gss, outs);
   const bool anyf = h.gflags[0] != 0, anyi = h.gflags[1] != 0;
 
   // ---- per-group summary and segmented union grids ----
@@ -373,7 +373,7 @@ static int spangroup_run_batch(Slot* ctx, const tsdbhip_sg_desc* d, uint32_t G, 
   };
   read_groups();  // sync 3
   readback(ctx, &h, sm, sizeof h);
-  if (h.err) return batch_one_by_one(ctx, dd, G, gss, outs);
+  if (h.err != ERR_NONE) return batch_one_by_one(ctx, dd, G, gss, outs);
   tm.n_grid = T_all;
 
   // ---- reduce: one k_reduce_seg + k_finalize_seg per reduce mode present,

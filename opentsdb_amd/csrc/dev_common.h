@@ -27,6 +27,20 @@ DEVI int64_t d2l(double d) {
 DEVI double bitsd(int64_t b) { return __longlong_as_double(b); }
 DEVI int64_t dbits(double d) { return __double_as_longlong(d); }
 
+// ---- errors: the first in the reference's evaluation order wins ----------
+// key = stage | order within the stage | -code, reduced with atomicMin (and
+// the same MIN across ranks). Stages: 0 Span.addRow while TsdbQuery.findSpans
+// scans rows (row-key order: base time, then span), 1 SpanGroup.add in span
+// order (TsdbQuery.java:301-307), 2 iteration.
+#define ERR_NONE (~0ull)
+DEVI void err_raise(unsigned long long* e, uint32_t stage, uint64_t order, int code) {
+  atomicMin(e, ((unsigned long long)stage << 62) | ((order & ((1ull << 54) - 1)) << 8) |
+                   (unsigned long long)(uint8_t)(-code));
+}
+DEVI uint64_t err_scan_order(uint32_t base_time, uint32_t span) {
+  return ((uint64_t)base_time << 22) | (span < (1u << 22) ? span : (1u << 22) - 1);
+}
+
 // ---- wave helpers ----------------------------------------------------------
 DEVI int lane_id() { return __lane_id(); }
 DEVI uint64_t ballot(bool p) { return __ballot(p); }

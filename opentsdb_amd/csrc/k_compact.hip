@@ -34,6 +34,7 @@ constexpr uint32_t CQ_SLOTS = 4096;      // 12-bit time deltas (Const.java:26)
 
 // row status (include/tsdbhip.h)
 constexpr uint8_t CQ_NONE = 0, CQ_SINGLE = 1, CQ_TRIVIAL = 2, CQ_COMPLEX = 3, CQ_ERROR = 4, CQ_OOB = 5;
+constexpr uint8_t CQ_PENDING = 0xFF;  // (k_compact_classify: not plain, for k_compact_rows)
 
 struct CompactArgs {
   uint64_t n_rows, n_kvs;
@@ -60,6 +61,8 @@ struct CompactArgs {
   uint32_t* list_lds;   // complex rows with <= CQ_LDS_CELLS cells
   uint32_t* list_big;   // the others
   uint64_t* big_cells;  // scratch: row r's cells at (row_qual_off[r]-row_qual_off[0])/2 + r
+  uint8_t* tile_bad;    // [tile] k_compact_quals skipped the tile (offsets out of bounds)
+  uint2* row_holes;     // [row] k_compact_classify: output positions of the first two legacy floats, ~0u none
 };
 
 // fixQualifierFlags (CompactionQueue.java:490-499), byte arithmetic.
@@ -718,9 +721,11 @@ DEVI uint8_t cq_complex_lds(TileLds& L, const RowLds& p, uint32_t nk, uint32_t n
   return CQ_COMPLEX;
 }
 
-// One row, LDS -> LDS (same classification as cq_row_global).
-DEVI void cq_row_lds(const CompactArgs& a, uint64_t r, const RowHdr& h, TileLds& L, const RowLds& p,
-                     uint32_t* keys, uint32_t* pay, uint32_t* runs, int lane) {
+// One row, LDS -> LDS (same classification as cq_row_global). Returns false
+// when the row went to the block kernels (complexCompact of > CT_SORT cells).
+DEVI bool cq_row_lds(const CompactArgs& a, uint64_t r, const RowHdr& h, TileLds& L, const RowLds& p,
+                     uint32_t* keys, uint32_t* pay, uint32_t* runs, int lane, uint32_t* qlen_out = nullptr,
+                     uint32_t* vlen_out = nullptr) {
   const uint32_t nk = (uint32_t)h.nk;
   uint32_t qcar = 0, vcar = 0, nvalid = 0, nmulti = 0, ncells = 0;
   int last_delta = -1;
@@ -804,7 +809,7 @@ DEVI void cq_row_lds(const CompactArgs& a, uint64_t r, const RowHdr& h, TileLds&
         if (ncells <= CQ_LDS_CELLS) a.list_lds[atomicAdd(&a.counters[0], 1u)] = (uint32_t)r;
         else a.list_big[atomicAdd(&a.counters[1], 1u)] = (uint32_t)r;
       }
-      return;
+      return false;
     }
   } else if (!any_fix && !any_junk) {
     // trivialCompact changes nothing: qualifiers and values pass through
@@ -848,6 +853,11 @@ DEVI void cq_row_lds(const CompactArgs& a, uint64_t r, const RowHdr& h, TileLds&
     ovl = nv + 1;
   }
   if (lane == 0) cq_finish(a, r, st, oql, ovl);
+  if (qlen_out) {
+    *qlen_out = oql;
+    *vlen_out = ovl;
+  }
+  return true;
 }
 
 __global__ void __launch_bounds__(256) k_compact_tiles(CompactArgs a) {
@@ -1029,5 +1039,526 @@ __global__ void __launch_bounds__(256) k_compact_dups(CompactArgs a) {
       cq_dup_row(a, g * WAVE + l, lane);
     }
   }
+}
+
+// ===========================================================================
+// The plain-row path. A row is plain when it holds >= 2 KVs, every qualifier
+// is 2 bytes, every value has 1..8 bytes, legacy floats are fixable and the
+// time deltas strictly increase in KV order: trivialCompact's output is then
+// the row's qualifier and value bytes with two local fix-ups, plus the 0 meta
+// byte (CompactionQueue.java:286-351, 450-474, fixes :490-544):
+//   * fixQualifierFlags: a qualifier's length bits become the fixed value's
+//     length - 1 (one byte patched in place);
+//   * fixFloatingPointValue: a legacy float's 8-byte value 00000000 || bits
+//     loses its 4-byte zero prefix (the row's later value bytes move down).
+// With the output placement of tsdbhip.h the qualifier stream is copied in
+// place and the value stream shifted by one byte per row. Four launches:
+//   k_compact_quals     the qualifier bytes, in place, 16-B stores
+//   k_compact_classify  one row per 16-lane quarter wave: the plain test;
+//                       flag fix-ups patched over the copied qualifiers; the
+//                       holes (output positions of the first two legacy
+//                       floats) recorded; plain rows get status / lengths /
+//                       write decision, the others CQ_PENDING
+//   k_compact_vals      the value bytes around the holes, 16-B stores
+//   k_compact_rows      the CQ_PENDING rows (gathered per 256-row range)
+//                       through the LDS row logic of k_compact_tiles
+// ===========================================================================
+constexpr uint32_t CC_ROWS = 64;  // rows per copy tile (one block)
+#ifndef CP_U
+#define CP_U 4  // KV batches of 16 per row whose loads are in flight together
+#endif
+
+// Inclusive scan inside each 16-lane DPP row (= one quarter of the wave).
+DEVI uint32_t quarter_incl_scan_u32(uint32_t x) {
+  x += dpp_u32<0x111, 0xf>(x);
+  x += dpp_u32<0x112, 0xf>(x);
+  x += dpp_u32<0x114, 0xf>(x);
+  x += dpp_u32<0x118, 0xf>(x);
+  return x;
+}
+// lane l gets lane l-1's x inside its quarter; a quarter's lane 0 gets `old`
+DEVI uint32_t quarter_shr1_u32(uint32_t x, uint32_t old) {
+  return (uint32_t)__builtin_amdgcn_update_dpp((int)old, (int)x, 0x111, 0xf, 0xf, false);
+}
+
+// Runs after k_compact_quals. One row per 16-lane quarter of a wave, its KVs
+// 16 x CP_U at a time (every load of a batch in flight together). Qualifier
+// fix-ups are written while the row's later KVs are still unseen: a row that
+// turns out not plain gets them too, inside its own output range, where
+// k_compact_rows then writes its real result.
+__global__ void __launch_bounds__(256) k_compact_classify(CompactArgs a) {
+  const int lane = lane_id(), sub = lane & 15, qtr = lane >> 4;
+  const uint64_t nw = (uint64_t)gridDim.x * 4;
+  const uint64_t Q0 = a.row_qual_off[0], V0 = a.row_val_off[0];
+  const uint64_t n_quads = (a.n_rows + 3) / 4;
+  for (uint64_t g = (uint64_t)blockIdx.x * 4 + threadIdx.x / WAVE; g < n_quads; g += nw) {
+    const uint64_t r = 4 * g + qtr;
+    const bool own = r < a.n_rows;
+    uint64_t kv = 0, kv_n = 0, qo = 0, qo_n = 0, vo = 0, vo_n = 0;
+    if (own) {
+      kv = a.row_kv_start[r];
+      kv_n = a.row_kv_start[r + 1];
+      qo = a.row_qual_off[r];
+      qo_n = a.row_qual_off[r + 1];
+      vo = a.row_val_off[r];
+      vo_n = a.row_val_off[r + 1];
+    }
+    // the row's own output ranges, when its offsets are sane (disjoint from
+    // every other row's then)
+    const bool sane = own && kv_n >= kv && kv_n <= a.n_kvs && qo_n >= qo && vo_n >= vo && qo >= Q0 && vo >= V0 &&
+                      qo_n <= a.qual_nbytes && vo_n <= a.val_nbytes && qo_n - Q0 <= a.qcap &&
+                      vo_n - V0 + r + 1 <= a.vcap && vo_n - vo < (1ull << 32);
+    const uint64_t nk = sane ? kv_n - kv : 0;
+    bool plain = sane && nk >= 2 && qo_n - qo == 2 * nk;
+    const uint64_t nkw = plain ? nk : 0;  // KVs walked
+    const uint64_t ovo = vo - V0 + r;
+    uint32_t vcar = 0, legs = 0, q_prev = 0;  // (uniform per quarter)
+    uint32_t h0 = ~0u, h1 = ~0u;  // output positions of the row's holes (legacy floats)
+    bool bad = false;
+    for (uint64_t i0 = 0; ballot(i0 < nkw); i0 += 16 * CP_U) {
+      uint32_t ql_[CP_U], vl_[CP_U], q_[CP_U];
+#pragma unroll
+      for (int u = 0; u < CP_U; u++) {
+        const uint64_t i = i0 + 16 * u + sub;
+        ql_[u] = vl_[u] = q_[u] = 0;
+        if (i < nkw) {
+          ql_[u] = a.kv_qual_len[kv + i];
+          vl_[u] = a.kv_val_len[kv + i];
+          q_[u] = ld_q16(a.qual, qo + 2 * i);  // (the qualifier if every one has 2 bytes)
+        }
+      }
+      uint32_t voff_[CP_U], fl_[CP_U];  // fl: 1 bad, 2 legacy, nleg << 2
+#pragma unroll
+      for (int u = 0; u < CP_U; u++) {
+        const uint64_t i = i0 + 16 * u + sub;
+        const bool act = i < nkw;
+        const uint32_t ql = ql_[u], vl = vl_[u], q = q_[u];
+        bool kbad = act && (ql != 2 || vl == 0 || vl > 8);
+        const bool legacy = act && !kbad && cq_legacy(q & 0xFFu, vl);  // floatingPointValueToFix :510-515
+        const uint32_t incl = quarter_incl_scan_u32(act ? vl : 0u);
+        const uint32_t vin = vcar + incl - (act ? vl : 0u);  // value offset inside the row
+        const uint64_t lm = (ballot(legacy) >> (16 * qtr)) & 0xFFFFu;
+        const uint32_t nleg = legs + (uint32_t)__popcll(lm & ((1u << sub) - 1));
+        const uint32_t qb = quarter_shr1_u32(q, q_prev);
+        if (act && !kbad) kbad = (uint64_t)vin + vl > vo_n - vo || (i > 0 && (q >> 4) <= (qb >> 4));
+        voff_[u] = vin;
+        fl_[u] = (kbad ? 1u : 0u) | (legacy ? 2u : 0u);
+        if (ballot(legacy)) {  // the holes: output positions of the first two legacy floats
+          const uint32_t P = vin - 4 * nleg;
+          const uint32_t f0 = (uint32_t)__builtin_ctz((uint32_t)lm | 0x10000u);
+          const uint32_t lm1 = (uint32_t)lm & ((uint32_t)lm - 1);
+          const uint32_t f1 = (uint32_t)__builtin_ctz(lm1 | 0x10000u);
+          const uint32_t p0 = (uint32_t)__shfl((int)P, (lane & 48) | (int)(f0 & 15));
+          const uint32_t p1 = (uint32_t)__shfl((int)P, (lane & 48) | (int)(f1 & 15));
+          if (lm) {
+            if (legs == 0) {
+              h0 = p0;
+              if (lm1) h1 = p1;
+            } else if (legs == 1) {
+              h1 = p0;
+            }
+          }
+        }
+        vcar += (uint32_t)__shfl((int)incl, lane | 15);
+        legs += (uint32_t)__popcll(lm);
+        q_prev = (uint32_t)__shfl((int)q, lane | 15);
+      }
+      // legacy floats: the 4-byte zero prefix (fixFloatingPointValue :530-544)
+      uint32_t pre_[CP_U];
+#pragma unroll
+      for (int u = 0; u < CP_U; u++) {
+        pre_[u] = 0;
+        if ((fl_[u] & 3u) == 2u) {
+          const uint64_t vf = vo + voff_[u];
+          pre_[u] = a.val[vf] | a.val[vf + 1] | a.val[vf + 2] | a.val[vf + 3];
+        }
+      }
+      // the qualifier fix-ups (speculatively), rows with a bad KV
+#pragma unroll
+      for (int u = 0; u < CP_U; u++) {
+        const uint64_t i = i0 + 16 * u + sub;
+        const bool act = i < nkw;
+        const bool legacy = (fl_[u] & 2u) != 0;
+        const bool kbad = act && ((fl_[u] & 1u) || pre_[u] != 0);
+        if (act && !kbad) {
+          const uint32_t q = q_[u];
+          const uint8_t f = (uint8_t)cq_fixq(q & 0xFFu, legacy ? 4u : vl_[u]);  // fixQualifierFlags :490-499
+          if (f != (uint8_t)q) a.oq[qo - Q0 + 2 * i + 1] = f;
+        }
+        if ((ballot(kbad) >> (16 * qtr)) & 0xFFFFu) bad = true;
+      }
+    }
+    if (plain) plain = !bad && legs <= 2 && vcar == vo_n - vo && !a.tile_bad[r / CC_ROWS];
+    if (sub == 0 && plain) {
+      const uint64_t vx = vo_n - vo;
+      a.out_qoff[r] = qo - Q0;
+      a.out_voff[r] = ovo;
+      a.row_holes[r] = make_uint2(h0, h1);
+      cq_finish(a, r, CQ_TRIVIAL, (uint32_t)(qo_n - qo), (uint32_t)(vx - 4ull * legs + 1));
+    }
+    if (sub == 0 && own && !plain) {
+      a.status[r] = CQ_PENDING;  // (to the LDS row kernel)
+      a.row_holes[r] = make_uint2(~0u, ~0u);
+    }
+  }
+}
+
+// 16 bytes at src + x (any alignment) from two aligned 16-B loads (the
+// buffers carry >= 16 bytes of slack past their ends).
+DEVI uint4 ld16_any(const uint8_t* src, uint64_t x) {
+  const uintptr_t pa = (uintptr_t)(src + x);
+  const uint4* p = (const uint4*)(pa & ~(uintptr_t)15);
+  const uint32_t sh = (uint32_t)(pa & 15);
+  const uint4 A = p[0];
+  if (sh == 0) return A;
+  const uint4 B = p[1];
+  const uint32_t w[8] = {A.x, A.y, A.z, A.w, B.x, B.y, B.z, B.w};
+  const uint32_t s4 = sh >> 2, sb = sh & 3;
+  uint32_t v[5];
+#pragma unroll
+  for (int i = 0; i < 5; i++) v[i] = s4 == 0 ? w[i] : s4 == 1 ? w[i + 1] : s4 == 2 ? w[i + 2] : w[i + 3];
+  return make_uint4(__builtin_amdgcn_alignbyte(v[1], v[0], sb), __builtin_amdgcn_alignbyte(v[2], v[1], sb),
+                    __builtin_amdgcn_alignbyte(v[3], v[2], sb), __builtin_amdgcn_alignbyte(v[4], v[3], sb));
+}
+
+// Select of two 16-byte vectors: bytes [0, p) from A, byte p = 0 when zp,
+// the rest from B (p in [0, 16]).
+DEVI uint4 cq_funnel(const uint4& A, const uint4& B, int p, bool zp) {
+  const uint32_t av[4] = {A.x, A.y, A.z, A.w}, bv[4] = {B.x, B.y, B.z, B.w};
+  uint32_t ov[4];
+#pragma unroll
+  for (int w = 0; w < 4; w++) {
+    const int d = p - 4 * w;  // p's index inside dword w
+    const uint32_t mA = d >= 4 ? ~0u : d <= 0 ? 0u : (1u << (8 * d)) - 1;
+    const uint32_t mZ = (zp && d >= 0 && d < 4) ? 0xFFu << (8 * d) : 0u;
+    ov[w] = (av[w] & mA) | (bv[w] & ~(mA | mZ));
+  }
+  return make_uint4(ov[0], ov[1], ov[2], ov[3]);
+}
+
+// Qualifiers of a tile of CC_ROWS rows copied in place (16-B stores, byte
+// stores only at the tile's two edges); tiles with offsets out of bounds are
+// flagged in tile_bad and left to the row kernel.
+__global__ void __launch_bounds__(256) k_compact_quals(CompactArgs a) {
+  const int tid = threadIdx.x;
+  const uint64_t Q0 = a.row_qual_off[0];
+  const uintptr_t oq_abs = (uintptr_t)a.oq;
+  for (uint64_t t = blockIdx.x; t * CC_ROWS < a.n_rows; t += gridDim.x) {
+    const uint64_t r0 = t * CC_ROWS;
+    const uint32_t nr = (uint32_t)min((uint64_t)CC_ROWS, a.n_rows - r0);
+    const uint64_t qa = a.row_qual_off[r0], qb = a.row_qual_off[r0 + nr];
+    const bool skip = qa < Q0 || qb < qa || qb > a.qual_nbytes || qb - Q0 > a.qcap;
+    if (tid == 0) a.tile_bad[t] = skip;
+    if (skip) continue;
+    const uintptr_t d0 = oq_abs + (qa - Q0), d1 = oq_abs + (qb - Q0);
+    for (uintptr_t c = (d0 & ~(uintptr_t)15) + 16ull * tid; c < d1; c += 16ull * 256) {
+      const uint64_t x = qa + (c - d0);  // input offset of byte c (c may precede d0)
+      if (c >= d0 && c + 16 <= d1) {
+        *(uint4*)c = ld16_any(a.qual, x);
+      } else {
+        for (int j = 0; j < 16; j++)
+          if (c + j >= d0 && c + j < d1) *(uint8_t*)(c + j) = a.qual[x + j];
+      }
+    }
+  }
+}
+
+// Values, after k_compact_classify: row r's output (region [s, e) = its input
+// value bytes + 1, placed at row_val_off[r] - V0 + r) is its input with the
+// 4-byte zero prefix of each legacy float removed (the row's holes: output
+// positions h, in(y) = row_val_off[r] + y + 4 * #{h <= y}), then its meta
+// byte 0; the 4 * holes bytes after the meta byte are unused. One row per
+// 16-lane quarter wave; every aligned 16-B output chunk is written once, by
+// the row holding its first byte (with the next row's head when the row ends
+// inside it). Chunks crossing two row ends or two holes go byte by byte.
+// Rows with offsets out of bounds write nothing (the row kernel fails the
+// call on them).
+struct CvRow {
+  uint64_t s, e, in;  // output region [s, e), input offset of the first byte
+  uint32_t h0, h1;
+  bool ok;
+};
+DEVI CvRow cv_row(const CompactArgs& a, uint64_t r, uint64_t V0) {
+  CvRow w;
+  const uint64_t v0 = a.row_val_off[r], v1 = a.row_val_off[r + 1];
+  const uint2 h = a.row_holes[r];
+  w.ok = v0 >= V0 && v1 >= v0 && v1 <= a.val_nbytes && v1 - V0 + r + 1 <= a.vcap;
+  w.s = v0 - V0 + r;
+  w.e = v1 - V0 + r + 1;
+  w.in = v0;
+  w.h0 = h.x;
+  w.h1 = h.y;
+  return w;
+}
+DEVI uint64_t cv_meta(const CvRow& w) { return w.e - 1 - 4ull * ((w.h0 != ~0u) + (w.h1 != ~0u)); }
+
+__global__ void __launch_bounds__(256) k_compact_vals(CompactArgs a) {
+  const int lane = lane_id(), sub = lane & 15, qtr = lane >> 4;
+  const uint64_t nw = (uint64_t)gridDim.x * 4;
+  const uint64_t V0 = a.row_val_off[0];
+  const uint64_t n_quads = (a.n_rows + 3) / 4;
+  const uintptr_t ov_abs = (uintptr_t)a.ov;
+  for (uint64_t g = (uint64_t)blockIdx.x * 4 + threadIdx.x / WAVE; g < n_quads; g += nw) {
+    const uint64_t r = 4 * g + qtr;
+    CvRow w = {}, n = {};
+    uint64_t nch = 0;
+    uintptr_t c0 = 0;
+    if (r < a.n_rows) {
+      w = cv_row(a, r, V0);
+      if (r + 1 < a.n_rows) n = cv_row(a, r + 1, V0);
+      if (w.ok) {  // chunks whose first byte is in [s, e)
+        c0 = (ov_abs + w.s + 15) & ~(uintptr_t)15;
+        nch = ov_abs + w.e > c0 ? (ov_abs + w.e - c0 + 15) / 16 : 0;
+      }
+    }
+    const uint64_t m = cv_meta(w);
+    for (uint64_t i0 = 0; ballot(i0 < nch); i0 += 16) {
+      const uint64_t k = i0 + sub;
+      if (k >= nch) continue;
+      const uintptr_t c = c0 + 16 * k;
+      const uint64_t o = c - ov_abs, y0 = o - w.s, x = w.in + y0;
+      const uint64_t xa = x + 4 * ((w.h0 <= y0) + (w.h1 <= y0));
+      const bool in0 = w.h0 > y0 && w.h0 < y0 + 16, in1 = w.h1 > y0 && w.h1 < y0 + 16;  // holes inside
+      bool done = false;
+      if (o + 16 <= m && !(in0 && in1)) {
+        if (!in0 && !in1) *(uint4*)c = ld16_any(a.val, xa);  // one source
+        else  // one hole inside: from it on, 4 bytes further down the input
+          *(uint4*)c = cq_funnel(ld16_any(a.val, xa), ld16_any(a.val, xa + 4), (int)((in0 ? w.h0 : w.h1) - y0), false);
+        done = true;
+      } else if (m < o + 16 && !in0 && !in1) {
+        // the meta byte at m - o; then the unused bytes; then the next row
+        // (one byte further down the input; 4 more when its first KV is a
+        // legacy float), which must have no hole and no end inside the chunk
+        bool ok = true;
+        uint64_t xb = x - 1;
+        if (w.e < o + 16) {
+          const uint64_t L = o + 16 - w.e;
+          ok = r + 1 < a.n_rows && n.ok && !(n.h0 > 0 && n.h0 < L) && !(n.h1 > 0 && n.h1 < L) && cv_meta(n) >= o + 16;
+          if (n.h0 == 0) xb += 4;
+        }
+        if (ok && xb + 1 != 0) {  // (B's source starts inside the buffer)
+          *(uint4*)c = cq_funnel(ld16_any(a.val, xa), ld16_any(a.val, xb), (int)(m - o), true);
+          done = true;
+        }
+      }
+      if (!done) {  // byte by byte, walking the rows
+        CvRow u = w;
+        uint64_t ru = r;
+        for (int b = 0; b < 16; b++) {
+          const uint64_t ob = o + b;
+          while (ob >= u.e && u.ok) {
+            if (++ru >= a.n_rows) u.ok = false;
+            else u = cv_row(a, ru, V0);
+          }
+          if (!u.ok) break;
+          const uint64_t mu = cv_meta(u);
+          if (ob > mu) continue;  // (unused)
+          const uint64_t y = ob - u.s;
+          *(uint8_t*)(c + b) = ob == mu ? (uint8_t)0 : a.val[u.in + y + 4 * ((u.h0 <= y) + (u.h1 <= y))];
+        }
+      }
+    }
+  }
+}
+
+// The listed (non-plain) rows through cq_row_lds, CT_ROWS per block at a
+// time, each row staged into its own LDS ranges (16-B loads) and written back
+// from its own output ranges (16-B stores inside the row); rows over the LDS
+// budget go through cq_row_global.
+DEVI void cq_unstage_wave(uint8_t* dst, const uint8_t* lds, uint32_t i0, uint64_t b0, uint64_t b1, int lane) {
+  if (b1 <= b0) return;
+  const uintptr_t s = (uintptr_t)(dst + b0), e = (uintptr_t)(dst + b1);
+  const uintptr_t a0 = (s + 15) & ~(uintptr_t)15, a1 = e & ~(uintptr_t)15;  // whole chunks [a0, a1)
+  if (a0 < a1) {
+    for (uintptr_t cs = a0 + 16ull * lane; cs < a1; cs += 16ull * WAVE)
+      *(uint4*)cs = *(const uint4*)(lds + i0 + (cs - s));
+  }
+  // the partial chunks at either end, one byte per lane (lanes 0-15 head,
+  // 16-31 tail; one range when the row lies inside a single chunk)
+  const uintptr_t h1 = a0 < e ? a0 : e;
+  const uintptr_t t0 = a1 > h1 ? a1 : h1;
+  uintptr_t x = 0;
+  if (lane < 16) x = s + lane;
+  else if (lane < 32) x = t0 + (lane - 16);
+  if ((lane < 16 && x < h1) || (lane >= 16 && lane < 32 && x < e)) dst[x - (uintptr_t)dst] = lds[i0 + (x - s)];
+}
+DEVI uint32_t cq_need(uint64_t len) { return (uint32_t)((len + 15 + 15) & ~15ull); }  // staged: head <= 15
+
+#ifndef CR_RANGE
+#define CR_RANGE 256u  // rows scanned for CQ_PENDING per block iteration
+#endif
+
+__global__ void __launch_bounds__(256) k_compact_rows(CompactArgs a) {
+  __shared__ TileLds L;
+  __shared__ RowHdr s_h[CT_ROWS];
+  __shared__ RowLds s_p[CT_ROWS];
+  __shared__ uint32_t s_fit[CT_ROWS];
+  // staging segments, l = 4 * row + stream (qualifiers, values, qualifier
+  // lengths, value lengths): aligned source, LDS byte offset, first chunk
+  __shared__ const uint4* s_src[4 * CT_ROWS];
+  __shared__ uint32_t s_dst[4 * CT_ROWS], s_c0[4 * CT_ROWS + 1];
+  __shared__ uint32_t s_list[CR_RANGE], s_wn[4];
+  static_assert(4 * CT_ROWS == WAVE, "one staging segment per lane of wave 0");
+  const int tid = threadIdx.x, lane = lane_id(), w = tid / WAVE;
+  const uint64_t Q0 = a.row_qual_off[0], V0 = a.row_val_off[0];
+  uint8_t* const Lb = (uint8_t*)&L;
+  if (tid == 0) L.n_complex = 0;
+  for (uint64_t rb = (uint64_t)blockIdx.x * CR_RANGE; rb < a.n_rows; rb += (uint64_t)gridDim.x * CR_RANGE) {
+    // ---- the range's CQ_PENDING rows, in row order, into s_list ----
+    __syncthreads();  // (the previous range's list consumed)
+    uint32_t pend[CR_RANGE / 256], wpos = 0;
+#pragma unroll
+    for (int u = 0; u < (int)(CR_RANGE / 256); u++) {
+      const uint64_t r = rb + (uint64_t)w * (CR_RANGE / 4) + u * WAVE + lane;  // (wave w: a quarter of the range)
+      const bool pd = r < a.n_rows && a.status[r] == CQ_PENDING;
+      const uint64_t m = ballot(pd);
+      pend[u] = pd ? wpos + (uint32_t)__popcll(m & lanemask_lt(lane)) : ~0u;
+      wpos += (uint32_t)__popcll(m);
+    }
+    if (lane == 0) s_wn[w] = wpos;
+    __syncthreads();
+    uint32_t woff = 0;
+    for (int v = 0; v < w; v++) woff += s_wn[v];
+    const uint32_t n = s_wn[0] + s_wn[1] + s_wn[2] + s_wn[3];
+#pragma unroll
+    for (int u = 0; u < (int)(CR_RANGE / 256); u++)
+      if (pend[u] != ~0u) s_list[woff + pend[u]] = (uint32_t)(rb + (uint64_t)w * (CR_RANGE / 4) + u * WAVE + lane);
+    const uint32_t* list = s_list;
+  for (uint32_t t = 0; t * CT_ROWS < n; t++) {
+    const uint32_t nr = min((uint32_t)CT_ROWS, n - t * CT_ROWS);
+    __syncthreads();  // (the previous tile's LDS consumed; s_list written)
+    if (w == 0) {
+      // ---- LDS ranges of each row, in order, while they fit ----
+      RowHdr h = {};
+      uint32_t nq = 0, nv = 0, nk = 0, noq = 0, nov = 0;
+      bool ok = false;
+      if ((uint32_t)lane < nr) {
+        h = cq_row(a, list[t * CT_ROWS + lane]);
+        s_h[lane] = h;
+        const uint32_t phq = (uint32_t)((uintptr_t)(a.oq + h.oqo) & 15u);
+        const uint32_t phv = (uint32_t)((uintptr_t)(a.ov + h.ovo) & 15u);
+        const uint64_t ql = h.qe - h.qs, vl = h.ve - h.vs;
+        ok = h.ok && h.qe >= h.qs && h.ve >= h.vs && ql <= CT_QB && vl <= CT_VB && h.nk <= CT_KB;
+        if (ok) {
+          nq = cq_need(ql);
+          nv = cq_need(vl);
+          nk = cq_need(2 * h.nk);
+          noq = (uint32_t)((phq + ql + 15) & ~15ull);
+          nov = (uint32_t)((phv + vl + 1 + 15) & ~15ull);
+        }
+        h.oqo = phq;  // (kept for the output positions below)
+        h.ovo = phv;
+      }
+      uint32_t bq = 0, bv = 0, bk = 0, boq = 0, bov = 0;  // (wave-uniform)
+      RowLds p = {};
+      bool fit = false;
+      for (uint32_t j = 0; j < nr; j++) {
+        const uint32_t jq = readlane_u32(nq, j), jv = readlane_u32(nv, j), jk = readlane_u32(nk, j);
+        const uint32_t joq = readlane_u32(noq, j), jov = readlane_u32(nov, j);
+        const bool f = readlane_u32(ok, j) && bq + jq <= CT_QB && bv + jv <= CT_VB && bk + jk <= 2 * CT_KB &&
+                       boq + joq <= CT_QB && bov + jov <= CT_VB;
+        if (lane == (int)j) {
+          fit = f;
+          p.k0 = p.kv0 = bk;  // (+ each source's head, once staged)
+          p.qi = bq;
+          p.vi = bv;
+          p.qo = boq + (uint32_t)h.oqo;
+          p.vo = bov + (uint32_t)h.ovo;
+        }
+        if (f) { bq += jq; bv += jv; bk += jk; boq += joq; bov += jov; }
+      }
+      if ((uint32_t)lane < nr) {
+        s_fit[lane] = fit;
+        s_p[lane] = p;
+      }
+      wave_lds_sync();
+      // ---- staging segments ----
+      const uint32_t j = (uint32_t)lane >> 2, sg = (uint32_t)lane & 3;
+      uint32_t nch = 0, dst = 0;
+      const uint8_t* src = nullptr;
+      if (j < nr && s_fit[j]) {
+        const RowHdr hj = s_h[j];
+        const RowLds pj = s_p[j];
+        uint64_t b0, b1;
+        if (sg == 0) { src = a.qual; b0 = hj.qs; b1 = hj.qe; dst = (uint32_t)(L.qin - Lb) + pj.qi; }
+        else if (sg == 1) { src = a.val; b0 = hj.vs; b1 = hj.ve; dst = (uint32_t)(L.vin - Lb) + pj.vi; }
+        else {
+          src = (const uint8_t*)(sg == 2 ? a.kv_qual_len : a.kv_val_len);
+          b0 = 2 * hj.kb;
+          b1 = 2 * (hj.kb + hj.nk);
+          dst = (uint32_t)((sg == 2 ? L.qlen : L.vlen) - Lb) + pj.k0;
+        }
+        const uintptr_t sp = (uintptr_t)(src + b0);
+        const uint32_t head = (uint32_t)(sp & 15u);
+        nch = b1 > b0 ? (uint32_t)((head + (b1 - b0) + 15) / 16) : 0u;
+        src = (const uint8_t*)(sp - head);
+      }
+      const uint32_t inc = wave_incl_scan_u32_dpp(nch);
+      s_src[lane] = (const uint4*)src;
+      s_dst[lane] = dst;
+      s_c0[lane] = inc - nch;
+      if (lane == WAVE - 1) s_c0[WAVE] = inc;
+    }
+    __syncthreads();
+    // ---- stage the fitting rows: every 16-B chunk of every segment, four
+    // loads in flight per thread ----
+    {
+      const uint32_t total = s_c0[WAVE];
+      // (four named register sets: an indexed array of them lands in scratch)
+      auto locate = [&](uint32_t cc, const uint4*& src, uint32_t& dst) {
+        uint32_t lo = 0;  // the last segment starting at or before cc
+#pragma unroll
+        for (int st = 32; st > 0; st >>= 1)
+          if (s_c0[lo + st] <= cc) lo += st;
+        src = s_src[lo] + (cc - s_c0[lo]);
+        dst = s_dst[lo] + 16 * (cc - s_c0[lo]);
+      };
+      for (uint32_t c = tid; c < total; c += 4 * 256) {
+        const uint4 *p0 = nullptr, *p1 = nullptr, *p2 = nullptr, *p3 = nullptr;
+        uint32_t d0 = 0, d1 = 0, d2 = 0, d3 = 0;
+        const bool b0 = c < total, b1 = c + 256 < total, b2 = c + 512 < total, b3 = c + 768 < total;
+        if (b0) locate(c, p0, d0);
+        if (b1) locate(c + 256, p1, d1);
+        if (b2) locate(c + 512, p2, d2);
+        if (b3) locate(c + 768, p3, d3);
+        uint4 v0 = {}, v1 = {}, v2 = {}, v3 = {};
+        if (b0) v0 = *p0;
+        if (b1) v1 = *p1;
+        if (b2) v2 = *p2;
+        if (b3) v3 = *p3;
+        if (b0) *(uint4*)(Lb + d0) = v0;
+        if (b1) *(uint4*)(Lb + d1) = v1;
+        if (b2) *(uint4*)(Lb + d2) = v2;
+        if (b3) *(uint4*)(Lb + d3) = v3;
+      }
+    }
+    __syncthreads();
+    // ---- compact (wave per row), unstage its own output ----
+    for (uint32_t j = w; j < nr; j += 4) {
+      const uint64_t r = list[t * CT_ROWS + j];
+      const RowHdr h = s_h[j];
+      if (lane == 0) {
+        a.out_qoff[r] = h.oqo;
+        a.out_voff[r] = h.ovo;
+      }
+      if (!s_fit[j]) {
+        cq_row_global(a, r, lane);
+        continue;
+      }
+      RowLds p = s_p[j];
+      p.qi += (uint32_t)((uintptr_t)(a.qual + h.qs) & 15u);  // (cq_stage's head)
+      p.vi += (uint32_t)((uintptr_t)(a.val + h.vs) & 15u);
+      p.k0 += (uint32_t)((uintptr_t)((const uint8_t*)a.kv_qual_len + 2 * h.kb) & 15u);
+      p.kv0 += (uint32_t)((uintptr_t)((const uint8_t*)a.kv_val_len + 2 * h.kb) & 15u);
+      uint32_t oql = 0, ovl = 0;
+      if (!cq_row_lds(a, r, h, L, p, L.keys[w], L.pay[w], L.runs[w], lane, &oql, &ovl)) continue;
+      wave_lds_sync();
+      cq_unstage_wave(a.oq, L.qout, p.qo, h.oqo, h.oqo + oql, lane);
+      cq_unstage_wave(a.ov, L.vout, p.vo, h.ovo, h.ovo + ovl, lane);
+    }
+  }
+  }
+  __syncthreads();
+  if (tid == 0 && L.n_complex) atomicAdd(&a.counters[3], L.n_complex);
 }
 }  // namespace tsdb

@@ -50,7 +50,7 @@ struct DecodeArgs {
   int32_t interval;           // 0 = no downsampling
   int32_t ds_agg;
   int32_t rate;
-  int32_t* err;
+  unsigned long long* err;  // [1] first error (err_raise key)
   unsigned int* gflags;       // [0] any float E point, [1] any int E point
   unsigned long long* range;  // [0] min grid-candidate ts, [1] max E ts
   unsigned long long* fstar;  // max first-E ts over spans whose first E point is float
@@ -173,7 +173,7 @@ __device__ void span_nods_general(const DecodeArgs& a, uint32_t k) {
     if (lane == 0) {
       a.e_len[k] = len;
       a.e_bad[k] = bad;
-      if (unsorted) atomicMin(a.err, -8 /*E_UNSORTED*/);
+      if (unsorted) err_raise(a.err, 2, k, -8 /*E_UNSORTED*/);
       if (anyf) atomicOr(&a.gflags[0], 1u);
       if (anyi) atomicOr(&a.gflags[1], 1u);
     }
@@ -393,9 +393,9 @@ __device__ void span_ds_general(const DecodeArgs& a, uint32_t k, int64_t* s_bits
     }
     if (lane == 0) {
       a.e_len[k] = (uint32_t)(ecount < cap ? ecount : cap);
-      if (ecount > cap) atomicMin(a.err, -4 /*E_CAPACITY*/);
+      if (ecount > cap) err_raise(a.err, 2, k, -4 /*E_CAPACITY*/);
       a.e_bad[k] = bad;
-      if (unsorted) atomicMin(a.err, -8 /*E_UNSORTED*/);
+      if (unsorted) err_raise(a.err, 2, k, -8 /*E_UNSORTED*/);
       if (anyf) atomicOr(&a.gflags[0], 1u);
       if (anyi) atomicOr(&a.gflags[1], 1u);
     }
@@ -436,7 +436,7 @@ __global__ void __launch_bounds__(256) k_span_summary(DecodeArgs a, const uint32
   fs = block_reduce_256(fs, mx, sh_fs);
   empty = block_reduce_256(empty, mx, sh_e);
   if (threadIdx.x == 0) {
-    if (empty) atomicMin(a.err, -3 /*E_EMPTY_SPAN*/);
+    if (empty) err_raise(a.err, 2, 0, -3 /*E_EMPTY_SPAN*/);
     if (fs) atomicMax(a.fstar, (unsigned long long)fs);
   }
 }

@@ -92,7 +92,7 @@ __global__ void __launch_bounds__(256) k_group_summary(const uint64_t* e_off, co
                                                        const uint32_t* e_ts, const uint8_t* e_flt, uint32_t n_kept,
                                                        int32_t rate, int32_t flags, const uint32_t* kgrp,
                                                        const uint32_t* d_info, const uint32_t* d_x0,
-                                                       GroupDev* gd, int32_t* err) {
+                                                       GroupDev* gd, unsigned long long* err) {
   const int lane = lane_id();
   const uint32_t wave = (blockIdx.x * blockDim.x + threadIdx.x) / WAVE;
   const uint32_t nwaves = gridDim.x * blockDim.x / WAVE;
@@ -114,7 +114,7 @@ __global__ void __launch_bounds__(256) k_group_summary(const uint64_t* e_off, co
       continue;
     }
     if (len == 0) {
-      if (lane == 0) atomicMin(err, -3 /*E_EMPTY_SPAN*/);
+      if (lane == 0) err_raise(err, 1, 0, -3 /*E_EMPTY_SPAN*/);
       continue;
     }
     if (lane == 0 && !rate && e_flt[eo]) {

@@ -23,6 +23,7 @@
 #include <cstdint>
 #include <cstring>
 #include <memory>
+#include <queue>
 #include <stdexcept>
 #include <string>
 #include <vector>
@@ -898,16 +899,30 @@ int oracle_spangroup_run(const tsdbhip_sg_desc* d, tsdbhip_sg_out* out) {
   auto t1 = t0;
   t_assemble = t_iterate = 0;
   try {
+    // TsdbQuery.findSpans (TsdbQuery.java:240-285) hands the scanner's rows to
+    // Span.addRow in row-key order: metric | base_time | tags, i.e. by base
+    // time, then span (TreeMap order of the tags). A merge of the spans' row
+    // sequences (each span's own rows in the order given).
     std::vector<std::unique_ptr<Span>> spans(d->n_spans);
+    std::vector<uint64_t> next(d->n_spans);
+    using Head = std::pair<std::pair<uint32_t, uint32_t>, uint64_t>;  // ((base, span), row)
+    std::priority_queue<Head, std::vector<Head>, std::greater<Head>> heads;
     for (uint32_t s = 0; s < d->n_spans; s++) {
       spans[s].reset(new Span());
-      for (uint64_t r = d->span_row_start[s]; r < d->span_row_start[s + 1]; r++) {
-        KeyValue kv;
-        kv.base_time = d->row_base[r];
-        kv.qualifier = slice(d->qual_bytes, d->row_qual_off[r], (uint64_t)d->row_ncells[r] * 2);
-        kv.value = slice(d->val_bytes, d->row_val_off[r], d->row_val_len[r]);
-        spans[s]->addRow(kv);
-      }
+      next[s] = d->span_row_start[s];
+      if (next[s] < d->span_row_start[s + 1]) heads.push({{d->row_base[next[s]], s}, next[s]});
+    }
+    while (!heads.empty()) {
+      const Head e = heads.top();
+      heads.pop();
+      const uint64_t r = e.second;
+      const uint32_t s = e.first.second;
+      KeyValue kv;
+      kv.base_time = d->row_base[r];
+      kv.qualifier = slice(d->qual_bytes, d->row_qual_off[r], (uint64_t)d->row_ncells[r] * 2);
+      kv.value = slice(d->val_bytes, d->row_val_off[r], d->row_val_len[r]);
+      if (++next[s] < d->span_row_start[s + 1]) heads.push({{d->row_base[next[s]], s}, next[s]});
+      spans[s]->addRow(kv);
     }
     SpanGroup g;
     g.start_time = d->start_time;

@@ -188,6 +188,17 @@ def test_pack_rejects_long_kv():
 
 
 # ------------------------------------------------------------------ GPU ----
+@pytest.fixture(autouse=True, params=["plain", "tiles"])
+def compact_path(request, monkeypatch):
+    """every GPU test twice: the plain-row path (classify / shifted copy /
+    LDS row kernel, the default) and all rows through the LDS tiles"""
+    if request.param == "tiles":
+        monkeypatch.setenv("TSDBHIP_COMPACT", "tiles")
+    else:
+        monkeypatch.delenv("TSDBHIP_COMPACT", raising=False)
+    return request.param
+
+
 def assert_same(g, o):
     assert np.array_equal(g.status, o.status)
     assert np.array_equal(g.qual_len, o.qual_len) and np.array_equal(g.val_len, o.val_len)

@@ -256,6 +256,21 @@ def test_empty_and_disjoint(ctx):
     assert_same(g, o)
 
 
+def test_error_priority_scan_before_group(ctx):
+    """Two errors: an empty span (thrown by SpanGroup.add) ahead of a row that
+    Span.addRow rejects in a later span. The scanner's addRow calls all run
+    before the group is built (TsdbQuery.java:240-307), so the later span's
+    error wins."""
+    T = T0
+    bad = packing.KeyValue(T + 3600, b"", b"")
+    for spans in ([I([(T + 1, 1), (T + 2, 2)]), [], I([(T + 5, 3)]) + [bad]],
+                  [I([(T + 1, 1)]), [], [bad]]):
+        ss = packing.pack_spans(spans)
+        g, o = run_both(ctx, ss)
+        assert o.code == _abi.E_OUT_OF_BOUNDS
+        assert_same(g, o)
+
+
 def test_single_point_rate(ctx):
     T = T0
     ss = packing.pack_spans([I([(T + 100, 5)]), I([(T + 50, 1), (T + 150, 9)])])

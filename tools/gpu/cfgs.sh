@@ -1,11 +1,12 @@
 #!/bin/bash
 # GPU box: bench lines of the given configs (no CPU baseline), one JSON each
-# under gpurun_out/cfgs/. Usage: cfgs.sh c3s c2 c1 ...
+# under gpurun_out/cfgs/ (suffixed _$TAG when TAG is set). Usage: cfgs.sh c3s c2 c1 ...
 set -o pipefail
 mkdir -p gpurun_out/cfgs
 for c in "$@"; do
-  timeout -k 10 300 python bench.py --config $c --steps 10 --warmup 3 --no-cpu > gpurun_out/cfgs/$c.json 2> gpurun_out/cfgs/$c.err || exit 1
-  python - "$c" <<'PY'
+  o=$c${TAG:+_$TAG}
+  timeout -k 10 300 python bench.py --config $c --steps 10 --warmup 3 --no-cpu > gpurun_out/cfgs/$o.json 2> gpurun_out/cfgs/$o.err || exit 1
+  python - "$o" <<'PY'
 import json,sys
 d=json.load(open(f"gpurun_out/cfgs/{sys.argv[1]}.json"))
 r=d.get("roofline",{})
