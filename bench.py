@@ -120,6 +120,22 @@ def pmc_traffic(config, kernel, world):
     return (tot, os.path.relpath(path, ROOT)) if tot else (None, None)
 
 
+# VALU issue peak: a wave64 VALU instruction takes 2 cycles of its SIMD
+# (MI355X_MICROARCH.md §SIMD); 256 CUs x 4 SIMDs at 2.4 GHz.
+VALU_PEAK_WIPS = 256 * 4 * 2.4e9 / 2
+
+
+def pmc_valu(config, kernel):
+    """VALU wave-instructions per launch of `kernel` (SQ_INSTS_VALU) from the
+    committed PMC summary of this config, or None."""
+    path = os.path.join(ROOT, "profiles", f"pmc_{config}.json")
+    if not os.path.exists(path):
+        return None, None
+    ks = json.load(open(path)).get("kernels", {})
+    tot = sum(e.get("valu_insts_per_launch") or 0 for name, e in ks.items() if name.split("<")[0] == kernel)
+    return (tot, os.path.relpath(path, ROOT)) if tot else (None, None)
+
+
 def dist_setup(n_gpus):
     world = int(os.environ.get("WORLD_SIZE", "1"))
     if world == 1:
@@ -635,12 +651,14 @@ def main():
             nc = ss.row_ncells.astype(np.int64)
             hot_bytes = int((ss.row_val_len.astype(np.int64) - (nc > 1)).sum())
     reduce_ms = float(np.mean(red_ms))
+    valu_bound = False
     if G == 1 and kname != "k_reduce" and reduce_ms > 2 * hot:
         # the cross-span reducer dominates (C4: VALU-bound lerps): roofline on
         # it, with its algorithmic bytes = the E points it reads (u32 ts, i64
         # bits, u8 flag) + the output it writes (T x 17 B)
         kname, hot = "k_reduce", reduce_ms
         hot_bytes = emitted[0] * 13 + emitted[1] * 17
+        valu_bound = True
     achieved = hot_bytes / (hot * 1e-3) / 1e9
     traffic, traffic_src = pmc_traffic(args.config, kname, world)
     if rank == 0:
@@ -689,6 +707,21 @@ def main():
                 "frac_of_read_stream": achieved / probe["read_stream"] if probe else None,
             },
         }
+        if valu_bound:
+            # C4: lerps on E spans make the reducer VALU-bound, so its roofline
+            # is the VALU issue rate (SQ_INSTS_VALU per launch from the
+            # committed PMC pass of this config over the live kernel time);
+            # the HBM figures stay beside it
+            vi, vsrc = pmc_valu(args.config, "k_reduce")
+            rl = res["roofline"]
+            rl["hbm"] = {k: rl.pop(k) for k in ("achieved", "peak", "unit", "frac")}
+            rl["bound"] = "valu"
+            rl["unit"] = "wave-instr/s"
+            rl["peak"] = VALU_PEAK_WIPS
+            rl["valu_insts_per_launch"] = vi
+            rl["valu_source"] = vsrc
+            rl["achieved"] = vi / (hot * 1e-3) if vi else None
+            rl["frac"] = rl["achieved"] / VALU_PEAK_WIPS if vi else None
         if rehearse:
             res["rehearsal"] = {"shards": rehearse, "note": f"shard 0 of {rehearse} on a 1-rank RCCL "
                                 "communicator; value = this shard's points/s, not a node figure"}

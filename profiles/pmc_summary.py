@@ -42,6 +42,9 @@ def main():
         for r in csv.DictReader(open(stats)):
             out["kernels"].setdefault(short(r["Name"]), {})["avg_ms"] = float(r["AverageNs"]) / 1e6
             out["kernels"][short(r["Name"])]["calls"] = int(r["Calls"])
+    valu = per_dispatch(os.path.join(d, "pmc_sq", "run_counter_collection.csv"), "SQ_INSTS_VALU")
+    for k, v in valu.items():  # VALU wave-instructions per launch (VALU-bound kernels' roofline)
+        out["kernels"].setdefault(k, {})["valu_insts_per_launch"] = v
     fetch = per_dispatch(os.path.join(d, "pmc_fetch", "run_counter_collection.csv"), "FETCH_SIZE")
     write = per_dispatch(os.path.join(d, "pmc_write", "run_counter_collection.csv"), "WRITE_SIZE")
     for k in set(fetch) | set(write):
