@@ -53,6 +53,9 @@ CONFIGS = {
     "c3r_sum": _cfg(1_000_000, 3600, 1, I64, SUM, rate=True, desc="C3: 1M series x 3600 pts @1s, rate, sum"),
     "c3r_max": _cfg(1_000_000, 3600, 1, I64, MAX, rate=True, desc="C3: 1M series x 3600 pts @1s, rate, max"),
     "c3r_dev": _cfg(1_000_000, 3600, 1, I64, DEV, rate=True, desc="C3: 1M series x 3600 pts @1s, rate, dev"),
+    "c3_dev": _cfg(1_000_000, 3600, 1, I64, DEV,
+                   desc="C3: 1M series x 3600 pts @1s, integer dev (no rate: the reference's sequential Welford)"),
+    "c3_dev_100k": _cfg(100_000, 3600, 1, I64, DEV, desc="C3 shape, 100k series, integer dev (no rate)"),
     "c4": _cfg(1000, 11500, 0, -1, SUM, gen="jitter",
                desc="C4: 1000 jittered series (gaps U{1..6960}s, ~11.5k pts each, 50% float32 series, "
                     "1% float cells), ~10M-point union grid, sum"),
