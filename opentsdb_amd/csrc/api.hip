@@ -71,6 +71,10 @@ struct Slot {
   tsdbhip_timing timing = {};
   Xchg* x = nullptr;  // the exchange of a sharded call (its rank / nranks)
   bool want_output = true;  // false: a non-zero rank of an in-process sharded call
+  // left by the previous spangroup_run that completed: its call state reset
+  // to the initial values, its grid bitmap all zero (k_call_end)
+  bool sm_ready = false, bitmap_clean = false;
+  std::map<std::string, Buf> zeroed;  // scratch_zero_kept: allocation last zeroed whole (not owned)
 };
 
 struct Multi;
@@ -700,6 +704,77 @@ static float ev_ms(hipEvent_t a, hipEvent_t b) {
   return ms;
 }
 
+// Device state of one spangroup_run call (err_raise keys, grid range, flags,
+// counters); read back at the call's host round trips.
+struct Small {
+  unsigned long long err;  // first error (err_raise key), ERR_NONE: none
+  uint32_t gflags[2];
+  uint32_t reserved;
+  unsigned long long range[2];
+  unsigned long long fstar;
+  unsigned long long n_input;
+  unsigned long long nan_t;
+  unsigned long long bad_at;
+  uint64_t n_kept;
+  uint64_t e_total;
+  uint64_t T;
+  unsigned long long bound[2];  // [min first ts, max last ts] of the kept spans
+  uint32_t cnt[6];  // list counters, zero at the start of a call (no memsets):
+                    // [0] assembly queue, [1] decode fallback, [2] direct list,
+                    // [3] [4] k_ds_spans int / float leftovers
+  uint32_t seg[CK_NSEG];  // k_ds_spans integer leftovers, per segment
+};
+
+static Small small_init() {
+  Small init = {};
+  init.err = ERR_NONE;
+  init.range[0] = ~0ull;
+  init.range[1] = 0;
+  init.nan_t = ~0ull;
+  init.bad_at = ~0ull;
+  init.bound[0] = ~0ull;
+  init.bound[1] = 0;
+  return init;
+}
+constexpr size_t OUT_HDR = 512;  // the Small snapshot ahead of the outputs
+static_assert(sizeof(Small) <= OUT_HDR, "Small must fit the output header");
+
+// End of a call, after the finalize: the call state is snapshot ahead of the
+// outputs (one D2H copy brings both back) and reset for the next call; the
+// words of the grid points are cleared, which leaves the bitmap zero.
+__global__ void __launch_bounds__(256) k_call_end(Small* sm, Small* snap, Small init, uint32_t* bitmap,
+                                                  const uint32_t* grid, uint64_t T, int64_t lo) {
+  if (blockIdx.x == 0 && threadIdx.x == 0) {
+    *snap = *sm;
+    *sm = init;
+  }
+  if (bitmap)
+    for (uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x; i < T; i += (uint64_t)gridDim.x * 256)
+      bitmap[(uint64_t)((int64_t)grid[i] - lo) >> 5] = 0u;
+}
+
+// TSDBHIP_CHECK_CLEAN: counts non-zero words of a buffer (debug of the
+// zero-on-entry invariants)
+__global__ void k_count_nonzero(const uint32_t* p, uint64_t n, unsigned long long* out) {
+  for (uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (uint64_t)gridDim.x * 256)
+    if (p[i]) atomicAdd(out, 1ull);
+}
+
+// grow-only scratch whose whole allocation is zero when `clean` (a new
+// allocation, or a buffer the last call left dirty, is zeroed once, all of it)
+template <typename T>
+static T* scratch_zero_kept(Slot* ctx, const char* name, size_t count, bool clean) {
+  T* p = scratch<T>(ctx, name, count);
+  Buf& b = ctx->bufs[name];
+  // (a grown buffer may come back at the same address: compare the size too)
+  Buf& seen = ctx->zeroed[name];
+  if (!clean || b.p != seen.p || b.n != seen.n) {
+    HIPCHK(hipMemsetAsync(b.p, 0, b.n, ctx->stream));
+    seen = b;
+  }
+  return p;
+}
+
 // ------------------------------------------------------- the hot path ----
 static int spangroup_run(Slot* ctx, const tsdbhip_sg_desc* d, tsdbhip_sg_out* out) {
   const bool dev = (d->flags & TSDBHIP_DESC_DEVICE) != 0;
@@ -732,38 +807,27 @@ static int spangroup_run(Slot* ctx, const tsdbhip_sg_desc* d, tsdbhip_sg_out* ou
   const uint8_t* qual = stage(ctx, "in_qual", d->qual_bytes, d->qual_nbytes, dev, 16);
   const uint8_t* val = stage(ctx, "in_val", d->val_bytes, d->val_nbytes, dev, 16);
 
-  // ---- small device state ----
-  struct Small {
-    unsigned long long err;  // first error (err_raise key), ERR_NONE: none
-    uint32_t gflags[2];
-    uint32_t reserved;
-    unsigned long long range[2];
-    unsigned long long fstar;
-    unsigned long long n_input;
-    unsigned long long nan_t;
-    unsigned long long bad_at;
-    uint64_t n_kept;
-    uint64_t e_total;
-    uint64_t T;
-    unsigned long long bound[2];  // [min first ts, max last ts] of the kept spans
-    uint32_t cnt[6];  // list counters, zeroed by the init copy below (no memsets):
-                      // [0] assembly queue, [1] decode fallback, [2] direct list,
-                      // [3] [4] k_ds_spans int / float leftovers
-    uint32_t seg[CK_NSEG];  // k_ds_spans integer leftovers, per segment
-  };
   Small* sm = scratch<Small>(ctx, "small", 1);
-  {
-    Small init = {};
-    init.err = ERR_NONE;
-    init.range[0] = ~0ull;
-    init.range[1] = 0;
-    init.nan_t = ~0ull;
-    init.bad_at = ~0ull;
-    init.bound[0] = ~0ull;
-    init.bound[1] = 0;
+  static const bool check_clean = getenv("TSDBHIP_CHECK_CLEAN") != nullptr;
+  if (check_clean && ctx->sm_ready) {  // (debug) the reset state must equal small_init()
+    Small cur, ini = small_init();
+    readback(ctx, &cur, sm, sizeof cur);
+    if (std::memcmp(&cur, &ini, sizeof cur) != 0) {
+      const uint8_t* a = (const uint8_t*)&cur; const uint8_t* b = (const uint8_t*)&ini;
+      size_t i = 0;
+      while (a[i] == b[i]) i++;
+      fprintf(stderr, "TSDBHIP_CHECK_CLEAN: call state not reset (first differing byte %zu)\n", i);
+    }
+  }
+  if (!ctx->sm_ready) {  // (a completed call leaves it reset: k_call_end)
+    const Small init = small_init();
     std::memcpy(ctx->host_small, &init, sizeof init);
     HIPCHK(hipMemcpyAsync(sm, ctx->host_small, sizeof init, hipMemcpyHostToDevice, st));
   }
+  ctx->sm_ready = false;
+  const bool bm_clean = ctx->bitmap_clean;
+  ctx->bitmap_clean = false;
+  static const bool detail = getenv("TSDBHIP_TIMING_DETAIL") != nullptr;  // decode / grid event pairs
   HIPCHK(hipEventRecord(ctx->ev[0], st));
 
   // ---- assemble ----
@@ -833,7 +897,17 @@ static int spangroup_run(Slot* ctx, const tsdbhip_sg_desc* d, tsdbhip_sg_out* ou
   if (h.bound[0] == ~0ull) hi = -1;
   const bool empty_grid = lo > hi;
   const uint64_t nwords = empty_grid ? 0 : (uint64_t)(hi - lo + 1 + 31) / 32;
-  uint32_t* bitmap = empty_grid ? nullptr : scratch<uint32_t>(ctx, "bitmap", nwords, true);
+  // (zero on entry without a memset: the last call's k_call_end cleared it)
+  uint32_t* bitmap = empty_grid ? nullptr : scratch_zero_kept<uint32_t>(ctx, "gbitmap", nwords, bm_clean);
+  if (check_clean && bitmap) {  // (debug) the bitmap must be zero on entry
+    unsigned long long* cnt = scratch<unsigned long long>(ctx, "chk_cnt", 1, true);
+    const uint64_t nall = ctx->bufs["gbitmap"].n / 4;
+    hipLaunchKernelGGL(k_count_nonzero, dim3(grid_for(nall, 256, 1024)), dim3(256), 0, st, bitmap, nall, cnt);
+    unsigned long long nz = 0;
+    readback(ctx, &nz, cnt, 8);
+    if (nz) fprintf(stderr, "TSDBHIP_CHECK_CLEAN: %llu non-zero bitmap words on entry (clean=%d, nwords=%llu)\n", nz,
+                    (int)bm_clean, (unsigned long long)nwords);
+  }
 
   // ---- decode (+ downsample) ----
   const uint64_t e_total = h.e_total;
@@ -850,7 +924,7 @@ static int spangroup_run(Slot* ctx, const tsdbhip_sg_desc* d, tsdbhip_sg_out* ou
   da.e_flt = e_flt; da.e_len = e_len; da.e_bad = e_bad; da.start = d->start_time; da.end = d->end_time;
   da.interval = interval; da.ds_agg = ds_agg; da.rate = rate; da.err = &sm->err; da.gflags = sm->gflags;
   da.range = sm->range; da.fstar = &sm->fstar;
-  HIPCHK(hipEventRecord(ctx->ev[1], st));
+  if (detail) HIPCHK(hipEventRecord(ctx->ev[1], st));
   bool chunk_marked = false;     // k_ds_spans marked G for the spans it took
   bool direct = false;           // k_direct_scan took the no-downsampling path
   DirectArgs dg = {};
@@ -876,7 +950,7 @@ static int spangroup_run(Slot* ctx, const tsdbhip_sg_desc* d, tsdbhip_sg_out* ou
     DecodeArgs ga = da;  // spans the streaming kernels hand to the general ones
     ga.use_fb = 1;
     ctx->hot_kernel = fast ? TSDBHIP_HOT_DECODE_FAST : TSDBHIP_HOT_DECODE_GEN;
-    HIPCHK(hipEventRecord(ctx->ev[8], st));
+    if (!direct) HIPCHK(hipEventRecord(ctx->ev[8], st));
     if (!fast) {
       if (interval == 0) hipLaunchKernelGGL(k_decode_nods, dim3(blocks), dim3(256), 0, st, da);
       else launch_agg<LaunchGeneralDs>(ds_agg, ctx, blocks, da);
@@ -937,7 +1011,7 @@ static int spangroup_run(Slot* ctx, const tsdbhip_sg_desc* d, tsdbhip_sg_out* ou
       launch_agg<LaunchGeneralDs>(ds_agg, ctx, std::min(blocks, 1024u), ga);
     }
   }
-  HIPCHK(hipEventRecord(ctx->ev[2], st));
+  if (detail) HIPCHK(hipEventRecord(ctx->ev[2], st));
   if (n_kept)
     hipLaunchKernelGGL(k_span_summary, dim3(grid_for(n_kept, 256, 1024)), dim3(256), 0, st, da, mark_list, mark_count);
   if (sharded) {
@@ -965,17 +1039,20 @@ static int spangroup_run(Slot* ctx, const tsdbhip_sg_desc* d, tsdbhip_sg_out* ou
   uint64_t T = 0;
   uint32_t* word_rank = nullptr;
   uint32_t* gridv = nullptr;
-  HIPCHK(hipEventRecord(ctx->ev[3], st));
+  if (detail) HIPCHK(hipEventRecord(ctx->ev[3], st));
   if (!empty_grid) {
     word_rank = scratch<uint32_t>(ctx, "word_rank", nwords);
     const uint64_t nb = (nwords + 1023) / 1024;
     uint32_t* bsum = scratch<uint32_t>(ctx, "grid_bsum", nb);
-    GridArgs ga;
+    GridArgs ga = {};
     ga.e_off = eoff; ga.e_len = e_len; ga.e_ts = e_ts; ga.n_kept = n_kept; ga.lo = lo; ga.hi = hi;
     ga.rate = rate; ga.bitmap = bitmap; ga.nwords = nwords; ga.word_rank = word_rank; ga.block_sum = bsum;
     ga.total = &sm->T;
     ga.list = mark_list;  // spans k_ds_spans did not mark (null: all)
     ga.list_count = mark_count;
+    // the direct path's verify appends to the direct / fallback lists again:
+    // k_grid_popc zeroes their counters (cnt[1], cnt[2])
+    ga.zero2 = direct && n_kept ? &sm->cnt[1] : nullptr;
     if (n_kept)
       hipLaunchKernelGGL(k_grid_mark, dim3(mark_list ? std::min(grid_for(n_kept, 4, 65536), 1024u) : grid_for(n_kept, 4, 65536)),
                          dim3(256), 0, st, ga);
@@ -992,15 +1069,20 @@ static int spangroup_run(Slot* ctx, const tsdbhip_sg_desc* d, tsdbhip_sg_out* ou
     T = h.T;
     gridv = scratch<uint32_t>(ctx, "grid", T);
     ga.grid = gridv;
-    hipLaunchKernelGGL(k_grid_emit, dim3(grid_for(nwords, 256)), dim3(256), 0, st, ga);
-    if (direct && n_kept) {
-      // candidates whose points are not consecutive grid ranks need E (their
-      // grid points are already marked; types, F* and errors already counted)
-      dg.word_rank = word_rank;
-      dg.bitmap = bitmap;
-      HIPCHK(hipMemsetAsync(dg.list_count, 0, 4, st));
-      HIPCHK(hipMemsetAsync(da.fb_count, 0, 4, st));
-      hipLaunchKernelGGL(k_direct_verify, dim3(grid_for(n_kept, 256)), dim3(256), 0, st, dg, n_kept);
+    // G emitted with the final word ranks (word_rank_f); in the same launch
+    // the direct candidates whose points are not consecutive grid ranks go
+    // to the E path (their grid points are already marked; types, F* and
+    // errors already counted)
+    uint32_t* word_rank_f = scratch<uint32_t>(ctx, "word_rank_f", nwords);
+    const bool verify = direct && n_kept;
+    dg.word_rank = word_rank;  // (block-local ranks + ga.block_sum)
+    dg.bitmap = bitmap;
+    const uint32_t eb = grid_for(nwords, 256);
+    hipLaunchKernelGGL(k_emit_verify, dim3(eb + (verify ? grid_for(n_kept, 256) : 0)), dim3(256), 0, st, ga,
+                       word_rank_f, dg, verify ? n_kept : 0u, eb);
+    word_rank = word_rank_f;
+    dg.word_rank = word_rank_f;
+    if (verify) {
       DecodeArgs fa = da;
       fa.span_list = dg.list;
       fa.span_count = dg.list_count;
@@ -1024,6 +1106,12 @@ static int spangroup_run(Slot* ctx, const tsdbhip_sg_desc* d, tsdbhip_sg_out* ou
     hipLaunchKernelGGL(k_bad_index, dim3(grid_for(n_kept, 256)), dim3(256), 0, st, e_bad, eoff, e_ts, n_kept,
                        (int32_t)rate, hi, bitmap, word_rank, lo, T, &sm->bad_at);
 
+  // ---- output block: [Small snapshot | ts T | bits T | is_int T] ----
+  uint8_t* outblk = scratch<uint8_t>(ctx, "outblk", OUT_HDR + 17 * T);
+  int64_t* o_ts = (int64_t*)(outblk + OUT_HDR);
+  int64_t* o_bits = o_ts + T;
+  uint8_t* o_isint = (uint8_t*)(o_bits + T);
+
   // ---- reduce ----
   if (T > 0) {
     const int mode = rate ? MODE_DBL : (!anyf ? MODE_INT : (!anyi ? MODE_DBL : MODE_DUAL));
@@ -1036,9 +1124,9 @@ static int spangroup_run(Slot* ctx, const tsdbhip_sg_desc* d, tsdbhip_sg_out* ou
     FinalArgs fin;
     std::memset(&fin, 0, sizeof fin);
     fin.T = T; fin.n_chunks = 1; fin.grid = gridv; fin.fstar = fstar; fin.rate = rate;
-    fin.out_ts = scratch<int64_t>(ctx, "out_ts", T);
-    fin.out_isint = scratch<uint8_t>(ctx, "out_isint", T);
-    fin.out_bits = scratch<int64_t>(ctx, "out_bits", T);
+    fin.out_ts = o_ts;
+    fin.out_isint = o_isint;
+    fin.out_bits = o_bits;
     fin.nan_t = &sm->nan_t;
     // per-t partial fields ([n][T] layout) under scratch names prefix + field
     auto partials = [&](ReduceArgs& r, const char* pre, uint64_t np) {
@@ -1097,9 +1185,9 @@ static int spangroup_run(Slot* ctx, const tsdbhip_sg_desc* d, tsdbhip_sg_out* ou
         r.i_wdv = init->p_wdv;
       }
       if (direct) {
-        uint32_t* ce = scratch<uint32_t>(ctx, "chunk_e", n_chunks, true);
-        if (n_kept)
-          hipLaunchKernelGGL(k_chunk_flags, dim3(grid_for(n_kept, 256)), dim3(256), 0, st, dg.info, n_kept, spc, ce);
+        uint32_t* ce = scratch<uint32_t>(ctx, "chunk_e", n_chunks);
+        hipLaunchKernelGGL(k_chunk_flags_w, dim3(grid_for(n_chunks, 4)), dim3(256), 0, st, dg.info, n_kept, spc,
+                           n_chunks, ce);
         r.chunk_e = ce;
       }
       r.ptr = scratch<uint32_t>(ctx, "cursor", n_waves * spc);
@@ -1116,8 +1204,6 @@ static int spangroup_run(Slot* ctx, const tsdbhip_sg_desc* d, tsdbhip_sg_out* ou
     };
     if (!sharded) {
       run_reduce(seq, true, nullptr);
-      HIPCHK(hipEventRecord(ctx->ev[5], st));
-      readback(ctx, &h, sm, sizeof h);  // sync 3
     } else {
       const int nr = X->nranks, rk = X->rank;
       ReduceArgs src;  // per-t partials the finalize merges ([n_src][T])
@@ -1185,20 +1271,29 @@ static int spangroup_run(Slot* ctx, const tsdbhip_sg_desc* d, tsdbhip_sg_out* ou
       f.n_chunks = n_src;
       src.n_chunks = n_src;
       dispatch_final(ctx, agg, mode, rate, src, f);
-      HIPCHK(hipEventRecord(ctx->ev[5], st));
-      readback(ctx, &h, sm, sizeof h);
-      tm.exchange_ms = ev_ms(ctx->ev[6], ctx->ev[7]);
     }
-  } else {
-    HIPCHK(hipEventRecord(ctx->ev[5], st));
-    if (sharded) X->allreduce(ctx, &sm->bad_at, 1, X_U64, X_MIN);
-    readback(ctx, &h, sm, sizeof h);
+  } else if (sharded) {
+    X->allreduce(ctx, &sm->bad_at, 1, X_U64, X_MIN);
   }
+  // ---- end of call: snapshot + reset of the call state, bitmap cleared ----
+  hipLaunchKernelGGL(k_call_end, dim3(grid_for(T, 256, 1024)), dim3(256), 0, st, sm, (Small*)outblk, small_init(),
+                     bitmap, (const uint32_t*)gridv, T, lo);
+  HIPCHK(hipEventRecord(ctx->ev[5], st));
+  // one D2H copy of the header and (small results) the outputs, one sync
+  const bool small_out = T * 17 <= (256u << 10) && ctx->want_output;
+  uint8_t* hb = (uint8_t*)host_buf(ctx, OUT_HDR + (small_out ? 17 * T : 0));
+  HIPCHK(hipMemcpyAsync(hb, outblk, OUT_HDR + (small_out ? 17 * T : 0), hipMemcpyDeviceToHost, st));
   HIPCHK(hipStreamSynchronize(st));
-  tm.decode_ms = ev_ms(ctx->ev[1], ctx->ev[2]);
+  std::memcpy(&h, hb, sizeof h);
+  ctx->sm_ready = true;
+  ctx->bitmap_clean = true;
+  if (sharded) tm.exchange_ms = T > 0 ? ev_ms(ctx->ev[6], ctx->ev[7]) : 0.f;
+  if (detail) {
+    tm.decode_ms = ev_ms(ctx->ev[1], ctx->ev[2]);
+    tm.grid_ms = ev_ms(ctx->ev[3], ctx->ev[4]);
+  }
   if (ctx->hot_kernel) tm.hot_ms = ev_ms(ctx->ev[8], ctx->ev[9]);
   tm.hot_kernel = ctx->hot_kernel;
-  tm.grid_ms = ev_ms(ctx->ev[3], ctx->ev[4]);
   tm.reduce_ms = ev_ms(ctx->ev[4], ctx->ev[5]);
   tm.total_ms = ev_ms(ctx->ev[0], ctx->ev[5]);
   tm.n_emitted = e_total;
@@ -1223,21 +1318,14 @@ static int spangroup_run(Slot* ctx, const tsdbhip_sg_desc* d, tsdbhip_sg_out* ou
   }
   if (!ctx->want_output) {
     // (a non-zero rank of an in-process sharded call: rank 0 returns the output)
-  } else if (n_ok && n_ok * 17 <= (256u << 10)) {
-    // small results: three async copies into pinned staging, one sync (a
-    // copy into pageable memory would synchronise once per array)
-    uint8_t* hb = (uint8_t*)host_buf(ctx, n_ok * 17);
-    HIPCHK(hipMemcpyAsync(hb, scratch<int64_t>(ctx, "out_ts", T), n_ok * 8, hipMemcpyDeviceToHost, st));
-    HIPCHK(hipMemcpyAsync(hb + 8 * n_ok, scratch<int64_t>(ctx, "out_bits", T), n_ok * 8, hipMemcpyDeviceToHost, st));
-    HIPCHK(hipMemcpyAsync(hb + 16 * n_ok, scratch<uint8_t>(ctx, "out_isint", T), n_ok, hipMemcpyDeviceToHost, st));
-    HIPCHK(hipStreamSynchronize(st));
-    std::memcpy(out->ts, hb, n_ok * 8);
-    std::memcpy(out->bits, hb + 8 * n_ok, n_ok * 8);
-    std::memcpy(out->is_int, hb + 16 * n_ok, n_ok);
+  } else if (n_ok && small_out) {  // (already in the pinned staging with the header)
+    std::memcpy(out->ts, hb + OUT_HDR, n_ok * 8);
+    std::memcpy(out->bits, hb + OUT_HDR + 8 * T, n_ok * 8);
+    std::memcpy(out->is_int, hb + OUT_HDR + 16 * T, n_ok);
   } else if (n_ok) {
-    HIPCHK(hipMemcpyAsync(out->ts, scratch<int64_t>(ctx, "out_ts", T), n_ok * 8, hipMemcpyDeviceToHost, st));
-    HIPCHK(hipMemcpyAsync(out->is_int, scratch<uint8_t>(ctx, "out_isint", T), n_ok, hipMemcpyDeviceToHost, st));
-    HIPCHK(hipMemcpyAsync(out->bits, scratch<int64_t>(ctx, "out_bits", T), n_ok * 8, hipMemcpyDeviceToHost, st));
+    HIPCHK(hipMemcpyAsync(out->ts, o_ts, n_ok * 8, hipMemcpyDeviceToHost, st));
+    HIPCHK(hipMemcpyAsync(out->is_int, o_isint, n_ok, hipMemcpyDeviceToHost, st));
+    HIPCHK(hipMemcpyAsync(out->bits, o_bits, n_ok * 8, hipMemcpyDeviceToHost, st));
     HIPCHK(hipStreamSynchronize(st));
   }
   out->n_out = n_ok;

@@ -329,7 +329,7 @@ static int spangroup_run_batch(Slot* ctx, const tsdbhip_sg_desc* d, uint32_t G, 
   if (direct && n_kept)
     hipLaunchKernelGGL(k_direct_mark_seg, dim3(grid_for(n_kept, 4 * WAVE, 16384)), dim3(256), 0, st, dg, n_kept,
                        kgrp, q, bitmap);
-  GridArgs ga;
+  GridArgs ga = {};
   std::memset(&ga, 0, sizeof ga);
   ga.bitmap = bitmap; ga.nwords = W; ga.word_rank = word_rank; ga.block_sum = bsum; ga.total = &sm->T;
   hipLaunchKernelGGL(k_grid_popc, dim3((unsigned)nb), dim3(256), 0, st, ga);

@@ -357,9 +357,9 @@ __global__ void __launch_bounds__(256) k_direct_scan(DecodeArgs a, DirectArgs g,
 }
 
 // After the grid: keep a candidate direct iff its grid points hold
-// consecutive ranks; record the rank of the first.
-__global__ void __launch_bounds__(256) k_direct_verify(DirectArgs g, uint32_t n_kept) {
-  const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
+// consecutive ranks; record the rank of the first. `bsum`: block offsets to
+// add to g.word_rank (block-local ranks, k_emit_verify), or null (final ranks).
+DEVI void direct_verify_one(const DirectArgs& g, uint32_t n_kept, uint32_t k, const uint32_t* bsum) {
   bool fail = false;
   if (k < n_kept) {
     const uint32_t info = g.info[k];
@@ -372,8 +372,10 @@ __global__ void __launch_bounds__(256) k_direct_verify(DirectArgs g, uint32_t n_
         g.ga[k] = 0;  // (rate with one point: inactive everywhere)
       } else {
         const int64_t xl = x0 + (int64_t)(ne - 1) * step;
-        const uint32_t ra = grid_rank(g.bitmap, g.word_rank, g.lo, xf);
-        const uint32_t rl = grid_rank(g.bitmap, g.word_rank, g.lo, xl);
+        const uint32_t ra = bsum ? grid_rank2(g.bitmap, g.word_rank, bsum, g.lo, xf)
+                                 : grid_rank(g.bitmap, g.word_rank, g.lo, xf);
+        const uint32_t rl = bsum ? grid_rank2(g.bitmap, g.word_rank, bsum, g.lo, xl)
+                                 : grid_rank(g.bitmap, g.word_rank, g.lo, xl);
         g.ga[k] = ra;
         if (rl - ra != np - 1) {
           fail = true;
@@ -391,6 +393,37 @@ __global__ void __launch_bounds__(256) k_direct_verify(DirectArgs g, uint32_t n_
     base = __shfl(base, __builtin_ctzll(m));
     if (fail) g.list[base + __popcll(m & lanemask_lt(lane))] = k;
   }
+}
+
+__global__ void __launch_bounds__(256) k_direct_verify(DirectArgs g, uint32_t n_kept) {
+  direct_verify_one(g, n_kept, blockIdx.x * blockDim.x + threadIdx.x, nullptr);
+}
+
+// k_grid_emit and k_direct_verify in one launch: blocks [0, emit_blocks) emit
+// G and write the final word ranks to rank_out; the rest verify the direct
+// candidates from the block-local ranks + block offsets (read-only here).
+__global__ void __launch_bounds__(256) k_emit_verify(GridArgs ga, uint32_t* rank_out, DirectArgs dg, uint32_t n_kept,
+                                                     uint32_t emit_blocks) {
+  if (blockIdx.x < emit_blocks) {
+    grid_emit_to(ga, (uint64_t)blockIdx.x * 256 + threadIdx.x, rank_out);
+  } else {
+    direct_verify_one(dg, n_kept, (blockIdx.x - emit_blocks) * 256 + threadIdx.x, ga.block_sum);
+  }
+}
+
+// Per reduce chunk of spc spans: 1 iff it holds an E span (a span whose
+// direct bit is off). A wave per chunk writes every flag (no memset first).
+__global__ void __launch_bounds__(256) k_chunk_flags_w(const uint32_t* d_info, uint32_t n_kept, uint32_t spc,
+                                                       uint32_t n_chunks, uint32_t* chunk_e) {
+  const uint32_t c = (blockIdx.x * blockDim.x + threadIdx.x) / WAVE;
+  if (c >= n_chunks) return;
+  const uint32_t a = c * spc, b = min(n_kept, a + spc);
+  bool any = false;
+  for (uint32_t k0 = a; k0 < b && !any; k0 += WAVE) {
+    const uint32_t k = k0 + lane_id();
+    any = ballot(k < b && !(d_info[k] & 1u)) != 0;
+  }
+  if (lane_id() == 0) chunk_e[c] = any ? 1u : 0u;
 }
 
 }  // namespace tsdb

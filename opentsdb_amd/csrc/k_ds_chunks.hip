@@ -177,29 +177,64 @@ DEVI int64_t ds_combine(int64_t x, int64_t y) {
   return y > x ? y : x;
 }
 
-// One row of a span: its 512-cell chunks. Returns true if a precondition
-// breaks (the span then goes to the serial path).
+// Position of one chunk in a span's row sequence (wave-uniform): the row's
+// fields, the span cell index of the row's first cell, the chunk's first
+// cell in the row. `done`: past the span's last chunk.
+struct ChunkPos {
+  uint64_t qoff, voff, r;
+  uint32_t base, nc, cell0, c0;
+  bool done;
+};
+
+// A span's 512-cell chunks, row after row, as one stream: two register sets,
+// the next chunk's loads (in this row or the next one) in flight while one
+// is processed, so a span of short rows (C2: 360 cells per row) does not wait
+// one full load latency per row. Rows [r0, r1) were checked by the caller
+// (row_ok, cells, width W, alignment). Returns true if a precondition breaks
+// (the span then goes to the serial path).
 template <int AGG, int W, bool FLT>
-DEVI bool ds_row(const DecodeArgs& a, const SpanDsArgs& g, DsState& st, uint64_t eo, uint32_t cap,
-                 uint64_t qoff, uint64_t voff, uint32_t base, uint32_t nc, uint32_t cell0, uint32_t* L_pt,
-                 uint64_t* L_v, BkLds& BK) {
+DEVI bool ds_span(const DecodeArgs& a, DsState& st, uint64_t eo, uint32_t cap, uint64_t r0, uint64_t r1,
+                  const uint32_t* ncells, uint32_t* L_pt, uint64_t* L_v, BkLds& BK) {
   constexpr bool PREFIX = AGG == 0 || AGG == 3;  // sum / avg: prefix differences; min / max: loops
   const int lane = lane_id();
   const int64_t I = a.interval;
-  const uint32_t clamp_c = (nc - 1) & ~7u;
   // ts delta (from the row base) of chunk cell x: the ts prefix differenced
   auto dtx = [&](uint32_t x) { return L_pt[x] - (x > 0 ? L_pt[x - 1] : 0u); };
+  auto row_at = [&](uint64_t r, uint32_t cell0) {
+    ChunkPos p;
+    p.r = r;
+    p.nc = sld(&ncells[r]);
+    p.qoff = sld(&a.row_qual_off[r]);
+    p.voff = sld(&a.row_val_off[r]);
+    p.base = sld(&a.row_base[r]);
+    p.cell0 = cell0;
+    p.c0 = 0;
+    p.done = false;
+    return p;
+  };
+  auto advance = [&](const ChunkPos& p) {
+    if (p.done) return p;
+    if (p.c0 + DCH < p.nc) {
+      ChunkPos q = p;
+      q.c0 += DCH;
+      return q;
+    }
+    if (p.r + 1 < r1) return row_at(p.r + 1, p.cell0 + p.nc);
+    ChunkPos q = p;
+    q.done = true;
+    return q;
+  };
   RawW<W> A, B;
-  auto issue = [&](uint32_t c0, RawW<W>& x) {
-    const uint32_t c = c0 + 8u * lane;
+  // (a done position re-loads its own cells: branch-free, cache hits)
+  auto issue = [&](const ChunkPos& p, RawW<W>& x) {
+    const uint32_t c = p.c0 + 8u * lane;
     __builtin_amdgcn_s_setprio(2);  // the chunk's loads ahead of other waves' VALU
-    load_raw<W>(a, qoff, voff, c < nc ? c : clamp_c, x);
+    load_raw<W>(a, p.qoff, p.voff, c < p.nc ? c : (p.nc - 1) & ~7u, x);
     __builtin_amdgcn_s_setprio(0);
   };
-  issue(0, A);
-  issue(DCH, B);
   bool bad = false;
-  auto step = [&](uint32_t c0, const RawW<W>& cur) {
+  auto step = [&](const ChunkPos& p, const RawW<W>& cur) {
+    const uint32_t c0 = p.c0, nc = p.nc, base = p.base, cell0 = p.cell0;
     const uint32_t nv = min(DCH, nc - c0);
     const uint32_t cs = cell0 + c0;  // span cell index of the chunk start
     // ---- decode: 8 cells per lane (loads past the row end were clamped) ----
@@ -418,11 +453,23 @@ DEVI bool ds_row(const DecodeArgs& a, const SpanDsArgs& g, DsState& st, uint64_t
     wave_lds_sync();
   };
   // two register sets: one chunk in flight while the other is processed
-  for (uint32_t c0 = 0; c0 < nc; c0 += 2 * DCH) {
-    step(c0, A);
-    issue(c0 + 2 * DCH, A);
-    if (c0 + DCH < nc) step(c0 + DCH, B);
-    issue(c0 + 3 * DCH, B);
+  ChunkPos p0 = row_at(r0, 0);
+  ChunkPos p1 = advance(p0);
+  issue(p0, A);
+  issue(p1, B);
+  // (a broken precondition ends the stream: the chain state past it is
+  // meaningless, and the span is redone by the serial kernels)
+  for (;;) {
+    step(p0, A);
+    if (p1.done || ballot(bad) != 0) break;
+    const ChunkPos p2 = advance(p1);
+    issue(p2, A);
+    step(p1, B);
+    if (p2.done || ballot(bad) != 0) break;
+    const ChunkPos p3 = advance(p2);
+    issue(p3, B);
+    p0 = p2;
+    p1 = p3;
   }
   return ballot(bad) != 0;
 }
@@ -468,46 +515,42 @@ __global__ void __launch_bounds__(256) k_ds_spans(DecodeArgs a, SpanDsArgs g, co
     const uint64_t r0 = sld(&a.span_row_start[s]), r1 = sld(&a.span_row_start[s + 1]);
     const uint32_t n = sld(&a.sp_ncells[s]);
     bool ok = sld(&a.sp_q1[s]) < 0 && sld(&a.sp_ovf_cell[s]) < 0 && n > 0 && r1 > r0 && a.interval > 0;
-    if (ok && r1 - r0 == 1) {  // (one row: the usual hourly span)
-      ok = sld_u8(&a.row_ok[r0]) != 0 && sld(&ncells[r0]) != 0;
-    } else {
-      for (uint64_t rb = r0; ok && rb < r1; rb += WAVE) {  // (uniform loop: keeps `ok` scalar)
-        const uint64_t r = rb + lane;
-        ok = ballot(r < r1 && (a.row_ok[r] == 0 || ncells[r] == 0)) == 0;
-      }
-    }
-    // value width of the span's rows (all must match and be aligned)
+    // value width of the span's rows: the first row's, every row must match
+    // it and be aligned (checked here, so the chunk stream never stops at a
+    // row boundary)
     uint32_t W = 0;
     if (ok) {
       const uint32_t nc = sld(&ncells[r0]), vl = sld(&vlen[r0]);
       const uint32_t vb = nc > 1 ? vl - 1 : vl;
-      W = vb == (vb / nc) * nc ? vb / nc : 0;
+      W = nc != 0 && vb == (vb / nc) * nc ? vb / nc : 0;
       ok = W == 8 || W == 4;
       // the first cell's type picks the instantiation: the other one leaves
       // the span without streaming it (float spans pass through the integer
       // kernel first)
       if (ok) ok = ((sld_u8(a.qual + sld(&a.row_qual_off[r0]) + 1) & 8u) != 0) == FLT;
     }
+    if (ok && r1 - r0 == 1) {  // (one row: the usual hourly span)
+      ok = sld_u8(&a.row_ok[r0]) != 0 && (sld(&a.row_qual_off[r0]) & 7) == 0 && (sld(&a.row_val_off[r0]) & 15) == 0;
+    } else {
+      for (uint64_t rb = r0; ok && rb < r1; rb += WAVE) {  // (uniform loop: keeps `ok` scalar)
+        const uint64_t r = rb + lane;
+        bool rbad = false;
+        if (r < r1) {
+          const uint32_t nc = ncells[r], vl = vlen[r];
+          const uint32_t vb = nc > 1 ? vl - 1 : vl;
+          rbad = a.row_ok[r] == 0 || nc == 0 || vb != W * nc || (a.row_qual_off[r] & 7) != 0 ||
+                 (a.row_val_off[r] & 15) != 0;
+        }
+        ok = ballot(rbad) == 0;
+      }
+    }
     const uint64_t eo = sld(&a.e_off[k]);
     const uint32_t cap = (uint32_t)sld(&a.sp_cap[s]);
     DsState st = {};
-    uint32_t cell = 0;
-    for (uint64_t r = r0; ok && r < r1; r++) {
-      const uint32_t nc = sld(&ncells[r]);
-      const uint32_t vl = sld(&vlen[r]);
-      const uint64_t qoff = sld(&a.row_qual_off[r]), voff = sld(&a.row_val_off[r]);
-      const uint32_t rbase = sld(&a.row_base[r]);
-      const uint32_t vb = nc > 1 ? vl - 1 : vl;
-      if (!(vb == W * nc && (qoff & 7) == 0 && (voff & 15) == 0)) {
-        ok = false;
-        break;
-      }
-      const bool fail = W == 8 ? ds_row<AGG, 8, FLT>(a, g, st, eo, cap, qoff, voff, rbase, nc, cell, s_pt[wib],
-                                                 s_v[wib], s_bk[wib])
-                               : ds_row<AGG, 4, FLT>(a, g, st, eo, cap, qoff, voff, rbase, nc, cell, s_pt[wib],
-                                                 s_v[wib], s_bk[wib]);
+    if (ok) {
+      const bool fail = W == 8 ? ds_span<AGG, 8, FLT>(a, st, eo, cap, r0, r1, ncells, s_pt[wib], s_v[wib], s_bk[wib])
+                               : ds_span<AGG, 4, FLT>(a, st, eo, cap, r0, r1, ncells, s_pt[wib], s_v[wib], s_bk[wib]);
       ok = !fail;
-      cell += nc;
     }
     uint32_t ts_last = 0, n_last = 0;  // the final flush (one lane per bucket)
     if (ok) {  // the last cell must lie inside the last bucket; then close it

@@ -27,6 +27,8 @@ struct GridArgs {
   uint64_t* total;      // [1] T
   const uint32_t* list;       // k_grid_mark: only these kept spans (null: all)
   const uint32_t* list_count;
+  uint32_t* zero2;            // k_grid_popc: two list counters to zero for the
+                              // kernels after the grid (null: none)
 };
 
 // Mark every candidate point. Many spans share timestamps (regular cadence),
@@ -79,6 +81,10 @@ __global__ void __launch_bounds__(256) k_grid_popc(GridArgs g) {
     if (w < g.nwords) g.word_rank[w] = run;
     run += c[i];
   }
+  if (t == 0 && blockIdx.x == 0 && g.zero2) {  // (their last readers ran before this kernel)
+    g.zero2[0] = 0;
+    g.zero2[1] = 0;
+  }
   if (t == 255) {
     g.block_sum[blockIdx.x] = woff + incl;
     if (gridDim.x == 1) {  // one block: its offset is 0 and its sum is T (no k_grid_scan_blocks)
@@ -127,11 +133,42 @@ __global__ void __launch_bounds__(256) k_grid_emit(GridArgs g) {
   }
 }
 
+// k_grid_emit that leaves the block-local ranks in place and writes the final
+// ones to rank_out, so a kernel fused beside it (k_emit_verify) can read them.
+DEVI void grid_emit_to(const GridArgs& g, uint64_t w, uint32_t* rank_out) {
+  if (w >= g.nwords) return;
+  const uint32_t r = g.word_rank[w] + g.block_sum[w >> 10];
+  rank_out[w] = r;
+  uint32_t bits = g.bitmap[w];
+  uint32_t i = r;
+  while (bits) {
+    const int b = __builtin_ctz(bits);
+    g.grid[i++] = (uint32_t)(g.lo + (int64_t)(w * 32 + b));
+    bits &= bits - 1;
+  }
+}
+
 // rank(t): number of grid points < t (t must lie in [lo, hi+1)).
 DEVI uint32_t grid_rank(const uint32_t* bitmap, const uint32_t* word_rank, int64_t lo, int64_t t) {
   const uint64_t b = (uint64_t)(t - lo);
   const uint64_t w = b >> 5;
   return word_rank[w] + __popc(bitmap[w] & ((1u << (b & 31)) - 1));
+}
+
+// the same from the block-local ranks and the block offsets (before k_grid_emit)
+DEVI uint32_t grid_rank2(const uint32_t* bitmap, const uint32_t* word_rank, const uint32_t* block_sum, int64_t lo,
+                         int64_t t) {
+  const uint64_t b = (uint64_t)(t - lo);
+  const uint64_t w = b >> 5;
+  return word_rank[w] + block_sum[w >> 10] + __popc(bitmap[w] & ((1u << (b & 31)) - 1));
+}
+
+// End of a single-group call (api.hip), after the finalize: every set bit of
+// the bitmap is a grid point, so clearing the word of each grid point leaves
+// the whole bitmap zero for the next call (no memset per call).
+__global__ void __launch_bounds__(256) k_bitmap_clear(uint32_t* bitmap, const uint32_t* grid, uint64_t T, int64_t lo) {
+  for (uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x; i < T; i += (uint64_t)gridDim.x * 256)
+    bitmap[(uint64_t)((int64_t)grid[i] - lo) >> 5] = 0u;
 }
 
 }  // namespace tsdb
