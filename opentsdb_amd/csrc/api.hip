@@ -63,6 +63,15 @@ struct Slot {
   hipStream_t stream = nullptr;
   std::map<std::string, Buf> bufs;  // grow-only named scratch (HBM)
   void* host_small = nullptr;       // pinned readback area
+  // mapped pinned host memory the kernels write directly: the call state at
+  // the two sizing round trips (host_publish + a spin on the flag instead of
+  // a copy and a stream sync), and the results with their header
+  uint64_t* map_state = nullptr;  // [0, 511]: state words, [512]: flag
+  uint64_t* map_state_dev = nullptr;
+  uint64_t pub_seq = 0;
+  uint8_t* map_out = nullptr;
+  uint8_t* map_out_dev = nullptr;
+  size_t map_out_n = 0;
   void* host_big = nullptr;         // grow-only pinned staging (group-by batches)
   size_t host_big_n = 0;
   hipEvent_t ev[10] = {};  // [8],[9] bracket the dominant kernel
@@ -176,6 +185,8 @@ static void slot_free(Slot* s) {
   for (auto& e : s->ev)
     if (e) hipEventDestroy(e);
   if (s->host_small) hipHostFree(s->host_small);
+  if (s->map_state) hipHostFree(s->map_state);
+  if (s->map_out) hipHostFree(s->map_out);
   if (s->host_big) hipHostFree(s->host_big);
   if (s->stream) hipStreamDestroy(s->stream);
   delete s;
@@ -188,6 +199,9 @@ static Slot* slot_new(int device) {
     HIPCHK(hipSetDevice(device));
     HIPCHK(hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking));
     HIPCHK(hipHostMalloc(&ctx->host_small, 4096, hipHostMallocDefault));
+    HIPCHK(hipHostMalloc((void**)&ctx->map_state, 8 * 520, hipHostMallocMapped | hipHostMallocCoherent));
+    HIPCHK(hipHostGetDevicePointer((void**)&ctx->map_state_dev, ctx->map_state, 0));
+    std::memset(ctx->map_state, 0, 8 * 520);
     for (auto& e : ctx->ev) HIPCHK(hipEventCreate(&e));
   } catch (Fail&) {
     slot_free(ctx);
@@ -510,6 +524,47 @@ static void readback(Slot* ctx, void* host, const void* dev, size_t bytes) {
   std::memcpy(host, ctx->host_small, bytes);
 }
 
+// The next host_publish of `bytes` of device state (a kernel argument).
+static HostPub next_pub(Slot* ctx, size_t bytes) {
+  HostPub p;
+  p.dst = ctx->map_state_dev;
+  p.flag = ctx->map_state_dev + 512;
+  p.seq = ++ctx->pub_seq;
+  p.nwords = (uint32_t)((bytes + 7) / 8);
+  return p;
+}
+// Waits for that publish and copies the state out: a spin on the mapped flag
+// (the stream is queried now and then: a stream that drained without the
+// flag means the producing kernel did not run).
+static void wait_pub(Slot* ctx, const HostPub& p, void* host, size_t bytes) {
+  const uint64_t* flag = ctx->map_state + 512;
+  for (uint32_t i = 1;; i++) {
+    if (__atomic_load_n(flag, __ATOMIC_ACQUIRE) == p.seq) break;
+    if ((i & 1023) == 0) {
+      const hipError_t e = hipStreamQuery(ctx->stream);
+      if (e == hipSuccess && __atomic_load_n(flag, __ATOMIC_ACQUIRE) != p.seq) {
+        set_error(ctx, "host publish %llu never arrived", (unsigned long long)p.seq);
+        throw Fail{TSDBHIP_E_HIP};
+      }
+      if (e != hipSuccess && e != hipErrorNotReady) HIPCHK(e);
+    }
+    __builtin_ia32_pause();
+  }
+  std::memcpy(host, ctx->map_state, bytes);
+}
+
+// grow-only mapped pinned result area (device pointer in map_out_dev)
+static void map_out_reserve(Slot* ctx, size_t bytes) {
+  if (ctx->map_out_n >= bytes) return;
+  const size_t n = std::max(bytes, ctx->map_out_n + ctx->map_out_n / 4);
+  if (ctx->map_out) HIPCHK(hipHostFree(ctx->map_out));
+  ctx->map_out = nullptr;
+  ctx->map_out_n = 0;
+  HIPCHK(hipHostMalloc((void**)&ctx->map_out, n, hipHostMallocMapped | hipHostMallocCoherent));
+  HIPCHK(hipHostGetDevicePointer((void**)&ctx->map_out_dev, ctx->map_out, 0));
+  ctx->map_out_n = n;
+}
+
 // runtime aggregator id -> F::template run<AGG>(args...)
 template <typename F, typename... A>
 static void launch_agg(int agg, A&&... args) {
@@ -582,7 +637,8 @@ template <int AGG, int MODE, bool RATE>
 static void launch_reduce(Slot* ctx, unsigned blocks, const ReduceArgs& r, const FinalArgs& f,
                           bool par, bool finalize) {
   if (ctx->time_reduce) HIPCHK(hipEventRecord(ctx->ev[8], ctx->stream));
-  if (r.d_info) hipLaunchKernelGGL((k_reduce<AGG, MODE, RATE, true>), dim3(blocks), dim3(256), 0, ctx->stream, r);
+  if (r.d_info && r.chunk_e)
+    hipLaunchKernelGGL((k_reduce<AGG, MODE, RATE, true>), dim3(blocks), dim3(256), 0, ctx->stream, r);
   hipLaunchKernelGGL((k_reduce<AGG, MODE, RATE, false>), dim3(blocks), dim3(256), 0, ctx->stream, r);
   if (ctx->time_reduce) HIPCHK(hipEventRecord(ctx->ev[9], ctx->stream));
   if (!finalize) return;
@@ -742,11 +798,29 @@ static_assert(sizeof(Small) <= OUT_HDR, "Small must fit the output header");
 // End of a call, after the finalize: the call state is snapshot ahead of the
 // outputs (one D2H copy brings both back) and reset for the next call; the
 // words of the grid points are cleared, which leaves the bitmap zero.
+// Small unsharded calls also compute the lazy error index here (block 0,
+// before the snapshot; bad.n_kept = 0: k_bad_index ran).
 __global__ void __launch_bounds__(256) k_call_end(Small* sm, Small* snap, Small init, uint32_t* bitmap,
-                                                  const uint32_t* grid, uint64_t T, int64_t lo) {
-  if (blockIdx.x == 0 && threadIdx.x == 0) {
-    *snap = *sm;
-    *sm = init;
+                                                  const uint32_t* grid, uint64_t T, int64_t lo, BadArgs bad) {
+  __shared__ unsigned long long s_min[4];
+  if (blockIdx.x == 0) {
+    if (bad.n_kept) {
+      unsigned long long m = ~0ull;
+      for (uint32_t k = threadIdx.x; k < bad.n_kept; k += 256) m = min(m, (unsigned long long)bad_key(bad, k));
+      for (int o = 1; o < WAVE; o <<= 1) m = min(m, (unsigned long long)shfl_xor_u64(m, o));
+      if (lane_id() == 0) s_min[threadIdx.x / WAVE] = m;
+      __syncthreads();
+      if (threadIdx.x == 0) {
+        m = min(min(s_min[0], s_min[1]), min(s_min[2], s_min[3]));
+        if (m != ~0ull) atomicMin(&sm->bad_at, m);
+        __threadfence();
+      }
+    }
+    if (threadIdx.x == 0) {
+      *snap = *sm;
+      *sm = init;
+    }
+    __syncthreads();  // (the ranks above read the bitmap cleared below)
   }
   if (bitmap)
     for (uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x; i < T; i += (uint64_t)gridDim.x * 256)
@@ -859,9 +933,14 @@ static int spangroup_run(Slot* ctx, const tsdbhip_sg_desc* d, tsdbhip_sg_out* ou
   }
   uint32_t* kept = scratch<uint32_t>(ctx, "kept", S);
   uint64_t* eoff = scratch<uint64_t>(ctx, "eoff", S);
+  // (unsharded groups of up to KC_MAX spans: the kept-list kernel hands the
+  // call state to the host itself, no readback)
+  const bool pub1 = !sharded && S && S <= KC_MAX;
+  const HostPub p1 = pub1 ? next_pub(ctx, sizeof(Small)) : HostPub{};
   if (S && S <= KC_MAX) {  // kept list, E offsets, counts and bounds: one launch
     hipLaunchKernelGGL(k_kept_compact, dim3(1), dim3(1024), 0, st, sp_kept, sp_cap, sp_ncells, S, kept, eoff,
-                       &sm->n_input, sp_first, sp_last, sm->bound, &sm->n_kept, &sm->e_total);
+                       &sm->n_input, sp_first, sp_last, sm->bound, &sm->n_kept, &sm->e_total, p1,
+                       (const uint64_t*)sm);
   } else if (S) {  // bigger groups: tile sums, then per-tile offsets + scatter
     const uint32_t nt = (S + 1023) / 1024;
     ulonglong2* ts = scratch<ulonglong2>(ctx, "kept_tiles", nt);
@@ -882,7 +961,8 @@ static int spangroup_run(Slot* ctx, const tsdbhip_sg_desc* d, tsdbhip_sg_out* ou
     X->group_end(ctx);
   }
   Small h;
-  readback(ctx, &h, sm, sizeof h);  // sync 1
+  if (pub1) wait_pub(ctx, p1, &h, sizeof h);  // sync 1
+  else readback(ctx, &h, sm, sizeof h);
   if (h.err != ERR_NONE) throw Fail{err_code(h.err)};
   const uint32_t n_kept = (uint32_t)h.n_kept;
   out->n_input_points = h.n_input;
@@ -1053,6 +1133,8 @@ static int spangroup_run(Slot* ctx, const tsdbhip_sg_desc* d, tsdbhip_sg_out* ou
     // the direct path's verify appends to the direct / fallback lists again:
     // k_grid_popc zeroes their counters (cnt[1], cnt[2])
     ga.zero2 = direct && n_kept ? &sm->cnt[1] : nullptr;
+    ga.pub = next_pub(ctx, sizeof(Small));  // (k_grid_popc or k_grid_scan_blocks, single block, publishes)
+    ga.pub_src = (const uint64_t*)sm;
     if (n_kept)
       hipLaunchKernelGGL(k_grid_mark, dim3(mark_list ? std::min(grid_for(n_kept, 4, 65536), 1024u) : grid_for(n_kept, 4, 65536)),
                          dim3(256), 0, st, ga);
@@ -1064,7 +1146,7 @@ static int spangroup_run(Slot* ctx, const tsdbhip_sg_desc* d, tsdbhip_sg_out* ou
     }
     hipLaunchKernelGGL(k_grid_popc, dim3((unsigned)nb), dim3(256), 0, st, ga);
     if (nb > 1) hipLaunchKernelGGL(k_grid_scan_blocks, dim3(1), dim3(256), 0, st, ga, (uint32_t)nb);
-    readback(ctx, &h, sm, sizeof h);  // sync 2: |G|, flags, F*, errors
+    wait_pub(ctx, ga.pub, &h, sizeof h);  // sync 2: |G|, flags, F*, errors
     after_sync2();
     T = h.T;
     gridv = scratch<uint32_t>(ctx, "grid", T);
@@ -1102,12 +1184,21 @@ static int spangroup_run(Slot* ctx, const tsdbhip_sg_desc* d, tsdbhip_sg_out* ou
   tm.n_grid = T;
   // lazy error index for illegal cells (every span's E and e_bad are final
   // here; sharded: a rank of the global grid, reduced with the exchange)
-  if (n_kept)
-    hipLaunchKernelGGL(k_bad_index, dim3(grid_for(n_kept, 256)), dim3(256), 0, st, e_bad, eoff, e_ts, n_kept,
-                       (int32_t)rate, hi, bitmap, word_rank, lo, T, &sm->bad_at);
+  BadArgs bad;
+  bad.e_bad = e_bad; bad.e_off = eoff; bad.e_ts = e_ts; bad.n_kept = n_kept; bad.rate = (int32_t)rate; bad.hi = hi;
+  bad.lo = lo; bad.bitmap = bitmap; bad.word_rank = word_rank; bad.T = T;
+  // (small unsharded calls: computed by k_call_end instead, one launch fewer)
+  // (k_call_end then runs as one block: its bitmap clearing must follow the
+  // error index's grid ranks)
+  const bool bad_at_end = !sharded && n_kept <= 4096 && T <= 65536;
+  if (n_kept && !bad_at_end)
+    hipLaunchKernelGGL(k_bad_index, dim3(grid_for(n_kept, 256)), dim3(256), 0, st, bad, &sm->bad_at);
 
-  // ---- output block: [Small snapshot | ts T | bits T | is_int T] ----
-  uint8_t* outblk = scratch<uint8_t>(ctx, "outblk", OUT_HDR + 17 * T);
+  // ---- output block: [Small snapshot | ts T | bits T | is_int T], written
+  // by the kernels straight into mapped pinned host memory when small ----
+  const bool small_out = T * 17 <= (256u << 10) && ctx->want_output;
+  map_out_reserve(ctx, OUT_HDR + (small_out ? 17 * T : 0));
+  uint8_t* outblk = small_out ? ctx->map_out_dev : scratch<uint8_t>(ctx, "outblk", OUT_HDR + 17 * T);
   int64_t* o_ts = (int64_t*)(outblk + OUT_HDR);
   int64_t* o_bits = o_ts + T;
   uint8_t* o_isint = (uint8_t*)(o_bits + T);
@@ -1184,7 +1275,9 @@ static int spangroup_run(Slot* ctx, const tsdbhip_sg_desc* d, tsdbhip_sg_out* ou
         r.i_dhas = init->p_dhas; r.i_wim = init->p_wim; r.i_wiv = init->p_wiv; r.i_wdm = init->p_wdm;
         r.i_wdv = init->p_wdv;
       }
-      if (direct) {
+      // (small reductions: the general instantiation takes every chunk, direct
+      // spans included; no flags, one launch)
+      if (direct && n_waves > 4096) {
         uint32_t* ce = scratch<uint32_t>(ctx, "chunk_e", n_chunks);
         hipLaunchKernelGGL(k_chunk_flags_w, dim3(grid_for(n_chunks, 4)), dim3(256), 0, st, dg.info, n_kept, spc,
                            n_chunks, ce);
@@ -1276,14 +1369,11 @@ static int spangroup_run(Slot* ctx, const tsdbhip_sg_desc* d, tsdbhip_sg_out* ou
     X->allreduce(ctx, &sm->bad_at, 1, X_U64, X_MIN);
   }
   // ---- end of call: snapshot + reset of the call state, bitmap cleared ----
-  hipLaunchKernelGGL(k_call_end, dim3(grid_for(T, 256, 1024)), dim3(256), 0, st, sm, (Small*)outblk, small_init(),
-                     bitmap, (const uint32_t*)gridv, T, lo);
+  hipLaunchKernelGGL(k_call_end, dim3(bad_at_end ? 1u : grid_for(T, 256, 1024)), dim3(256), 0, st, sm, (Small*)ctx->map_out_dev,
+                     small_init(), bitmap, (const uint32_t*)gridv, T, lo, bad_at_end ? bad : BadArgs{});
   HIPCHK(hipEventRecord(ctx->ev[5], st));
-  // one D2H copy of the header and (small results) the outputs, one sync
-  const bool small_out = T * 17 <= (256u << 10) && ctx->want_output;
-  uint8_t* hb = (uint8_t*)host_buf(ctx, OUT_HDR + (small_out ? 17 * T : 0));
-  HIPCHK(hipMemcpyAsync(hb, outblk, OUT_HDR + (small_out ? 17 * T : 0), hipMemcpyDeviceToHost, st));
-  HIPCHK(hipStreamSynchronize(st));
+  HIPCHK(hipStreamSynchronize(st));  // (the header and small results are already in host memory)
+  const uint8_t* hb = ctx->map_out;
   std::memcpy(&h, hb, sizeof h);
   ctx->sm_ready = true;
   ctx->bitmap_clean = true;

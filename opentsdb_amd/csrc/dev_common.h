@@ -140,6 +140,28 @@ DEVI void wave_lds_sync() {
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
+// Host-visible publish of a small device state (a call's host round trip
+// without a copy and a stream sync): one wave copies nwords 8-byte words of
+// src (device-coherent loads) into mapped pinned host memory, fences at
+// system scope, then lane 0 stores `seq` to the flag the host spins on.
+// Vector stores only. Call from one whole wave after the state is final.
+struct HostPub {
+  uint64_t* dst;   // mapped host words (device pointer), null: no publish
+  uint64_t* flag;  // mapped host flag
+  uint64_t seq;
+  uint32_t nwords;
+};
+DEVI void host_publish(const HostPub& p, const uint64_t* src) {
+  const int lane = threadIdx.x & (WAVE - 1);
+  for (uint32_t i = lane; i < p.nwords; i += WAVE) {
+    const uint64_t v = __hip_atomic_load(src + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(p.dst + i, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  }
+  __threadfence_system();
+  __builtin_amdgcn_wave_barrier();
+  if (lane == 0) __hip_atomic_store(p.flag, p.seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
 // Position of the (j+1)-th set bit of m (j per lane); requires j < popc(m).
 DEVI int select_bit(uint64_t m, int j) {
   int p = 0;

@@ -29,6 +29,8 @@ struct GridArgs {
   const uint32_t* list_count;
   uint32_t* zero2;            // k_grid_popc: two list counters to zero for the
                               // kernels after the grid (null: none)
+  HostPub pub;                // the call state to the host once T is known (the
+  const uint64_t* pub_src;    // single-block kernel that writes T publishes it)
 };
 
 // Mark every candidate point. Many spans share timestamps (regular cadence),
@@ -90,7 +92,12 @@ __global__ void __launch_bounds__(256) k_grid_popc(GridArgs g) {
     if (gridDim.x == 1) {  // one block: its offset is 0 and its sum is T (no k_grid_scan_blocks)
       g.block_sum[0] = 0;
       g.total[0] = woff + incl;
+      __threadfence();
     }
+  }
+  if (gridDim.x == 1 && g.pub.dst && t >= 192) {  // (the wave holding thread 255)
+    __builtin_amdgcn_wave_barrier();
+    host_publish(g.pub, g.pub_src);
   }
 }
 
@@ -115,7 +122,14 @@ __global__ void __launch_bounds__(256) k_grid_scan_blocks(GridArgs g, uint32_t n
     if (t == 255) s_carry = carry + woff + incl;
     __syncthreads();
   }
-  if (t == 0) g.total[0] = s_carry;
+  if (t == 0) {
+    g.total[0] = s_carry;
+    __threadfence();
+  }
+  if (g.pub.dst && t < WAVE) {
+    __builtin_amdgcn_wave_barrier();
+    host_publish(g.pub, g.pub_src);
+  }
 }
 
 // Adds block offsets and materializes G.

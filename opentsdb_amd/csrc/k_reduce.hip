@@ -332,8 +332,9 @@ DEVI void reduce_wave(const ReduceArgs& r, const uint32_t wave) {
   if (wave >= n_waves) return;
   const uint32_t chunk = wave % r.n_chunks;
   const uint32_t tg = wave / r.n_chunks;
-  if (r.d_info && (r.chunk_e[chunk] != 0) == DONLY) return;  // the other instantiation's chunk
-  if (!r.d_info && DONLY) return;
+  // (no chunk flags: the general instantiation takes every chunk)
+  if (r.d_info && r.chunk_e && (r.chunk_e[chunk] != 0) == DONLY) return;  // the other instantiation's chunk
+  if ((!r.d_info || !r.chunk_e) && DONLY) return;
   const uint32_t k0 = chunk * r.spans_per_chunk;
   const uint32_t k1 = min(r.n_kept, k0 + r.spans_per_chunk);
   const uint64_t n_tiles = (r.T + WAVE - 1) / WAVE;

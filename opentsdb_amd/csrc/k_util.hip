@@ -110,7 +110,7 @@ __global__ void __launch_bounds__(1024) k_kept_compact(const uint8_t* kept, cons
                                                        uint64_t* eoff_k, unsigned long long* n_input,
                                                        const int64_t* sp_first, const int64_t* sp_last,
                                                        unsigned long long* bound, uint64_t* n_kept_out,
-                                                       uint64_t* e_total_out) {
+                                                       uint64_t* e_total_out, HostPub pub, const uint64_t* pub_src) {
   __shared__ uint64_t s_wk[16], s_we[16];
   __shared__ uint64_t s_c[16];
   __shared__ int64_t s_f[16], s_l[16];
@@ -189,6 +189,11 @@ __global__ void __launch_bounds__(1024) k_kept_compact(const uint8_t* kept, cons
       atomicMin(&bound[0], (unsigned long long)f);
       atomicMax(&bound[1], (unsigned long long)l);
     }
+  }
+  if (pub.dst && t < WAVE) {  // the call state, final here, to the host (wave 0)
+    __threadfence();
+    __builtin_amdgcn_wave_barrier();
+    host_publish(pub, pub_src);
   }
 }
 
@@ -295,24 +300,37 @@ __global__ void __launch_bounds__(256) k_kept_scatter_tiles(const uint8_t* kept,
 // A bad cell in E point k is read when point k-1 moves into the current slot
 // (SpanGroup.java:583-608), i.e. while emitting ts(e_{k-1}); points 0 (and 1
 // for rate) are read by the SGIterator constructor.
-__global__ void k_bad_index(const int64_t* e_bad, const uint64_t* e_off, const uint32_t* e_ts,
-                            uint32_t n_kept, int32_t rate, int64_t hi, const uint32_t* bitmap,
-                            const uint32_t* word_rank, int64_t lo, uint64_t T,
-                            unsigned long long* out) {
-  const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
-  if (k >= n_kept) return;
-  const int64_t b = e_bad[k];
-  if (b < 0) return;
-  const uint64_t idx = (uint64_t)(b >> 4), code = (uint64_t)(b & 15);
+struct BadArgs {
+  const int64_t* e_bad;
+  const uint64_t* e_off;
+  const uint32_t* e_ts;
+  uint32_t n_kept;
+  int32_t rate;
+  int64_t hi, lo;
+  const uint32_t* bitmap;
+  const uint32_t* word_rank;
+  uint64_t T;
+};
+// kept span k's error key (grid rank << 4 | code), ~0: none
+DEVI uint64_t bad_key(const BadArgs& b, uint32_t k) {
+  const int64_t e = b.e_bad[k];
+  if (e < 0) return ~0ull;
+  const uint64_t idx = (uint64_t)(e >> 4), code = (uint64_t)(e & 15);
   uint64_t at;
-  if (idx == 0 || (rate && idx == 1)) {
+  if (idx == 0 || (b.rate && idx == 1)) {
     at = 0;
   } else {
-    const int64_t tp = e_ts[e_off[k] + idx - 1];
-    if (tp > hi) return;  // never consumed
-    at = T == 0 ? 0 : grid_rank(bitmap, word_rank, lo, tp);
+    const int64_t tp = b.e_ts[b.e_off[k] + idx - 1];
+    if (tp > b.hi) return ~0ull;  // never consumed
+    at = b.T == 0 ? 0 : grid_rank(b.bitmap, b.word_rank, b.lo, tp);
   }
-  atomicMin(out, (unsigned long long)((at << 4) | code));
+  return (at << 4) | code;
+}
+__global__ void k_bad_index(BadArgs b, unsigned long long* out) {
+  const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
+  if (k >= b.n_kept) return;
+  const uint64_t key = bad_key(b, k);
+  if (key != ~0ull) atomicMin(out, (unsigned long long)key);
 }
 
 // ---- synthetic KeyValues (bit-identical to opentsdb_amd/synth.py) -----------
