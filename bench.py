@@ -298,19 +298,17 @@ def bench_c5(args):
 
     for _ in range(args.warmup):
         step_once()
+    ctx.timing_totals(reset=True)  # (per-call HIP-event timings, summed by the library)
     torch.cuda.synchronize()
-    hot, tot, cx, cls, rows_k = [], [], [], [], []
     t0 = time.perf_counter()
     for _ in range(args.steps):
         step_once()
-        tm = ctx.timing()
-        hot.append(tm.hot_ms)
-        tot.append(tm.total_ms)
-        cx.append(tm.reduce_ms)
-        cls.append(tm.decode_ms)
-        rows_k.append(tm.grid_ms)
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
+    tsum, ncalls = ctx.timing_totals()
+    ncalls = max(ncalls, 1)
+    hot, tot, cx = [tsum.hot_ms / ncalls], [tsum.total_ms / ncalls], [tsum.reduce_ms / ncalls]
+    cls, rows_k = [tsum.decode_ms / ncalls], [tsum.grid_ms / ncalls]
     st = o["st"].cpu().numpy()
     ql = o["ql"].cpu().numpy().astype(np.int64)
     vl = o["vl"].cpu().numpy().astype(np.int64)
@@ -357,11 +355,14 @@ def shard_ranges(n_series, world):
     return [(n_series * r // world, n_series * (r + 1) // world) for r in range(world)]
 
 
-def timed_loop(step_once, sync, barrier, steps, warmup, after_step=None):
+def timed_loop(step_once, sync, barrier, steps, warmup, after_step=None, before_timed=None):
     """W untimed steps, then exactly K steps bracketed by barrier + device
-    sync on both sides; returns this rank's elapsed seconds."""
+    sync on both sides; returns this rank's elapsed seconds. before_timed():
+    after the warm-up, ahead of the opening barrier."""
     for _ in range(warmup):
         step_once()
+    if before_timed:
+        before_timed()
     barrier()
     sync()
     t0 = time.perf_counter()
@@ -606,19 +607,15 @@ def main():
         def step_once():
             ctx.check(L.tsdbhip_spangroup_run_batch(ctx.handle, C.byref(d), Gl, _abi.ptr(gss, C.c_uint32), outs))
 
-    hot_ms, total_ms, hot_kernel, red_ms, emitted = [], [], [0], [], [0, 0]
-
-    def record():
-        tm = ctx.timing()
-        hot_ms.append(tm.hot_ms)
-        total_ms.append(tm.total_ms)
-        red_ms.append(tm.reduce_ms)
-        hot_kernel[0] = tm.hot_kernel
-        emitted[0], emitted[1] = int(tm.n_emitted), int(tm.n_grid)
-
+    # per-call HIP-event timings of the timed steps, summed by the library
+    # (tsdbhip_timing_totals: no readout call inside the timed loop)
     elapsed = max_over_ranks(dist, timed_loop(step_once, torch.cuda.synchronize, barrier, args.steps,
-                                              args.warmup, record))
-    hot_kernel = hot_kernel[0]
+                                              args.warmup, before_timed=lambda: ctx.timing_totals(reset=True)))
+    tsum, ncalls = ctx.timing_totals()
+    ncalls = max(ncalls, 1)
+    hot_ms, total_ms, red_ms = [tsum.hot_ms / ncalls], [tsum.total_ms / ncalls], [tsum.reduce_ms / ncalls]
+    emitted = [int(tsum.n_emitted) // ncalls, int(tsum.n_grid) // ncalls]
+    hot_kernel = tsum.hot_kernel
     # achievable bandwidth on this box, same buffers (tsdbhip_bw_probe): a
     # streaming read with the downsampler's geometry and a D2D copy
     probe = {}

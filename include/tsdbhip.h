@@ -300,6 +300,10 @@ int tsdbhip_host_unregister(tsdbhip_ctx* ctx, void* p);
 int tsdbhip_spangroup_run(tsdbhip_ctx* ctx, const tsdbhip_sg_desc* desc,
                           tsdbhip_sg_out* out);
 int tsdbhip_last_timing(tsdbhip_ctx* ctx, tsdbhip_timing* t);
+/* Sums of the float timing fields (and of n_grid / n_emitted) over every
+ * call on ctx since the last reset, and their count: a caller times many
+ * calls without a per-call readout. reset != 0 zeroes them after reading. */
+int tsdbhip_timing_totals(tsdbhip_ctx* ctx, tsdbhip_timing* sum, uint64_t* n_calls, int32_t reset);
 
 /* ---- group-by batching ------------------------------------------------- */
 /*

@@ -24,6 +24,7 @@ EXPORTS = [
     "tsdbhip_comm_init", "tsdbhip_synth_generate", "tsdbhip_synth_free",
     "tsdbhip_desc_download", "tsdbhip_bw_probe", "tsdbhip_spangroup_run_batch",
     "tsdbhip_format_points", "tsdbhip_open_devices", "tsdbhip_open_mask", "tsdbhip_ranks",
+    "tsdbhip_timing_totals",
 ]
 
 
@@ -77,6 +78,7 @@ def lib():
                                         P(C.c_uint8), P(C.c_int64), C.c_uint64, C.c_char_p, C.c_uint64]
     L.tsdbhip_format_points.restype = C.c_int64
     L.tsdbhip_last_timing.argtypes = [C.c_void_p, P(_abi.Timing)]
+    L.tsdbhip_timing_totals.argtypes = [C.c_void_p, P(_abi.Timing), P(C.c_uint64), C.c_int32]
     L.tsdbhip_compact_rows.argtypes = [C.c_void_p, P(_abi.RowsDesc), P(_abi.RowsOut)]
     L.tsdbhip_compact_rows.restype = C.c_int
     L.tsdbhip_comm_unique_id.argtypes = [C.c_char_p]
@@ -127,6 +129,12 @@ class Context:
         t = _abi.Timing()
         self._lib.tsdbhip_last_timing(self._h, C.byref(t))
         return t
+
+    def timing_totals(self, reset=False):
+        """(sums of the timing fields over the calls since the last reset, number of calls)"""
+        t, n = _abi.Timing(), C.c_uint64()
+        self._lib.tsdbhip_timing_totals(self._h, C.byref(t), C.byref(n), 1 if reset else 0)
+        return t, int(n.value)
 
     def comm_init(self, nranks, rank, uid):
         self.check(self._lib.tsdbhip_comm_init(self._h, nranks, rank, uid))

@@ -93,6 +93,8 @@ struct tsdbhip_ctx {
   std::vector<Slot*> slots, free_slots;
   std::map<std::string, Buf> owned;  // tsdbhip_synth_generate datasets
   tsdbhip_timing last = {};
+  tsdbhip_timing sum = {};  // tsdbhip_timing_totals
+  uint64_t n_sum = 0;
   // one process per GPU (tsdbhip_comm_init): sharded calls serialise on the
   // communicator (every rank must issue its collectives in the same order)
   std::mutex comm_mu;
@@ -212,6 +214,21 @@ static Slot* slot_new(int device) {
 
 static constexpr size_t MAX_SLOTS = 64;  // concurrent calls per context
 
+static void timing_add(tsdbhip_ctx* c, const tsdbhip_timing& t) {  // (c->mu held)
+  c->sum.total_ms += t.total_ms;
+  c->sum.decode_ms += t.decode_ms;
+  c->sum.grid_ms += t.grid_ms;
+  c->sum.reduce_ms += t.reduce_ms;
+  c->sum.exchange_ms += t.exchange_ms;
+  c->sum.hot_ms += t.hot_ms;
+  c->sum.hot_kernel = t.hot_kernel;
+  c->sum.decode_bytes += t.decode_bytes;
+  c->sum.alg_bytes += t.alg_bytes;
+  c->sum.n_grid += t.n_grid;
+  c->sum.n_emitted += t.n_emitted;
+  c->n_sum++;
+}
+
 // A slot held for the duration of one call.
 struct Lease {
   tsdbhip_ctx* c;
@@ -243,6 +260,7 @@ struct Lease {
     g_last_timing = s->timing;
     std::lock_guard<std::mutex> lk(c->mu);
     c->last = s->timing;
+    timing_add(c, s->timing);
     c->free_slots.push_back(s);
   }
 };
@@ -451,6 +469,18 @@ extern "C" int tsdbhip_last_timing(tsdbhip_ctx* ctx, tsdbhip_timing* t) {
   }
   std::lock_guard<std::mutex> lk(ctx->mu);
   *t = ctx->last;
+  return TSDBHIP_OK;
+}
+
+extern "C" int tsdbhip_timing_totals(tsdbhip_ctx* ctx, tsdbhip_timing* sum, uint64_t* n_calls, int32_t reset) {
+  if (!ctx) return TSDBHIP_E_INVALID_ARG;
+  std::lock_guard<std::mutex> lk(ctx->mu);
+  if (sum) *sum = ctx->sum;
+  if (n_calls) *n_calls = ctx->n_sum;
+  if (reset) {
+    ctx->sum = tsdbhip_timing();
+    ctx->n_sum = 0;
+  }
   return TSDBHIP_OK;
 }
 
@@ -798,6 +828,23 @@ static_assert(sizeof(Small) <= OUT_HDR, "Small must fit the output header");
 // End of a call, after the finalize: the call state is snapshot ahead of the
 // outputs (one D2H copy brings both back) and reset for the next call; the
 // words of the grid points are cleared, which leaves the bitmap zero.
+// Groups of up to 1024 spans: the assembly (thread per span, then the
+// deferred spans a wave each) and the kept-list compaction in one 1024-thread
+// block, one launch instead of three.
+__global__ void __launch_bounds__(1024) k_assemble_small(AssembleArgs a, KeptArgs K) {
+  __shared__ uint32_t s_list[1024];
+  __shared__ uint32_t s_n;
+  const uint32_t t = threadIdx.x;
+  if (t == 0) s_n = 0;
+  __syncthreads();
+  if (t < a.n_spans && assemble_fast_one(a, t)) s_list[atomicAdd(&s_n, 1u)] = t;
+  __syncthreads();
+  const uint32_t nd = s_n;
+  for (uint32_t w = t / WAVE; w < nd; w += 1024 / WAVE) assemble_span_wave(a, s_list[w]);
+  __syncthreads();  // (the block's global writes visible to the whole block)
+  kept_compact_block(K);
+}
+
 // Small unsharded calls also compute the lazy error index here (block 0,
 // before the snapshot; bad.n_kept = 0: k_bad_index ran).
 __global__ void __launch_bounds__(256) k_call_end(Small* sm, Small* snap, Small init, uint32_t* bitmap,
@@ -915,6 +962,10 @@ static int spangroup_run(Slot* ctx, const tsdbhip_sg_desc* d, tsdbhip_sg_out* ou
   int64_t* sp_q1 = scratch<int64_t>(ctx, "sp_q1", S);
   int32_t* sp_q1s = scratch<int32_t>(ctx, "sp_q1s", S);
   int64_t* sp_ovf = scratch<int64_t>(ctx, "sp_ovf", S);
+  uint32_t* kept = nullptr;
+  uint64_t* eoff = nullptr;
+  bool pub1 = false;
+  HostPub p1 = {};
   {
     AssembleArgs a;
     a.span_row_start = span_row_start; a.row_base = row_base; a.row_ncells = row_ncells;
@@ -923,31 +974,35 @@ static int spangroup_run(Slot* ctx, const tsdbhip_sg_desc* d, tsdbhip_sg_out* ou
     a.row_ok = row_ok; a.row_cell0 = row_cell0; a.sp_ncells = sp_ncells; a.sp_first = sp_first;
     a.sp_last = sp_last; a.sp_kept = sp_kept; a.sp_cap = sp_cap; a.sp_q1 = sp_q1;
     a.sp_q1_shift = sp_q1s; a.sp_ovf_cell = sp_ovf; a.err = &sm->err;
-    if (S) {  // thread per span, then a wave per span for the ones it queued
+    // kept list, E offsets, counts and bounds (unsharded groups of up to
+    // KC_MAX spans: the kernel hands the call state to the host itself)
+    kept = scratch<uint32_t>(ctx, "kept", S);
+    eoff = scratch<uint64_t>(ctx, "eoff", S);
+    pub1 = !sharded && S && S <= KC_MAX;
+    p1 = pub1 ? next_pub(ctx, sizeof(Small)) : HostPub{};
+    KeptArgs K;
+    K.kept = sp_kept; K.cap = sp_cap; K.ncells = sp_ncells; K.n = S; K.kept_list = kept; K.eoff_k = eoff;
+    K.n_input = &sm->n_input; K.sp_first = sp_first; K.sp_last = sp_last; K.bound = sm->bound;
+    K.n_kept_out = &sm->n_kept; K.e_total_out = &sm->e_total; K.pub = p1; K.pub_src = (const uint64_t*)sm;
+    if (S && S <= 1024) {  // one block: assembly + kept list in one launch
+      hipLaunchKernelGGL(k_assemble_small, dim3(1), dim3(1024), 0, st, a, K);
+    } else if (S) {  // thread per span, then a wave per span for the ones it queued
       uint32_t* alist = scratch<uint32_t>(ctx, "asm_list", S);
       uint32_t* acount = &sm->cnt[0];
       hipLaunchKernelGGL(k_assemble_fast, dim3(grid_for(S, 256)), dim3(256), 0, st, a, alist, acount);
       hipLaunchKernelGGL(k_assemble, dim3(grid_for(S, 4, 4096)), dim3(256), 0, st, a, (const uint32_t*)alist,
                          (const uint32_t*)acount);
+      if (S <= KC_MAX) {
+        hipLaunchKernelGGL(k_kept_compact, dim3(1), dim3(1024), 0, st, K);
+      } else {  // bigger groups: tile sums, then per-tile offsets + scatter
+        const uint32_t nt = (S + 1023) / 1024;
+        ulonglong2* ts = scratch<ulonglong2>(ctx, "kept_tiles", nt);
+        hipLaunchKernelGGL(k_kept_tiles, dim3(nt), dim3(256), 0, st, sp_kept, sp_cap, S, ts);
+        hipLaunchKernelGGL(k_kept_scatter_tiles, dim3(nt), dim3(256), 0, st, sp_kept, sp_cap, sp_ncells, S,
+                           (const ulonglong2*)ts, kept, eoff, &sm->n_input, sp_first, sp_last, sm->bound,
+                           &sm->n_kept, &sm->e_total);
+      }
     }
-  }
-  uint32_t* kept = scratch<uint32_t>(ctx, "kept", S);
-  uint64_t* eoff = scratch<uint64_t>(ctx, "eoff", S);
-  // (unsharded groups of up to KC_MAX spans: the kept-list kernel hands the
-  // call state to the host itself, no readback)
-  const bool pub1 = !sharded && S && S <= KC_MAX;
-  const HostPub p1 = pub1 ? next_pub(ctx, sizeof(Small)) : HostPub{};
-  if (S && S <= KC_MAX) {  // kept list, E offsets, counts and bounds: one launch
-    hipLaunchKernelGGL(k_kept_compact, dim3(1), dim3(1024), 0, st, sp_kept, sp_cap, sp_ncells, S, kept, eoff,
-                       &sm->n_input, sp_first, sp_last, sm->bound, &sm->n_kept, &sm->e_total, p1,
-                       (const uint64_t*)sm);
-  } else if (S) {  // bigger groups: tile sums, then per-tile offsets + scatter
-    const uint32_t nt = (S + 1023) / 1024;
-    ulonglong2* ts = scratch<ulonglong2>(ctx, "kept_tiles", nt);
-    hipLaunchKernelGGL(k_kept_tiles, dim3(nt), dim3(256), 0, st, sp_kept, sp_cap, S, ts);
-    hipLaunchKernelGGL(k_kept_scatter_tiles, dim3(nt), dim3(256), 0, st, sp_kept, sp_cap, sp_ncells, S,
-                       (const ulonglong2*)ts, kept, eoff, &sm->n_input, sp_first, sp_last, sm->bound, &sm->n_kept,
-                       &sm->e_total);
   }
   if (sharded) {
     // every rank needs the same bitmap geometry and the same error: the kept
@@ -1591,6 +1646,7 @@ static int multi_run(tsdbhip_ctx* mc, const tsdbhip_sg_desc* desc, tsdbhip_sg_ou
   {
     std::lock_guard<std::mutex> l2(mc->mu);
     mc->last = g_last_timing;
+    timing_add(mc, g_last_timing);
   }
   int rc = rcs[0];
   int first = -1;

@@ -197,10 +197,11 @@ DEVI void assemble_finish(const AssembleArgs& a, uint32_t s, bool has_rows) {
 // chain after the other: spans of many rows — a day of hourly rows — go to
 // the wave kernel, which loads 64 rows at once.)
 constexpr uint32_t ASM_ROWS = 4;
-__global__ void __launch_bounds__(256) k_assemble_fast(AssembleArgs a, uint32_t* list, uint32_t* count) {
-  const uint32_t s = blockIdx.x * blockDim.x + threadIdx.x;
+// The thread-per-span case for span s (< n_spans); true: deferred to the
+// wave walk.
+DEVI bool assemble_fast_one(const AssembleArgs& a, uint32_t s) {
   bool defer = false;
-  if (s < a.n_spans) {
+  {
     const uint64_t r0 = a.span_row_start[s], r1 = a.span_row_start[s + 1];
     bool ok = r1 > r0 && r1 - r0 <= ASM_ROWS;
     int64_t pb = -1, pl = -1, first_ts = 0;
@@ -236,6 +237,12 @@ __global__ void __launch_bounds__(256) k_assemble_fast(AssembleArgs a, uint32_t*
       defer = true;
     }
   }
+  return defer;
+}
+
+__global__ void __launch_bounds__(256) k_assemble_fast(AssembleArgs a, uint32_t* list, uint32_t* count) {
+  const uint32_t s = blockIdx.x * blockDim.x + threadIdx.x;
+  const bool defer = s < a.n_spans && assemble_fast_one(a, s);
   // queue the deferred spans (one atomic per wave)
   const uint64_t m = ballot(defer);
   if (m) {
@@ -318,13 +325,9 @@ DEVI bool assemble_walk(const AssembleArgs& a, uint32_t s, uint64_t r0, uint64_t
 // after the previous one ended, no RowSeq merge possible) is verified
 // wave-parallel; anything else falls back to an exact sequential walk by
 // lane 0 (the reference's own algorithm, O(rows)).
-__global__ void __launch_bounds__(256) k_assemble(AssembleArgs a, const uint32_t* list, const uint32_t* count) {
+DEVI void assemble_span_wave(const AssembleArgs& a, uint32_t s) {
   const int lane = lane_id();
-  const uint32_t wave = (blockIdx.x * blockDim.x + threadIdx.x) / WAVE;
-  const uint32_t nwaves = gridDim.x * blockDim.x / WAVE;
-  const uint32_t nw = list ? *count : a.n_spans;
-  for (uint32_t w = wave; w < nw; w += nwaves) {
-    const uint32_t s = list ? list[w] : w;
+  {
     const uint64_t r0 = a.span_row_start[s], r1 = a.span_row_start[s + 1];
     bool ok = r1 > r0;
     int64_t prev_last = -1, prev_base = -1;
@@ -377,6 +380,13 @@ __global__ void __launch_bounds__(256) k_assemble(AssembleArgs a, const uint32_t
       assemble_finish(a, s, r1 > r0);
     }
   }
+}
+
+__global__ void __launch_bounds__(256) k_assemble(AssembleArgs a, const uint32_t* list, const uint32_t* count) {
+  const uint32_t wave = (blockIdx.x * blockDim.x + threadIdx.x) / WAVE;
+  const uint32_t nwaves = gridDim.x * blockDim.x / WAVE;
+  const uint32_t nw = list ? *count : a.n_spans;
+  for (uint32_t w = wave; w < nw; w += nwaves) assemble_span_wave(a, list ? list[w] : w);
 }
 
 }  // namespace tsdb

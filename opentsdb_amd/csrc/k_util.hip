@@ -105,12 +105,29 @@ __global__ void __launch_bounds__(256) k_kept_scatter(const uint8_t* kept, const
 // multi-block single pass would need a look-back across the XCDs' separate
 // L2s, i.e. device-scope fences per tile: slower than the scan kernels.)
 constexpr uint32_t KC_MAX = 1u << 14;
-__global__ void __launch_bounds__(1024) k_kept_compact(const uint8_t* kept, const uint64_t* cap,
-                                                       const uint32_t* ncells, uint32_t n, uint32_t* kept_list,
-                                                       uint64_t* eoff_k, unsigned long long* n_input,
-                                                       const int64_t* sp_first, const int64_t* sp_last,
-                                                       unsigned long long* bound, uint64_t* n_kept_out,
-                                                       uint64_t* e_total_out, HostPub pub, const uint64_t* pub_src) {
+struct KeptArgs {
+  const uint8_t* kept;
+  const uint64_t* cap;
+  const uint32_t* ncells;
+  uint32_t n;
+  uint32_t* kept_list;
+  uint64_t* eoff_k;
+  unsigned long long* n_input;
+  const int64_t* sp_first;
+  const int64_t* sp_last;
+  unsigned long long* bound;
+  uint64_t* n_kept_out;
+  uint64_t* e_total_out;
+  HostPub pub;
+  const uint64_t* pub_src;
+};
+// (a 1024-thread block)
+DEVI void kept_compact_block(const KeptArgs& A) {
+  const uint8_t* kept = A.kept; const uint64_t* cap = A.cap; const uint32_t* ncells = A.ncells;
+  const uint32_t n = A.n; uint32_t* kept_list = A.kept_list; uint64_t* eoff_k = A.eoff_k;
+  unsigned long long* n_input = A.n_input; const int64_t* sp_first = A.sp_first; const int64_t* sp_last = A.sp_last;
+  unsigned long long* bound = A.bound; uint64_t* n_kept_out = A.n_kept_out; uint64_t* e_total_out = A.e_total_out;
+  const HostPub& pub = A.pub; const uint64_t* pub_src = A.pub_src;
   __shared__ uint64_t s_wk[16], s_we[16];
   __shared__ uint64_t s_c[16];
   __shared__ int64_t s_f[16], s_l[16];
@@ -196,6 +213,7 @@ __global__ void __launch_bounds__(1024) k_kept_compact(const uint8_t* kept, cons
     host_publish(pub, pub_src);
   }
 }
+__global__ void __launch_bounds__(1024) k_kept_compact(KeptArgs A) { kept_compact_block(A); }
 
 // Bigger groups in two launches: per tile of 1024 spans its (kept, capacity)
 // sums; then each tile adds up its predecessors' sums itself (at most a few
