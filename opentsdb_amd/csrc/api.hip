@@ -621,6 +621,14 @@ struct LaunchFastDs {
     hipLaunchKernelGGL((k_decode_fast<AGG, true>), dim3(blocks), dim3(256), 0, ctx->stream, a, ncells, vlen);
   }
 };
+// (a leftover list: the general code inline, one launch)
+struct LaunchFastDsInl {
+  template <int AGG>
+  static void run(Slot* ctx, unsigned blocks, const DecodeArgs& a, const uint32_t* ncells,
+                  const uint32_t* vlen) {
+    hipLaunchKernelGGL((k_decode_fast<AGG, true, true>), dim3(blocks), dim3(256), 0, ctx->stream, a, ncells, vlen);
+  }
+};
 
 // Streaming downsampling of regular-cadence integer spans (k_ds_spans, wave
 // per span); leaves the spans it did not take in fa.span_list for
@@ -1120,10 +1128,14 @@ static int spangroup_run(Slot* ctx, const tsdbhip_sg_desc* d, tsdbhip_sg_out* ou
         mark_list = dg.list;
         mark_count = dg.list_count;
       }
-      const unsigned lblocks = fa.span_list ? std::min(blocks, 1024u) : blocks;
-      hipLaunchKernelGGL((k_decode_fast<0, false>), dim3(lblocks), dim3(256), 0, st, fa, row_ncells, row_val_len);
-      if (!direct) HIPCHK(hipEventRecord(ctx->ev[9], st));
-      hipLaunchKernelGGL(k_decode_nods, dim3(std::min(blocks, 1024u)), dim3(256), 0, st, ga);
+      if (fa.span_list) {  // (the direct scan's leftovers: general code inline)
+        hipLaunchKernelGGL((k_decode_fast<0, false, true>), dim3(std::min(blocks, 1024u)), dim3(256), 0, st, fa,
+                           row_ncells, row_val_len);
+      } else {
+        hipLaunchKernelGGL((k_decode_fast<0, false>), dim3(blocks), dim3(256), 0, st, fa, row_ncells, row_val_len);
+        HIPCHK(hipEventRecord(ctx->ev[9], st));
+        hipLaunchKernelGGL(k_decode_nods, dim3(std::min(blocks, 1024u)), dim3(256), 0, st, ga);
+      }
     } else {
       DecodeArgs fa = da;
       if (chunks && ds_agg != 4) {
@@ -1139,26 +1151,18 @@ static int spangroup_run(Slot* ctx, const tsdbhip_sg_desc* d, tsdbhip_sg_out* ou
         mark_list = fa.span_list;
         mark_count = fa.span_count;
       }
-      // (grid-stride over the spans left by k_ds_spans: usually few)
-      const unsigned lblocks = fa.span_list ? std::min(blocks, 1024u) : blocks;
-      launch_agg<LaunchFastDs>(ds_agg, ctx, lblocks, fa, row_ncells, row_val_len);
-      if (ctx->hot_kernel == TSDBHIP_HOT_DECODE_FAST) HIPCHK(hipEventRecord(ctx->ev[9], st));
-      launch_agg<LaunchGeneralDs>(ds_agg, ctx, std::min(blocks, 1024u), ga);
+      if (fa.span_list) {  // (grid-stride over the spans left by k_ds_spans: usually few; general inline)
+        launch_agg<LaunchFastDsInl>(ds_agg, ctx, std::min(blocks, 1024u), fa, row_ncells, row_val_len);
+      } else {
+        launch_agg<LaunchFastDs>(ds_agg, ctx, blocks, fa, row_ncells, row_val_len);
+        if (ctx->hot_kernel == TSDBHIP_HOT_DECODE_FAST) HIPCHK(hipEventRecord(ctx->ev[9], st));
+        launch_agg<LaunchGeneralDs>(ds_agg, ctx, std::min(blocks, 1024u), ga);
+      }
     }
   }
   if (detail) HIPCHK(hipEventRecord(ctx->ev[2], st));
-  if (n_kept)
-    hipLaunchKernelGGL(k_span_summary, dim3(grid_for(n_kept, 256, 1024)), dim3(256), 0, st, da, mark_list, mark_count);
-  if (sharded) {
-    // agree on the int/float flags, F*, the error and the input count across
-    // ranks, in place, ahead of the one readback
-    X->group_start(ctx);
-    X->allreduce(ctx, sm->gflags, 2, X_U32, X_MAX);
-    X->allreduce(ctx, &sm->fstar, 1, X_U64, X_MAX);
-    X->allreduce(ctx, &sm->err, 1, X_U64, X_MIN);
-    X->allreduce(ctx, &sm->n_input, 1, X_U64, X_SUM);
-    X->group_end(ctx);
-  }
+  // (k_span_summary's work, empty spans and F*, is done by k_grid_mark below:
+  // a kept span implies a non-empty grid range)
   // (no readback here: the flags, F*, errors and input count come back with
   // |G| below. A decode error leaves every e_len <= its capacity, so the grid
   // kernels stay inside E before the error is thrown.)
@@ -1190,9 +1194,22 @@ static int spangroup_run(Slot* ctx, const tsdbhip_sg_desc* d, tsdbhip_sg_out* ou
     ga.zero2 = direct && n_kept ? &sm->cnt[1] : nullptr;
     ga.pub = next_pub(ctx, sizeof(Small));  // (k_grid_popc or k_grid_scan_blocks, single block, publishes)
     ga.pub_src = (const uint64_t*)sm;
+    ga.e_flt = e_flt;
+    ga.err = &sm->err;
+    ga.fstar = &sm->fstar;
     if (n_kept)
       hipLaunchKernelGGL(k_grid_mark, dim3(mark_list ? std::min(grid_for(n_kept, 4, 65536), 1024u) : grid_for(n_kept, 4, 65536)),
                          dim3(256), 0, st, ga);
+    if (sharded) {
+      // agree on the int/float flags, F*, the error and the input count across
+      // ranks, in place, ahead of the one readback
+      X->group_start(ctx);
+      X->allreduce(ctx, sm->gflags, 2, X_U32, X_MAX);
+      X->allreduce(ctx, &sm->fstar, 1, X_U64, X_MAX);
+      X->allreduce(ctx, &sm->err, 1, X_U64, X_MIN);
+      X->allreduce(ctx, &sm->n_input, 1, X_U64, X_SUM);
+      X->group_end(ctx);
+    }
     if (sharded) {
       uint32_t* all = scratch<uint32_t>(ctx, "bitmap_all", nwords * X->nranks);
       X->allgather(ctx, bitmap, all, nwords * 4);
@@ -1223,13 +1240,18 @@ static int spangroup_run(Slot* ctx, const tsdbhip_sg_desc* d, tsdbhip_sg_out* ou
       DecodeArgs fa = da;
       fa.span_list = dg.list;
       fa.span_count = dg.list_count;
-      hipLaunchKernelGGL((k_decode_fast<0, false>), dim3(std::min(grid_for(n_kept, 4, 65536), 1024u)), dim3(256), 0,
-                         st, fa, row_ncells, row_val_len);
-      DecodeArgs gfa = da;
-      gfa.use_fb = 1;
-      hipLaunchKernelGGL(k_decode_nods, dim3(std::min(grid_for(n_kept, 4, 65536), 1024u)), dim3(256), 0, st, gfa);
+      hipLaunchKernelGGL((k_decode_fast<0, false, true>), dim3(std::min(grid_for(n_kept, 4, 65536), 1024u)), dim3(256),
+                         0, st, fa, row_ncells, row_val_len);
     }
   } else {
+    if (sharded) {  // (the same agreement as above)
+      X->group_start(ctx);
+      X->allreduce(ctx, sm->gflags, 2, X_U32, X_MAX);
+      X->allreduce(ctx, &sm->fstar, 1, X_U64, X_MAX);
+      X->allreduce(ctx, &sm->err, 1, X_U64, X_MIN);
+      X->allreduce(ctx, &sm->n_input, 1, X_U64, X_SUM);
+      X->group_end(ctx);
+    }
     readback(ctx, &h, sm, sizeof h);  // sync 2 (no grid)
     after_sync2();
   }

@@ -162,9 +162,14 @@ DEVI void ffinalize(const DecodeArgs& a, const FBucket& b, uint64_t eidx, uint64
   a.e_flt[eo + eidx] = !allint;
 }
 
-template <int AGG, bool DS>
+// INL: the spans this kernel cannot take go straight to the general code in
+// the same wave (k_decode.hip) instead of a list for a second launch; for the
+// short leftover lists of k_direct_scan / k_ds_spans (one launch fewer).
+template <int AGG, bool DS, bool INL = false>
 __global__ void __launch_bounds__(256, 3) k_decode_fast(DecodeArgs a, const uint32_t* ncells, const uint32_t* vlen) {
   __shared__ FastLds lds[4];
+  __shared__ int64_t s_gbits[INL && DS ? 4 : 1][WAVE];
+  __shared__ uint8_t s_gflt[INL && DS ? 4 : 1][WAVE];
   const int lane = lane_id();
   const int wib = threadIdx.x / WAVE;
   FastLds& L = lds[wib];
@@ -452,8 +457,13 @@ __global__ void __launch_bounds__(256, 3) k_decode_fast(DecodeArgs a, const uint
         continue;
       }
     }
-    // ---- fallback: queue the span for the general kernel (rewrites its E) ----
-    if (lane == 0) a.fb_list[atomicAdd(a.fb_count, 1u)] = k;
+    // ---- fallback: the general code rewrites the span's E ----
+    if (INL) {
+      if (DS) span_ds_general<AGG>(a, k, s_gbits[INL && DS ? wib : 0], s_gflt[INL && DS ? wib : 0]);
+      else span_nods_general(a, k);
+    } else if (lane == 0) {  // (queued for the general kernel)
+      a.fb_list[atomicAdd(a.fb_count, 1u)] = k;
+    }
   }
 }
 

@@ -29,6 +29,11 @@ struct GridArgs {
   const uint32_t* list_count;
   uint32_t* zero2;            // k_grid_popc: two list counters to zero for the
                               // kernels after the grid (null: none)
+  // k_grid_mark also does k_span_summary's work for its spans when err is set:
+  // an empty E raises E_EMPTY_SPAN, a float first point raises F* (non-rate)
+  const uint8_t* e_flt;
+  unsigned long long* err;
+  unsigned long long* fstar;
   HostPub pub;                // the call state to the host once T is known (the
   const uint64_t* pub_src;    // single-block kernel that writes T publishes it)
 };
@@ -40,10 +45,16 @@ __global__ void __launch_bounds__(256) k_grid_mark(GridArgs g) {
   const uint32_t wave = (blockIdx.x * blockDim.x + threadIdx.x) / WAVE;
   const uint32_t nwaves = gridDim.x * blockDim.x / WAVE;
   const uint32_t n = g.list ? *g.list_count : g.n_kept;
+  int64_t fs = 0;  // F* + 1 of this wave's spans (0: none)
+  bool empty = false;
   for (uint32_t w = wave; w < n; w += nwaves) {
     const uint32_t k = g.list ? g.list[w] : w;
     const uint64_t eo = g.e_off[k];
     const uint32_t len = g.e_len[k];
+    if (g.err) {
+      empty |= len == 0;
+      if (len && !g.rate && g.e_flt[eo]) fs = max(fs, (int64_t)g.e_ts[eo] + 1);
+    }
     for (uint32_t i0 = g.rate ? 1 : 0; i0 < len; i0 += WAVE) {
       const uint32_t i = i0 + lane;
       if (i >= len) break;
@@ -55,6 +66,11 @@ __global__ void __launch_bounds__(256) k_grid_mark(GridArgs g) {
       uint32_t* w = &g.bitmap[b >> 5];
       if (!(*w & bit)) atomicOr(w, bit);
     }
+  }
+  if (g.err && lane == 0) {  // (wave-uniform values)
+    if (empty) err_raise(g.err, 2, 0, -3 /*E_EMPTY_SPAN*/);
+    if (fs && (unsigned long long)fs > *(volatile unsigned long long*)g.fstar)
+      atomicMax(g.fstar, (unsigned long long)fs);
   }
 }
 
