@@ -66,9 +66,9 @@ extern "C" {
 #define TSDBHIP_E_OUT_OF_BOUNDS -9  /* reference would throw
                                        ArrayIndexOutOfBoundsException */
 #define TSDBHIP_E_NO_DEVICE    -10
-#define TSDBHIP_E_UNSUPPORTED  -11 /* Q1 stale-qualifier seek whose shifted
-                                       reads cross merged rows (never on the
-                                       TsdbQuery path)      */
+#define TSDBHIP_E_UNSUPPORTED  -11 /* reserved (ABI v3 raised it for a Q1
+                                       seek whose shifted reads cross merged
+                                       rows; those are now reproduced)       */
 
 /* ---- aggregator op codes (Aggregators.java:44-48 names) --------------- */
 #define TSDBHIP_AGG_SUM 0

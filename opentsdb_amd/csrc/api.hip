@@ -969,6 +969,7 @@ static int spangroup_run(Slot* ctx, const tsdbhip_sg_desc* d, tsdbhip_sg_out* ou
   uint64_t* sp_cap = scratch<uint64_t>(ctx, "sp_cap", S);
   int64_t* sp_q1 = scratch<int64_t>(ctx, "sp_q1", S);
   int32_t* sp_q1s = scratch<int32_t>(ctx, "sp_q1s", S);
+  int64_t* sp_q1rs = scratch<int64_t>(ctx, "sp_q1rs", 2ull * S);
   int64_t* sp_ovf = scratch<int64_t>(ctx, "sp_ovf", S);
   uint32_t* kept = nullptr;
   uint64_t* eoff = nullptr;
@@ -981,7 +982,7 @@ static int spangroup_run(Slot* ctx, const tsdbhip_sg_desc* d, tsdbhip_sg_out* ou
     a.n_spans = S; a.start = d->start_time; a.end = d->end_time; a.interval = interval;
     a.row_ok = row_ok; a.row_cell0 = row_cell0; a.sp_ncells = sp_ncells; a.sp_first = sp_first;
     a.sp_last = sp_last; a.sp_kept = sp_kept; a.sp_cap = sp_cap; a.sp_q1 = sp_q1;
-    a.sp_q1_shift = sp_q1s; a.sp_ovf_cell = sp_ovf; a.err = &sm->err;
+    a.sp_q1_shift = sp_q1s; a.sp_q1_rs = sp_q1rs; a.sp_ovf_cell = sp_ovf; a.err = &sm->err;
     // kept list, E offsets, counts and bounds (unsharded groups of up to
     // KC_MAX spans: the kernel hands the call state to the host itself)
     kept = scratch<uint32_t>(ctx, "kept", S);
@@ -1063,6 +1064,7 @@ static int spangroup_run(Slot* ctx, const tsdbhip_sg_desc* d, tsdbhip_sg_out* ou
   da.span_row_start = span_row_start; da.row_base = row_base; da.row_qual_off = row_qual_off;
   da.row_val_off = row_val_off; da.qual = qual; da.val = val; da.row_ok = row_ok; da.row_cell0 = row_cell0;
   da.kept = kept; da.n_kept = n_kept; da.sp_ncells = sp_ncells; da.sp_q1 = sp_q1; da.sp_q1_shift = sp_q1s;
+  da.sp_q1_rs = sp_q1rs; da.row_ncells = row_ncells; da.row_val_len = row_val_len;
   da.sp_ovf_cell = sp_ovf; da.sp_cap = sp_cap; da.e_off = eoff; da.e_ts = e_ts; da.e_val = e_val;
   da.e_flt = e_flt; da.e_len = e_len; da.e_bad = e_bad; da.start = d->start_time; da.end = d->end_time;
   da.interval = interval; da.ds_agg = ds_agg; da.rate = rate; da.err = &sm->err; da.gflags = sm->gflags;

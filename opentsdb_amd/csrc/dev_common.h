@@ -330,6 +330,25 @@ DEVI bool decode_value(const uint8_t* vals, uint64_t off, uint32_t flags, int64_
   return false;
 }
 
+// decode_value of a value already assembled: u = its bytes, big-endian, in
+// the low bits (len = (flags & 7) + 1 bytes)
+DEVI bool decode_be(uint64_t u, uint32_t flags, int64_t* bits) {
+  const int lm = flags & 7;
+  if (flags & 8) {
+    if (lm == 7) { *bits = (int64_t)u; return true; }
+    if (lm == 3) { *bits = dbits((double)__uint_as_float((uint32_t)u)); return true; }
+    *bits = 0;
+    return false;
+  }
+  if (lm == 7 || lm == 3 || lm == 1 || lm == 0) {
+    const int sh = 64 - 8 * (lm + 1);
+    *bits = (int64_t)(u << sh) >> sh;  // sign-extend
+    return true;
+  }
+  *bits = 0;
+  return false;
+}
+
 // toDouble() of a decoded cell / E point.
 DEVI double to_double(int64_t bits, bool is_float) { return is_float ? bitsd(bits) : (double)bits; }
 

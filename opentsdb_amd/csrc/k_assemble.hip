@@ -35,6 +35,7 @@ struct AssembleArgs {
   uint64_t* sp_cap;       // [n_spans] E capacity (0 if not kept)
   int64_t* sp_q1;         // [n_spans] Q1: row read with shifted offsets, -1 none
   int32_t* sp_q1_shift;   // [n_spans]
+  int64_t* sp_q1_rs;      // [2 n_spans] rows [rs0, rs1) of the RowSeq the seek lands in
   int64_t* sp_ovf_cell;   // [n_spans] span cell index that overflows the
                           // RowSeq.Iterator `short` value_index, -1 none
   unsigned long long* err;  // [1] first error (err_raise key)
@@ -150,22 +151,20 @@ __device__ void assemble_slow(const AssembleArgs& a, uint32_t s, uint64_t r0, ui
       }
     }
     const int32_t shift = (int32_t)slen - (int32_t)k;
-    // does the seek RowSeq continue past crow (merged rows read shifted too)?
-    bool more = false;
-    for (uint64_t r = crow + 1; r < r1; r++) {
-      if (!a.row_ok[r]) continue;
-      more = a.row_ok[r] == 1;
-      break;
-    }
+    // the seek RowSeq ends at the next row that starts a RowSeq: its cells from
+    // the seek on are read at their offsets in the merged values array minus
+    // the shift, across its merged rows (RowSeq.java:92-172, 405-421)
+    uint64_t rs1 = r1;
+    for (uint64_t r = crow + 1; r < r1; r++)
+      if (a.row_ok[r] == 2) { rs1 = r; break; }
     if (shift != 0) {
-      if (crow != seek_rs_row0 || rows_in_rs > 1 || more) {
-        err_raise(a.err, 2, s, TSDBHIP_E_UNSUPPORTED);  // shifted reads across merged rows
-      } else {
-        a.sp_q1[s] = (int64_t)crow;
-        a.sp_q1_shift[s] = shift;
-      }
+      a.sp_q1[s] = (int64_t)crow;
+      a.sp_q1_shift[s] = shift;
+      a.sp_q1_rs[2ull * s] = (int64_t)seek_rs_row0;
+      a.sp_q1_rs[2ull * s + 1] = (int64_t)rs1;
     }
     (void)seek_rs_cell0;
+    (void)rows_in_rs;
   }
 }
 

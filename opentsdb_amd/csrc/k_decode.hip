@@ -38,6 +38,9 @@ struct DecodeArgs {
   const uint32_t* sp_ncells;
   const int64_t* sp_q1;
   const int32_t* sp_q1_shift;
+  const int64_t* sp_q1_rs;    // [2 n_spans] the seek RowSeq's rows [rs0, rs1)
+  const uint32_t* row_ncells;
+  const uint32_t* row_val_len;
   const int64_t* sp_ovf_cell;
   const uint64_t* sp_cap;
   const uint64_t* e_off;      // [n_kept]
@@ -70,11 +73,42 @@ struct CellChunk {
   int64_t bits;
 };
 
+// Quirk Q1 across merged rows (RowSeq.java:405-421): the RowSeq's values
+// array is its rows' value bytes (meta bytes stripped) concatenated
+// (RowSeq.java:152-165); a cell at offset `off` of its row `row` is read at
+// its merged offset minus `shift`, gathered byte by byte from the rows
+// [rs0, rs1) (the read may start in an earlier row or straddle two).
+DEVI uint32_t dec_row_vbytes(const DecodeArgs& a, uint64_t q) {
+  const uint32_t n = a.row_ncells[q], vl = a.row_val_len[q];
+  return n > 1 && vl > 0 ? vl - 1 : vl;
+}
+DEVI bool q1_merged_read(const DecodeArgs& a, uint64_t rs0, uint64_t rs1, uint64_t row, uint64_t off, int32_t shift,
+                         uint32_t fl, int64_t* bits) {
+  uint64_t acc = 0;
+  for (uint64_t q = rs0; q < row; q++)
+    if (a.row_ok[q]) acc += dec_row_vbytes(a, q);
+  const uint64_t p = acc + off - (uint64_t)(int64_t)shift;
+  const uint32_t lm = fl & 7;
+  const uint32_t len = (fl & 8) ? (lm == 7 ? 8u : 4u) : lm + 1;
+  uint64_t u = 0, seg = 0, q = rs0;
+  for (uint32_t b = 0; b < len; b++) {
+    const uint64_t pos = p + b;
+    while (q < rs1 && (!a.row_ok[q] || pos >= seg + dec_row_vbytes(a, q))) {
+      if (a.row_ok[q]) seg += dec_row_vbytes(a, q);
+      q++;
+    }
+    const uint32_t byte = q < rs1 ? a.val[a.row_val_off[q] + (pos - seg)] : 0u;
+    u = (u << 8) | byte;
+  }
+  return decode_be(u, fl, bits);
+}
+
 // Decodes cell c0+lane of span (rows [r0,r1)). Carries the running value
 // offset of the row that continues into the next chunk.
 DEVI void decode_chunk(const DecodeArgs& a, uint64_t r0, uint64_t r1, uint32_t n, uint32_t c0,
                        int64_t q1_row, int32_t q1_shift, int64_t ovf_cell,
-                       int64_t& carry_row, uint64_t& carry_off, CellChunk& o) {
+                       int64_t& carry_row, uint64_t& carry_off, CellChunk& o, uint64_t q1_rs0 = 0,
+                       uint64_t q1_rs1 = 0) {
   const int lane = lane_id();
   const uint32_t c = c0 + lane;
   o.valid = c < n;
@@ -115,9 +149,11 @@ DEVI void decode_chunk(const DecodeArgs& a, uint64_t r0, uint64_t r1, uint32_t n
   o.okv = true;
   o.bits = 0;
   if (o.valid) {
-    uint64_t voff = off;
-    if (row == q1_row && o.in_e) voff -= (uint64_t)(int64_t)q1_shift;  // quirk Q1
-    if (o.in_e) o.okv = decode_value(a.val, a.row_val_off[row] + voff, fl, &o.bits);
+    const bool q1 = q1_row >= 0 && o.in_e && row >= q1_row && (uint64_t)row < q1_rs1;  // quirk Q1
+    if (q1 && (q1_rs0 != (uint64_t)q1_row || q1_rs1 != (uint64_t)q1_row + 1))
+      o.okv = q1_merged_read(a, q1_rs0, q1_rs1, (uint64_t)row, off, q1_shift, fl, &o.bits);
+    else if (o.in_e)  // (a one-row RowSeq: its own bytes, shifted)
+      o.okv = decode_value(a.val, a.row_val_off[row] + off - (q1 ? (uint64_t)(int64_t)q1_shift : 0ull), fl, &o.bits);
     if ((int64_t)c >= ovf_cell && ovf_cell >= 0) o.okv = false;
   }
 }
@@ -139,6 +175,8 @@ __device__ void span_nods_general(const DecodeArgs& a, uint32_t k) {
     const uint32_t n = a.sp_ncells[s];
     const int64_t q1_row = a.sp_q1[s], ovf = a.sp_ovf_cell[s];
     const int32_t q1_shift = a.sp_q1_shift[s];
+    const uint64_t q1_rs0 = q1_row >= 0 ? (uint64_t)a.sp_q1_rs[2ull * s] : 0ull;
+    const uint64_t q1_rs1 = q1_row >= 0 ? (uint64_t)a.sp_q1_rs[2ull * s + 1] : 0ull;
     const uint64_t eo = a.e_off[k];
     int64_t carry_row = -1; uint64_t carry_off = 0;
     int64_t prev_ts = -1;
@@ -147,7 +185,7 @@ __device__ void span_nods_general(const DecodeArgs& a, uint32_t k) {
     bool unsorted = false, anyf = false, anyi = false;
     for (uint32_t c0 = 0; c0 < n; c0 += WAVE) {
       CellChunk o;
-      decode_chunk(a, r0, r1, n, c0, q1_row, q1_shift, ovf, carry_row, carry_off, o);
+      decode_chunk(a, r0, r1, n, c0, q1_row, q1_shift, ovf, carry_row, carry_off, o, q1_rs0, q1_rs1);
       int64_t pts = (int64_t)shfl_up_u64((uint64_t)o.ts, 1);
       if (lane == 0) pts = prev_ts;
       if (ballot(o.valid && o.ts <= pts) != 0) unsorted = true;
@@ -244,6 +282,8 @@ __device__ void span_ds_general(const DecodeArgs& a, uint32_t k, int64_t* s_bits
     const uint32_t n = a.sp_ncells[s];
     const int64_t q1_row = a.sp_q1[s], ovf = a.sp_ovf_cell[s];
     const int32_t q1_shift = a.sp_q1_shift[s];
+    const uint64_t q1_rs0 = q1_row >= 0 ? (uint64_t)a.sp_q1_rs[2ull * s] : 0ull;
+    const uint64_t q1_rs1 = q1_row >= 0 ? (uint64_t)a.sp_q1_rs[2ull * s + 1] : 0ull;
     const uint64_t eo = a.e_off[k], cap = a.sp_cap[s];
     // dev always needs the ordered Welford; others start FAST (int path only)
     bool seq = (AGG == 4);
@@ -259,7 +299,7 @@ __device__ void span_ds_general(const DecodeArgs& a, uint32_t k, int64_t* s_bits
     wf_init(cb.wf); cb.bad = false;
     for (uint32_t c0 = 0; c0 < n; c0 += WAVE) {
       CellChunk o;
-      decode_chunk(a, r0, r1, n, c0, q1_row, q1_shift, ovf, carry_row, carry_off, o);
+      decode_chunk(a, r0, r1, n, c0, q1_row, q1_shift, ovf, carry_row, carry_off, o, q1_rs0, q1_rs1);
       const int lastv = (int)((n - c0) < 64u ? (n - c0) : 64u) - 1;
       int64_t pts = (int64_t)shfl_up_u64((uint64_t)o.ts, 1);
       if (lane == 0) pts = prev_ts;

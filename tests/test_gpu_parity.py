@@ -226,6 +226,35 @@ def test_q1_seek_inside_row_minimal_widths(ctx):
         assert_same(g, o, exact_double=True)
 
 
+@pytest.mark.parametrize("start_off", [3200, 3560, 3700, 3890])
+def test_q1_seek_across_merged_rows(ctx, start_off):
+    """Quirk Q1 where the RowSeq the seek lands in holds two merged hourly rows
+    (the second row ends less than 4096 s after the first row's base,
+    RowSeq.java:92-172): every later cell of the RowSeq is read at its offset
+    in the merged values array minus the shift, so reads straddle the rows
+    and, for a seek inside the second row, start in the first row's bytes."""
+    T = T0
+    rng = np.random.default_rng(start_off)
+    mags = [0, 7, 15, 31, 40, 62]
+
+    def vals(n):
+        return [int(rng.integers(-(1 << 62), 1 << 62)) >> int(rng.choice(mags)) for _ in range(n)]
+
+    pts_a = [T + 3000 + 7 * i for i in range(80)] + [T + 3600 + 5 * i for i in range(60)] + \
+        [T + 7200 + 11 * i for i in range(30)]
+    pts_b = [T + 3100 + 9 * i for i in range(50)] + [T + 3601 + 3 * i for i in range(90)]
+    spans = [I(list(zip(pts_a, vals(len(pts_a)))), minimal=True),
+             I(list(zip(pts_b, vals(len(pts_b)))), minimal=True),
+             I([(T + 2900 + 13 * i, 5 * i) for i in range(100)], minimal=False)]
+    ss = packing.pack_spans(spans)
+    for agg in AGGS:
+        g, o = run_both(ctx, ss, start=T + start_off, agg=agg, exact=True)
+        assert_same(g, o, exact_double=True)
+    for dsi, dsa in ((60, 0), (45, 2)):
+        g, o = run_both(ctx, ss, start=T + start_off, agg=0, ds_interval=dsi, ds_agg=dsa, exact=True)
+        assert_same(g, o, exact_double=True)
+
+
 def test_minimal_width_ints(ctx):
     T = T0
     rng = np.random.default_rng(9)
