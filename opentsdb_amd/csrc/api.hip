@@ -993,7 +993,10 @@ static int spangroup_run(Slot* ctx, const tsdbhip_sg_desc* d, tsdbhip_sg_out* ou
     K.kept = sp_kept; K.cap = sp_cap; K.ncells = sp_ncells; K.n = S; K.kept_list = kept; K.eoff_k = eoff;
     K.n_input = &sm->n_input; K.sp_first = sp_first; K.sp_last = sp_last; K.bound = sm->bound;
     K.n_kept_out = &sm->n_kept; K.e_total_out = &sm->e_total; K.pub = p1; K.pub_src = (const uint64_t*)sm;
-    if (S && S <= 1024) {  // one block: assembly + kept list in one launch
+    // one block: assembly + kept list in one launch, for groups with few rows
+    // (the block's 16 waves walk the deferred spans: a group of long spans of
+    // many rows, C4's, needs the wave-per-span kernel's whole grid)
+    if (S && S <= 1024 && R <= 8192) {
       hipLaunchKernelGGL(k_assemble_small, dim3(1), dim3(1024), 0, st, a, K);
     } else if (S) {  // thread per span, then a wave per span for the ones it queued
       uint32_t* alist = scratch<uint32_t>(ctx, "asm_list", S);
