@@ -366,6 +366,21 @@ DEVI void wf_push(Welford& w, double x) {
   w.var += (x - w.mean) * (x - nm);
   w.mean = nm;
 }
+// The same with (x - mean) / n as a product with a refined reciprocal of n
+// (within an ulp or two of the quotient): for double-path dev outside
+// TSDBHIP_EXACT_ORDER, whose tolerance (1e-9 relative) already admits the
+// chunk-merge reordering; integer dev and EXACT_ORDER keep the division.
+DEVI void wf_push_rcp(Welford& w, double x) {
+  if (w.n == 0) { w.mean = x; w.n = 1; return; }
+  w.n++;
+  const double dn = (double)w.n;
+  double r = __builtin_amdgcn_rcp(dn);
+  r = __builtin_fma(__builtin_fma(-dn, r, 1.0), r, r);  // one Newton step
+  const double d = x - w.mean;
+  const double nm = __builtin_fma(d, r, w.mean);
+  w.var += d * (x - nm);
+  w.mean = nm;
+}
 // Chan et al. merge (A precedes B); used only across span chunks/ranks.
 DEVI void wf_merge(Welford& a, const Welford& b) {
   if (b.n == 0) return;

@@ -128,11 +128,13 @@ struct Acc {
   int64_t ia;
   double da;
   Welford wi, wd;
+  bool fastdiv;    // wd pushes through wf_push_rcp (not EXACT_ORDER)
 };
 
 DEVI void acc_init(Acc& a) {
   a.cnt = 0; a.flag = 0; a.dhas = 0; a.ia = 0; a.da = 0;
   wf_init(a.wi); wf_init(a.wd);
+  a.fastdiv = false;
 }
 
 template <int AGG, int MODE>
@@ -146,7 +148,10 @@ DEVI void acc_push(Acc& a, int64_t yi, double yd) {
     else a.ia = ladd(a.ia, yi);
   }
   if (MODE != MODE_INT) {
-    if (AGG == 4) wf_push(a.wd, yd);
+    if (AGG == 4) {
+      if (a.fastdiv) wf_push_rcp(a.wd, yd);
+      else wf_push(a.wd, yd);
+    }
     else if (AGG == 1 || AGG == 2) {
       if (yd != yd) { if (first) a.flag |= 2u; }
       else if (!a.dhas) { a.da = yd; a.dhas = 1; }
@@ -418,6 +423,7 @@ DEVI void reduce_wave(const ReduceArgs& r, const uint32_t wave) {
     Acc acc;
     if (gv) acc_start<AGG, MODE>(r, g, acc);
     else acc_init(acc);
+    acc.fastdiv = AGG == 4 && MODE != MODE_INT && !r.exact;
     // dual mode: t before the latest float-first point is on the double path
     // whatever the spans hold (F*, SpanGroup.java:632-645); once every lane's
     // t is known to be double, no long lerp of this tile is ever read
