@@ -1210,8 +1210,7 @@ DEVI uint4 ld16_any(const uint8_t* src, uint64_t x) {
   const uint4* p = (const uint4*)(pa & ~(uintptr_t)15);
   const uint32_t sh = (uint32_t)(pa & 15);
   const uint4 A = p[0];
-  if (sh == 0) return A;
-  const uint4 B = p[1];
+  const uint4 B = p[1];  // (also when aligned: no branch; alignbyte by 0 keeps A)
   const uint32_t w[8] = {A.x, A.y, A.z, A.w, B.x, B.y, B.z, B.w};
   const uint32_t s4 = sh >> 2, sb = sh & 3;
   uint32_t v[5];
@@ -1312,36 +1311,33 @@ __global__ void __launch_bounds__(256) k_compact_vals(CompactArgs a) {
       }
     }
     const uint64_t m = cv_meta(w);
+    // (branch-light: the scalar unit, shared by the CU's waves, bounded the
+    // branchy version — 780 SALU per wave)
     for (uint64_t i0 = 0; ballot(i0 < nch); i0 += 16) {
       const uint64_t k = i0 + sub;
-      if (k >= nch) continue;
+      const bool act = k < nch;
       const uintptr_t c = c0 + 16 * k;
       const uint64_t o = c - ov_abs, y0 = o - w.s, x = w.in + y0;
       const uint64_t xa = x + 4 * ((w.h0 <= y0) + (w.h1 <= y0));
       const bool in0 = w.h0 > y0 && w.h0 < y0 + 16, in1 = w.h1 > y0 && w.h1 < y0 + 16;  // holes inside
-      bool done = false;
-      if (o + 16 <= m && !(in0 && in1)) {
-        if (!in0 && !in1) *(uint4*)c = ld16_any(a.val, xa);  // one source
-        else  // one hole inside: from it on, 4 bytes further down the input
-          *(uint4*)c = cq_funnel(ld16_any(a.val, xa), ld16_any(a.val, xa + 4), (int)((in0 ? w.h0 : w.h1) - y0), false);
-        done = true;
-      } else if (m < o + 16 && !in0 && !in1) {
-        // the meta byte at m - o; then the unused bytes; then the next row
-        // (one byte further down the input; 4 more when its first KV is a
-        // legacy float), which must have no hole and no end inside the chunk
-        bool ok = true;
-        uint64_t xb = x - 1;
-        if (w.e < o + 16) {
-          const uint64_t L = o + 16 - w.e;
-          ok = r + 1 < a.n_rows && n.ok && !(n.h0 > 0 && n.h0 < L) && !(n.h1 > 0 && n.h1 < L) && cv_meta(n) >= o + 16;
-          if (n.h0 == 0) xb += 4;
-        }
-        if (ok && xb + 1 != 0) {  // (B's source starts inside the buffer)
-          *(uint4*)c = cq_funnel(ld16_any(a.val, xa), ld16_any(a.val, xb), (int)(m - o), true);
-          done = true;
-        }
+      // one source, or one hole inside (from it on, 4 bytes further down the input)
+      const bool c1 = o + 16 <= m && !(in0 && in1);
+      // the meta byte at m - o; then the unused bytes; then the next row (one
+      // byte further down the input; 4 more when its first KV is a legacy
+      // float), which must have no hole and no end inside the chunk
+      uint64_t xb = x - 1;
+      bool ok = true;
+      if (w.e < o + 16) {
+        const uint64_t L = o + 16 - w.e;
+        ok = r + 1 < a.n_rows && n.ok && !(n.h0 > 0 && n.h0 < L) && !(n.h1 > 0 && n.h1 < L) && cv_meta(n) >= o + 16;
+        if (n.h0 == 0) xb += 4;
       }
-      if (!done) {  // byte by byte, walking the rows
+      const bool c2 = !c1 && m < o + 16 && !in0 && !in1 && ok && xb + 1 != 0;  // (B inside the buffer)
+      if (act && (c1 || c2)) {
+        const uint64_t xB = c1 ? xa + 4 : xb;
+        const int pos = c1 ? (in0 ? (int)(w.h0 - y0) : in1 ? (int)(w.h1 - y0) : 16) : (int)(m - o);
+        *(uint4*)c = cq_funnel(ld16_any(a.val, xa), ld16_any(a.val, xB), pos, !c1);
+      } else if (act) {  // byte by byte, walking the rows (two boundaries in the chunk)
         CvRow u = w;
         uint64_t ru = r;
         for (int b = 0; b < 16; b++) {
