@@ -458,8 +458,8 @@ __global__ void __launch_bounds__(256) k_compact_complex(CompactArgs a) {
 // ===========================================================================
 constexpr int CT_ROWS = 16;    // rows per tile
 constexpr int CT_QB = 4096;    // qualifier bytes per tile
-constexpr int CT_VB = 8192;    // value bytes per tile
-constexpr int CT_KB = 1536;    // KVs per tile
+constexpr int CT_VB = 7168;    // value bytes per tile (with CT_KB: k_compact_rows fits 4 blocks per CU)
+constexpr int CT_KB = 1280;    // KVs per tile
 constexpr int CT_SORT = 256;   // cells of an in-wave complexCompact
 constexpr int CQ_RUNS_SLOTS = 12;
 
