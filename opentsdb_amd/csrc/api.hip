@@ -836,6 +836,10 @@ static_assert(sizeof(Small) <= OUT_HDR, "Small must fit the output header");
 // End of a call, after the finalize: the call state is snapshot ahead of the
 // outputs (one D2H copy brings both back) and reset for the next call; the
 // words of the grid points are cleared, which leaves the bitmap zero.
+// The call state to the host (host_publish) after a producer that could not
+// publish it itself (a multi-block kernel, a collective).
+__global__ void __launch_bounds__(64) k_publish(HostPub pub, const uint64_t* src) { host_publish(pub, src); }
+
 // Groups of up to 1024 spans: the assembly (thread per span, then the
 // deferred spans a wave each) and the kept-list compaction in one 1024-thread
 // block, one launch instead of three.
@@ -1028,8 +1032,11 @@ static int spangroup_run(Slot* ctx, const tsdbhip_sg_desc* d, tsdbhip_sg_out* ou
     X->group_end(ctx);
   }
   Small h;
-  if (pub1) wait_pub(ctx, p1, &h, sizeof h);  // sync 1
-  else readback(ctx, &h, sm, sizeof h);
+  if (!pub1) {  // (the state's last writer cannot publish it: a one-wave kernel does)
+    p1 = next_pub(ctx, sizeof(Small));
+    hipLaunchKernelGGL(k_publish, dim3(1), dim3(64), 0, st, p1, (const uint64_t*)sm);
+  }
+  wait_pub(ctx, p1, &h, sizeof h);  // sync 1
   if (h.err != ERR_NONE) throw Fail{err_code(h.err)};
   const uint32_t n_kept = (uint32_t)h.n_kept;
   out->n_input_points = h.n_input;
