@@ -830,12 +830,66 @@ static Small small_init() {
   init.bound[1] = 0;
   return init;
 }
+// Several MIN / MAX agreements on call-state fields as one MIN allreduce of a
+// packed buffer (across GPUs each collective costs a latency of its own;
+// one rank: the plain per-field calls)
+struct XField { void* p; uint8_t kind; };  // kind: 0 u64 MIN, 1 u64 MAX, 2 u32 MAX
+static void xchg_minmax(Slot* ctx, Xchg* X, const XField* f, uint32_t n, uint64_t* sum_u64 = nullptr);
 constexpr size_t OUT_HDR = 512;  // the Small snapshot ahead of the outputs
 static_assert(sizeof(Small) <= OUT_HDR, "Small must fit the output header");
 
 // End of a call, after the finalize: the call state is snapshot ahead of the
 // outputs (one D2H copy brings both back) and reset for the next call; the
 // words of the grid points are cleared, which leaves the bitmap zero.
+// Packing of small call-state fields for one MIN allreduce (a MAX field
+// travels complemented): one thread moves up to 8 words in or out of a
+// contiguous u64 buffer. kinds: 0 u64, 1 ~u64, 2 ~u32 (to u64); out: the same
+// inverses.
+struct XMove {
+  uint32_t n;
+  uint8_t kind[8];
+  uint64_t* buf;     // [n] the packed words
+  void* field[8];    // the call-state fields
+  int32_t out;       // 0: fields -> buf, 1: buf -> fields
+};
+__global__ void k_xmove(XMove m) {
+  for (uint32_t i = 0; i < m.n; i++) {
+    if (!m.out) {
+      uint64_t v = m.kind[i] == 2 ? (uint64_t)*(const uint32_t*)m.field[i] : *(const uint64_t*)m.field[i];
+      m.buf[i] = m.kind[i] ? ~v : v;
+    } else {
+      const uint64_t v = m.kind[i] ? ~m.buf[i] : m.buf[i];
+      if (m.kind[i] == 2) *(uint32_t*)m.field[i] = (uint32_t)v;
+      else *(uint64_t*)m.field[i] = v;
+    }
+  }
+}
+
+// (sum_u64: one more field, a u64 SUM, in the same collective group. The
+// pack / unpack kernels stay outside the group: RCCL issues a group's
+// collectives at its end.)
+static void xchg_minmax(Slot* ctx, Xchg* X, const XField* f, uint32_t n, uint64_t* sum_u64) {
+  if (X->nranks == 1) {
+    X->group_start(ctx);
+    for (uint32_t i = 0; i < n; i++)
+      X->allreduce(ctx, f[i].p, 1, f[i].kind == 2 ? X_U32 : X_U64, f[i].kind ? X_MAX : X_MIN);
+    if (sum_u64) X->allreduce(ctx, sum_u64, 1, X_U64, X_SUM);
+    X->group_end(ctx);
+    return;
+  }
+  XMove m = {};
+  m.n = n;
+  m.buf = scratch<uint64_t>(ctx, "x_pack", 8);
+  for (uint32_t i = 0; i < n; i++) { m.kind[i] = f[i].kind; m.field[i] = f[i].p; }
+  hipLaunchKernelGGL(k_xmove, dim3(1), dim3(1), 0, ctx->stream, m);
+  X->group_start(ctx);
+  X->allreduce(ctx, m.buf, n, X_U64, X_MIN);
+  if (sum_u64) X->allreduce(ctx, sum_u64, 1, X_U64, X_SUM);
+  X->group_end(ctx);
+  m.out = 1;
+  hipLaunchKernelGGL(k_xmove, dim3(1), dim3(1), 0, ctx->stream, m);
+}
+
 // The call state to the host (host_publish) after a producer that could not
 // publish it itself (a multi-block kernel, a collective).
 __global__ void __launch_bounds__(64) k_publish(HostPub pub, const uint64_t* src) { host_publish(pub, src); }
@@ -1025,11 +1079,8 @@ static int spangroup_run(Slot* ctx, const tsdbhip_sg_desc* d, tsdbhip_sg_out* ou
     // spans' bounds (min first, max last; ranks without kept spans hold the
     // neutral ~0 / 0) and the error code (most negative) are reduced in place,
     // so the one readback below returns the agreed values
-    X->group_start(ctx);
-    X->allreduce(ctx, &sm->bound[0], 1, X_U64, X_MIN);
-    X->allreduce(ctx, &sm->bound[1], 1, X_U64, X_MAX);
-    X->allreduce(ctx, &sm->err, 1, X_U64, X_MIN);
-    X->group_end(ctx);
+    const XField fa[3] = {{&sm->bound[0], 0}, {&sm->bound[1], 1}, {&sm->err, 0}};
+    xchg_minmax(ctx, X, fa, 3);
   }
   Small h;
   if (!pub1) {  // (the state's last writer cannot publish it: a one-wave kernel does)
@@ -1215,12 +1266,8 @@ static int spangroup_run(Slot* ctx, const tsdbhip_sg_desc* d, tsdbhip_sg_out* ou
     if (sharded) {
       // agree on the int/float flags, F*, the error and the input count across
       // ranks, in place, ahead of the one readback
-      X->group_start(ctx);
-      X->allreduce(ctx, sm->gflags, 2, X_U32, X_MAX);
-      X->allreduce(ctx, &sm->fstar, 1, X_U64, X_MAX);
-      X->allreduce(ctx, &sm->err, 1, X_U64, X_MIN);
-      X->allreduce(ctx, &sm->n_input, 1, X_U64, X_SUM);
-      X->group_end(ctx);
+      const XField fb[4] = {{&sm->gflags[0], 2}, {&sm->gflags[1], 2}, {&sm->fstar, 1}, {&sm->err, 0}};
+      xchg_minmax(ctx, X, fb, 4, (uint64_t*)&sm->n_input);
     }
     if (sharded) {
       uint32_t* all = scratch<uint32_t>(ctx, "bitmap_all", nwords * X->nranks);
@@ -1257,12 +1304,8 @@ static int spangroup_run(Slot* ctx, const tsdbhip_sg_desc* d, tsdbhip_sg_out* ou
     }
   } else {
     if (sharded) {  // (the same agreement as above)
-      X->group_start(ctx);
-      X->allreduce(ctx, sm->gflags, 2, X_U32, X_MAX);
-      X->allreduce(ctx, &sm->fstar, 1, X_U64, X_MAX);
-      X->allreduce(ctx, &sm->err, 1, X_U64, X_MIN);
-      X->allreduce(ctx, &sm->n_input, 1, X_U64, X_SUM);
-      X->group_end(ctx);
+      const XField fb[4] = {{&sm->gflags[0], 2}, {&sm->gflags[1], 2}, {&sm->fstar, 1}, {&sm->err, 0}};
+      xchg_minmax(ctx, X, fb, 4, (uint64_t*)&sm->n_input);
     }
     readback(ctx, &h, sm, sizeof h);  // sync 2 (no grid)
     after_sync2();
