@@ -587,6 +587,16 @@ def main():
     out = _abi.SgOut(capacity=cap, ts=_abi.ptr(ts, C.c_int64), is_int=_abi.ptr(isi, C.c_uint8),
                      bits=_abi.ptr(bits, C.c_int64))
 
+    def pin(*arrs):
+        # result buffers page-locked, as the JNI bridge registers its
+        # DirectByteBuffers (tsdbhip_host_register): the D2H
+        # of a large result is then one DMA
+        for a in arrs:
+            if a.nbytes:
+                ctx.check(L.tsdbhip_host_register(ctx.handle, a.ctypes.data_as(C.c_void_p), a.nbytes))
+
+    pin(ts, isi, bits)
+
     def step_once():
         ctx.check(L.tsdbhip_spangroup_run(ctx.handle, C.byref(d), C.byref(out)))
 
@@ -597,6 +607,7 @@ def main():
         g_ts = np.zeros(Gl * gcap, np.int64)
         g_isi = np.zeros(Gl * gcap, np.uint8)
         g_bits = np.zeros(Gl * gcap, np.int64)
+        pin(g_ts, g_isi, g_bits)
         outs = (_abi.SgOut * Gl)()
         for g in range(Gl):
             outs[g].capacity = gcap
