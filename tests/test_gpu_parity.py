@@ -342,6 +342,35 @@ def test_row_assembly_rules(ctx):
             assert_same(g, o, exact_double=True)
 
 
+@pytest.mark.parametrize("seed,p_short", [(11, 0.5), (12, 1.0), (13, 0.15), (14, 0.85)])
+def test_hourly_row_pairs(ctx, seed, p_short):
+    """Spans of many hourly rows where a row whose cells end within 496 s of
+    the hour merges into the RowSeq its predecessor started (Span.java:117,
+    last - base < 4096), so merges alternate along runs of such rows; runs
+    cross the 64-row batches of the wave walk. The last span also holds a
+    row two hours on (no merge), and one span repeats a row (slow walk)."""
+    T = T0
+    rng = np.random.default_rng(seed)
+    spans = []
+    for n_rows in (150, 129, 65, 64, 3):
+        rows = []
+        for k in range(n_rows):
+            base = T + 3600 * k
+            hi = 490 if rng.random() < p_short else 3599
+            offs = sorted(set(int(x) for x in rng.integers(0, hi + 1, 6)))
+            rows.append(synth.compact_cells(base, [(base + o, 0x7, int(rng.integers(-1 << 40, 1 << 40)).to_bytes(
+                8, "big", signed=True)) for o in offs]))
+        spans.append(rows)
+    b = T + 3600 * 151
+    spans[-1] = spans[-1] + [synth.compact_cells(b, [(b + 5, 0x0, bytes([3]))])]
+    spans.append(spans[1][:71] + [spans[1][70]] + spans[1][71:])
+    ss = packing.pack_spans(spans)
+    for agg in AGGS:
+        for ds in ((0, 0), (600, 3)):
+            g, o = run_both(ctx, ss, agg=agg, ds_interval=ds[0], ds_agg=ds[1], exact=True)
+            assert_same(g, o, exact_double=True)
+
+
 def test_short_overflow_merged_rowseq(ctx):
     """RowSeq.Iterator's short value_index overflows past 32767 value bytes."""
     T = T0
