@@ -508,30 +508,6 @@ DEVI void reduce_wave(const ReduceArgs& r, const uint32_t wave) {
       }
       return jn;
     };
-    // A span with no point in this tile (its next point j lies past t_last):
-    // every lane's bracket is (j-1, j), all from the cache.
-    auto cached = [&](uint32_t j, uint32_t len, uint2 x, longlong2 y, double rv, uint32_t f, double y0d, double dyd,
-                      double rinv) {
-      if (!gv || j >= len) return;  // expired (all points consumed before this tile)
-      if (RATE) {  // cur = j-1 (j >= 1), constant over the tile; active: tl <= last
-        if (len >= 2) acc_push<AGG, MODE>(acc, 0, rv);
-        return;
-      }
-      if (j == 0) return;  // not started (F* covers the float look-ahead)
-      const bool fc = (f & 1u) != 0, fn = (f & 2u) != 0;
-      if (MODE == MODE_DUAL && (fc || fn)) acc.flag |= 1u;
-      int64_t yi = 0;
-      double yd = 0.0;
-      if (need_long(fc, fn)) yi = lerp_long(tl, (int64_t)x.x, y.x, (int64_t)x.y, y.y);
-      if (MODE != MODE_INT) {
-        // y0 + ((double)(t - x0) * (y1 - y0)) / (double)(x1 - x0), with y0 and
-        // y1 - y0 converted once per batch; outside TSDBHIP_EXACT_ORDER the
-        // division is a product with the batch-computed reciprocal (<= 1 ulp)
-        const double num = (double)(uint32_t)(tl - (int64_t)x.x) * dyd;
-        yd = r.exact ? y0d + num / (double)(uint32_t)(x.y - x.x) : y0d + num * rinv;
-      }
-      acc_push<AGG, MODE>(acc, yi, yd);
-    };
     // A direct span (k_direct.hip) at lane g: E index e = g - ga; its value
     // is the cell itself (non-rate: active iff 0 <= e < n), or its constant-
     // step difference (rate: e = j - 1 for point j; e < 0 is the Q5 state
@@ -609,6 +585,18 @@ DEVI void reduce_wave(const ReduceArgs& r, const uint32_t wave) {
         dyd_l = to_double(y_l.y, MODE == MODE_DBL || (f_l & 2u)) - y0d_l;
         rinv_l = 1.0 / (double)(x_l.y - x_l.x);
       }
+      // the long lerp of the cached bracket: |y1 - y0| (bit 31: negative), or
+      // UINT32_MAX when it is 2^31 - 1 or more (general lerp); |y1 - y0| / d
+      uint32_t im_l = UINT32_MAX;
+      double magr_l = 0.0;
+      if (!RATE && MODE != MODE_DBL && el && (f_l & 4u) && x_l.y > x_l.x) {
+        const int64_t dy = lsub(y_l.y, y_l.x);
+        const uint64_t mag = dy < 0 ? (uint64_t)0 - (uint64_t)dy : (uint64_t)dy;
+        if (mag < 0x7fffffffull) {
+          im_l = (uint32_t)mag | (dy < 0 ? 0x80000000u : 0u);
+          magr_l = (double)mag / (double)(x_l.y - x_l.x);
+        }
+      }
       const uint64_t dmask = ballot(dl);
       uint32_t dga_l = 0, dn_l = 0, dx0_l = 0, dstep_l = 0;
       uint64_t dvo_l = 0;
@@ -641,6 +629,58 @@ DEVI void reduce_wave(const ReduceArgs& r, const uint32_t wave) {
       }
       const uint64_t smask = ballot(sc && (int64_t)x2_l > t_last);
       const uint32_t nb = min((uint32_t)WAVE, k1 - kb);
+      // A span with no point in this tile (its next point j lies past t_last):
+      // every lane's bracket is (j-1, j), all from the cache (the span's lane
+      // i of the batch registers above; only what the lerp reads is broadcast).
+      auto cached = [&](uint32_t i) {
+        const uint32_t j = readlane_u32(j_l, (int)i), len = readlane_u32(len_l, (int)i);
+        if (!gv || j >= len) return;  // expired (all points consumed before this tile)
+        if (RATE) {  // cur = j-1 (j >= 1), constant over the tile; active: tl <= last
+          if (len >= 2)
+            acc_push<AGG, MODE>(acc, 0, __longlong_as_double((long long)readlane_u64((uint64_t)__double_as_longlong(rv_l), (int)i)));
+          return;
+        }
+        if (j == 0) return;  // not started (F* covers the float look-ahead)
+        const uint32_t f = readlane_u32(f_l, (int)i);
+        const bool fc = (f & 1u) != 0, fn = (f & 2u) != 0;
+        if (MODE == MODE_DUAL && (fc || fn)) acc.flag |= 1u;
+        const uint32_t x0 = readlane_u32(x_l.x, (int)i);
+        const uint32_t u = (uint32_t)(tl - (int64_t)x0);  // 0 < u < x1 - x0
+        int64_t yi = 0;
+        double yd = 0.0;
+        if (need_long(fc, fn)) {
+          const uint32_t x1 = readlane_u32(x_l.y, (int)i);
+          const int64_t y0 = (int64_t)readlane_u64((uint64_t)y_l.x, (int)i);
+          const uint32_t im = readlane_u32(im_l, (int)i);
+          if (im != UINT32_MAX) {
+            // |y1 - y0| < 2^31: the long product cannot wrap, and the quotient
+            // is the double estimate u * (|dy| / d) (error < 2^-20) made exact
+            // by one remainder check
+            const double magr = __longlong_as_double((long long)readlane_u64((uint64_t)__double_as_longlong(magr_l), (int)i));
+            const uint32_t mag = im & 0x7fffffffu, d = x1 - x0;
+            uint32_t q = (uint32_t)((double)u * magr);
+            const int64_t rem = (int64_t)((uint64_t)u * mag) - (int64_t)((uint64_t)q * d);
+            q = rem < 0 ? q - 1u : (rem >= (int64_t)d ? q + 1u : q);
+            yi = ladd(y0, (im >> 31) ? -(int64_t)q : (int64_t)q);
+          } else {
+            yi = lerp_long(tl, (int64_t)x0, y0, (int64_t)x1, (int64_t)readlane_u64((uint64_t)y_l.y, (int)i));
+          }
+        }
+        if (MODE != MODE_INT) {
+          // y0 + ((double)(t - x0) * (y1 - y0)) / (double)(x1 - x0), with y0 and
+          // y1 - y0 converted once per batch; outside TSDBHIP_EXACT_ORDER the
+          // division is a product with the batch-computed reciprocal (<= 1 ulp)
+          const double y0d = __longlong_as_double((long long)readlane_u64((uint64_t)__double_as_longlong(y0d_l), (int)i));
+          const double dyd = __longlong_as_double((long long)readlane_u64((uint64_t)__double_as_longlong(dyd_l), (int)i));
+          const double num = (double)u * dyd;
+          if (r.exact) {
+            yd = y0d + num / (double)(readlane_u32(x_l.y, (int)i) - x0);
+          } else {
+            yd = y0d + num * __longlong_as_double((long long)readlane_u64((uint64_t)__double_as_longlong(rinv_l), (int)i));
+          }
+        }
+        acc_push<AGG, MODE>(acc, yi, yd);
+      };
       for (uint32_t i = 0; i < nb;) {
         if ((dsingle >> i) & 1) {
           // a run of single-row direct spans with this span's width and type
@@ -740,20 +780,7 @@ DEVI void reduce_wave(const ReduceArgs& r, const uint32_t wave) {
           continue;
         }
         if ((cmask >> i) & 1) {
-          const uint2 x = make_uint2(readlane_u32(x_l.x, (int)i), readlane_u32(x_l.y, (int)i));
-          longlong2 y = make_longlong2(0, 0);
-          double rv = 0.0;
-          if (RATE) rv = __longlong_as_double((long long)readlane_u64((uint64_t)__double_as_longlong(rv_l), (int)i));
-          else y = make_longlong2((long long)readlane_u64((uint64_t)y_l.x, (int)i),
-                                  (long long)readlane_u64((uint64_t)y_l.y, (int)i));
-          double y0d = 0.0, dyd = 0.0, rinv = 0.0;
-          if (!RATE && MODE != MODE_INT) {
-            y0d = __longlong_as_double((long long)readlane_u64((uint64_t)__double_as_longlong(y0d_l), (int)i));
-            dyd = __longlong_as_double((long long)readlane_u64((uint64_t)__double_as_longlong(dyd_l), (int)i));
-            rinv = __longlong_as_double((long long)readlane_u64((uint64_t)__double_as_longlong(rinv_l), (int)i));
-          }
-          cached(readlane_u32(j_l, (int)i), readlane_u32(len_l, (int)i), x, y, rv, readlane_u32(f_l, (int)i), y0d,
-                 dyd, rinv);
+          cached(i);
           i++;
           continue;
         }

@@ -255,6 +255,31 @@ def test_q1_seek_across_merged_rows(ctx, start_off):
         assert_same(g, o, exact_double=True)
 
 
+@pytest.mark.parametrize("seed", [21, 22])
+def test_cached_long_lerp_bounds(ctx, seed):
+    """Long lerp of a span with no point in a tile (the cached bracket):
+    |y1 - y0| just under, at and over 2^31 - 1 (the double-estimate quotient
+    vs the general 64-bit division), both signs, quotients that land exactly
+    on integers, and brackets up to 2^24 s wide under a dense span."""
+    T = T0
+    rng = np.random.default_rng(seed)
+    dense = I([(T + 1 + 3 * i, int(v)) for i, v in enumerate(rng.integers(-9, 9, 3000))], minimal=True)
+    spans = [dense]
+    M31 = (1 << 31) - 1
+    for dy in (M31 - 2, M31 - 1, M31, M31 + 1, 1 << 40, 8999, 9000, 1):
+        for sign in (1, -1):
+            y0 = int(rng.integers(-(1 << 50), 1 << 50))
+            d = int(rng.choice([9000, 7, 4096, 1 << 24]))
+            x0 = T + int(rng.integers(0, 40))
+            spans.append(I([(x0, y0), (x0 + d, y0 + sign * dy), (x0 + d + 5, y0)], minimal=True))
+    ss = packing.pack_spans(spans)
+    for agg in AGGS:
+        g, o = run_both(ctx, ss, agg=agg, exact=True)
+        assert_same(g, o, exact_double=True)
+        g, o = run_both(ctx, ss, agg=agg)
+        assert_same(g, o)
+
+
 def test_minimal_width_ints(ctx):
     T = T0
     rng = np.random.default_rng(9)
