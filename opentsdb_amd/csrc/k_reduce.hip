@@ -242,6 +242,29 @@ DEVI int64_t lerp_long(int64_t x, int64_t x0, int64_t y0, int64_t x1, int64_t y1
 DEVI double lerp_double(int64_t x, int64_t x0, double y0, int64_t x1, double y1) {
   return y0 + ((double)(x - x0) * (y1 - y0)) / (double)(x1 - x0);
 }
+// The long lerp of a bracket fixed over a tile, prepared once per span
+// (lane-parallel): im = |y1 - y0| with bit 31 its sign, or UINT32_MAX when
+// |y1 - y0| >= 2^31 - 1; magr = |y1 - y0| / (x1 - x0).
+DEVI void lerp_long_prep(int64_t y0, int64_t y1, uint32_t d, uint32_t& im, double& magr) {
+  const int64_t dy = lsub(y1, y0);
+  const uint64_t mag = dy < 0 ? (uint64_t)0 - (uint64_t)dy : (uint64_t)dy;
+  im = UINT32_MAX;
+  magr = 0.0;
+  if (mag < 0x7fffffffull && d > 0) {
+    im = (uint32_t)mag | (dy < 0 ? 0x80000000u : 0u);
+    magr = (double)mag / (double)d;
+  }
+}
+// lerp_long for 0 < u = x - x0 < d = x1 - x0 and a prepared im != UINT32_MAX:
+// the product u * dy cannot wrap, and its truncated quotient by d is the
+// double estimate u * magr (error < 2^-20) made exact by one remainder check.
+DEVI int64_t lerp_long_prepped(uint32_t u, uint32_t d, int64_t y0, uint32_t im, double magr) {
+  const uint32_t mag = im & 0x7fffffffu;
+  uint32_t q = (uint32_t)((double)u * magr);
+  const int64_t rem = (int64_t)((uint64_t)u * mag) - (int64_t)((uint64_t)q * d);
+  q = rem < 0 ? q - 1u : (rem >= (int64_t)d ? q + 1u : q);
+  return ladd(y0, (im >> 31) ? -(int64_t)q : (int64_t)q);
+}
 
 // acc_push on active lanes only, without a branch: the push is computed on
 // a copy and selected (no exec-mask juggling on the scalar unit).
@@ -589,14 +612,8 @@ DEVI void reduce_wave(const ReduceArgs& r, const uint32_t wave) {
       // UINT32_MAX when it is 2^31 - 1 or more (general lerp); |y1 - y0| / d
       uint32_t im_l = UINT32_MAX;
       double magr_l = 0.0;
-      if (!RATE && MODE != MODE_DBL && el && (f_l & 4u) && x_l.y > x_l.x) {
-        const int64_t dy = lsub(y_l.y, y_l.x);
-        const uint64_t mag = dy < 0 ? (uint64_t)0 - (uint64_t)dy : (uint64_t)dy;
-        if (mag < 0x7fffffffull) {
-          im_l = (uint32_t)mag | (dy < 0 ? 0x80000000u : 0u);
-          magr_l = (double)mag / (double)(x_l.y - x_l.x);
-        }
-      }
+      if (!RATE && MODE != MODE_DBL && el && (f_l & 4u) && x_l.y > x_l.x)
+        lerp_long_prep(y_l.x, y_l.y, x_l.y - x_l.x, im_l, magr_l);
       const uint64_t dmask = ballot(dl);
       uint32_t dga_l = 0, dn_l = 0, dx0_l = 0, dstep_l = 0;
       uint64_t dvo_l = 0;
@@ -627,6 +644,11 @@ DEVI void reduce_wave(const ReduceArgs& r, const uint32_t wave) {
         y2_l = r.e_val[eo_l + j_l + 1];
         f2_l = r.e_flt[eo_l + j_l + 1];
       }
+      // (the long lerp of the bracket (j, j+1), prepared as im_l / magr_l)
+      uint32_t im2_l = UINT32_MAX;
+      double magr2_l = 0.0;
+      if (!RATE && MODE != MODE_DBL && sc && j_l + 1 < len_l && x2_l > x_l.y)
+        lerp_long_prep(y_l.y, y2_l, x2_l - x_l.y, im2_l, magr2_l);
       const uint64_t smask = ballot(sc && (int64_t)x2_l > t_last);
       const uint32_t nb = min((uint32_t)WAVE, k1 - kb);
       // A span with no point in this tile (its next point j lies past t_last):
@@ -653,15 +675,8 @@ DEVI void reduce_wave(const ReduceArgs& r, const uint32_t wave) {
           const int64_t y0 = (int64_t)readlane_u64((uint64_t)y_l.x, (int)i);
           const uint32_t im = readlane_u32(im_l, (int)i);
           if (im != UINT32_MAX) {
-            // |y1 - y0| < 2^31: the long product cannot wrap, and the quotient
-            // is the double estimate u * (|dy| / d) (error < 2^-20) made exact
-            // by one remainder check
             const double magr = __longlong_as_double((long long)readlane_u64((uint64_t)__double_as_longlong(magr_l), (int)i));
-            const uint32_t mag = im & 0x7fffffffu, d = x1 - x0;
-            uint32_t q = (uint32_t)((double)u * magr);
-            const int64_t rem = (int64_t)((uint64_t)u * mag) - (int64_t)((uint64_t)q * d);
-            q = rem < 0 ? q - 1u : (rem >= (int64_t)d ? q + 1u : q);
-            yi = ladd(y0, (im >> 31) ? -(int64_t)q : (int64_t)q);
+            yi = lerp_long_prepped(u, x1 - x0, y0, im, magr);
           } else {
             yi = lerp_long(tl, (int64_t)x0, y0, (int64_t)x1, (int64_t)readlane_u64((uint64_t)y_l.y, (int)i));
           }
@@ -749,7 +764,14 @@ DEVI void reduce_wave(const ReduceArgs& r, const uint32_t wave) {
                 if (MODE == MODE_DUAL && (fc || fn)) acc.flag |= 1u;
                 int64_t yi = 0;
                 double yd = 0.0;
-                if (need_long(fc, fn)) yi = lerp_long(tl, xc, yc, xn, yn);
+                if (need_long(fc, fn)) {
+                  const uint32_t im = readlane_u32(im_l, (int)i);
+                  if (im != UINT32_MAX)
+                    yi = lerp_long_prepped((uint32_t)(tl - xc), (uint32_t)(xn - xc), yc, im,
+                                           __longlong_as_double((long long)readlane_u64((uint64_t)__double_as_longlong(magr_l), (int)i)));
+                  else
+                    yi = lerp_long(tl, xc, yc, xn, yn);
+                }
                 if (MODE != MODE_INT)
                   yd = lerp_double(tl, xc, to_double(yc, MODE == MODE_DBL || fc), xn, to_double(yn, MODE == MODE_DBL || fn));
                 acc_push<AGG, MODE>(acc, yi, yd);
@@ -761,7 +783,14 @@ DEVI void reduce_wave(const ReduceArgs& r, const uint32_t wave) {
               if (MODE == MODE_DUAL && (fn || ff)) acc.flag |= 1u;
               int64_t yi = 0;
               double yd = 0.0;
-              if (need_long(fn, ff)) yi = lerp_long(tl, xn, yn, x2, y2);
+              if (need_long(fn, ff)) {
+                const uint32_t im = readlane_u32(im2_l, (int)i);
+                if (im != UINT32_MAX)
+                  yi = lerp_long_prepped((uint32_t)(tl - xn), (uint32_t)(x2 - xn), yn, im,
+                                         __longlong_as_double((long long)readlane_u64((uint64_t)__double_as_longlong(magr2_l), (int)i)));
+                else
+                  yi = lerp_long(tl, xn, yn, x2, y2);
+              }
               if (MODE != MODE_INT)
                 yd = lerp_double(tl, xn, to_double(yn, MODE == MODE_DBL || fn), x2, to_double(y2, MODE == MODE_DBL || ff));
               acc_push<AGG, MODE>(acc, yi, yd);
