@@ -148,9 +148,68 @@ def dist_setup(n_gpus):
     return dist, dist.get_rank(), dist.get_world_size(), int(os.environ.get("LOCAL_RANK", "0"))
 
 
+def host_threads():
+    """P = every core this process may run on (independent
+    SpanGroups on nproc threads, TsdbQuery.java:322-362)."""
+    try:
+        return max(1, len(os.sched_getaffinity(0)))
+    except AttributeError:
+        return max(1, os.cpu_count() or 1)
+
+
+def cpu_model():
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    import platform
+    return platform.processor() or "unknown"
+
+
+def cpu_quota():
+    """CPUs the cgroup grants this process (cpu.max), or None when unlimited:
+    the GPU box shows the whole machine's cores but may grant a share."""
+    try:
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        return None if q == "max" else max(1.0, int(q) / int(per))
+    except (OSError, ValueError):
+        return None
+
+
+def run_pool(fn, probe, seconds):
+    """Runs fn() (one independent unit: a SpanGroup or a row batch) on
+    host_threads() threads pulling from one work counter, sized so the run
+    takes ~`seconds` wall time at the parallelism the machine grants.
+    Returns (units done, wall seconds, threads, granted CPUs)."""
+    threads = host_threads()
+    quota = cpu_quota()
+    eff = min(threads, quota) if quota else threads
+    total = max(threads, int(seconds * eff / max(probe, 1e-4)))
+    left = [total]
+    lock = threading.Lock()
+
+    def work():
+        while True:
+            with lock:
+                if left[0] <= 0:
+                    return
+                left[0] -= 1
+            fn()
+
+    ths = [threading.Thread(target=work) for _ in range(threads)]
+    t = time.perf_counter()
+    for th in ths:
+        th.start()
+    for th in ths:
+        th.join()
+    return total, time.perf_counter() - t, threads, quota
+
+
 def cpu_baseline(cfg_name, seconds=10.0):
     """The oracle (C++ restatement of the reference's Java iterators) on the
-    host cores, independent SpanGroups per thread (group-by style,
+    host cores: independent SpanGroups on P = nproc threads (group-by style,
     TsdbQuery.java:322-362); a bounded sample of the same workload shape."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle
@@ -160,41 +219,24 @@ def cpu_baseline(cfg_name, seconds=10.0):
         sample_series = max(1, min(cfg["n_series"], 200_000 // max(1, n_points // 100)))
         ss = synth.regular(sample_series, n_points, cfg["kind"], seed=1, step=cfg["step"])
         what = f"{sample_series} series x {n_points} pts of the same workload"
+        cap = n_points if not cfg["dsi"] else n_points * cfg["step"] // cfg["dsi"] + 2
     else:
         sample_series = 20
         ss = host_spanset(dict(cfg, n_series=sample_series), 0, sample_series, seed=11)
         what = f"{sample_series} series of the same generator (~{cfg['n_points']} pts each)"
+        cap = ss.n_cells() + 16
     args = (0, (1 << 32) - 1, cfg["agg"], cfg["rate"], cfg["dsi"], cfg["dsa"])
     oracle.lib()
-    # probe one run, then size the sample to ~`seconds` of CPU work
+    # probe one run, then size the sample to ~`seconds` of wall time
     t = time.perf_counter()
-    r = oracle.spangroup(ss, *args, capacity=ss.n_cells())
+    r = oracle.spangroup(ss, *args, capacity=cap)
     probe = time.perf_counter() - t
-    threads = max(1, min(16, os.cpu_count() or 1))
-    reps_per_thread = max(1, int(seconds / max(probe, 1e-3)))
-    total = [0]
-    lock = threading.Lock()
-
-    def work():
-        n = 0
-        for _ in range(reps_per_thread):
-            rr = oracle.spangroup(ss, *args, capacity=ss.n_cells())
-            n += rr.n_input_points
-        with lock:
-            total[0] += n
-
-    ths = [threading.Thread(target=work) for _ in range(threads)]
-    t = time.perf_counter()
-    for th in ths:
-        th.start()
-    for th in ths:
-        th.join()
-    wall = time.perf_counter() - t
-    one_core = r.n_input_points / probe
+    n, wall, threads, quota = run_pool(lambda: oracle.spangroup(ss, *args, capacity=cap), probe, seconds)
     return {
-        "value": total[0] / wall, "unit": "input points/s", "cores": threads, "kind": "port",
-        "value_1core": one_core,
-        "sample": f"{what}, {threads} threads x {reps_per_thread} SpanGroups, {wall:.1f} s wall "
+        "value": n * r.n_input_points / wall, "unit": "input points/s", "cores": threads, "kind": "port",
+        "cpu_model": cpu_model(), "cgroup_cpus": quota,
+        "value_1core": r.n_input_points / probe,
+        "sample": f"{what}, {n} SpanGroups on {threads} threads, {wall:.1f} s wall "
                   f"(oracle/oracle.cc: C++ restatement of SpanGroup/Span/RowSeq/Aggregators; "
                   f"no JVM in the image)",
     }
@@ -202,7 +244,8 @@ def cpu_baseline(cfg_name, seconds=10.0):
 
 def cpu_baseline_c5(batch, seconds=10.0):
     """oracle_compact_rows (C++ restatement of CompactionQueue.compact) on
-    the host cores: independent row batches per thread, a bounded sample."""
+    the host cores: independent row batches on P = nproc threads, a bounded
+    sample."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle
     from opentsdb_amd import compaction
@@ -215,29 +258,13 @@ def cpu_baseline_c5(batch, seconds=10.0):
     t = time.perf_counter()
     oracle.compact_rows(sub)
     probe = time.perf_counter() - t
-    threads = max(1, min(16, os.cpu_count() or 1))
-    reps = max(1, int(seconds / max(probe, 1e-3)))
-    done = [0]
-    lock = threading.Lock()
-
-    def work():
-        for _ in range(reps):
-            oracle.compact_rows(sub)
-        with lock:
-            done[0] += reps
-
-    ths = [threading.Thread(target=work) for _ in range(threads)]
-    t = time.perf_counter()
-    for th in ths:
-        th.start()
-    for th in ths:
-        th.join()
-    wall = time.perf_counter() - t
-    return {"value": done[0] * cells / wall, "unit": "raw cells/s", "cores": threads, "kind": "port",
+    n, wall, threads, quota = run_pool(lambda: oracle.compact_rows(sub), probe, seconds)
+    return {"value": n * cells / wall, "unit": "raw cells/s", "cores": threads, "kind": "port",
+            "cpu_model": cpu_model(), "cgroup_cpus": quota,
             "value_1core": cells / probe,
-            "sample": f"first {rows} rows ({cells} cells) of the same batch, {threads} threads x {reps} "
-                      f"batches, {wall:.1f} s wall (oracle/oracle.cc: C++ restatement of "
-                      f"CompactionQueue.compact; no JVM in the image)"}
+            "sample": f"first {rows} rows ({cells} cells) of the same batch, {n} batches on {threads} threads, "
+                      f"{wall:.1f} s wall (oracle/oracle.cc: C++ restatement of CompactionQueue.compact; "
+                      f"no JVM in the image)"}
 
 
 _JSON_OUT = None
@@ -575,6 +602,7 @@ def main():
     d.agg, d.rate, d.ds_interval, d.ds_agg = agg, int(rate), dsi, dsa
     if (world > 1 or rehearse) and G == 1:
         d.flags |= _abi.SHARDED
+        d.span0 = lo
     if args.exact:
         d.flags |= _abi.EXACT_ORDER
     if cfg["gen"] == "device":

@@ -49,7 +49,7 @@
 extern "C" {
 #endif
 
-#define TSDBHIP_ABI_VERSION 3
+#define TSDBHIP_ABI_VERSION 4
 
 /* ---- return codes ---------------------------------------------------- */
 #define TSDBHIP_OK               0
@@ -66,9 +66,9 @@ extern "C" {
 #define TSDBHIP_E_OUT_OF_BOUNDS -9  /* reference would throw
                                        ArrayIndexOutOfBoundsException */
 #define TSDBHIP_E_NO_DEVICE    -10
-#define TSDBHIP_E_UNSUPPORTED  -11 /* reserved (ABI v3 raised it for a Q1
+#define TSDBHIP_E_UNSUPPORTED  -11 /* reserved (ABI v2 raised it for a Q1
                                        seek whose shifted reads cross merged
-                                       rows; those are now reproduced)       */
+                                       rows; v3 reproduces those reads)      */
 
 /* ---- aggregator op codes (Aggregators.java:44-48 names) --------------- */
 #define TSDBHIP_AGG_SUM 0
@@ -125,6 +125,10 @@ typedef struct tsdbhip_sg_desc {
   uint64_t        qual_nbytes;
   const uint8_t*  val_bytes;
   uint64_t        val_nbytes;
+  uint64_t        span0;    /* TSDBHIP_SHARDED: global index (TreeMap order)
+                               of this shard's first span; the ranks agree on
+                               the error the reference throws first by global
+                               span order (ABI v4). 0 otherwise.           */
 } tsdbhip_sg_desc;
 
 /* Result of one SpanGroup, in emission order (SGIterator order). */

@@ -6,7 +6,7 @@ and the test harness.
 """
 import ctypes as C
 
-ABI_VERSION = 3
+ABI_VERSION = 4
 
 OK = 0
 E_ILLEGAL_DATA = -1
@@ -69,6 +69,7 @@ class SgDesc(C.Structure):
         ("qual_nbytes", C.c_uint64),
         ("val_bytes", P8),
         ("val_nbytes", C.c_uint64),
+        ("span0", C.c_uint64),
     ]
 
 

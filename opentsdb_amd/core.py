@@ -128,9 +128,10 @@ class Span:
 
 
 def run_spanset(ctx, spanset: SpanSet, start, end, agg, rate=False, ds_interval=0, ds_agg=0,
-                exact=False, capacity=None, device_desc=None, sharded=False):
+                exact=False, capacity=None, device_desc=None, sharded=False, span0=0):
     """Low-level: one tsdbhip_spangroup_run. Returns (code, ts, is_int, bits,
-    n_input_points, err_index)."""
+    n_input_points, err_index). sharded: this rank's shard of a group whose
+    first span has global index span0."""
     desc = _abi.SgDesc()
     if device_desc is not None:
         C.pointer(desc)[0] = device_desc
@@ -144,6 +145,7 @@ def run_spanset(ctx, spanset: SpanSet, start, end, agg, rate=False, ds_interval=
         desc.flags |= _abi.EXACT_ORDER
     if sharded:  # this rank's shard; exchange over the ctx communicator
         desc.flags |= _abi.SHARDED
+        desc.span0 = int(span0)
     cap = capacity
     if cap is None:
         cap = max(1, spanset.n_cells()) if spanset is not None else 1 << 20

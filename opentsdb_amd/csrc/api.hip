@@ -251,8 +251,12 @@ struct Lease {
     }
     s->x = nullptr;
     s->want_output = true;
-    Slot* ctx = s;
-    HIPCHK(hipSetDevice(c->device));
+    if (hipSetDevice(c->device) != hipSuccess) {  // (the destructor will not run: hand the slot back here)
+      set_error(c, "hipSetDevice(%d) failed", c->device);
+      std::lock_guard<std::mutex> lk(c->mu);
+      c->free_slots.push_back(s);
+      throw Fail{TSDBHIP_E_HIP};
+    }
   }
   ~Lease() {
     s->x = nullptr;
@@ -1041,6 +1045,7 @@ static int spangroup_run(Slot* ctx, const tsdbhip_sg_desc* d, tsdbhip_sg_out* ou
     a.row_ok = row_ok; a.row_cell0 = row_cell0; a.sp_ncells = sp_ncells; a.sp_first = sp_first;
     a.sp_last = sp_last; a.sp_kept = sp_kept; a.sp_cap = sp_cap; a.sp_q1 = sp_q1;
     a.sp_q1_shift = sp_q1s; a.sp_q1_rs = sp_q1rs; a.sp_ovf_cell = sp_ovf; a.err = &sm->err;
+    a.span0 = sharded ? d->span0 : 0;
     // kept list, E offsets, counts and bounds (unsharded groups of up to
     // KC_MAX spans: the kernel hands the call state to the host itself)
     kept = scratch<uint32_t>(ctx, "kept", S);
@@ -1077,8 +1082,9 @@ static int spangroup_run(Slot* ctx, const tsdbhip_sg_desc* d, tsdbhip_sg_out* ou
   if (sharded) {
     // every rank needs the same bitmap geometry and the same error: the kept
     // spans' bounds (min first, max last; ranks without kept spans hold the
-    // neutral ~0 / 0) and the error code (most negative) are reduced in place,
-    // so the one readback below returns the agreed values
+    // neutral ~0 / 0) and the error key (MIN of the stage | global order |
+    // code keys, err_raise) are reduced in place, so the one readback below
+    // returns the agreed values
     const XField fa[3] = {{&sm->bound[0], 0}, {&sm->bound[1], 1}, {&sm->err, 0}};
     xchg_minmax(ctx, X, fa, 3);
   }
@@ -1129,7 +1135,7 @@ static int spangroup_run(Slot* ctx, const tsdbhip_sg_desc* d, tsdbhip_sg_out* ou
   da.sp_ovf_cell = sp_ovf; da.sp_cap = sp_cap; da.e_off = eoff; da.e_ts = e_ts; da.e_val = e_val;
   da.e_flt = e_flt; da.e_len = e_len; da.e_bad = e_bad; da.start = d->start_time; da.end = d->end_time;
   da.interval = interval; da.ds_agg = ds_agg; da.rate = rate; da.err = &sm->err; da.gflags = sm->gflags;
-  da.range = sm->range; da.fstar = &sm->fstar;
+  da.range = sm->range; da.fstar = &sm->fstar; da.span0 = sharded ? d->span0 : 0;
   if (detail) HIPCHK(hipEventRecord(ctx->ev[1], st));
   bool chunk_marked = false;     // k_ds_spans marked G for the spans it took
   bool direct = false;           // k_direct_scan took the no-downsampling path
@@ -1203,7 +1209,7 @@ static int spangroup_run(Slot* ctx, const tsdbhip_sg_desc* d, tsdbhip_sg_out* ou
       DecodeArgs fa = da;
       if (chunks && ds_agg != 4) {
         SpanDsArgs g = {};
-        g.bitmap = getenv("TSDBHIP_EXP_NOMARK") ? nullptr : bitmap;
+        g.bitmap = bitmap;
         g.lo = lo;
         g.hi = hi;
         g.rate = rate;
@@ -1631,6 +1637,7 @@ static void plan_shards(tsdbhip_ctx* mc, const tsdbhip_sg_desc* desc, std::vecto
     const uint32_t s0 = b[r], s1 = b[r + 1];
     const uint64_t r0 = srs[s0], r1 = srs[s1];
     x.d = *desc;
+    x.d.span0 = desc->span0 + s0;  // (global span order of the shard's errors)
     x.d.n_spans = s1 - s0;
     x.d.n_rows = r1 - r0;
     x.srs.resize((size_t)(s1 - s0) + 1);

@@ -161,6 +161,7 @@ static int spangroup_run_batch(Slot* ctx, const tsdbhip_sg_desc* d, uint32_t G, 
     a.row_ok = row_ok; a.row_cell0 = row_cell0; a.sp_ncells = sp_ncells; a.sp_first = sp_first;
     a.sp_last = sp_last; a.sp_kept = sp_kept; a.sp_cap = sp_cap; a.sp_q1 = sp_q1;
     a.sp_q1_shift = sp_q1s; a.sp_q1_rs = sp_q1rs; a.sp_ovf_cell = sp_ovf; a.err = &sm->err;
+    a.span0 = 0;
     uint32_t* alist = scratch<uint32_t>(ctx, "asm_list", S);
     uint32_t* acount = scratch<uint32_t>(ctx, "asm_count", 1, true);
     hipLaunchKernelGGL(k_assemble_fast, dim3(grid_for(S, 256)), dim3(256), 0, st, a, alist, acount);
@@ -238,7 +239,7 @@ static int spangroup_run_batch(Slot* ctx, const tsdbhip_sg_desc* d, uint32_t G, 
   da.sp_q1_shift = sp_q1s; da.sp_q1_rs = sp_q1rs; da.sp_ovf_cell = sp_ovf; da.sp_cap = sp_cap; da.e_off = eoff; da.e_ts = e_ts;
   da.e_val = e_val; da.e_flt = e_flt; da.e_len = e_len; da.e_bad = e_bad; da.start = d->start_time;
   da.end = d->end_time; da.interval = interval; da.ds_agg = ds_agg; da.rate = rate; da.err = &sm->err;
-  da.gflags = sm->gflags; da.range = sm->range; da.fstar = &sm->fstar;
+  da.gflags = sm->gflags; da.range = sm->range; da.fstar = &sm->fstar; da.span0 = 0;
   da.row_ncells = dd.row_ncells; da.row_val_len = dd.row_val_len;
   HIPCHK(hipEventRecord(ctx->ev[1], st));
   bool direct = false;  // k_direct_scan took the no-downsampling path

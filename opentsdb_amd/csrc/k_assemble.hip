@@ -39,6 +39,8 @@ struct AssembleArgs {
   int64_t* sp_ovf_cell;   // [n_spans] span cell index that overflows the
                           // RowSeq.Iterator `short` value_index, -1 none
   unsigned long long* err;  // [1] first error (err_raise key)
+  uint64_t span0;           // global index of span 0 (a shard's offset): the
+                            // error order across ranks is the global span order
 };
 
 DEVI int64_t row_first_ts(const AssembleArgs& a, uint64_t r) {
@@ -65,7 +67,7 @@ __device__ void assemble_slow(const AssembleArgs& a, uint32_t s, uint64_t r0, ui
   for (uint64_t r = r0; r < r1; r++) a.row_ok[r] = 0;
   for (uint64_t r = r0; r < r1; r++) {
     const uint32_t n = a.row_ncells[r];
-    if (n == 0) { err_raise(a.err, 0, err_scan_order(a.row_base[r], s), -9 /*E_OUT_OF_BOUNDS*/); return; }
+    if (n == 0) { err_raise(a.err, 0, err_scan_order(a.row_base[r], a.span0 + s), -9 /*E_OUT_OF_BOUNDS*/); return; }
     const int64_t base = a.row_base[r];
     const int64_t first = row_first_ts(a, r), last = row_last_ts(a, r);
     if (rs_base < 0) {
@@ -75,7 +77,7 @@ __device__ void assemble_slow(const AssembleArgs& a, uint32_t s, uint64_t r0, ui
     if (last - rs_base < 4096) {  // merge into the last RowSeq (Span.java:117-121)
       const int64_t time_adj = base - rs_base;
       if (time_adj <= 0) {
-        if (time_adj != 0) { err_raise(a.err, 0, err_scan_order((uint32_t)base, s), -1 /*E_ILLEGAL_DATA*/); return; }
+        if (time_adj != 0) { err_raise(a.err, 0, err_scan_order((uint32_t)base, a.span0 + s), -1 /*E_ILLEGAL_DATA*/); return; }
         // same row again (scanner restart): RowSeq restarts from this row
         for (uint64_t q = rs_start; q < r; q++) a.row_ok[q] = 0;
         a.row_ok[r] = 2; rs_start = r; rs_vbytes = row_value_bytes(a, r); last_ts = last;
@@ -174,7 +176,7 @@ DEVI void assemble_finish(const AssembleArgs& a, uint32_t s, bool has_rows) {
   const int64_t f = a.sp_first[s], l = a.sp_last[s];
   // Span.timestamp(0) of an empty span throws (SpanGroup.java:135-139)
   (void)has_rows;
-  if (n == 0) err_raise(a.err, 1, s, -3 /*E_EMPTY_SPAN*/);
+  if (n == 0) err_raise(a.err, 1, a.span0 + s, -3 /*E_EMPTY_SPAN*/);
   const bool kept = n > 0 && f <= a.end && l >= a.start;  // SpanGroup.java:135-139
   a.sp_kept[s] = kept;
   uint64_t cap = 0;

@@ -54,6 +54,7 @@ struct DecodeArgs {
   int32_t ds_agg;
   int32_t rate;
   unsigned long long* err;  // [1] first error (err_raise key)
+  uint64_t span0;           // global index of span 0 (error order across shards)
   unsigned int* gflags;       // [0] any float E point, [1] any int E point
   unsigned long long* range;  // [0] min grid-candidate ts, [1] max E ts
   unsigned long long* fstar;  // max first-E ts over spans whose first E point is float
@@ -211,7 +212,7 @@ __device__ void span_nods_general(const DecodeArgs& a, uint32_t k) {
     if (lane == 0) {
       a.e_len[k] = len;
       a.e_bad[k] = bad;
-      if (unsorted) err_raise(a.err, 2, k, -8 /*E_UNSORTED*/);
+      if (unsorted) err_raise(a.err, 2, a.span0 + s, -8 /*E_UNSORTED*/);
       if (anyf) atomicOr(&a.gflags[0], 1u);
       if (anyi) atomicOr(&a.gflags[1], 1u);
     }
@@ -433,9 +434,9 @@ __device__ void span_ds_general(const DecodeArgs& a, uint32_t k, int64_t* s_bits
     }
     if (lane == 0) {
       a.e_len[k] = (uint32_t)(ecount < cap ? ecount : cap);
-      if (ecount > cap) err_raise(a.err, 2, k, -4 /*E_CAPACITY*/);
+      if (ecount > cap) err_raise(a.err, 2, a.span0 + s, -4 /*E_CAPACITY*/);
       a.e_bad[k] = bad;
-      if (unsorted) err_raise(a.err, 2, k, -8 /*E_UNSORTED*/);
+      if (unsorted) err_raise(a.err, 2, a.span0 + s, -8 /*E_UNSORTED*/);
       if (anyf) atomicOr(&a.gflags[0], 1u);
       if (anyi) atomicOr(&a.gflags[1], 1u);
     }

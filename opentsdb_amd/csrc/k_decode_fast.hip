@@ -448,9 +448,9 @@ __global__ void __launch_bounds__(256, 3) k_decode_fast(DecodeArgs a, const uint
       if (!general) {
         if (lane == 0) {
           a.e_len[k] = (uint32_t)(ecount < cap ? ecount : cap);
-          if (ecount > cap) err_raise(a.err, 2, k, -4 /*E_CAPACITY*/);
+          if (ecount > cap) err_raise(a.err, 2, a.span0 + s, -4 /*E_CAPACITY*/);
           a.e_bad[k] = -1;
-          if (unsorted) err_raise(a.err, 2, k, -8 /*E_UNSORTED*/);
+          if (unsorted) err_raise(a.err, 2, a.span0 + s, -8 /*E_UNSORTED*/);
           if (anyf) atomicOr(&a.gflags[0], 1u);
           if (anyi) atomicOr(&a.gflags[1], 1u);
         }

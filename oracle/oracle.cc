@@ -1114,6 +1114,10 @@ struct ShardRes {
   uint64_t n_input = 0;
   std::vector<int64_t> ts, bits;
   std::vector<uint8_t> isint;
+  // dev on the double path: the shard's Welford state per t (count, mean,
+  // M2), the loop of Aggregators.java:219-238 run over the shard's values
+  std::vector<int64_t> wn;
+  std::vector<double> wmean, wm2;
 };
 
 static void run_regular_shard(uint64_t seed, uint32_t s0, uint32_t s1, uint32_t n_points, uint32_t t0, uint32_t step,
@@ -1143,6 +1147,21 @@ static void run_regular_shard(uint64_t seed, uint32_t s0, uint32_t s1, uint32_t 
       const bool isint = it.isInteger();
       res.isint.push_back(isint ? 1 : 0);
       res.bits.push_back(isint ? it.longValue() : dbits(it.doubleValue()));
+      if (agg == TSDBHIP_AGG_DEV && !isint) {  // the state behind doubleValue()'s sqrt
+        it.pos = -1;
+        double mean = it.nextDoubleValue(), m2 = 0;
+        int64_t n = 1;
+        while (it.hasNextValue()) {
+          const double x = it.nextDoubleValue();
+          n++;
+          const double nm = mean + (x - mean) / (double)n;
+          m2 += (x - mean) * (x - nm);
+          mean = nm;
+        }
+        res.wn.push_back(n);
+        res.wmean.push_back(mean);
+        res.wm2.push_back(m2);
+      }
     }
   } catch (JavaException& e) {
     res.code = e.code;
@@ -1156,7 +1175,11 @@ int oracle_regular_sharded(uint64_t seed, uint32_t n_spans, uint32_t n_points, u
   out->n_input_points = 0;
   out->err_code = 0;
   out->err_index = -1;
-  if (agg != TSDBHIP_AGG_SUM && agg != TSDBHIP_AGG_MIN && agg != TSDBHIP_AGG_MAX) return TSDBHIP_E_INVALID_ARG;
+  // (dev: double path only, i.e. rate or float series; the long dev truncates
+  // a sequential Welford and admits no merge)
+  const bool dev = agg == TSDBHIP_AGG_DEV;
+  if (agg != TSDBHIP_AGG_SUM && agg != TSDBHIP_AGG_MIN && agg != TSDBHIP_AGG_MAX && !dev) return TSDBHIP_E_INVALID_ARG;
+  if (dev && !rate && kind == TSDBHIP_SYN_INT64_COUNTER) return TSDBHIP_E_INVALID_ARG;
   if (!n_spans || !n_points || !step || 3600 % step || t0 % 3600 || kind > 2 || !shard_spans) return TSDBHIP_E_INVALID_ARG;
   const uint32_t n_shards = (n_spans + shard_spans - 1) / shard_spans;
   std::vector<ShardRes> res(n_shards);
@@ -1180,11 +1203,28 @@ int oracle_regular_sharded(uint64_t seed, uint32_t n_spans, uint32_t n_points, u
     out->bits[t] = a0.bits[t];
   }
   uint64_t n_input = 0;
+  std::vector<int64_t> wn;
+  std::vector<double> wmean, wm2;
+  if (dev) {
+    if (a0.wn.size() != T) return out->err_code = TSDBHIP_E_INVALID_ARG;
+    wn = a0.wn; wmean = a0.wmean; wm2 = a0.wm2;
+  }
   for (uint32_t sh = 0; sh < n_shards; sh++) {
     const ShardRes& r = res[sh];
     n_input += r.n_input;
     if (sh == 0) continue;
     if (r.ts != a0.ts || r.isint != a0.isint) return out->err_code = TSDBHIP_E_INVALID_ARG;  // not aligned
+    if (dev) {  // pairwise Welford merge in shard order (Chan et al.)
+      for (size_t t = 0; t < T; t++) {
+        const double na = (double)wn[t], nb = (double)r.wn[t], n = na + nb;
+        const double delta = r.wmean[t] - wmean[t];
+        wmean[t] += delta * (nb / n);
+        wm2[t] += r.wm2[t] + delta * delta * (na * nb / n);
+        wn[t] += r.wn[t];
+        out->bits[t] = dbits(std::sqrt(wm2[t] / (double)wn[t]));
+      }
+      continue;
+    }
     for (size_t t = 0; t < T; t++) {
       if (a0.isint[t]) {
         const int64_t x = r.bits[t], y = out->bits[t];

@@ -86,7 +86,8 @@ def regular_sharded(n_spans, n_points, kind, seed, step, start, end, agg, rate=F
     """The synthetic regular SpanGroup of synth.regular / tsdbhip_synth_generate
     at full size, generated and iterated shard by shard on host threads and
     combined in shard order (oracle.cc: oracle_regular_sharded; sum / min /
-    max on aligned grids only)."""
+    max on aligned grids only, and dev on the double path as a pairwise merge
+    of the shards' Welford states)."""
     from opentsdb_amd import synth
     t0 = synth.T0 if t0 is None else t0
     cap = int(capacity or max(1, n_points if not ds_interval else n_points * step // ds_interval + 2))

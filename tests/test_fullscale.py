@@ -6,11 +6,23 @@ bench.py's own workloads were never validated).
   shard by shard on the host cores and combined in shard order
   (oracle.regular_sharded: sum / max over an aligned grid, where the per-shard
   outputs combine exactly; ints bit-exact, rate doubles at 1e-9 relative).
+  Rate dev (Aggregators.java:219-238) combines the shards' Welford states
+  pairwise in shard order (1e-9 relative).
+* C2 (10k float32 series x 8640 points @10 s, avg + 1m-avg downsample, the
+  device generator's bytes) against the whole-group oracle on the host
+  generator's identical bytes (Span.java:377-422, Aggregators.java:150-175):
+  1e-9 relative, and bit-exact under TSDBHIP_EXACT_ORDER.
 * C4 / C4-int (synth.jittered_packed, the bench's generator) at a size whose
-  union grid holds > 1M points over the 40M-s range, whole-group oracle.
+  union grid holds > 1M points over the 40M-s range, whole-group oracle; and
+  at the bench's own size (1000 series, a ~10.5M-point union) against the
+  digests of the whole-group oracle in tests/golden/fullsize_digests.json
+  (tests/golden/make_fullsize_digests.py: ~3 min of oracle per case).
 The CPU tests pin the sharded oracle against the plain oracle on
 synth.regular at small sizes."""
 import ctypes as C
+import hashlib
+import json
+import os
 
 import numpy as np
 import pytest
@@ -30,6 +42,8 @@ I64, F32 = _abi.SYN_INT64_COUNTER, _abi.SYN_FLOAT32
     (I64, 1, _abi.AGG_MAX, True, 0, 0),
     (F32, 10, _abi.AGG_SUM, False, 60, _abi.AGG_AVG),
     (I64, 10, _abi.AGG_MIN, False, 60, _abi.AGG_SUM),
+    (I64, 1, _abi.AGG_DEV, True, 0, 0),
+    (F32, 10, _abi.AGG_DEV, False, 60, _abi.AGG_AVG),
 ])
 def test_sharded_oracle_matches_whole_group(kind, step, agg, rate, dsi, dsa):
     """oracle_regular_sharded (C generator + shard combine) == the oracle on
@@ -45,6 +59,24 @@ def test_sharded_oracle_matches_whole_group(kind, step, agg, rate, dsi, dsa):
 
 def test_sharded_oracle_rejects_unaligned():
     assert oracle.regular_sharded(4, 100, I64, 1, 1, 0, U32MAX, _abi.AGG_AVG).code == _abi.E_INVALID_ARG
+    # the long dev (no rate, int series) truncates a sequential Welford: no merge
+    assert oracle.regular_sharded(4, 100, I64, 1, 1, 0, U32MAX, _abi.AGG_DEV).code == _abi.E_INVALID_ARG
+
+
+DIGESTS = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "fullsize_digests.json")
+
+
+def sha(a, dt):
+    return hashlib.sha256(np.ascontiguousarray(a.astype(dt)).tobytes()).hexdigest()
+
+
+def test_fullsize_digests_fixture():
+    """The committed oracle digests describe bench.py's C4 workloads."""
+    d = json.load(open(DIGESTS))
+    for name in ("c4_sum", "c4i_sum", "c4_avg"):
+        e = d[name]
+        assert e["code"] == 0 and e["n_series"] == 1000 and e["n_points"] == 11500 and e["seed"] == 4
+        assert e["n_out"] > 10_000_000 and e["n_input"] > 11_000_000
 
 
 # ------------------------------------------------------------------- GPU ----
@@ -58,9 +90,10 @@ def c3_desc(ctx):
     ctx._lib.tsdbhip_synth_free(ctx.handle, C.byref(d))
 
 
-def run_device(ctx, d, agg, rate=False, dsi=0, dsa=0, cap=3600):
+def run_device(ctx, d, agg, rate=False, dsi=0, dsa=0, cap=3600, exact=False):
     d.start_time, d.end_time = 0, U32MAX
     d.agg, d.rate, d.ds_interval, d.ds_agg = agg, int(rate), dsi, dsa
+    d.flags = _abi.DESC_DEVICE | (_abi.EXACT_ORDER if exact else 0)
     ts, isi, bits = np.zeros(cap, np.int64), np.zeros(cap, np.uint8), np.zeros(cap, np.int64)
     out = _abi.SgOut(capacity=cap, ts=_abi.ptr(ts, C.c_int64), is_int=_abi.ptr(isi, C.c_uint8),
                      bits=_abi.ptr(bits, C.c_int64))
@@ -76,6 +109,7 @@ def run_device(ctx, d, agg, rate=False, dsi=0, dsa=0, cap=3600):
     ("C3 sum", _abi.AGG_SUM, False, 0, 0),
     ("C3 rate sum", _abi.AGG_SUM, True, 0, 0),
     ("C3 rate max", _abi.AGG_MAX, True, 0, 0),
+    ("C3 rate dev", _abi.AGG_DEV, True, 0, 0),
 ])
 def test_c3_full_size(ctx, c3_desc, name, agg, rate, dsi, dsa):
     g = run_device(ctx, c3_desc, agg, rate, dsi, dsa)
@@ -99,3 +133,48 @@ def test_c4_million_point_union(ctx, gen, agg):
     o = oracle.spangroup(ss, 0, U32MAX, agg, capacity=ss.n_cells() + 16)
     assert o.code == 0 and len(o.ts) > 1_000_000
     assert_same(g, o)
+
+
+@pytest.mark.gpu
+@pytest.mark.timeout(600)
+def test_c2_full_size(ctx):
+    """configs[1] at its size: 10k float32 series x 1 day @10 s, avg with
+    1m-avg downsampling (the device generator's bytes, bench.py --config c2),
+    whole-group oracle on synth.regular's identical bytes."""
+    d = _abi.SgDesc()
+    p = _abi.SynthParams(seed=3, n_spans=10_000, n_points=8640, t0=synth.T0, step=10, kind=F32, span0=0)
+    ctx.check(ctx._lib.tsdbhip_synth_generate(ctx.handle, C.byref(p), C.byref(d)))
+    try:
+        g = run_device(ctx, d, _abi.AGG_AVG, False, 60, _abi.AGG_AVG, cap=2000)
+        gx = run_device(ctx, d, _abi.AGG_AVG, False, 60, _abi.AGG_AVG, cap=2000, exact=True)
+    finally:
+        ctx._lib.tsdbhip_synth_free(ctx.handle, C.byref(d))
+    ss = synth.regular(10_000, 8640, F32, seed=3, step=10)
+    o = oracle.spangroup(ss, 0, U32MAX, _abi.AGG_AVG, False, 60, _abi.AGG_AVG, capacity=2000)
+    del ss
+    assert o.code == 0 and o.n_input_points == 86_400_000 and len(o.ts) == 1440
+    assert not o.is_int.any()
+    assert_same(g, o, rtol=1e-9)
+    assert_same(gx, o, exact_double=True)
+
+
+@pytest.mark.gpu
+@pytest.mark.timeout(600)
+@pytest.mark.parametrize("name", ["c4_sum", "c4i_sum", "c4_avg"])
+def test_c4_full_size(ctx, name):
+    """bench.py's C4 / C4-int line at its own size (1000 jittered series,
+    ~11.7M cells, a ~10.5M-point union grid; SpanGroup.java:702-784 lerps)
+    against the whole-group oracle's digests: timestamps, isInteger and the
+    long values bit-exactly; doubles bit-exactly under TSDBHIP_EXACT_ORDER and
+    within 1e-9 of that run in the default (chunk-parallel) order."""
+    e = json.load(open(DIGESTS))[name]
+    ff, fc = (0.5, 0.01) if e["gen"] == "jitter" else (0.0, 0.0)
+    ss = synth.jittered_packed(e["n_series"], e["n_points"], seed=e["seed"], float_frac=ff, float_cell_frac=fc)
+    gx = core.run_spanset(ctx, ss, 0, U32MAX, e["agg"], exact=True)
+    g = core.run_spanset(ctx, ss, 0, U32MAX, e["agg"])
+    rc, ts, isi, bits, n_in, _ = gx
+    assert rc == e["code"] and n_in == e["n_input"] and len(ts) == e["n_out"]
+    assert sha(ts, "<i8") == e["ts"], "timestamps differ from the oracle"
+    assert sha(isi, "u1") == e["is_int"], "isInteger differs from the oracle"
+    assert sha(bits, "<i8") == e["bits"], "value bits (EXACT_ORDER) differ from the oracle"
+    assert_same(g, oracle.Result(0, ts, isi, bits, n_in, -1), rtol=1e-9)

@@ -140,6 +140,27 @@ def test_empty_span_and_nan_in_a_later_rank(mctx):
 
 
 @pytest.mark.gpu
+def test_error_order_is_global_span_order(mctx, ctx):
+    """Two Span.addRow errors at the same base time in different ranks: the
+    one in the lower global span wins (the scan's row-key order: base time,
+    then span), whatever its index inside its own shard. Span 1
+    (rank 0, local index 1) holds a row that goes back in time (-1, the
+    IllegalDataException of Span.java:117-121), span 2 (rank 1, local index 0)
+    an empty row at the same base (-9). Rows out of base order are outside the
+    header's contract, so the expectation is the unsharded call's code."""
+    T = T0
+    n = 2 * mctx.ranks  # 10 cells per span: rank r holds spans 2r and 2r + 1
+    spans = [I([(T + 3600 + i, i) for i in range(10)]) for _ in range(n)]
+    spans[1] = I([(T + 3600 + i, i) for i in range(5)]) + I([(T + 100 + i, i) for i in range(5)])
+    spans[2] = [packing.KeyValue(T, b"", b"")] + I([(T + 3600 + i, i) for i in range(10)])
+    ss = packing.pack_spans(spans)
+    whole = core.run_spanset(ctx, ss, 0, U32MAX, 0)
+    assert whole[0] == _abi.E_ILLEGAL_DATA
+    g = core.run_spanset(mctx, ss, 0, U32MAX, 0)
+    assert g[0] == whole[0]
+
+
+@pytest.mark.gpu
 def test_device_desc_sharded(mctx):
     """device-resident input (tsdbhip_synth_generate) split by span count"""
     import ctypes as C
