@@ -761,6 +761,8 @@ def main():
             rl["valu_source"] = vsrc
             rl["achieved"] = vi / (hot * 1e-3) if vi else None
             rl["frac"] = rl["achieved"] / VALU_PEAK_WIPS if vi else None
+        if world > 1 or rehearse:  # collective launches per call on this rank (RCCL groups)
+            res["collectives_per_call"] = tsum.n_collectives / ncalls
         if rehearse:
             res["rehearsal"] = {"shards": rehearse, "note": f"shard 0 of {rehearse} on a 1-rank RCCL "
                                 "communicator; value = this shard's points/s, not a node figure"}

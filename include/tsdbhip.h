@@ -157,7 +157,8 @@ typedef struct tsdbhip_timing {
   float    exchange_ms;     /* RCCL exchange (sharded runs)                 */
   float    hot_ms;          /* the dominant HBM-streaming kernel alone      */
   uint32_t hot_kernel;      /* TSDBHIP_HOT_*: which kernel hot_ms timed      */
-  float    reserved;
+  uint32_t n_collectives;   /* sharded calls: collective launches this rank
+                               issued (one per RCCL group)                  */
   uint64_t decode_bytes;    /* algorithmic bytes read+written by decode      */
   uint64_t alg_bytes;       /* SURVEY §8(d) algorithmic bytes of the call   */
   uint64_t n_grid;          /* |G|                                           */

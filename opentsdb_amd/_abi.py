@@ -100,7 +100,7 @@ class Timing(C.Structure):
         ("exchange_ms", C.c_float),
         ("hot_ms", C.c_float),
         ("hot_kernel", C.c_uint32),
-        ("reserved", C.c_float),
+        ("n_collectives", C.c_uint32),
         ("decode_bytes", C.c_uint64),
         ("alg_bytes", C.c_uint64),
         ("n_grid", C.c_uint64),

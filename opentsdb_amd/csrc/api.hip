@@ -83,6 +83,7 @@ struct Slot {
   // left by the previous spangroup_run that completed: its call state reset
   // to the initial values, its grid bitmap all zero (k_call_end)
   bool sm_ready = false, bitmap_clean = false;
+  bool bitmapx_clean = false;  // the same for "gbitmap_x" (sharded calls whose grids differ)
   std::map<std::string, Buf> zeroed;  // scratch_zero_kept: allocation last zeroed whole (not owned)
 };
 
@@ -222,6 +223,7 @@ static void timing_add(tsdbhip_ctx* c, const tsdbhip_timing& t) {  // (c->mu hel
   c->sum.exchange_ms += t.exchange_ms;
   c->sum.hot_ms += t.hot_ms;
   c->sum.hot_kernel = t.hot_kernel;
+  c->sum.n_collectives += t.n_collectives;
   c->sum.decode_bytes += t.decode_bytes;
   c->sum.alg_bytes += t.alg_bytes;
   c->sum.n_grid += t.n_grid;
@@ -821,7 +823,14 @@ struct Small {
                     // [0] assembly queue, [1] decode fallback, [2] direct list,
                     // [3] [4] k_ds_spans int / float leftovers
   uint32_t seg[CK_NSEG];  // k_ds_spans integer leftovers, per segment
+  // sharded calls: two 64-bit hashes of the rank's grid bitmap (k_grid_popc /
+  // k_grid_scan_blocks), and the agreed header words of the one collective
+  // after the local grids (XH_*: MIN, or complemented MAX, over the ranks)
+  unsigned long long ghash[2];
+  unsigned long long xh[10];
 };
+// Small.xh slots of the grid-agreement header
+enum { XH_ERR = 0, XH_GF0, XH_GF1, XH_FSTAR, XH_LO, XH_HI, XH_H1MIN, XH_H1MAX, XH_H2MIN, XH_H2MAX, XH_N };
 
 static Small small_init() {
   Small init = {};
@@ -837,8 +846,13 @@ static Small small_init() {
 // Several MIN / MAX agreements on call-state fields as one MIN allreduce of a
 // packed buffer (across GPUs each collective costs a latency of its own;
 // one rank: the plain per-field calls)
-struct XField { void* p; uint8_t kind; };  // kind: 0 u64 MIN, 1 u64 MAX, 2 u32 MAX
-static void xchg_minmax(Slot* ctx, Xchg* X, const XField* f, uint32_t n, uint64_t* sum_u64 = nullptr);
+// kind: 0 u64 MIN, 1 u64 MAX, 2 u32 MAX (written back to the field);
+// 3 immediate MIN, 4 immediate MAX, 5 u64 field MIN, 6 u64 field MAX (left in
+// the packed buffer only)
+struct XField { void* p; uint8_t kind; uint64_t imm; };
+constexpr uint32_t XM_MAX = 12;
+static void xchg_minmax(Slot* ctx, Xchg* X, const XField* f, uint32_t n, uint64_t* sum_u64 = nullptr,
+                        uint64_t* buf = nullptr);
 constexpr size_t OUT_HDR = 512;  // the Small snapshot ahead of the outputs
 static_assert(sizeof(Small) <= OUT_HDR, "Small must fit the output header");
 
@@ -851,19 +865,23 @@ static_assert(sizeof(Small) <= OUT_HDR, "Small must fit the output header");
 // inverses.
 struct XMove {
   uint32_t n;
-  uint8_t kind[8];
-  uint64_t* buf;     // [n] the packed words
-  void* field[8];    // the call-state fields
-  int32_t out;       // 0: fields -> buf, 1: buf -> fields
+  uint8_t kind[XM_MAX];
+  uint64_t* buf;          // [n] the packed words
+  void* field[XM_MAX];    // the call-state fields
+  uint64_t imm[XM_MAX];   // kinds 3 / 4
+  int32_t out;            // 0: fields -> buf, 1: buf -> fields
 };
 __global__ void k_xmove(XMove m) {
   for (uint32_t i = 0; i < m.n; i++) {
+    const uint8_t k = m.kind[i];
+    const bool cpl = k == 1 || k == 2 || k == 4 || k == 6;  // MAX kinds travel complemented
     if (!m.out) {
-      uint64_t v = m.kind[i] == 2 ? (uint64_t)*(const uint32_t*)m.field[i] : *(const uint64_t*)m.field[i];
-      m.buf[i] = m.kind[i] ? ~v : v;
-    } else {
-      const uint64_t v = m.kind[i] ? ~m.buf[i] : m.buf[i];
-      if (m.kind[i] == 2) *(uint32_t*)m.field[i] = (uint32_t)v;
+      const uint64_t v = k == 2 ? (uint64_t)*(const uint32_t*)m.field[i]
+                         : (k == 3 || k == 4) ? m.imm[i] : *(const uint64_t*)m.field[i];
+      m.buf[i] = cpl ? ~v : v;
+    } else if (k <= 2) {
+      const uint64_t v = cpl ? ~m.buf[i] : m.buf[i];
+      if (k == 2) *(uint32_t*)m.field[i] = (uint32_t)v;
       else *(uint64_t*)m.field[i] = v;
     }
   }
@@ -872,19 +890,11 @@ __global__ void k_xmove(XMove m) {
 // (sum_u64: one more field, a u64 SUM, in the same collective group. The
 // pack / unpack kernels stay outside the group: RCCL issues a group's
 // collectives at its end.)
-static void xchg_minmax(Slot* ctx, Xchg* X, const XField* f, uint32_t n, uint64_t* sum_u64) {
-  if (X->nranks == 1) {
-    X->group_start(ctx);
-    for (uint32_t i = 0; i < n; i++)
-      X->allreduce(ctx, f[i].p, 1, f[i].kind == 2 ? X_U32 : X_U64, f[i].kind ? X_MAX : X_MIN);
-    if (sum_u64) X->allreduce(ctx, sum_u64, 1, X_U64, X_SUM);
-    X->group_end(ctx);
-    return;
-  }
+static void xchg_minmax(Slot* ctx, Xchg* X, const XField* f, uint32_t n, uint64_t* sum_u64, uint64_t* buf) {
   XMove m = {};
   m.n = n;
-  m.buf = scratch<uint64_t>(ctx, "x_pack", 8);
-  for (uint32_t i = 0; i < n; i++) { m.kind[i] = f[i].kind; m.field[i] = f[i].p; }
+  m.buf = buf ? buf : scratch<uint64_t>(ctx, "x_pack", XM_MAX);
+  for (uint32_t i = 0; i < n; i++) { m.kind[i] = f[i].kind; m.field[i] = f[i].p; m.imm[i] = f[i].imm; }
   hipLaunchKernelGGL(k_xmove, dim3(1), dim3(1), 0, ctx->stream, m);
   X->group_start(ctx);
   X->allreduce(ctx, m.buf, n, X_U64, X_MIN);
@@ -892,6 +902,20 @@ static void xchg_minmax(Slot* ctx, Xchg* X, const XField* f, uint32_t n, uint64_
   X->group_end(ctx);
   m.out = 1;
   hipLaunchKernelGGL(k_xmove, dim3(1), dim3(1), 0, ctx->stream, m);
+}
+
+// dst (global geometry [dst_lo, ...]) = src (a rank's bitmap over [src_lo,
+// ...], src_lo >= dst_lo) shifted into place; bits outside src read as 0.
+__global__ void __launch_bounds__(256) k_bitmap_remap(const uint32_t* src, uint64_t src_words, int64_t src_lo,
+                                                      uint32_t* dst, uint64_t dst_words, int64_t dst_lo) {
+  const uint64_t w = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+  if (w >= dst_words) return;
+  const int64_t sb = (int64_t)(32 * w) - (src_lo - dst_lo);  // src bit of dst bit 32 w
+  const int64_t i0 = sb >= 0 ? sb / 32 : -((31 - sb) / 32);   // floor(sb / 32)
+  const uint32_t sh = (uint32_t)(sb - 32 * i0);
+  auto at = [&](int64_t i) { return i >= 0 && (uint64_t)i < src_words ? src[i] : 0u; };
+  const uint32_t a = at(i0), b = at(i0 + 1);
+  dst[w] = sh ? (a >> sh) | (b << (32 - sh)) : a;
 }
 
 // The call state to the host (host_publish) after a producer that could not
@@ -973,6 +997,7 @@ static int spangroup_run(Slot* ctx, const tsdbhip_sg_desc* d, tsdbhip_sg_out* ou
   // (a 1-rank communicator runs the same exchange code: tests use it)
   Xchg* X = (d->flags & TSDBHIP_SHARDED) ? ctx->x : nullptr;
   const bool sharded = X != nullptr;
+  if (X) X->n_coll = 0;
   const uint32_t S = d->n_spans;
   const uint64_t R = d->n_rows;
   const bool rate = d->rate != 0;
@@ -1050,7 +1075,7 @@ static int spangroup_run(Slot* ctx, const tsdbhip_sg_desc* d, tsdbhip_sg_out* ou
     // KC_MAX spans: the kernel hands the call state to the host itself)
     kept = scratch<uint32_t>(ctx, "kept", S);
     eoff = scratch<uint64_t>(ctx, "eoff", S);
-    pub1 = !sharded && S && S <= KC_MAX;
+    pub1 = S && S <= KC_MAX;
     p1 = pub1 ? next_pub(ctx, sizeof(Small)) : HostPub{};
     KeptArgs K;
     K.kept = sp_kept; K.cap = sp_cap; K.ncells = sp_ncells; K.n = S; K.kept_list = kept; K.eoff_k = eoff;
@@ -1079,37 +1104,35 @@ static int spangroup_run(Slot* ctx, const tsdbhip_sg_desc* d, tsdbhip_sg_out* ou
       }
     }
   }
-  if (sharded) {
-    // every rank needs the same bitmap geometry and the same error: the kept
-    // spans' bounds (min first, max last; ranks without kept spans hold the
-    // neutral ~0 / 0) and the error key (MIN of the stage | global order |
-    // code keys, err_raise) are reduced in place, so the one readback below
-    // returns the agreed values
-    const XField fa[3] = {{&sm->bound[0], 0}, {&sm->bound[1], 1}, {&sm->err, 0}};
-    xchg_minmax(ctx, X, fa, 3);
-  }
+  // (sharded: no collective here. Each rank builds its grid on its own
+  // bounds; one collective after the local grids tells whether they agree,
+  // and only when they do not are the bitmaps remapped and exchanged.)
   Small h;
   if (!pub1) {  // (the state's last writer cannot publish it: a one-wave kernel does)
     p1 = next_pub(ctx, sizeof(Small));
     hipLaunchKernelGGL(k_publish, dim3(1), dim3(64), 0, st, p1, (const uint64_t*)sm);
   }
   wait_pub(ctx, p1, &h, sizeof h);  // sync 1
-  if (h.err != ERR_NONE) throw Fail{err_code(h.err)};
-  const uint32_t n_kept = (uint32_t)h.n_kept;
+  // a rank whose own scan failed still takes part in the agreement below (its
+  // peers wait there for it), with nothing kept; every rank throws after it
+  const bool poisoned = h.err != ERR_NONE;
+  if (poisoned && !sharded) throw Fail{err_code(h.err)};
+  const uint32_t n_kept = poisoned ? 0u : (uint32_t)h.n_kept;
   out->n_input_points = h.n_input;
   uint64_t n_input_global = h.n_input;
 
   // ---- union-grid bitmap range: every E point lies in [first, last] of its
   // span and in [start, ...]; G keeps those <= end (SURVEY.md §8a closed form).
   // A kept span has first <= end and last >= start, so [lo, hi] is non-empty
-  // whenever some (rank's) span is kept.
+  // whenever some span (of this rank) is kept.
   int64_t lo = std::max<int64_t>(d->start_time, h.bound[0] == ~0ull ? INT64_MAX : (int64_t)h.bound[0]);
   int64_t hi = std::min<int64_t>(d->end_time, (int64_t)h.bound[1]);
-  if (h.bound[0] == ~0ull) hi = -1;
-  const bool empty_grid = lo > hi;
-  const uint64_t nwords = empty_grid ? 0 : (uint64_t)(hi - lo + 1 + 31) / 32;
+  if (h.bound[0] == ~0ull || poisoned) hi = -1;
+  bool empty_grid = lo > hi;
+  uint64_t nwords = empty_grid ? 0 : (uint64_t)(hi - lo + 1 + 31) / 32;
   // (zero on entry without a memset: the last call's k_call_end cleared it)
   uint32_t* bitmap = empty_grid ? nullptr : scratch_zero_kept<uint32_t>(ctx, "gbitmap", nwords, bm_clean);
+  bool used_bitmap_x = false;  // (sharded, grids not agreed: the global bitmap is "gbitmap_x")
   if (check_clean && bitmap) {  // (debug) the bitmap must be zero on entry
     unsigned long long* cnt = scratch<unsigned long long>(ctx, "chk_cnt", 1, true);
     const uint64_t nall = ctx->bufs["gbitmap"].n / 4;
@@ -1248,43 +1271,94 @@ static int spangroup_run(Slot* ctx, const tsdbhip_sg_desc* d, tsdbhip_sg_out* ou
   uint32_t* word_rank = nullptr;
   uint32_t* gridv = nullptr;
   if (detail) HIPCHK(hipEventRecord(ctx->ev[3], st));
-  if (!empty_grid) {
+  GridArgs ga = {};
+  ga.e_off = eoff; ga.e_len = e_len; ga.e_ts = e_ts; ga.n_kept = n_kept; ga.rate = rate; ga.total = &sm->T;
+  ga.e_flt = e_flt; ga.err = &sm->err; ga.fstar = &sm->fstar;
+  ga.list = mark_list;  // spans k_ds_spans / the direct scan did not mark (null: all)
+  ga.list_count = mark_count;
+  // the direct path's verify appends to the direct / fallback lists again:
+  // k_grid_popc zeroes their counters (cnt[1], cnt[2])
+  ga.zero2 = direct && n_kept ? &sm->cnt[1] : nullptr;
+  ga.pub_src = (const uint64_t*)sm;
+  // word ranks (block-local) and block sums of the bitmap (lo, nwords); the
+  // single-block kernel that finishes T publishes the call state when `pub`
+  auto grid_ranks = [&](bool pub, bool hash) {
     word_rank = scratch<uint32_t>(ctx, "word_rank", nwords);
     const uint64_t nb = (nwords + 1023) / 1024;
-    uint32_t* bsum = scratch<uint32_t>(ctx, "grid_bsum", nb);
-    GridArgs ga = {};
-    ga.e_off = eoff; ga.e_len = e_len; ga.e_ts = e_ts; ga.n_kept = n_kept; ga.lo = lo; ga.hi = hi;
-    ga.rate = rate; ga.bitmap = bitmap; ga.nwords = nwords; ga.word_rank = word_rank; ga.block_sum = bsum;
-    ga.total = &sm->T;
-    ga.list = mark_list;  // spans k_ds_spans did not mark (null: all)
-    ga.list_count = mark_count;
-    // the direct path's verify appends to the direct / fallback lists again:
-    // k_grid_popc zeroes their counters (cnt[1], cnt[2])
-    ga.zero2 = direct && n_kept ? &sm->cnt[1] : nullptr;
-    ga.pub = next_pub(ctx, sizeof(Small));  // (k_grid_popc or k_grid_scan_blocks, single block, publishes)
-    ga.pub_src = (const uint64_t*)sm;
-    ga.e_flt = e_flt;
-    ga.err = &sm->err;
-    ga.fstar = &sm->fstar;
+    ga.lo = lo; ga.hi = hi; ga.bitmap = bitmap; ga.nwords = nwords; ga.word_rank = word_rank;
+    ga.block_sum = scratch<uint32_t>(ctx, "grid_bsum", nb);
+    ga.hash = hash ? sm->ghash : nullptr;
+    ga.block_hash = hash && nb > 1 ? scratch<unsigned long long>(ctx, "grid_bhash", 2 * nb) : nullptr;
+    ga.pub = pub ? next_pub(ctx, sizeof(Small)) : HostPub{};
+    hipLaunchKernelGGL(k_grid_popc, dim3((unsigned)nb), dim3(256), 0, st, ga);
+    if (nb > 1) hipLaunchKernelGGL(k_grid_scan_blocks, dim3(1), dim3(256), 0, st, ga, (uint32_t)nb);
+  };
+  if (!empty_grid) {
+    ga.lo = lo; ga.hi = hi; ga.bitmap = bitmap; ga.nwords = nwords;
     if (n_kept)
       hipLaunchKernelGGL(k_grid_mark, dim3(mark_list ? std::min(grid_for(n_kept, 4, 65536), 1024u) : grid_for(n_kept, 4, 65536)),
                          dim3(256), 0, st, ga);
-    if (sharded) {
-      // agree on the int/float flags, F*, the error and the input count across
-      // ranks, in place, ahead of the one readback
-      const XField fb[4] = {{&sm->gflags[0], 2}, {&sm->gflags[1], 2}, {&sm->fstar, 1}, {&sm->err, 0}};
-      xchg_minmax(ctx, X, fb, 4, (uint64_t*)&sm->n_input);
-    }
-    if (sharded) {
+    grid_ranks(!sharded, sharded);
+  }
+  if (sharded) {
+    // One collective: the error, the int / float flags and F* (agreed in
+    // place), the input count (sum), and each rank's grid geometry and bitmap
+    // hashes as MIN / MAX pairs. Equal geometry and hashes on every rank: the
+    // local grid is the global one (aligned series, C3 / C3*), nothing else is
+    // exchanged before the partials. Otherwise the bitmaps are remapped onto
+    // the global [lo, hi] and OR-ed over the ranks (allgather) below.
+    // (an empty local grid: hashes 0, never a non-empty grid's, so the ranks
+    // agree only when every grid is empty)
+    const uint64_t elo = empty_grid ? ~0ull : (uint64_t)lo, ehi = empty_grid ? 0ull : (uint64_t)hi;
+    if (empty_grid) HIPCHK(hipMemsetAsync(sm->ghash, 0, sizeof sm->ghash, st));
+    const XField fx[XH_N] = {{&sm->err, 0, 0}, {&sm->gflags[0], 2, 0}, {&sm->gflags[1], 2, 0}, {&sm->fstar, 1, 0},
+                             {nullptr, 3, elo}, {nullptr, 4, ehi}, {&sm->ghash[0], 5, 0}, {&sm->ghash[0], 6, 0},
+                             {&sm->ghash[1], 5, 0}, {&sm->ghash[1], 6, 0}};
+    xchg_minmax(ctx, X, fx, XH_N, (uint64_t*)&sm->n_input, (uint64_t*)sm->xh);
+    const HostPub p2 = next_pub(ctx, sizeof(Small));
+    hipLaunchKernelGGL(k_publish, dim3(1), dim3(64), 0, st, p2, (const uint64_t*)sm);
+    wait_pub(ctx, p2, &h, sizeof h);  // sync 2: agreed error / flags / count, the grids' geometry and hashes
+    after_sync2();
+    const int64_t glo = (int64_t)h.xh[XH_LO], ghi = (int64_t)~h.xh[XH_HI];
+    const bool all_empty = h.xh[XH_LO] == ~0ull;
+    const bool agreed = all_empty || (h.xh[XH_LO] == (uint64_t)lo && ghi == hi && !empty_grid &&
+                                      h.xh[XH_H1MIN] == ~h.xh[XH_H1MAX] && h.xh[XH_H2MIN] == ~h.xh[XH_H2MAX] &&
+                                      h.xh[XH_H1MIN] == h.ghash[0] && h.xh[XH_H2MIN] == h.ghash[1]);
+    if (!agreed) {
+      // the global geometry: this rank's bitmap shifted onto [glo, ghi] (a
+      // separate buffer; the local one is cleared), then OR-ed over the ranks
+      const uint64_t gw = (uint64_t)(ghi - glo + 1 + 31) / 32;
+      const bool clean_x = ctx->bitmapx_clean;
+      ctx->bitmapx_clean = false;
+      uint32_t* gbm = scratch_zero_kept<uint32_t>(ctx, "gbitmap_x", gw, clean_x);
+      if (!empty_grid) {
+        hipLaunchKernelGGL(k_bitmap_remap, dim3(grid_for(gw, 256)), dim3(256), 0, st, (const uint32_t*)bitmap, nwords,
+                           lo, gbm, gw, glo);
+        HIPCHK(hipMemsetAsync(bitmap, 0, nwords * 4, st));
+      }
+      bitmap = gbm;
+      lo = glo;
+      hi = ghi;
+      nwords = gw;
+      empty_grid = false;
+      used_bitmap_x = true;
       uint32_t* all = scratch<uint32_t>(ctx, "bitmap_all", nwords * X->nranks);
       X->allgather(ctx, bitmap, all, nwords * 4);
       hipLaunchKernelGGL(k_bitmap_or, dim3(grid_for(nwords, 256)), dim3(256), 0, st, all, (uint32_t)X->nranks,
                          nwords, bitmap);
+      grid_ranks(true, false);
+      wait_pub(ctx, ga.pub, &h, sizeof h);  // sync 3: |G| of the global grid
     }
-    hipLaunchKernelGGL(k_grid_popc, dim3((unsigned)nb), dim3(256), 0, st, ga);
-    if (nb > 1) hipLaunchKernelGGL(k_grid_scan_blocks, dim3(1), dim3(256), 0, st, ga, (uint32_t)nb);
+    dg.lo = lo;
+    dg.hi = hi;
+  } else if (!empty_grid) {
     wait_pub(ctx, ga.pub, &h, sizeof h);  // sync 2: |G|, flags, F*, errors
     after_sync2();
+  } else {
+    readback(ctx, &h, sm, sizeof h);  // sync 2 (no grid)
+    after_sync2();
+  }
+  if (!empty_grid) {
     T = h.T;
     gridv = scratch<uint32_t>(ctx, "grid", T);
     ga.grid = gridv;
@@ -1308,13 +1382,6 @@ static int spangroup_run(Slot* ctx, const tsdbhip_sg_desc* d, tsdbhip_sg_out* ou
       hipLaunchKernelGGL((k_decode_fast<0, false, true>), dim3(std::min(grid_for(n_kept, 4, 65536), 1024u)), dim3(256),
                          0, st, fa, row_ncells, row_val_len);
     }
-  } else {
-    if (sharded) {  // (the same agreement as above)
-      const XField fb[4] = {{&sm->gflags[0], 2}, {&sm->gflags[1], 2}, {&sm->fstar, 1}, {&sm->err, 0}};
-      xchg_minmax(ctx, X, fb, 4, (uint64_t*)&sm->n_input);
-    }
-    readback(ctx, &h, sm, sizeof h);  // sync 2 (no grid)
-    after_sync2();
   }
   const bool anyf = h.gflags[0] != 0, anyi = h.gflags[1] != 0;
   const uint64_t fstar = h.fstar;
@@ -1515,7 +1582,11 @@ static int spangroup_run(Slot* ctx, const tsdbhip_sg_desc* d, tsdbhip_sg_out* ou
   std::memcpy(&h, hb, sizeof h);
   ctx->sm_ready = true;
   ctx->bitmap_clean = true;
-  if (sharded) tm.exchange_ms = T > 0 ? ev_ms(ctx->ev[6], ctx->ev[7]) : 0.f;
+  if (used_bitmap_x) ctx->bitmapx_clean = true;
+  if (sharded) {
+    tm.exchange_ms = T > 0 ? ev_ms(ctx->ev[6], ctx->ev[7]) : 0.f;
+    tm.n_collectives = X->n_coll;
+  }
   if (detail) {
     tm.decode_ms = ev_ms(ctx->ev[1], ctx->ev[2]);
     tm.grid_ms = ev_ms(ctx->ev[3], ctx->ev[4]);

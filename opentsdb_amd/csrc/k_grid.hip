@@ -36,7 +36,22 @@ struct GridArgs {
   unsigned long long* fstar;
   HostPub pub;                // the call state to the host once T is known (the
   const uint64_t* pub_src;    // single-block kernel that writes T publishes it)
+  // sharded calls: two independent 64-bit hashes of the bitmap words (word
+  // value and index), summed over words, so ranks can tell whether their
+  // local grids agree; null: not computed
+  unsigned long long* hash;        // [2]
+  unsigned long long* block_hash;  // [2 nblocks] (more than one block)
 };
+
+// the per-word terms of the two grid hashes (splitmix64 finalisers of the
+// word and its index; a sum of them over all words)
+DEVI uint64_t gh_mix(uint64_t z) {
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  return z ^ (z >> 31);
+}
+DEVI uint64_t gh_term1(uint32_t word, uint64_t w) { return gh_mix(((uint64_t)word << 32 | (w & 0xFFFFFFFFull)) + 0x9E3779B97F4A7C15ull); }
+DEVI uint64_t gh_term2(uint32_t word, uint64_t w) { return gh_mix((uint64_t)word * 0xD1B54A32D192ED03ull ^ (w * 0x8CB92BA72F3D8DD7ull + 1)); }
 
 // Mark every candidate point. Many spans share timestamps (regular cadence),
 // so test before the atomic: a word that already has the bit skips it.
@@ -77,15 +92,32 @@ __global__ void __launch_bounds__(256) k_grid_mark(GridArgs g) {
 // Per-block (1024 words) exclusive popcount prefix.
 __global__ void __launch_bounds__(256) k_grid_popc(GridArgs g) {
   __shared__ uint32_t s_wave[4];
+  __shared__ unsigned long long s_h[2][4];
   const uint64_t base = (uint64_t)blockIdx.x * 1024;
   const int t = threadIdx.x;
   uint32_t c[4];
   uint32_t tot = 0;
+  uint64_t h1 = 0, h2 = 0;
 #pragma unroll
   for (int i = 0; i < 4; i++) {
     const uint64_t w = base + t * 4 + i;
-    c[i] = w < g.nwords ? __popc(g.bitmap[w]) : 0;
+    const uint32_t word = w < g.nwords ? g.bitmap[w] : 0u;
+    c[i] = __popc(word);
     tot += c[i];
+    if (g.hash && w < g.nwords) {
+      h1 += gh_term1(word, w);
+      h2 += gh_term2(word, w);
+    }
+  }
+  if (g.hash) {  // (block sums of the two hashes)
+    for (int o = 1; o < WAVE; o <<= 1) {
+      h1 += shfl_xor_u64(h1, o);
+      h2 += shfl_xor_u64(h2, o);
+    }
+    if ((t & 63) == 0) {
+      s_h[0][t >> 6] = h1;
+      s_h[1][t >> 6] = h2;
+    }
   }
   const uint32_t incl = wave_incl_scan_u32(tot);
   if ((t & 63) == 63) s_wave[t >> 6] = incl;
@@ -105,6 +137,17 @@ __global__ void __launch_bounds__(256) k_grid_popc(GridArgs g) {
   }
   if (t == 255) {
     g.block_sum[blockIdx.x] = woff + incl;
+    if (g.hash) {  // (s_h is complete: the __syncthreads above)
+      const uint64_t b1 = s_h[0][0] + s_h[0][1] + s_h[0][2] + s_h[0][3];
+      const uint64_t b2 = s_h[1][0] + s_h[1][1] + s_h[1][2] + s_h[1][3];
+      if (gridDim.x == 1) {
+        g.hash[0] = b1 | 1ull;  // (never 0: 0 stands for an empty grid)
+        g.hash[1] = b2;
+      } else {
+        g.block_hash[2 * blockIdx.x] = b1;
+        g.block_hash[2 * blockIdx.x + 1] = b2;
+      }
+    }
     if (gridDim.x == 1) {  // one block: its offset is 0 and its sum is T (no k_grid_scan_blocks)
       g.block_sum[0] = 0;
       g.total[0] = woff + incl;
@@ -137,6 +180,21 @@ __global__ void __launch_bounds__(256) k_grid_scan_blocks(GridArgs g, uint32_t n
     __syncthreads();
     if (t == 255) s_carry = carry + woff + incl;
     __syncthreads();
+  }
+  if (g.hash && t < WAVE) {  // the block hashes summed (wrapping), wave 0
+    uint64_t h1 = 0, h2 = 0;
+    for (uint32_t b = t; b < nblocks; b += WAVE) {
+      h1 += g.block_hash[2 * b];
+      h2 += g.block_hash[2 * b + 1];
+    }
+    for (int o = 1; o < WAVE; o <<= 1) {
+      h1 += shfl_xor_u64(h1, o);
+      h2 += shfl_xor_u64(h2, o);
+    }
+    if (t == 0) {
+      g.hash[0] = h1 | 1ull;
+      g.hash[1] = h2;
+    }
   }
   if (t == 0) {
     g.total[0] = s_carry;

@@ -32,15 +32,42 @@ static size_t xsize(XType t) {
 
 struct Xchg {
   int nranks = 1, rank = 0;
+  // collective launches of the current call: one per group (RCCL issues a
+  // group's operations as one launch at its end) or ungrouped operation
+  uint32_t n_coll = 0;
+  int depth = 0;
   virtual ~Xchg() {}
-  virtual void group_start(Slot* ctx) {}
-  virtual void group_end(Slot* ctx) {}
+  void group_start(Slot* ctx) {
+    if (depth++ == 0) do_group_start(ctx);
+  }
+  void group_end(Slot* ctx) {
+    if (--depth == 0) {
+      do_group_end(ctx);
+      n_coll++;
+    }
+  }
+  void allreduce(Slot* ctx, void* buf, size_t count, XType t, XOp op) {
+    if (!depth) n_coll++;
+    do_allreduce(ctx, buf, count, t, op);
+  }
+  void allgather(Slot* ctx, const void* send, void* recv, size_t bytes) {
+    if (!depth) n_coll++;
+    do_allgather(ctx, send, recv, bytes);
+  }
+  void broadcast(Slot* ctx, const void* send, void* recv, size_t bytes, int root) {
+    if (!depth) n_coll++;
+    do_broadcast(ctx, send, recv, bytes, root);
+  }
+
+ protected:
+  virtual void do_group_start(Slot* ctx) {}
+  virtual void do_group_end(Slot* ctx) {}
   // in place, element-wise over the ranks
-  virtual void allreduce(Slot* ctx, void* buf, size_t count, XType t, XOp op) = 0;
+  virtual void do_allreduce(Slot* ctx, void* buf, size_t count, XType t, XOp op) = 0;
   // recv[r * bytes, (r+1) * bytes) = rank r's send
-  virtual void allgather(Slot* ctx, const void* send, void* recv, size_t bytes) = 0;
+  virtual void do_allgather(Slot* ctx, const void* send, void* recv, size_t bytes) = 0;
   // every rank's recv = root's send (the root's recv too)
-  virtual void broadcast(Slot* ctx, const void* send, void* recv, size_t bytes, int root) = 0;
+  virtual void do_broadcast(Slot* ctx, const void* send, void* recv, size_t bytes, int root) = 0;
 };
 
 // ---------------------------------------------------------------- RCCL ----
@@ -57,16 +84,16 @@ static ncclDataType_t nccl_type(XType t) {
 
 struct RcclXchg : Xchg {
   ncclComm_t comm = nullptr;
-  void group_start(Slot* ctx) override { NCCLCHK(ncclGroupStart()); }
-  void group_end(Slot* ctx) override { NCCLCHK(ncclGroupEnd()); }
-  void allreduce(Slot* ctx, void* buf, size_t count, XType t, XOp op) override {
+  void do_group_start(Slot* ctx) override { NCCLCHK(ncclGroupStart()); }
+  void do_group_end(Slot* ctx) override { NCCLCHK(ncclGroupEnd()); }
+  void do_allreduce(Slot* ctx, void* buf, size_t count, XType t, XOp op) override {
     const ncclRedOp_t o = op == X_SUM ? ncclSum : op == X_MIN ? ncclMin : ncclMax;
     NCCLCHK(ncclAllReduce(buf, buf, count, nccl_type(t), o, comm, ctx->stream));
   }
-  void allgather(Slot* ctx, const void* send, void* recv, size_t bytes) override {
+  void do_allgather(Slot* ctx, const void* send, void* recv, size_t bytes) override {
     NCCLCHK(ncclAllGather(send, recv, bytes, ncclUint8, comm, ctx->stream));
   }
-  void broadcast(Slot* ctx, const void* send, void* recv, size_t bytes, int root) override {
+  void do_broadcast(Slot* ctx, const void* send, void* recv, size_t bytes, int root) override {
     NCCLCHK(ncclBroadcast(send, recv, bytes, ncclUint8, root, comm, ctx->stream));
   }
 };
@@ -151,7 +178,7 @@ struct LocalXchg : Xchg {
     for (int q = 0; q < nranks; q++)
       if (q != rank) HIPCHK(hipStreamWaitEvent(ctx->stream, G->done[q], 0));
   }
-  void allgather(Slot* ctx, const void* send, void* recv, size_t bytes) override {
+  void do_allgather(Slot* ctx, const void* send, void* recv, size_t bytes) override {
     publish(ctx, send);
     for (int q = 0; q < nranks; q++) {
       if (q != rank) HIPCHK(hipStreamWaitEvent(ctx->stream, G->ready[q], 0));
@@ -159,16 +186,16 @@ struct LocalXchg : Xchg {
     }
     retire(ctx);
   }
-  void broadcast(Slot* ctx, const void* send, void* recv, size_t bytes, int root) override {
+  void do_broadcast(Slot* ctx, const void* send, void* recv, size_t bytes, int root) override {
     publish(ctx, send);
     if (rank != root) HIPCHK(hipStreamWaitEvent(ctx->stream, G->ready[root], 0));
     if (rank != root || send != recv) copy_from(ctx, recv, root, G->ptr[root], bytes);
     retire(ctx);
   }
-  void allreduce(Slot* ctx, void* buf, size_t count, XType t, XOp op) override {
+  void do_allreduce(Slot* ctx, void* buf, size_t count, XType t, XOp op) override {
     const size_t bytes = count * xsize(t);
     uint8_t* all = scratch<uint8_t>(ctx, "x_allreduce", bytes * nranks);
-    allgather(ctx, buf, all, bytes);
+    do_allgather(ctx, buf, all, bytes);
     if (!count) return;
     const dim3 g(grid_for(count, 256)), b(256);
     const uint32_t n = (uint32_t)nranks;

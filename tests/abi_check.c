@@ -45,7 +45,7 @@ static int layout(void) {
   BEGIN(tsdbhip_timing);
   F(tsdbhip_timing, total_ms); F(tsdbhip_timing, decode_ms); F(tsdbhip_timing, grid_ms);
   F(tsdbhip_timing, reduce_ms); F(tsdbhip_timing, exchange_ms); F(tsdbhip_timing, hot_ms);
-  F(tsdbhip_timing, hot_kernel); F(tsdbhip_timing, reserved); F(tsdbhip_timing, decode_bytes);
+  F(tsdbhip_timing, hot_kernel); F(tsdbhip_timing, n_collectives); F(tsdbhip_timing, decode_bytes);
   F(tsdbhip_timing, alg_bytes); F(tsdbhip_timing, n_grid); F(tsdbhip_timing, n_emitted);
   END();
   BEGIN(tsdbhip_rows_desc);

@@ -140,6 +140,24 @@ def test_empty_span_and_nan_in_a_later_rank(mctx):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("dsi", [60, 0])
+def test_aligned_grids_skip_the_grid_exchange(mctx, dsi):
+    """Aligned shards (C3* / C3: every series on the same cadence): each
+    rank's local grid is the global one, which the agreement header proves,
+    so a call issues two collective launches, the header and the partials
+    (SURVEY.md §8(e)); shards whose grids differ also exchange bitmaps."""
+    ss = synth.regular(64, 600, _abi.SYN_INT64_COUNTER, seed=2, step=1)
+    for agg in (0, 2):
+        g, o = both(mctx, ss, agg=agg, dsi=dsi, dsa=3)
+        assert_same(g, o)
+        assert mctx.timing().n_collectives == 2
+    ss = synth.jittered(13, 70, seed=1, span_range=400_000, max_gap=700)
+    g, o = both(mctx, ss, agg=0)
+    assert_same(g, o)
+    assert mctx.timing().n_collectives == 3
+
+
+@pytest.mark.gpu
 def test_error_order_is_global_span_order(mctx, ctx):
     """Two Span.addRow errors at the same base time in different ranks: the
     one in the lower global span wins (the scan's row-key order: base time,
