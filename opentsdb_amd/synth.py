@@ -200,13 +200,16 @@ def jittered(n_spans, mean_pts, seed=4, t0=T0, span_range=40_000_000, max_gap=69
 
 
 def jittered_packed(n_spans, mean_pts, seed=4, t0=T0, span_range=40_000_000, max_gap=6960,
-                    float_frac=0.5, float_cell_frac=0.01):
+                    float_frac=0.5, float_cell_frac=0.01, absval=False):
     """C4, vectorised: ~mean_pts points per series with
     jittered gaps U{1..max_gap} s from a start in the first quarter of
     `span_range`; `float_frac` of the series float32 (~100 + N(0,1)), the
     others minimal-width longs with `float_cell_frac` float cells. One
     compacted KeyValue per hour row (trivialCompact layout, as series_rows),
-    packed like packing.pack_spans (rows 8-B / 16-B aligned)."""
+    packed like packing.pack_spans (rows 8-B / 16-B aligned). `absval`: the
+    same series with |value| (same timestamps and cell types; by convexity a
+    lerp of the |y| bounds the |lerp| of the y, so the group's sum over them
+    bounds the sum of |terms| a double result is rounded against)."""
     rng = np.random.default_rng(seed)
     n = rng.integers(max(2, mean_pts // 2), mean_pts * 3 // 2 + 1, n_spans).astype(np.int64)
     N = int(n.sum())
@@ -222,6 +225,8 @@ def jittered_packed(n_spans, mean_pts, seed=4, t0=T0, span_range=40_000_000, max
     fval = np.where(is_fs[sid], 100.0 + rng.standard_normal(N),
                     rng.integers(-1000, 1000, N).astype(np.float64) + 0.5).astype(">f4")
     ival = rng.integers(-10**6, 10**6, N).astype(np.int64)
+    if absval:
+        fval, ival = np.abs(fval).astype(">f4"), np.abs(ival)
     # minimal long widths (TSDB.java:240-250)
     iw = np.where((ival >= -128) & (ival <= 127), 1,
                   np.where((ival >= -32768) & (ival <= 32767), 2,
