@@ -34,6 +34,7 @@
 #include "k_util.hip"
 #include "k_decode_fast.hip"
 #include "k_ds_chunks.hip"
+#include "k_ds_reg.hip"
 #include "k_compact.hip"
 #include "k_direct.hip"
 #include "k_group.hip"
@@ -636,28 +637,44 @@ struct LaunchFastDsInl {
   }
 };
 
-// Streaming downsampling of regular-cadence integer spans (k_ds_spans, wave
-// per span); leaves the spans it did not take in fa.span_list for
+// Streaming downsampling: constant-step spans by formula (k_ds_reg, up to 4
+// waves per span), then chain-proved regular-cadence spans (k_ds_spans,
+// integer, then float); leaves the spans neither took in fa.span_list for
 // k_decode_fast.
 constexpr uint32_t CK_NSEG = 64;
 struct LaunchChunks {
   template <int AGG>
   static void run(Slot* ctx, const DecodeArgs& da, DecodeArgs& fa, const uint32_t* ncells,
-                  const uint32_t* vlen, SpanDsArgs g, uint32_t* zeroed2 = nullptr, uint32_t* zeroed_seg = nullptr) {
+                  const uint32_t* vlen, SpanDsArgs g, uint64_t n_rows, bool use_reg = true,
+                  uint32_t* zeroed2 = nullptr, uint32_t* zeroed_seg = nullptr, uint32_t* zeroed_seg2 = nullptr) {
     if (AGG == 4) return;  // dev: Welford is order-dependent, serial kernels only
     hipStream_t st = ctx->stream;
     const uint32_t n_kept = da.n_kept;
-    const unsigned iblocks = grid_for(n_kept, 4, 1u << 20);
-    // the integer instantiation's leftovers: 64 segments (block % 64)
+    // (zeroed*: list counters already zero on the device, no memsets)
+    // k_ds_reg: a span's rows split over 1 << wps_log2 waves of a block
+    const uint64_t rps = n_rows / std::max<uint32_t>(n_kept, 1);
+    const uint32_t wps_log2 = rps >= 12 ? 2 : (rps >= 6 ? 1 : 0);
+    const uint32_t rblocks = (uint32_t)(((uint64_t)n_kept * (1u << wps_log2) + 3) / 4);
+    SpanDsArgs gr = g;
+    gr.nseg = CK_NSEG;
+    gr.seg_cap = (4u >> wps_log2) * ((rblocks + CK_NSEG - 1) / CK_NSEG);
+    gr.list = scratch<uint32_t>(ctx, "cr_list", (uint64_t)gr.seg_cap * CK_NSEG);
+    gr.list_count = zeroed_seg2 ? zeroed_seg2 : scratch<uint32_t>(ctx, "cr_seg_count", CK_NSEG, true);
+    gr.in_list = nullptr;
+    gr.in_count = nullptr;
+    gr.in_nseg = gr.in_seg_cap = 0;
+    // k_ds_spans<integer> over k_ds_reg's leftovers (usually few: a capped,
+    // grid-stride launch), its own leftovers in 64 segments (block % 64)
+    const unsigned iblocks = std::min(grid_for(n_kept, 4, 1u << 20), use_reg ? 4096u : (1u << 20));
     g.nseg = CK_NSEG;
-    g.seg_cap = 4 * ((iblocks + CK_NSEG - 1) / CK_NSEG);
+    g.seg_cap = 4 * ((iblocks + CK_NSEG - 1) / CK_NSEG) * ((n_kept + 4 * iblocks - 1) / (4 * iblocks));
     g.list = scratch<uint32_t>(ctx, "ck_list", (uint64_t)g.seg_cap * CK_NSEG);
-    // (zeroed2 / zeroed_seg: list counters already zero on the device, no memsets)
     g.list_count = zeroed_seg ? zeroed_seg : scratch<uint32_t>(ctx, "ck_seg_count", CK_NSEG, true);
-    g.in_list = nullptr;
-    g.in_count = nullptr;
-    g.in_nseg = g.in_seg_cap = 0;
-    // integer spans over every kept span, then float spans over the ones left
+    g.in_list = use_reg ? gr.list : nullptr;  // (!use_reg: every kept span, the full grid)
+    g.in_count = use_reg ? gr.list_count : nullptr;
+    g.in_nseg = use_reg ? gr.nseg : 0;
+    g.in_seg_cap = use_reg ? gr.seg_cap : 0;
+    // then float spans over the ones left
     SpanDsArgs gf = g;
     gf.in_list = g.list;
     gf.in_count = g.list_count;
@@ -667,7 +684,9 @@ struct LaunchChunks {
     gf.list = scratch<uint32_t>(ctx, "ck_list2", n_kept);
     gf.list_count = zeroed2 ? zeroed2 + 1 : scratch<uint32_t>(ctx, "ck_list2_count", 1, true);
     HIPCHK(hipEventRecord(ctx->ev[8], st));
-    hipLaunchKernelGGL((k_ds_spans<AGG, false>), dim3(iblocks), dim3(256), 0, st, da, g, ncells, vlen);
+    if (use_reg) hipLaunchKernelGGL((k_ds_reg<AGG>), dim3(rblocks), dim3(256), 0, st, da, gr, ncells, vlen, wps_log2);
+    hipLaunchKernelGGL((k_ds_spans<AGG, false>), dim3(use_reg ? iblocks : grid_for(n_kept, 4, 1u << 20)), dim3(256), 0,
+                       st, da, g, ncells, vlen);
     hipLaunchKernelGGL((k_ds_spans<AGG, true>), dim3(std::min(grid_for(n_kept, 4, 1u << 20), 1024u)), dim3(256), 0,
                        st, da, gf, ncells, vlen);
     HIPCHK(hipEventRecord(ctx->ev[9], st));
@@ -823,6 +842,7 @@ struct Small {
                     // [0] assembly queue, [1] decode fallback, [2] direct list,
                     // [3] [4] k_ds_spans int / float leftovers
   uint32_t seg[CK_NSEG];  // k_ds_spans integer leftovers, per segment
+  uint32_t seg2[CK_NSEG];  // k_ds_reg leftovers, per segment
   // sharded calls: two 64-bit hashes of the rank's grid bitmap (k_grid_popc /
   // k_grid_scan_blocks), and the agreed header words of the one collective
   // after the local grids (XH_*: MIN, or complemented MAX, over the ranks)
@@ -853,7 +873,7 @@ struct XField { void* p; uint8_t kind; uint64_t imm; };
 constexpr uint32_t XM_MAX = 12;
 static void xchg_minmax(Slot* ctx, Xchg* X, const XField* f, uint32_t n, uint64_t* sum_u64 = nullptr,
                         uint64_t* buf = nullptr);
-constexpr size_t OUT_HDR = 512;  // the Small snapshot ahead of the outputs
+constexpr size_t OUT_HDR = 1024;  // the Small snapshot ahead of the outputs
 static_assert(sizeof(Small) <= OUT_HDR, "Small must fit the output header");
 
 // End of a call, after the finalize: the call state is snapshot ahead of the
@@ -1176,6 +1196,9 @@ static int spangroup_run(Slot* ctx, const tsdbhip_sg_desc* d, tsdbhip_sg_out* ou
     if (force && !strcmp(force, "general")) fast = chunks = direct = false;
     if (force && !strcmp(force, "fast")) { fast = true; chunks = direct = false; }
     if (force && !strcmp(force, "chunks")) { fast = chunks = true; direct = false; }
+    // "spans": the chain-proved downsampler alone (k_ds_spans, no k_ds_reg first)
+    const bool use_reg = !(force && !strcmp(force, "spans"));
+    if (!use_reg) { fast = chunks = true; direct = false; }
     if (force && !strcmp(force, "direct")) { fast = chunks = true; direct = interval == 0 && bitmap != nullptr; }
     da.fb_list = scratch<uint32_t>(ctx, "fb_list", n_kept);
     da.fb_count = &sm->cnt[1];
@@ -1236,7 +1259,8 @@ static int spangroup_run(Slot* ctx, const tsdbhip_sg_desc* d, tsdbhip_sg_out* ou
         g.lo = lo;
         g.hi = hi;
         g.rate = rate;
-        launch_agg<LaunchChunks>(ds_agg, ctx, da, fa, row_ncells, row_val_len, g, &sm->cnt[3], sm->seg);
+        launch_agg<LaunchChunks>(ds_agg, ctx, da, fa, row_ncells, row_val_len, g, R, use_reg, &sm->cnt[3], sm->seg,
+                                 sm->seg2);
         chunk_marked = bitmap != nullptr && fa.span_list != nullptr;
       }
       if (chunk_marked) {
@@ -1259,7 +1283,12 @@ static int spangroup_run(Slot* ctx, const tsdbhip_sg_desc* d, tsdbhip_sg_out* ou
   // |G| below. A decode error leaves every e_len <= its capacity, so the grid
   // kernels stay inside E before the error is thrown.)
   auto after_sync2 = [&]() {
-    if (h.err != ERR_NONE) throw Fail{err_code(h.err)};
+    if (h.err != ERR_NONE) {
+      // (a scan / SpanGroup.add error: no SpanGroup, aggregatedSize() never
+      // reached; a sharded rank may have set its local count at sync 1)
+      if ((h.err >> 62) < 2) out->n_input_points = 0;
+      throw Fail{err_code(h.err)};
+    }
     if (sharded) {
       n_input_global = h.n_input;
       out->n_input_points = n_input_global;

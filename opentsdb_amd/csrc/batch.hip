@@ -302,7 +302,7 @@ static int spangroup_run_batch(Slot* ctx, const tsdbhip_sg_desc* d, uint32_t G, 
         SpanDsArgs sg = {};
         sg.bitmap = nullptr;  // group grids are marked after decode
         sg.rate = rate;
-        launch_agg<LaunchChunks>(ds_agg, ctx, da, fa, row_ncells, row_val_len, sg);
+        launch_agg<LaunchChunks>(ds_agg, ctx, da, fa, row_ncells, row_val_len, sg, R);
       }
       const unsigned lblocks = fa.span_list ? std::min(blocks, 1024u) : blocks;
       launch_agg<LaunchFastDs>(ds_agg, ctx, lblocks, fa, row_ncells, row_val_len);

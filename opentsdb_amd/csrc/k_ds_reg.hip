@@ -1,0 +1,380 @@
+// k_ds_reg.hip — greedy downsampling of constant-step spans by formula: the
+// first pass over a downsampled SpanGroup's kept spans.
+//
+// Span.DownsamplingIterator (Span.java:377-422) chains buckets serially: a
+// bucket starts at the first point at/after the previous start + interval.
+// On a span whose cells sit at ts = t0 + c * step (c = span cell index, every
+// cell, every row), the chain is closed-form: kk = ceil(interval / step) cells
+// per bucket, heads at c = 0, kk, 2kk, ..., so bucket b holds cells
+// [b kk, min((b+1) kk, n)) and its timestamp ⌊Σts / m⌋ (Span.java:399) is
+// t0 + b kk step + ⌊step (m - 1) / 2⌋ (m cells) — no chain proof, no
+// timestamp scan, no division. The wave proves the premise instead: each
+// lane compares its 8 qualifiers with the expected ones ((t0 + c step - base)
+// << 4 | flags, one xor per pair of cells), and each row's first / last delta
+// lies in [0, 4095]. Buckets close inside the chunk that holds their last
+// cell; value sums are differences of an LDS prefix (exact, wrapping), double
+// buckets (and min / max) a lane per bucket in point order
+// (Aggregators.java:86-180). The bucket still open at the end of a chunk is
+// carried in a wave-uniform register.
+//
+// The bucket heads being known up front, a span of many rows (C2: 24 hourly
+// rows of 360 cells) is split over up to 4 waves of one block, each taking a
+// contiguous run of rows that starts at a bucket head; the waves agree on the
+// span's fate at one block barrier before its grid points are marked.
+// Anything else — a cadence break, mixed widths or types, a first cell before
+// `start`, a piece boundary inside a bucket, dropped rows, Q1 / short
+// overflow — sends the whole span to k_ds_spans (chain-proved cadence), and
+// from there to the serial kernels, which rewrite its E.
+#pragma once
+#include "dev_common.h"
+#include "k_ds_chunks.hip"
+
+namespace tsdb {
+
+// x / d for u32 x by one multiply-high (round-up magic number, exact for
+// every u32 x; Granlund & Montgomery): set up once per span, wave-uniform.
+struct UDiv {
+  uint32_t m, s1, s2;
+  DEVI void init(uint32_t d) {
+    if (d == 1) { m = 0; s1 = 0; s2 = 0; return; }
+    const uint32_t l = 32 - __clz(d - 1);
+    m = (uint32_t)(((1ull << 32) * ((1ull << l) - d)) / d) + 1;
+    s1 = 1;
+    s2 = l - 1;
+  }
+  DEVI uint32_t div(uint32_t x) const {
+    const uint32_t t = __umulhi(x, m);
+    return (t + ((x - t) >> s1)) >> s2;
+  }
+};
+
+// wave-uniform description of a constant-step span
+struct RegSpan {
+  uint32_t t0, step, kk, n;  // first ts, cadence, cells per bucket, cells
+  uint64_t eo;               // E offset
+  uint32_t cap;              // E capacity
+  UDiv dkk;                  // / kk
+};
+
+// E entries of buckets [b0, b0 + cnt) (cnt <= 64) from the per-wave bucket
+// buffer (their values over their cells; timestamps by formula): one lane per
+// bucket, so the avg divisions (Span.java:399-420 with Aggregators.Avg)
+// leave the chunk loop.
+template <int AGG, bool FLT>
+DEVI void reg_flush(const DecodeArgs& a, const RegSpan& sp, const int64_t* BK, uint32_t b0, uint32_t cnt) {
+  wave_lds_sync();
+  const uint32_t i = lane_id();
+  if (i < cnt) {
+    const uint32_t b = b0 + i;
+    const uint32_t sb = b * sp.kk, m = min(sb + sp.kk, sp.n) - sb;
+    const int64_t v = BK[i];
+    const uint64_t o = sp.eo + b;
+    a.e_ts[o] = sp.t0 + sb * sp.step + (uint32_t)((uint64_t)sp.step * (m - 1) / 2);
+    if (FLT)  // Aggregators.Avg.runDouble: sum / n
+      a.e_val[o] = AGG == 3 ? dbits(bitsd(v) / (double)(int32_t)m) : v;
+    else
+      a.e_val[o] = AGG == 3 ? ldiv64_32(v, m) : v;
+    a.e_flt[o] = FLT ? 1 : 0;
+  }
+  wave_lds_sync();
+}
+
+// The chunks of rows [ra, rb) of one span (two register sets, the next
+// chunk's loads in flight while one is processed, as ds_span); buckets that
+// close in these rows go to E. Returns true if the premise breaks. The
+// caller checked the rows (reg_rows_ok) and that ra starts a bucket.
+template <int AGG, int W, bool FLT>
+DEVI bool reg_piece(const DecodeArgs& a, const RegSpan& sp, uint64_t ra, uint64_t rb, const uint32_t* ncells,
+                    uint64_t* L_v, int64_t* BK) {
+  constexpr bool PREFIX = (AGG == 0 || AGG == 3) && !FLT;  // wrapping sums: prefix differences
+  const int lane = lane_id();
+  const uint32_t fl = (FLT ? 8u : 0u) | (uint32_t)(W - 1);
+  const uint32_t nb = sp.dkk.div(sp.n + sp.kk - 1);
+  auto row_at = [&](uint64_t r) {
+    ChunkPos p;
+    p.r = r;
+    p.nc = sld(&ncells[r]);
+    p.qoff = sld(&a.row_qual_off[r]);
+    p.voff = sld(&a.row_val_off[r]);
+    p.base = sld(&a.row_base[r]);
+    p.cell0 = sld(&a.row_cell0[r]);
+    p.c0 = 0;
+    p.done = false;
+    return p;
+  };
+  auto advance = [&](const ChunkPos& p) {
+    if (p.done) return p;
+    if (p.c0 + DCH < p.nc) {
+      ChunkPos q = p;
+      q.c0 += DCH;
+      return q;
+    }
+    if (p.r + 1 < rb) return row_at(p.r + 1);
+    ChunkPos q = p;
+    q.done = true;
+    return q;
+  };
+  RawW<W> A, B;
+  auto issue = [&](const ChunkPos& p, RawW<W>& x) {
+    const uint32_t c = p.c0 + 8u * lane;
+    __builtin_amdgcn_s_setprio(2);
+    load_raw<W>(a, p.qoff, p.voff, c < p.nc ? c : (p.nc - 1) & ~7u, x);
+    __builtin_amdgcn_s_setprio(0);
+  };
+  bool bad = false;
+  int64_t carry = 0;  // the open bucket's value over its cells in earlier chunks
+  // bucket of the next chunk's first cell and that cell's place in it
+  uint32_t bcur = sp.dkk.div(sld(&a.row_cell0[ra])), ph = 0;
+  uint32_t fbase = bcur;  // first bucket held in BK
+  uint32_t bclosed = bcur;  // buckets closed so far: [.., bclosed)
+  // decode + qualifier check + LDS staging of one chunk (FULL: 512 cells)
+  auto stage = [&](auto full, const ChunkPos& p, const RawW<W>& cur, uint32_t nv, uint32_t cs) {
+    constexpr bool FULL = decltype(full)::value;
+    const uint32_t nmine = FULL ? 8u : (nv > 8u * lane ? min(8u, nv - 8u * lane) : 0u);
+    {  // (t0 + c step - base) << 4 | flags, two cells per dword
+      const uint32_t d0 = sp.t0 + (cs + 8u * lane) * sp.step - p.base;
+      uint32_t e = ((d0 << 4) | fl) * 0x00010001u + (sp.step << 20);
+      const uint32_t inc = sp.step * 0x00200020u;
+      const uint32_t qw[4] = {cur.q.x, cur.q.y, cur.q.z, cur.q.w};
+      uint32_t miss = 0;
+#pragma unroll
+      for (int i = 0; i < 4; i++) {
+        uint32_t x = qpair(qw[i]) ^ e;
+        if (!FULL) x &= nmine >= 2u * i + 2 ? 0xFFFFFFFFu : (nmine == 2u * i + 1 ? 0x0000FFFFu : 0u);
+        miss |= x;
+        e += inc;
+      }
+      bad |= miss != 0;
+    }
+    int64_t bits[8];
+#pragma unroll
+    for (int j = 0; j < 8; j++) {
+      bits[j] = raw_value<W>(cur, j);
+      if (W == 4 && FLT) bits[j] = dbits((double)__int_as_float((int32_t)bits[j]));
+      if (!FULL && (uint32_t)j >= nmine) bits[j] = 0;
+    }
+    uint64_t pv = 0, pvi[8];
+#pragma unroll
+    for (int j = 0; j < 8; j++) {
+      pv += (uint64_t)bits[j];
+      pvi[j] = PREFIX ? pv : (uint64_t)bits[j];
+    }
+    const uint64_t xv = PREFIX ? wave_incl_scan_u64_dpp(pv) - pv : 0ull;
+#pragma unroll
+    for (int j = 0; j < 8; j += 2) {
+      ulonglong2 v2;
+      v2.x = pvi[j] + xv;
+      v2.y = pvi[j + 1] + xv;
+      *(ulonglong2*)&L_v[8 * lane + j] = v2;
+    }
+  };
+  auto step = [&](const ChunkPos& p, const RawW<W>& cur) {
+    const uint32_t nv = ufl(min(DCH, p.nc - p.c0));
+    const uint32_t cs = ufl(p.cell0 + p.c0);  // span cell index of the chunk start
+    if (nv == DCH) stage(std::integral_constant<bool, true>(), p, cur, nv, cs);
+    else stage(std::integral_constant<bool, false>(), p, cur, nv, cs);
+    wave_lds_sync();
+    // ---- buckets ending in [cs, cend), then the one still open at cend ----
+    const uint32_t cend = cs + nv;
+    const uint32_t kk = sp.kk;
+    const uint32_t adv = sp.dkk.div(ph + nv);  // buckets whose last cell is in the chunk (full ones)
+    const uint32_t b_lo = bcur;
+    const uint32_t b_end = cend == sp.n ? nb : b_lo + adv;  // first bucket not closed here
+    ph = ph + nv - adv * kk;
+    bcur = b_lo + adv;
+    const bool open = cend < sp.n && ph != 0;  // bucket b_end takes later cells
+    const uint32_t nclose = b_end - b_lo;
+    bclosed = b_end;
+    const uint32_t ntot = nclose + (open ? 1u : 0u);
+    int64_t carry_next = 0;
+    for (uint32_t jb = 0; jb < ntot; jb += WAVE) {
+      const uint32_t j = jb + lane;
+      const bool act = j < ntot;
+      const uint32_t b = b_lo + (act ? j : 0u);
+      const uint32_t sb = b * kk;
+      const uint32_t eb = act && j < nclose ? min(sb + kk, sp.n) - 1 : cend - 1;  // (open: its cells so far)
+      const uint32_t la = sb > cs ? sb - cs : 0u, lb = eb - cs;
+      const bool cont = sb < cs;  // began in an earlier chunk
+      int64_t v;
+      if (PREFIX) {
+        v = (int64_t)(L_v[lb] - (la > 0 ? L_v[la - 1] : 0ull));
+        if (cont) v = ladd(v, carry);
+      } else if (FLT) {
+        double d = cont ? bitsd(carry) : bitsd((int64_t)L_v[la]);
+        for (uint32_t i = cont ? la : la + 1; act && i <= lb; i++) d = ds_dcombine<AGG>(d, bitsd((int64_t)L_v[i]));
+        v = dbits(d);
+      } else {
+        v = cont ? carry : (int64_t)L_v[la];
+        for (uint32_t i = cont ? la : la + 1; act && i <= lb; i++) v = ds_combine<AGG>(v, (int64_t)L_v[i]);
+      }
+      // closed buckets -> the bucket buffer (room for this pass's first)
+      const uint32_t pc = min(nclose - min(nclose, jb), (uint32_t)WAVE);
+      if (pc) {
+        if (b_lo + jb + pc - fbase > WAVE) {
+          reg_flush<AGG, FLT>(a, sp, BK, fbase, b_lo + jb - fbase);
+          fbase = b_lo + jb;
+        }
+        if (act && j < nclose) BK[b - fbase] = v;
+      }
+      if (open && jb + WAVE >= ntot) carry_next = (int64_t)readlane_u64((uint64_t)v, (int)(ntot - 1 - jb));
+    }
+    carry = carry_next;
+    wave_lds_sync();
+  };
+  ChunkPos p0 = row_at(ra);
+  ChunkPos p1 = advance(p0);
+  issue(p0, A);
+  issue(p1, B);
+  for (;;) {
+    step(p0, A);
+    if (p1.done || ballot(bad) != 0) break;
+    const ChunkPos p2 = advance(p1);
+    issue(p2, A);
+    step(p1, B);
+    if (p2.done || ballot(bad) != 0) break;
+    const ChunkPos p3 = advance(p2);
+    issue(p3, B);
+    p0 = p2;
+    p1 = p3;
+  }
+  // the piece ends at the span's end or at a bucket boundary (else the next
+  // piece does not start a bucket: the whole span is redone)
+  bad |= bclosed != nb && ph != 0;
+  if (ballot(bad) != 0) return true;
+  if (bclosed > fbase) reg_flush<AGG, FLT>(a, sp, BK, fbase, bclosed - fbase);
+  return false;
+}
+
+// Row checks of rows [ra, rb) of a span in constant-step form: kept, cells of
+// width W (value bytes = W n, + the meta byte of a compacted row), aligned,
+// every delta t0 + c step - base inside [0, 4095] (monotone in c: the first
+// and the last cell of the row decide).
+DEVI bool reg_rows_ok(const DecodeArgs& a, const RegSpan& sp, uint64_t ra, uint64_t rb, uint32_t W) {
+  const int lane = lane_id();
+  bool ok = true;
+  for (uint64_t rr = ra; ok && rr < rb; rr += WAVE) {  // (uniform loop: keeps `ok` scalar)
+    const uint64_t r = rr + lane;
+    bool rbad = false;
+    if (r < rb) {
+      const uint32_t nc = a.row_ncells[r], vl = a.row_val_len[r];
+      const uint32_t vb = nc > 1 ? vl - 1 : vl;
+      const int64_t d0 = (int64_t)sp.t0 + (int64_t)a.row_cell0[r] * sp.step - (int64_t)a.row_base[r];
+      const int64_t d1 = d0 + (int64_t)(nc - 1) * sp.step;
+      rbad = a.row_ok[r] == 0 || nc == 0 || vb != W * nc || (a.row_qual_off[r] & 7) != 0 ||
+             (a.row_val_off[r] & 15) != 0 || d0 < 0 || d1 > 4095;
+    }
+    ok = ballot(rbad) == 0;
+  }
+  return ok;
+}
+
+// Blocks of 4 waves; 1 << wps_log2 waves per span (a span's rows split into
+// that many contiguous pieces), 4 >> wps_log2 spans per block.
+template <int AGG>
+__global__ void __launch_bounds__(256) k_ds_reg(DecodeArgs a, SpanDsArgs g, const uint32_t* ncells,
+                                                const uint32_t* vlen, uint32_t wps_log2) {
+  __shared__ uint64_t s_v[4][DCH];
+  __shared__ int64_t s_bk[4][WAVE];
+  __shared__ uint32_t s_bad[4];
+  const int lane = lane_id();
+  const uint32_t wib = ufl(threadIdx.x / WAVE);  // (uniform: the span prologue and the row walk use scalar loads)
+  const uint32_t wps = 1u << wps_log2;
+  const uint32_t piece = wib & (wps - 1);
+  const uint32_t k = blockIdx.x * (4u >> wps_log2) + (wib >> wps_log2);
+  const int64_t I = a.interval;
+  bool ok = k < a.n_kept && I > 0;
+  uint32_t s = 0, W = 0, nb = 0;
+  bool flt = false;
+  RegSpan sp = {};
+  uint64_t r0 = 0, r1 = 0, ra = 0, rb = 0;
+  if (ok) {
+    s = sld(&a.kept[k]);
+    r0 = sld(&a.span_row_start[s]);
+    r1 = sld(&a.span_row_start[s + 1]);
+    sp.n = sld(&a.sp_ncells[s]);
+    ok = sld(&a.sp_q1[s]) < 0 && sld(&a.sp_ovf_cell[s]) < 0 && sp.n > 0 && r1 > r0;
+  }
+  if (ok) {  // the first row: width, type, t0 and the cadence from its first two cells
+    const uint32_t nc = sld(&ncells[r0]), vl = sld(&vlen[r0]);
+    const uint32_t vb = nc > 1 ? vl - 1 : vl;
+    W = nc != 0 && vb == (vb / nc) * nc ? vb / nc : 0;
+    const uint64_t qo = sld(&a.row_qual_off[r0]);
+    ok = (W == 8 || W == 4) && sld_u8(&a.row_ok[r0]) != 0 && (qo & 7) == 0 && (sp.n == 1 || nc >= 2);
+    if (ok) {
+      const uint32_t w = sld((const uint32_t*)(a.qual + qo));  // cells 0 and 1, big-endian
+      const uint32_t q0 = ((w & 0xFF) << 8) | ((w >> 8) & 0xFF), q1 = ((w >> 16) & 0xFF) << 8 | (w >> 24);
+      const uint32_t base = sld(&a.row_base[r0]);
+      flt = (q0 & 8) != 0;
+      sp.t0 = base + (q0 >> 4);
+      const int64_t st = sp.n == 1 ? 1 : (int64_t)(base + (q1 >> 4)) - (int64_t)sp.t0;
+      ok = st >= 1 && (int64_t)sp.t0 >= a.start &&
+           (int64_t)sp.t0 + (int64_t)(sp.n - 1) * st <= 0xFFFFFFFFll;  // (no seek inside the span)
+      sp.step = (uint32_t)st;
+      sp.kk = (uint32_t)((I + st - 1) / st);
+      sp.dkk.init(sp.kk);
+      nb = (sp.n + sp.kk - 1) / sp.kk;
+      sp.eo = sld(&a.e_off[k]);
+      sp.cap = (uint32_t)sld(&a.sp_cap[s]);
+      ok = ok && nb <= sp.cap;
+    }
+  }
+  if (ok) {  // this wave's rows: a contiguous piece that starts at a bucket head
+    const uint64_t rp = (r1 - r0 + wps - 1) >> wps_log2;
+    ra = min(r0 + piece * rp, r1);
+    rb = min(ra + rp, r1);
+    if (ra < rb && piece > 0) ok = sld(&a.row_cell0[ra]) % sp.kk == 0;
+    if (ok && ra < rb) ok = reg_rows_ok(a, sp, ra, rb, W);
+  }
+  if (ok && ra < rb) {
+    bool fail;
+    if (W == 8)
+      fail = flt ? reg_piece<AGG, 8, true>(a, sp, ra, rb, ncells, s_v[wib], s_bk[wib])
+                 : reg_piece<AGG, 8, false>(a, sp, ra, rb, ncells, s_v[wib], s_bk[wib]);
+    else
+      fail = flt ? reg_piece<AGG, 4, true>(a, sp, ra, rb, ncells, s_v[wib], s_bk[wib])
+                 : reg_piece<AGG, 4, false>(a, sp, ra, rb, ncells, s_v[wib], s_bk[wib]);
+    ok = !fail;
+  }
+  if (wps > 1) {  // the span's pieces agree (every wave of the block reaches this)
+    if (lane == 0) s_bad[wib] = ok ? 0u : 1u;
+    __syncthreads();
+    uint32_t any = 0;
+    for (uint32_t i = 0; i < wps; i++) any |= s_bad[(wib & ~(wps - 1)) + i];
+    ok = any == 0;
+  }
+  if (k >= a.n_kept) return;
+  if (!ok) {
+    if (piece == 0 && lane == 0) {  // the whole span to k_ds_spans
+      const uint32_t sg = blockIdx.x % g.nseg;
+      g.list[(uint64_t)sg * g.seg_cap + atomicAdd(&g.list_count[sg], 1u)] = k;
+    }
+    return;
+  }
+  if (piece == 0 && lane == 0) {
+    a.e_len[k] = nb;
+    a.e_bad[k] = -1;
+    if (flt) {
+      if (!a.gflags[0]) atomicOr(&a.gflags[0], 1u);
+      if (!a.rate) {  // F*: the first bucket's ts + 1
+        const int64_t fs = (int64_t)sp.t0 + (int64_t)((uint64_t)sp.step * (min(sp.kk, sp.n) - 1) / 2) + 1;
+        if ((unsigned long long)fs > *(volatile unsigned long long*)a.fstar) atomicMax(a.fstar, (unsigned long long)fs);
+      }
+    } else if (!a.gflags[1]) {
+      atomicOr(&a.gflags[1], 1u);
+    }
+  }
+  if (g.bitmap) {  // G: the span's bucket timestamps <= end (rate: from the second)
+    for (uint32_t b = piece * WAVE + lane; b < nb; b += WAVE * wps) {
+      if (g.rate && b == 0) continue;
+      const uint32_t sb = b * sp.kk, m = min(sb + sp.kk, sp.n) - sb;
+      const int64_t t = (int64_t)sp.t0 + (int64_t)sb * sp.step + (int64_t)((uint64_t)sp.step * (m - 1) / 2);
+      if (t > g.hi || t < g.lo) continue;
+      const uint64_t off = (uint64_t)(t - g.lo);
+      const uint32_t bit = 1u << (off & 31);
+      uint32_t* w = &g.bitmap[off >> 5];
+      if (!(*w & bit)) atomicOr(w, bit);
+    }
+  }
+}
+
+}  // namespace tsdb

@@ -14,12 +14,13 @@ pytestmark = pytest.mark.gpu
 AGGS = [0, 1, 2, 3, 4]
 
 
-@pytest.fixture(autouse=True, params=["auto", "general", "fast", "chunks", "direct"])
+@pytest.fixture(autouse=True, params=["auto", "general", "fast", "chunks", "spans", "direct"])
 def decode_path(request, monkeypatch):
-    """Run every case through the chunk-parallel downsampler, the streaming
-    decode kernel (each with its fallback queue), the general per-span
-    kernel, and (no downsampling) the direct path of k_direct.hip forced on
-    whatever the row sizes."""
+    """Run every case through the streaming downsamplers (chunks: the
+    constant-step k_ds_reg first, then the chain-proved k_ds_spans; spans:
+    k_ds_spans alone), the streaming decode kernel (each with its fallback
+    queue), the general per-span kernel, and (no downsampling) the direct
+    path of k_direct.hip forced on whatever the row sizes."""
     if request.param != "auto":
         monkeypatch.setenv("TSDBHIP_DECODE", request.param)
     else:
