@@ -344,16 +344,19 @@ def bench_c5(args):
     row_v = np.diff(b.row_val_off.astype(np.int64))
     n_cx = int(out.n_complex)
     alg_all = int(row_q.sum() + row_v.sum() + ql.sum() + vl.sum())
-    # k_compact_quals + k_compact_vals move every row's qualifier and value
-    # bytes (in and out); classification, the LDS row kernel (non-plain
-    # rows) and the complex kernels are the rest of the call (call_achieved)
-    alg_rows = alg_all
     cells = int(b.kv_qual_len.astype(np.int64).sum() // 2)
+    # the roofline is the whole call's: every kernel of tsdbhip_compact_rows
+    # (qualifier / value copies, classification, the LDS row kernel for the
+    # non-plain rows, complex rows, duplicate decisions) between the call's
+    # first and last HIP event (the copies alone overstate it)
+    call_ms = float(np.mean(tot))
     hot_ms = float(np.mean(hot))
-    achieved = alg_rows / (hot_ms * 1e-3) / 1e9
-    kname = ("k_compact_tiles" if os.environ.get("TSDBHIP_COMPACT") == "tiles"
-             else "k_compact_quals+k_compact_vals")
-    traffic, traffic_src = pmc_traffic("c5", kname, 1)
+    achieved = alg_all / (call_ms * 1e-3) / 1e9
+    kname = "tsdbhip_compact_rows (whole call)"
+    call_kernels = ("k_compact_tiles+k_compact_complex+k_compact_dups" if os.environ.get("TSDBHIP_COMPACT") == "tiles"
+                    else "k_compact_quals+k_compact_classify+k_compact_vals+k_compact_rows+k_compact_complex"
+                         "+k_compact_dups")
+    traffic, traffic_src = pmc_traffic("c5", call_kernels, 1)
     res = {
         "metric": "raw cells/sec compacted (CompactionQueue.compact) + % HBM roofline, 1 MI355X",
         "value": cells / (elapsed / args.steps), "unit": "raw cells/s", "n_gpus": 1, "steps": args.steps,
@@ -365,11 +368,11 @@ def bench_c5(args):
                    "rows_complex": n_cx, "status_counts": np.bincount(st, minlength=6).tolist()},
         "roofline": {"bound": "hbm", "kernel": kname, "achieved": achieved, "peak": HBM_PEAK_GBS,
                      "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
-                     "traffic_source": traffic_src, "alg_bytes_per_launch": alg_rows, "kernel_ms": hot_ms,
+                     "traffic_source": traffic_src, "traffic_kernels": call_kernels,
+                     "alg_bytes_per_launch": alg_all, "kernel_ms": call_ms,
+                     "copy_kernels_ms": hot_ms, "copy_kernels_achieved": alg_all / (hot_ms * 1e-3) / 1e9,
                      "complex_kernel_ms": float(np.mean(cx)), "classify_kernel_ms": float(np.mean(cls)),
-                     "rows_kernel_ms": float(np.mean(rows_k)), "step_device_ms": float(np.mean(tot)),
-                     "call_alg_bytes": alg_all,
-                     "call_achieved": alg_all / (float(np.mean(tot)) * 1e-3) / 1e9},
+                     "rows_kernel_ms": float(np.mean(rows_k))},
     }
     if not args.no_cpu:
         res["cpu_baseline"] = cpu_baseline_c5(b, args.cpu_seconds)
@@ -761,6 +764,10 @@ def main():
             rl["valu_source"] = vsrc
             rl["achieved"] = vi / (hot * 1e-3) if vi else None
             rl["frac"] = rl["achieved"] / VALU_PEAK_WIPS if vi else None
+        # which variants ran (tsdbhip_timing.paths): the aligned-group reduction
+        # (k_ds_reg's block partials instead of E + k_reduce) or its rerun
+        res["paths"] = {"aligned_group": bool(tsum.paths & _abi.PATH_ALIGNED_GROUP),
+                        "aligned_rerun": bool(tsum.paths & _abi.PATH_ALIGNED_RERUN)}
         if world > 1 or rehearse:  # collective launches per call on this rank (RCCL groups)
             res["collectives_per_call"] = tsum.n_collectives / ncalls
         if rehearse:

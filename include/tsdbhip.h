@@ -49,7 +49,7 @@
 extern "C" {
 #endif
 
-#define TSDBHIP_ABI_VERSION 4
+#define TSDBHIP_ABI_VERSION 5
 
 /* ---- return codes ---------------------------------------------------- */
 #define TSDBHIP_OK               0
@@ -79,7 +79,7 @@ extern "C" {
 
 /* tsdbhip_timing.hot_kernel */
 #define TSDBHIP_HOT_NONE        0
-#define TSDBHIP_HOT_DS_CHUNKS   1 /* k_ds_spans: streaming decode+downsample */
+#define TSDBHIP_HOT_DS_CHUNKS   1 /* k_ds_reg (+ k_ds_spans): streaming decode+downsample */
 #define TSDBHIP_HOT_DECODE_FAST 2 /* streaming per-span decode(+downsample) */
 #define TSDBHIP_HOT_DECODE_GEN  3 /* general per-span decode(+downsample)   */
 #define TSDBHIP_HOT_REDUCE_DIRECT 5 /* k_reduce over direct spans (no-downsampling path) */
@@ -163,7 +163,14 @@ typedef struct tsdbhip_timing {
   uint64_t alg_bytes;       /* SURVEY §8(d) algorithmic bytes of the call   */
   uint64_t n_grid;          /* |G|                                           */
   uint64_t n_emitted;       /* Σ|E_s| (points after downsampling)           */
+  uint32_t paths;           /* TSDBHIP_PATH_* bits: which variants ran (ABI v5) */
+  uint32_t reserved;
 } tsdbhip_timing;
+/* tsdbhip_timing.paths */
+#define TSDBHIP_PATH_ALIGNED_GROUP 1u  /* k_ds_reg's aligned-group reduction
+                                          stood for E + the reduce            */
+#define TSDBHIP_PATH_ALIGNED_RERUN 2u  /* it was tried, a span fell outside the
+                                          group: E rewritten, usual reduce    */
 
 /* ---- row compaction (CompactionQueue.compact) -------------------------- */
 /*

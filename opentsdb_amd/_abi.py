@@ -6,7 +6,9 @@ and the test harness.
 """
 import ctypes as C
 
-ABI_VERSION = 4
+ABI_VERSION = 5
+PATH_ALIGNED_GROUP = 1  # tsdbhip_timing.paths (include/tsdbhip.h)
+PATH_ALIGNED_RERUN = 2
 
 OK = 0
 E_ILLEGAL_DATA = -1
@@ -88,7 +90,7 @@ class SgOut(C.Structure):
 
 
 HOT_NONE, HOT_DS_CHUNKS, HOT_DECODE_FAST, HOT_DECODE_GEN = 0, 1, 2, 3
-HOT_NAMES = {1: "k_ds_spans", 2: "k_decode_fast", 3: "k_decode_general", 4: "k_compact_quals+k_compact_vals", 5: "k_reduce"}
+HOT_NAMES = {1: "k_ds_reg+k_ds_spans", 2: "k_decode_fast", 3: "k_decode_general", 4: "k_compact_quals+k_compact_vals", 5: "k_reduce"}
 
 
 class Timing(C.Structure):
@@ -105,6 +107,8 @@ class Timing(C.Structure):
         ("alg_bytes", C.c_uint64),
         ("n_grid", C.c_uint64),
         ("n_emitted", C.c_uint64),
+        ("paths", C.c_uint32),
+        ("reserved", C.c_uint32),
     ]
 
 

@@ -229,6 +229,7 @@ static void timing_add(tsdbhip_ctx* c, const tsdbhip_timing& t) {  // (c->mu hel
   c->sum.alg_bytes += t.alg_bytes;
   c->sum.n_grid += t.n_grid;
   c->sum.n_emitted += t.n_emitted;
+  c->sum.paths |= t.paths;
   c->n_sum++;
 }
 
@@ -642,11 +643,19 @@ struct LaunchFastDsInl {
 // integer, then float); leaves the spans neither took in fa.span_list for
 // k_decode_fast.
 constexpr uint32_t CK_NSEG = 64;
+// an aligned-group reduction of this call (k_ds_reg.hip FapArgs) and what its
+// rerun needs
+struct FapPlan {
+  FapArgs a = {};
+  SpanDsArgs g = {};
+  unsigned blocks = 0, pad = 0;
+};
 struct LaunchChunks {
   template <int AGG>
   static void run(Slot* ctx, const DecodeArgs& da, DecodeArgs& fa, const uint32_t* ncells,
                   const uint32_t* vlen, SpanDsArgs g, uint64_t n_rows, bool use_reg = true,
-                  uint32_t* zeroed2 = nullptr, uint32_t* zeroed_seg = nullptr, uint32_t* zeroed_seg2 = nullptr) {
+                  uint32_t* zeroed2 = nullptr, uint32_t* zeroed_seg = nullptr, uint32_t* zeroed_seg2 = nullptr,
+                  FapPlan* fp = nullptr) {
     if (AGG == 4) return;  // dev: Welford is order-dependent, serial kernels only
     hipStream_t st = ctx->stream;
     const uint32_t n_kept = da.n_kept;
@@ -663,36 +672,56 @@ struct LaunchChunks {
     gr.in_list = nullptr;
     gr.in_count = nullptr;
     gr.in_nseg = gr.in_seg_cap = 0;
-    // k_ds_spans<integer> over k_ds_reg's leftovers (usually few: a capped,
-    // grid-stride launch), its own leftovers in 64 segments (block % 64)
-    const unsigned iblocks = std::min(grid_for(n_kept, 4, 1u << 20), use_reg ? 4096u : (1u << 20));
-    g.nseg = CK_NSEG;
-    g.seg_cap = 4 * ((iblocks + CK_NSEG - 1) / CK_NSEG) * ((n_kept + 4 * iblocks - 1) / (4 * iblocks));
-    g.list = scratch<uint32_t>(ctx, "ck_list", (uint64_t)g.seg_cap * CK_NSEG);
-    g.list_count = zeroed_seg ? zeroed_seg : scratch<uint32_t>(ctx, "ck_seg_count", CK_NSEG, true);
-    g.in_list = use_reg ? gr.list : nullptr;  // (!use_reg: every kept span, the full grid)
+    // k_ds_spans (integer and float spans, one launch) over k_ds_reg's
+    // leftovers (usually few: a capped, grid-stride launch), or over every
+    // kept span without k_ds_reg; its own leftovers to k_decode_fast
+    const unsigned iblocks = use_reg ? std::min(grid_for(n_kept, 4, 1u << 20), 4096u) : grid_for(n_kept, 4, 1u << 20);
+    g.in_list = use_reg ? gr.list : nullptr;
     g.in_count = use_reg ? gr.list_count : nullptr;
     g.in_nseg = use_reg ? gr.nseg : 0;
     g.in_seg_cap = use_reg ? gr.seg_cap : 0;
-    // then float spans over the ones left
-    SpanDsArgs gf = g;
-    gf.in_list = g.list;
-    gf.in_count = g.list_count;
-    gf.in_nseg = g.nseg;
-    gf.in_seg_cap = g.seg_cap;
-    gf.nseg = gf.seg_cap = 0;
-    gf.list = scratch<uint32_t>(ctx, "ck_list2", n_kept);
-    gf.list_count = zeroed2 ? zeroed2 + 1 : scratch<uint32_t>(ctx, "ck_list2_count", 1, true);
+    g.nseg = g.seg_cap = 0;
+    g.list = scratch<uint32_t>(ctx, "ck_list2", n_kept);
+    g.list_count = zeroed2 ? zeroed2 + 1 : scratch<uint32_t>(ctx, "ck_list2_count", 1, true);
     HIPCHK(hipEventRecord(ctx->ev[8], st));
-    if (use_reg) hipLaunchKernelGGL((k_ds_reg<AGG>), dim3(rblocks), dim3(256), 0, st, da, gr, ncells, vlen, wps_log2);
-    hipLaunchKernelGGL((k_ds_spans<AGG, false>), dim3(use_reg ? iblocks : grid_for(n_kept, 4, 1u << 20)), dim3(256), 0,
-                       st, da, g, ncells, vlen);
-    hipLaunchKernelGGL((k_ds_spans<AGG, true>), dim3(std::min(grid_for(n_kept, 4, 1u << 20), 1024u)), dim3(256), 0,
-                       st, da, gf, ncells, vlen);
+    // one wave per span (long rows, C3*): 4 resident blocks per CU (LDS
+    // padding) measured faster than the 6 its registers allow; split spans
+    // (C2) prefer the full occupancy
+    static const int pad_env = getenv("TSDBHIP_REG_LDS") ? atoi(getenv("TSDBHIP_REG_LDS")) : -1;
+    const unsigned pad = pad_env >= 0 ? (unsigned)pad_env : (wps_log2 == 0 ? 22000u : 0u);
+    // the aligned-group reduction (one wave per span): a partial row per block
+    FapArgs fa0 = {};
+    fa0.op = -1;
+    if (fp && (!use_reg || wps_log2 != 0)) fp->a.op = -1;
+    if (fp && fp->a.op >= 0) {
+      fp->a.nrows = rblocks;
+      fp->a.part = scratch<int64_t>(ctx, "fap_part", (uint64_t)rblocks * WAVE);
+      fp->g = gr;  // (the rerun after a broken FAP pass: the same launch, E only)
+      fp->blocks = rblocks;
+      fp->pad = pad;
+    }
+    if (use_reg)
+      hipLaunchKernelGGL((k_ds_reg<AGG>), dim3(rblocks), dim3(256), pad, st, da, gr, ncells, vlen, wps_log2,
+                         fp ? fp->a : fa0);
+    hipLaunchKernelGGL((k_ds_spans<AGG, 2>), dim3(iblocks), dim3(256), 0, st, da, g, ncells, vlen);
     HIPCHK(hipEventRecord(ctx->ev[9], st));
     ctx->hot_kernel = TSDBHIP_HOT_DS_CHUNKS;
-    fa.span_list = gf.list;
-    fa.span_count = gf.list_count;
+    fa.span_list = g.list;
+    fa.span_count = g.list_count;
+  }
+};
+
+// the rerun of k_ds_reg after a broken aligned-group pass: E of the spans it
+// takes (the FAP members), no list, no marks, no flags
+struct LaunchRegRerun {
+  template <int AGG>
+  static void run(Slot* ctx, const DecodeArgs& da, const FapPlan& fp, const uint32_t* ncells, const uint32_t* vlen) {
+    if (AGG == 4) return;
+    FapArgs a = fp.a;
+    a.op = -1;
+    a.rewrite = 1;
+    hipLaunchKernelGGL((k_ds_reg<AGG>), dim3(fp.blocks), dim3(256), fp.pad, ctx->stream, da, fp.g, ncells, vlen, 0u,
+                       a);
   }
 };
 
@@ -837,12 +866,16 @@ struct Small {
   uint64_t n_kept;
   uint64_t e_total;
   uint64_t T;
-  unsigned long long bound[2];  // [min first ts, max last ts] of the kept spans
+  unsigned long long bound[4];  // [min first ts, max last ts, max first ts, min last ts] of the kept spans
   uint32_t cnt[6];  // list counters, zero at the start of a call (no memsets):
                     // [0] assembly queue, [1] decode fallback, [2] direct list,
                     // [3] [4] k_ds_spans int / float leftovers
   uint32_t seg[CK_NSEG];  // k_ds_spans integer leftovers, per segment
   uint32_t seg2[CK_NSEG];  // k_ds_reg leftovers, per segment
+  // k_ds_reg's aligned-group reduction (FAP): the spans' class keys
+  // (t0 << 32 | n, step) as [min, max, min, max], and a span outside it
+  unsigned long long fap_key[4];
+  uint32_t fap_broken, fap_pad;
   // sharded calls: two 64-bit hashes of the rank's grid bitmap (k_grid_popc /
   // k_grid_scan_blocks), and the agreed header words of the one collective
   // after the local grids (XH_*: MIN, or complemented MAX, over the ranks)
@@ -861,6 +894,9 @@ static Small small_init() {
   init.bad_at = ~0ull;
   init.bound[0] = ~0ull;
   init.bound[1] = 0;
+  init.bound[2] = 0;
+  init.bound[3] = ~0ull;
+  init.fap_key[0] = init.fap_key[2] = ~0ull;
   return init;
 }
 // Several MIN / MAX agreements on call-state fields as one MIN allreduce of a
@@ -1163,6 +1199,21 @@ static int spangroup_run(Slot* ctx, const tsdbhip_sg_desc* d, tsdbhip_sg_out* ou
                     (int)bm_clean, (unsigned long long)nwords);
   }
 
+  // ---- aligned-group reduction (k_ds_reg.hip FapArgs): tried when every
+  // kept span has the same first and last timestamp (Small.bound), the group
+  // downsamples, and the aggregation is exact integer (no rate, no dev) ----
+  FapPlan fap;
+  fap.a.op = -1;
+  static const bool fap_off = getenv("TSDBHIP_FAP") && !strcmp(getenv("TSDBHIP_FAP"), "0");  // (tests / A/B)
+  if (!fap_off && interval > 0 && !rate && ds_agg <= 3 && agg <= 3 && !(sharded && exact) && n_kept > 0 &&
+      h.bound[0] == h.bound[2] && h.bound[1] == h.bound[3] && h.bound[1] - h.bound[0] <= 62ull * (uint64_t)interval) {
+    // (at most 64 buckets a span: a partial row holds them)
+    fap.a.op = agg == TSDBHIP_AGG_MIN ? 1 : (agg == TSDBHIP_AGG_MAX ? 2 : 0);
+    fap.a.key = sm->fap_key;
+    fap.a.broken = &sm->fap_broken;
+  }
+  bool fap_ran = false;
+
   // ---- decode (+ downsample) ----
   const uint64_t e_total = h.e_total;
   uint32_t* e_ts = scratch<uint32_t>(ctx, "e_ts", e_total);
@@ -1259,8 +1310,10 @@ static int spangroup_run(Slot* ctx, const tsdbhip_sg_desc* d, tsdbhip_sg_out* ou
         g.lo = lo;
         g.hi = hi;
         g.rate = rate;
+        if (!bitmap) fap.a.op = -1;
         launch_agg<LaunchChunks>(ds_agg, ctx, da, fa, row_ncells, row_val_len, g, R, use_reg, &sm->cnt[3], sm->seg,
-                                 sm->seg2);
+                                 sm->seg2, &fap);
+        fap_ran = fap.a.op >= 0;
         chunk_marked = bitmap != nullptr && fa.span_list != nullptr;
       }
       if (chunk_marked) {
@@ -1329,6 +1382,7 @@ static int spangroup_run(Slot* ctx, const tsdbhip_sg_desc* d, tsdbhip_sg_out* ou
                          dim3(256), 0, st, ga);
     grid_ranks(!sharded, sharded);
   }
+  bool grids_agreed = true;  // (sharded: every rank's local grid is the global one)
   if (sharded) {
     // One collective: the error, the int / float flags and F* (agreed in
     // place), the input count (sum), and each rank's grid geometry and bitmap
@@ -1353,6 +1407,7 @@ static int spangroup_run(Slot* ctx, const tsdbhip_sg_desc* d, tsdbhip_sg_out* ou
     const bool agreed = all_empty || (h.xh[XH_LO] == (uint64_t)lo && ghi == hi && !empty_grid &&
                                       h.xh[XH_H1MIN] == ~h.xh[XH_H1MAX] && h.xh[XH_H2MIN] == ~h.xh[XH_H2MAX] &&
                                       h.xh[XH_H1MIN] == h.ghash[0] && h.xh[XH_H2MIN] == h.ghash[1]);
+    grids_agreed = agreed;
     if (!agreed) {
       // the global geometry: this rank's bitmap shifted onto [glo, ghi] (a
       // separate buffer; the local one is cleared), then OR-ed over the ranks
@@ -1414,6 +1469,14 @@ static int spangroup_run(Slot* ctx, const tsdbhip_sg_desc* d, tsdbhip_sg_out* ou
   }
   const bool anyf = h.gflags[0] != 0, anyi = h.gflags[1] != 0;
   const uint64_t fstar = h.fstar;
+  // the aligned-group partials stand for the reduce iff every kept span was in
+  // the one class (no span outside it, one key) and G is the class's bucket
+  // sequence (sharded: the local grid is the global one); else the members'
+  // E is written now by a rerun of k_ds_reg
+  const bool fap_use = fap_ran && !h.fap_broken && h.fap_key[0] == h.fap_key[1] && h.fap_key[2] == h.fap_key[3] &&
+                       !anyf && T > 0 && T <= WAVE && grids_agreed;
+  if (fap_ran && !fap_use) launch_agg<LaunchRegRerun>(ds_agg, ctx, da, fap, row_ncells, row_val_len);
+  tm.paths |= fap_use ? TSDBHIP_PATH_ALIGNED_GROUP : (fap_ran ? TSDBHIP_PATH_ALIGNED_RERUN : 0u);
   HIPCHK(hipEventRecord(ctx->ev[4], st));
   tm.n_grid = T;
   // lazy error index for illegal cells (every span's E and e_bad are final
@@ -1425,7 +1488,8 @@ static int spangroup_run(Slot* ctx, const tsdbhip_sg_desc* d, tsdbhip_sg_out* ou
   // (k_call_end then runs as one block: its bitmap clearing must follow the
   // error index's grid ranks)
   const bool bad_at_end = !sharded && n_kept <= 4096 && T <= 65536;
-  if (n_kept && !bad_at_end)
+  // (an aligned group holds no E span, hence no bad cell)
+  if (n_kept && !bad_at_end && !fap_use)
     hipLaunchKernelGGL(k_bad_index, dim3(grid_for(n_kept, 256)), dim3(256), 0, st, bad, &sm->bad_at);
 
   // ---- output block: [Small snapshot | ts T | bits T | is_int T], written
@@ -1529,8 +1593,37 @@ static int spangroup_run(Slot* ctx, const tsdbhip_sg_desc* d, tsdbhip_sg_out* ou
       dispatch_reduce(ctx, agg, mode, rate, blocks, r, f, n_chunks >= 64, finalize);
       return r;
     };
+    // the aligned group: its block partials reduced into the 1-chunk layout
+    auto fap_reduce = [&](bool finalize) {
+      ReduceArgs r;
+      std::memset(&r, 0, sizeof r);
+      r.T = T;
+      r.n_chunks = 1;
+      r.n_kept = n_kept;
+      partials(r, "p_", T);
+      const uint32_t nrows = fap.a.nrows;
+      // (16-wave blocks, >= 128 rows each, at most 256 of them)
+      const unsigned g1 = std::max(1u, std::min(256u, nrows / 128));
+      int64_t* tmp = scratch<int64_t>(ctx, "fap_tmp", (uint64_t)g1 * WAVE);
+      auto go = [&](auto opc) {
+        constexpr int OP = decltype(opc)::value;
+        hipLaunchKernelGGL((k_fap_rows<OP>), dim3(g1), dim3(1024), 0, st, (const int64_t*)fap.a.part, nrows, tmp);
+        hipLaunchKernelGGL((k_fap_final<OP>), dim3(1), dim3(1024), 0, st, (const int64_t*)tmp, g1, T, n_kept, r.p_i,
+                           r.p_cnt, r.p_flag);
+      };
+      if (fap.a.op == 1) go(std::integral_constant<int, 1>());
+      else if (fap.a.op == 2) go(std::integral_constant<int, 2>());
+      else go(std::integral_constant<int, 0>());
+      if (finalize) {
+        FinalArgs f = fin;
+        f.n_chunks = 1;
+        dispatch_final(ctx, agg, mode, rate, r, f);
+      }
+      return r;
+    };
     if (!sharded) {
-      run_reduce(seq, true, nullptr);
+      if (fap_use) fap_reduce(true);
+      else run_reduce(seq, true, nullptr);
     } else {
       const int nr = X->nranks, rk = X->rank;
       ReduceArgs src;  // per-t partials the finalize merges ([n_src][T])
@@ -1556,7 +1649,7 @@ static int spangroup_run(Slot* ctx, const tsdbhip_sg_desc* d, tsdbhip_sg_out* ou
         src = S;
       } else {
         // this rank's chunks combined in order into one slot per t
-        ReduceArgs loc = run_reduce(false, false, nullptr);
+        ReduceArgs loc = fap_use ? fap_reduce(false) : run_reduce(false, false, nullptr);
         if (mode == MODE_INT && agg != TSDBHIP_AGG_DEV) {
           // exact integer partials: one allreduce per field (wrapping u64
           // sum, i64 min / max, count sum), no ordering needed

@@ -474,11 +474,10 @@ DEVI bool ds_span(const DecodeArgs& a, DsState& st, uint64_t eo, uint32_t cap, u
   return ballot(bad) != 0;
 }
 
-// One wave per kept span.
-// FLT: spans whose cells are all float (double buckets); the integer
-// instantiation runs over every kept span first, the float one over the
-// spans it left (g.in_list), so neither carries the other's branches.
-template <int AGG, bool FLT>
+// One wave per kept span (or per span of g.in_list). FLTM 0: integer spans,
+// 1: float spans (double buckets), 2: either, by the span's first cell (one
+// launch for k_ds_reg's few leftovers).
+template <int AGG, int FLTM>
 __global__ void __launch_bounds__(256) k_ds_spans(DecodeArgs a, SpanDsArgs g, const uint32_t* ncells,
                                                   const uint32_t* vlen) {
   __shared__ uint32_t s_pt[4][DCH];
@@ -519,6 +518,7 @@ __global__ void __launch_bounds__(256) k_ds_spans(DecodeArgs a, SpanDsArgs g, co
     // it and be aligned (checked here, so the chunk stream never stops at a
     // row boundary)
     uint32_t W = 0;
+    bool FLT = FLTM == 1;
     if (ok) {
       const uint32_t nc = sld(&ncells[r0]), vl = sld(&vlen[r0]);
       const uint32_t vb = nc > 1 ? vl - 1 : vl;
@@ -527,7 +527,11 @@ __global__ void __launch_bounds__(256) k_ds_spans(DecodeArgs a, SpanDsArgs g, co
       // the first cell's type picks the instantiation: the other one leaves
       // the span without streaming it (float spans pass through the integer
       // kernel first)
-      if (ok) ok = ((sld_u8(a.qual + sld(&a.row_qual_off[r0]) + 1) & 8u) != 0) == FLT;
+      if (ok) {
+        const bool f0 = (sld_u8(a.qual + sld(&a.row_qual_off[r0]) + 1) & 8u) != 0;
+        if (FLTM == 2) FLT = f0;
+        ok = f0 == FLT;
+      }
     }
     if (ok && r1 - r0 == 1) {  // (one row: the usual hourly span)
       ok = sld_u8(&a.row_ok[r0]) != 0 && (sld(&a.row_qual_off[r0]) & 7) == 0 && (sld(&a.row_val_off[r0]) & 15) == 0;
@@ -548,8 +552,13 @@ __global__ void __launch_bounds__(256) k_ds_spans(DecodeArgs a, SpanDsArgs g, co
     const uint32_t cap = (uint32_t)sld(&a.sp_cap[s]);
     DsState st = {};
     if (ok) {
-      const bool fail = W == 8 ? ds_span<AGG, 8, FLT>(a, st, eo, cap, r0, r1, ncells, s_pt[wib], s_v[wib], s_bk[wib])
-                               : ds_span<AGG, 4, FLT>(a, st, eo, cap, r0, r1, ncells, s_pt[wib], s_v[wib], s_bk[wib]);
+      bool fail;
+      if (FLTM != 1 && !FLT)
+        fail = W == 8 ? ds_span<AGG, 8, false>(a, st, eo, cap, r0, r1, ncells, s_pt[wib], s_v[wib], s_bk[wib])
+                      : ds_span<AGG, 4, false>(a, st, eo, cap, r0, r1, ncells, s_pt[wib], s_v[wib], s_bk[wib]);
+      else
+        fail = W == 8 ? ds_span<AGG, 8, true>(a, st, eo, cap, r0, r1, ncells, s_pt[wib], s_v[wib], s_bk[wib])
+                      : ds_span<AGG, 4, true>(a, st, eo, cap, r0, r1, ncells, s_pt[wib], s_v[wib], s_bk[wib]);
       ok = !fail;
     }
     uint32_t ts_last = 0, n_last = 0;  // the final flush (one lane per bucket)

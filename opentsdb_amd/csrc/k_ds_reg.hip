@@ -60,10 +60,26 @@ struct RegSpan {
 // buffer (their values over their cells; timestamps by formula): one lane per
 // bucket, so the avg divisions (Span.java:399-420 with Aggregators.Avg)
 // leave the chunk loop.
+// fop >= 0 (an aligned group, FapArgs): integer bucket values go into the
+// block's partial per bucket index instead (the cross-series aggregator's
+// combine: 0 wrapping add, 1 min, 2 max), no E.
 template <int AGG, bool FLT>
-DEVI void reg_flush(const DecodeArgs& a, const RegSpan& sp, const int64_t* BK, uint32_t b0, uint32_t cnt) {
+DEVI void reg_flush(const DecodeArgs& a, const RegSpan& sp, const int64_t* BK, uint32_t b0, uint32_t cnt, int fop,
+                    int64_t* part) {
   wave_lds_sync();
   const uint32_t i = lane_id();
+  if (!FLT && fop >= 0) {
+    if (i < cnt) {
+      const uint32_t b = b0 + i;
+      const uint32_t sb = b * sp.kk, m = min(sb + sp.kk, sp.n) - sb;
+      const int64_t v = AGG == 3 ? ldiv64_32(BK[i], m) : BK[i];
+      if (fop == 0) atomicAdd((unsigned long long*)&part[b], (unsigned long long)v);
+      else if (fop == 1) atomicMin((long long*)&part[b], (long long)v);
+      else atomicMax((long long*)&part[b], (long long)v);
+    }
+    wave_lds_sync();
+    return;
+  }
   if (i < cnt) {
     const uint32_t b = b0 + i;
     const uint32_t sb = b * sp.kk, m = min(sb + sp.kk, sp.n) - sb;
@@ -85,7 +101,7 @@ DEVI void reg_flush(const DecodeArgs& a, const RegSpan& sp, const int64_t* BK, u
 // caller checked the rows (reg_rows_ok) and that ra starts a bucket.
 template <int AGG, int W, bool FLT>
 DEVI bool reg_piece(const DecodeArgs& a, const RegSpan& sp, uint64_t ra, uint64_t rb, const uint32_t* ncells,
-                    uint64_t* L_v, int64_t* BK) {
+                    uint64_t* L_v, int64_t* BK, int fop, int64_t* part) {
   constexpr bool PREFIX = (AGG == 0 || AGG == 3) && !FLT;  // wrapping sums: prefix differences
   const int lane = lane_id();
   const uint32_t fl = (FLT ? 8u : 0u) | (uint32_t)(W - 1);
@@ -211,7 +227,7 @@ DEVI bool reg_piece(const DecodeArgs& a, const RegSpan& sp, uint64_t ra, uint64_
       const uint32_t pc = min(nclose - min(nclose, jb), (uint32_t)WAVE);
       if (pc) {
         if (b_lo + jb + pc - fbase > WAVE) {
-          reg_flush<AGG, FLT>(a, sp, BK, fbase, b_lo + jb - fbase);
+          reg_flush<AGG, FLT>(a, sp, BK, fbase, b_lo + jb - fbase, fop, part);
           fbase = b_lo + jb;
         }
         if (act && j < nclose) BK[b - fbase] = v;
@@ -241,7 +257,7 @@ DEVI bool reg_piece(const DecodeArgs& a, const RegSpan& sp, uint64_t ra, uint64_
   // piece does not start a bucket: the whole span is redone)
   bad |= bclosed != nb && ph != 0;
   if (ballot(bad) != 0) return true;
-  if (bclosed > fbase) reg_flush<AGG, FLT>(a, sp, BK, fbase, bclosed - fbase);
+  if (bclosed > fbase) reg_flush<AGG, FLT>(a, sp, BK, fbase, bclosed - fbase, fop, part);
   return false;
 }
 
@@ -268,19 +284,54 @@ DEVI bool reg_rows_ok(const DecodeArgs& a, const RegSpan& sp, uint64_t ra, uint6
   return ok;
 }
 
+// The aligned-group reduction (FAP, SURVEY.md §8(e)'s "skip the grid
+// exchange when all shards agree", taken one step further): when every kept
+// span of the group is a constant-step integer span with the same first ts,
+// cadence and length (C3*: series written in lockstep), they share one bucket
+// sequence, the union grid G is that sequence (bucket ts <= end), and every
+// span is active at every t of G (SpanGroup.java:510-608), so the
+// cross-series integer aggregate at G[b] is the combine of bucket b over the
+// spans (wrapping sum / min / max, exact in any order; avg divides the sum by
+// the span count in the finalize, Aggregators.java:76-180). Each block then
+// combines its spans' buckets in LDS and writes one partial row instead of
+// the spans' E; k_fap_rows / k_fap_final reduce the rows into the 1-chunk
+// partial layout k_reduce would write. Any span outside the class sets
+// `broken` and the host reruns k_ds_reg with `rewrite` (E for the spans it
+// takes, nothing else), then reduces as usual.
+struct FapArgs {
+  int32_t op;        // -1: off; else 0 wrapping add (sum, avg), 1 min, 2 max
+  int32_t rewrite;   // 1: the rerun after a broken FAP pass
+  int64_t* part;     // [gridDim.x][64] block partials per bucket index
+  unsigned long long* key;  // [4] Small.fap_key
+  uint32_t* broken;         // Small.fap_broken
+  uint32_t nrows;           // (host) partial rows written: the launch's blocks
+};
+
+DEVI int64_t fap_neutral(int op) { return op == 1 ? INT64_MAX : (op == 2 ? INT64_MIN : 0); }
+
 // Blocks of 4 waves; 1 << wps_log2 waves per span (a span's rows split into
-// that many contiguous pieces), 4 >> wps_log2 spans per block.
+// that many contiguous pieces), 4 >> wps_log2 spans per block. (FAP: one wave
+// per span.)
 template <int AGG>
 __global__ void __launch_bounds__(256) k_ds_reg(DecodeArgs a, SpanDsArgs g, const uint32_t* ncells,
-                                                const uint32_t* vlen, uint32_t wps_log2) {
+                                                const uint32_t* vlen, uint32_t wps_log2, FapArgs fap) {
   __shared__ uint64_t s_v[4][DCH];
   __shared__ int64_t s_bk[4][WAVE];
+  __shared__ int64_t s_part[WAVE];
   __shared__ uint32_t s_bad[4];
+  // (dynamic LDS: padding that caps the resident blocks per CU, see LaunchChunks)
+  extern __shared__ uint8_t s_pad[];
+  if (threadIdx.x == 0 && a.n_kept == 0xFFFFFFFFu) s_pad[0] = 1;
   const int lane = lane_id();
   const uint32_t wib = ufl(threadIdx.x / WAVE);  // (uniform: the span prologue and the row walk use scalar loads)
   const uint32_t wps = 1u << wps_log2;
   const uint32_t piece = wib & (wps - 1);
   const uint32_t k = blockIdx.x * (4u >> wps_log2) + (wib >> wps_log2);
+  const int fop = fap.op;
+  if (fop >= 0) {
+    if (threadIdx.x < WAVE) s_part[threadIdx.x] = fap_neutral(fop);
+    __syncthreads();
+  }
   const int64_t I = a.interval;
   bool ok = k < a.n_kept && I > 0;
   uint32_t s = 0, W = 0, nb = 0;
@@ -325,14 +376,17 @@ __global__ void __launch_bounds__(256) k_ds_reg(DecodeArgs a, SpanDsArgs g, cons
     if (ra < rb && piece > 0) ok = sld(&a.row_cell0[ra]) % sp.kk == 0;
     if (ok && ra < rb) ok = reg_rows_ok(a, sp, ra, rb, W);
   }
+  // an aligned-group member: its buckets go to the block partial, not to E
+  const bool fused = fop >= 0 && ok && !flt && nb <= WAVE;
+  const int sfop = fused ? fop : -1;
   if (ok && ra < rb) {
     bool fail;
     if (W == 8)
-      fail = flt ? reg_piece<AGG, 8, true>(a, sp, ra, rb, ncells, s_v[wib], s_bk[wib])
-                 : reg_piece<AGG, 8, false>(a, sp, ra, rb, ncells, s_v[wib], s_bk[wib]);
+      fail = flt ? reg_piece<AGG, 8, true>(a, sp, ra, rb, ncells, s_v[wib], s_bk[wib], -1, s_part)
+                 : reg_piece<AGG, 8, false>(a, sp, ra, rb, ncells, s_v[wib], s_bk[wib], sfop, s_part);
     else
-      fail = flt ? reg_piece<AGG, 4, true>(a, sp, ra, rb, ncells, s_v[wib], s_bk[wib])
-                 : reg_piece<AGG, 4, false>(a, sp, ra, rb, ncells, s_v[wib], s_bk[wib]);
+      fail = flt ? reg_piece<AGG, 4, true>(a, sp, ra, rb, ncells, s_v[wib], s_bk[wib], -1, s_part)
+                 : reg_piece<AGG, 4, false>(a, sp, ra, rb, ncells, s_v[wib], s_bk[wib], sfop, s_part);
     ok = !fail;
   }
   if (wps > 1) {  // the span's pieces agree (every wave of the block reaches this)
@@ -342,38 +396,112 @@ __global__ void __launch_bounds__(256) k_ds_reg(DecodeArgs a, SpanDsArgs g, cons
     for (uint32_t i = 0; i < wps; i++) any |= s_bad[(wib & ~(wps - 1)) + i];
     ok = any == 0;
   }
-  if (k >= a.n_kept) return;
-  if (!ok) {
-    if (piece == 0 && lane == 0) {  // the whole span to k_ds_spans
-      const uint32_t sg = blockIdx.x % g.nseg;
-      g.list[(uint64_t)sg * g.seg_cap + atomicAdd(&g.list_count[sg], 1u)] = k;
+  if (fop >= 0 && k < a.n_kept && lane == 0) {  // the group's class: one key, no span outside it
+    if (!(ok && fused)) {
+      if (!*(volatile uint32_t*)fap.broken) atomicOr(fap.broken, 1u);
+    } else {
+      const unsigned long long k1 = ((unsigned long long)sp.t0 << 32) | sp.n, k2 = sp.step;
+      volatile unsigned long long* kv = fap.key;
+      if (k1 < kv[0]) atomicMin(&fap.key[0], k1);
+      if (k1 > kv[1]) atomicMax(&fap.key[1], k1);
+      if (k2 < kv[2]) atomicMin(&fap.key[2], k2);
+      if (k2 > kv[3]) atomicMax(&fap.key[3], k2);
     }
-    return;
   }
-  if (piece == 0 && lane == 0) {
-    a.e_len[k] = nb;
-    a.e_bad[k] = -1;
-    if (flt) {
-      if (!a.gflags[0]) atomicOr(&a.gflags[0], 1u);
-      if (!a.rate) {  // F*: the first bucket's ts + 1
-        const int64_t fs = (int64_t)sp.t0 + (int64_t)((uint64_t)sp.step * (min(sp.kk, sp.n) - 1) / 2) + 1;
-        if ((unsigned long long)fs > *(volatile unsigned long long*)a.fstar) atomicMax(a.fstar, (unsigned long long)fs);
+  if (k < a.n_kept) {
+    if (!ok) {
+      if (piece == 0 && lane == 0 && !fap.rewrite) {  // the whole span to k_ds_spans
+        const uint32_t sg = blockIdx.x % g.nseg;
+        g.list[(uint64_t)sg * g.seg_cap + atomicAdd(&g.list_count[sg], 1u)] = k;
       }
-    } else if (!a.gflags[1]) {
-      atomicOr(&a.gflags[1], 1u);
+    } else if (!fap.rewrite) {
+      if (piece == 0 && lane == 0) {
+        a.e_len[k] = nb;
+        a.e_bad[k] = -1;
+        if (flt) {
+          if (!a.gflags[0]) atomicOr(&a.gflags[0], 1u);
+          if (!a.rate) {  // F*: the first bucket's ts + 1
+            const int64_t fs = (int64_t)sp.t0 + (int64_t)((uint64_t)sp.step * (min(sp.kk, sp.n) - 1) / 2) + 1;
+            if ((unsigned long long)fs > *(volatile unsigned long long*)a.fstar)
+              atomicMax(a.fstar, (unsigned long long)fs);
+          }
+        } else if (!a.gflags[1]) {
+          atomicOr(&a.gflags[1], 1u);
+        }
+      }
+      if (g.bitmap) {  // G: the span's bucket timestamps <= end (rate: from the second)
+        for (uint32_t b = piece * WAVE + lane; b < nb; b += WAVE * wps) {
+          if (g.rate && b == 0) continue;
+          const uint32_t sb = b * sp.kk, m = min(sb + sp.kk, sp.n) - sb;
+          const int64_t t = (int64_t)sp.t0 + (int64_t)sb * sp.step + (int64_t)((uint64_t)sp.step * (m - 1) / 2);
+          if (t > g.hi || t < g.lo) continue;
+          const uint64_t off = (uint64_t)(t - g.lo);
+          const uint32_t bit = 1u << (off & 31);
+          uint32_t* w = &g.bitmap[off >> 5];
+          if (!(*w & bit)) atomicOr(w, bit);
+        }
+      }
     }
   }
-  if (g.bitmap) {  // G: the span's bucket timestamps <= end (rate: from the second)
-    for (uint32_t b = piece * WAVE + lane; b < nb; b += WAVE * wps) {
-      if (g.rate && b == 0) continue;
-      const uint32_t sb = b * sp.kk, m = min(sb + sp.kk, sp.n) - sb;
-      const int64_t t = (int64_t)sp.t0 + (int64_t)sb * sp.step + (int64_t)((uint64_t)sp.step * (m - 1) / 2);
-      if (t > g.hi || t < g.lo) continue;
-      const uint64_t off = (uint64_t)(t - g.lo);
-      const uint32_t bit = 1u << (off & 31);
-      uint32_t* w = &g.bitmap[off >> 5];
-      if (!(*w & bit)) atomicOr(w, bit);
-    }
+  if (fop >= 0) {  // the block's partial row
+    __syncthreads();
+    if (threadIdx.x < WAVE) fap.part[(uint64_t)blockIdx.x * WAVE + threadIdx.x] = s_part[threadIdx.x];
+  }
+}
+
+// FAP rows -> one 1-chunk partial per t: block b (16 waves) combines rows
+// b * 16 + w + i * 16 gridDim.x (a wave per 512-B row, four rows in flight),
+// then its waves in LDS, into tmp[b].
+template <int OP>
+DEVI int64_t fap_comb(int64_t x, int64_t y) {
+  if (OP == 0) return ladd(x, y);
+  if (OP == 1) return y < x ? y : x;
+  return y > x ? y : x;
+}
+template <int OP>
+DEVI int64_t fap_rows_wave(const int64_t* rows, uint32_t r, uint32_t stride, uint32_t nrows) {
+  const int lane = lane_id();
+  int64_t acc = fap_neutral(OP);
+  for (; r + 3 * stride < nrows; r += 4 * stride) {
+    const int64_t v0 = rows[(uint64_t)r * WAVE + lane], v1 = rows[(uint64_t)(r + stride) * WAVE + lane];
+    const int64_t v2 = rows[(uint64_t)(r + 2 * stride) * WAVE + lane], v3 = rows[(uint64_t)(r + 3 * stride) * WAVE + lane];
+    acc = fap_comb<OP>(fap_comb<OP>(acc, v0), fap_comb<OP>(fap_comb<OP>(v1, v2), v3));
+  }
+  for (; r < nrows; r += stride) acc = fap_comb<OP>(acc, rows[(uint64_t)r * WAVE + lane]);
+  return acc;
+}
+template <int OP>
+DEVI int64_t fap_block_comb(int64_t acc, int64_t (*s)[WAVE]) {
+  const int lane = lane_id();
+  const uint32_t w = threadIdx.x / WAVE;
+  s[w][lane] = acc;
+  __syncthreads();
+  if (w == 0)
+    for (uint32_t i = 1; i < 16; i++) acc = fap_comb<OP>(acc, s[i][lane]);
+  return acc;
+}
+template <int OP>
+__global__ void __launch_bounds__(1024) k_fap_rows(const int64_t* part, uint32_t nrows, int64_t* tmp) {
+  __shared__ int64_t s[16][WAVE];
+  const uint32_t w = threadIdx.x / WAVE;
+  int64_t acc = fap_rows_wave<OP>(part, blockIdx.x * 16 + w, gridDim.x * 16, nrows);
+  acc = fap_block_comb<OP>(acc, s);
+  if (w == 0) tmp[(uint64_t)blockIdx.x * WAVE + lane_id()] = acc;
+}
+// ... then the rows of tmp in one block; p_* as k_reduce's acc_store for a
+// 1-chunk MODE_INT reduce: every kept span active at every t
+template <int OP>
+__global__ void __launch_bounds__(1024) k_fap_final(const int64_t* tmp, uint32_t n, uint64_t T, uint32_t n_kept,
+                                                    int64_t* p_i, uint32_t* p_cnt, uint8_t* p_flag) {
+  __shared__ int64_t s[16][WAVE];
+  const int lane = lane_id();
+  const uint32_t w = threadIdx.x / WAVE;
+  int64_t acc = fap_rows_wave<OP>(tmp, w, 16, n);
+  acc = fap_block_comb<OP>(acc, s);
+  if (w == 0 && (uint64_t)lane < T) {
+    p_i[lane] = acc;
+    p_cnt[lane] = n_kept;
+    p_flag[lane] = 0;
   }
 }
 

@@ -130,11 +130,11 @@ DEVI void kept_compact_block(const KeptArgs& A) {
   const HostPub& pub = A.pub; const uint64_t* pub_src = A.pub_src;
   __shared__ uint64_t s_wk[16], s_we[16];
   __shared__ uint64_t s_c[16];
-  __shared__ int64_t s_f[16], s_l[16];
+  __shared__ int64_t s_f[16], s_l[16], s_fx[16], s_ln[16];
   const int t = threadIdx.x, lane = lane_id(), w = t / WAVE;
   uint64_t ck = 0, ce = 0;  // carries: kept spans / E capacity before this round
   uint64_t cnt = 0;
-  int64_t f = INT64_MAX, l = INT64_MIN;
+  int64_t f = INT64_MAX, l = INT64_MIN, fx = INT64_MIN, ln = INT64_MAX;
   for (uint64_t base0 = 0; base0 < n; base0 += 4096) {
     const uint64_t base = base0 + 4 * t;
     uint32_t fk[4];
@@ -173,6 +173,8 @@ DEVI void kept_compact_block(const KeptArgs& A) {
         cnt += ncells[s];
         f = min(f, sp_first[s]);
         l = max(l, sp_last[s]);
+        fx = max(fx, sp_first[s]);
+        ln = min(ln, sp_last[s]);
       }
       rk += fk[i];
       re += fe[i];
@@ -186,11 +188,15 @@ DEVI void kept_compact_block(const KeptArgs& A) {
     cnt += shfl_xor_u64(cnt, m);
     f = min(f, (int64_t)shfl_xor_u64((uint64_t)f, m));
     l = max(l, (int64_t)shfl_xor_u64((uint64_t)l, m));
+    fx = max(fx, (int64_t)shfl_xor_u64((uint64_t)fx, m));
+    ln = min(ln, (int64_t)shfl_xor_u64((uint64_t)ln, m));
   }
   if (lane == 0) {
     s_c[w] = cnt;
     s_f[w] = f;
     s_l[w] = l;
+    s_fx[w] = fx;
+    s_ln[w] = ln;
   }
   __syncthreads();
   if (t == 0) {
@@ -198,6 +204,8 @@ DEVI void kept_compact_block(const KeptArgs& A) {
       cnt += s_c[i];
       f = min(f, s_f[i]);
       l = max(l, s_l[i]);
+      fx = max(fx, s_fx[i]);
+      ln = min(ln, s_ln[i]);
     }
     *n_kept_out = ck;
     *e_total_out = ce;
@@ -205,6 +213,8 @@ DEVI void kept_compact_block(const KeptArgs& A) {
       atomicAdd(n_input, (unsigned long long)cnt);
       atomicMin(&bound[0], (unsigned long long)f);
       atomicMax(&bound[1], (unsigned long long)l);
+      atomicMax(&bound[2], (unsigned long long)fx);
+      atomicMin(&bound[3], (unsigned long long)ln);
     }
   }
   if (pub.dst && t < WAVE) {  // the call state, final here, to the host (wave 0)
@@ -290,7 +300,7 @@ __global__ void __launch_bounds__(256) k_kept_scatter_tiles(const uint8_t* kept,
     *e_total_out = re + se;
   }
   uint64_t cnt = 0;
-  int64_t f = INT64_MAX, l = INT64_MIN;
+  int64_t f = INT64_MAX, l = INT64_MIN, fx = INT64_MIN, ln = INT64_MAX;
 #pragma unroll
   for (int i = 0; i < 4; i++) {
     const uint64_t s = base + i;
@@ -300,6 +310,8 @@ __global__ void __launch_bounds__(256) k_kept_scatter_tiles(const uint8_t* kept,
       cnt += ncells[s];
       f = min(f, sp_first[s]);
       l = max(l, sp_last[s]);
+      fx = max(fx, sp_first[s]);
+      ln = min(ln, sp_last[s]);
     }
     rk += fk[i];
     re += fe[i];
@@ -307,10 +319,16 @@ __global__ void __launch_bounds__(256) k_kept_scatter_tiles(const uint8_t* kept,
   cnt = block_reduce_256(cnt, [](uint64_t x, uint64_t y) { return x + y; }, sh_c);
   f = block_reduce_256(f, [](int64_t x, int64_t y) { return min(x, y); }, sh_f);
   l = block_reduce_256(l, [](int64_t x, int64_t y) { return max(x, y); }, sh_l);
+  __syncthreads();
+  fx = block_reduce_256(fx, [](int64_t x, int64_t y) { return max(x, y); }, sh_f);
+  __syncthreads();
+  ln = block_reduce_256(ln, [](int64_t x, int64_t y) { return min(x, y); }, sh_l);
   if (t == 0 && cnt) {
     atomicAdd(n_input, (unsigned long long)cnt);
     atomicMin(&bound[0], (unsigned long long)f);
     atomicMax(&bound[1], (unsigned long long)l);
+    atomicMax(&bound[2], (unsigned long long)fx);
+    atomicMin(&bound[3], (unsigned long long)ln);
   }
 }
 

@@ -3,7 +3,7 @@
 # C3*, C2 and the 8-way C3* rehearsal bench lines.
 set -o pipefail
 mkdir -p gpurun_out
-timeout -k 10 600 python -u -m pytest tests/test_gpu_parity.py tests/test_fullscale.py tests/test_direct.py tests/test_multirank.py tests/test_groupby.py -q -x --timeout 300 --timeout-method thread -m gpu > gpurun_out/pytest_ds.log 2>&1
+timeout -k 10 600 python -u -m pytest tests/test_aligned_group.py tests/test_gpu_parity.py tests/test_fullscale.py tests/test_direct.py tests/test_multirank.py tests/test_groupby.py -q -x --timeout 300 --timeout-method thread -m gpu > gpurun_out/pytest_ds.log 2>&1
 rc=$?; tail -3 gpurun_out/pytest_ds.log; [ $rc -eq 0 ] || exit $rc
 for c in c3s c2; do
   timeout -k 10 300 python -u bench.py --no-cpu --steps 10 --warmup 3 --config $c > gpurun_out/q_$c.json 2>gpurun_out/q_$c.err || exit 1
