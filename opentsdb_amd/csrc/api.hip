@@ -1605,20 +1605,25 @@ static int spangroup_run(Slot* ctx, const tsdbhip_sg_desc* d, tsdbhip_sg_out* ou
       // (16-wave blocks, >= 128 rows each, at most 256 of them)
       const unsigned g1 = std::max(1u, std::min(256u, nrows / 128));
       int64_t* tmp = scratch<int64_t>(ctx, "fap_tmp", (uint64_t)g1 * WAVE);
+      FinalArgs f = fin;
+      f.n_chunks = 1;
       auto go = [&](auto opc) {
         constexpr int OP = decltype(opc)::value;
         hipLaunchKernelGGL((k_fap_rows<OP>), dim3(g1), dim3(1024), 0, st, (const int64_t*)fap.a.part, nrows, tmp);
-        hipLaunchKernelGGL((k_fap_final<OP>), dim3(1), dim3(1024), 0, st, (const int64_t*)tmp, g1, T, n_kept, r.p_i,
-                           r.p_cnt, r.p_flag);
+        if (!finalize) {
+          hipLaunchKernelGGL((k_fap_final<OP>), dim3(1), dim3(1024), 0, st, (const int64_t*)tmp, g1, T, n_kept, r.p_i,
+                             r.p_cnt, r.p_flag);
+          return;
+        }
+        // (the cross-series aggregator: OP 0 is sum or avg)
+        if (OP == 1) hipLaunchKernelGGL((k_fap_final_out<OP, 1>), dim3(1), dim3(1024), 0, st, (const int64_t*)tmp, g1, n_kept, f);
+        else if (OP == 2) hipLaunchKernelGGL((k_fap_final_out<OP, 2>), dim3(1), dim3(1024), 0, st, (const int64_t*)tmp, g1, n_kept, f);
+        else if (agg == TSDBHIP_AGG_AVG) hipLaunchKernelGGL((k_fap_final_out<0, 3>), dim3(1), dim3(1024), 0, st, (const int64_t*)tmp, g1, n_kept, f);
+        else hipLaunchKernelGGL((k_fap_final_out<0, 0>), dim3(1), dim3(1024), 0, st, (const int64_t*)tmp, g1, n_kept, f);
       };
       if (fap.a.op == 1) go(std::integral_constant<int, 1>());
       else if (fap.a.op == 2) go(std::integral_constant<int, 2>());
       else go(std::integral_constant<int, 0>());
-      if (finalize) {
-        FinalArgs f = fin;
-        f.n_chunks = 1;
-        dispatch_final(ctx, agg, mode, rate, r, f);
-      }
       return r;
     };
     if (!sharded) {
@@ -1654,11 +1659,13 @@ static int spangroup_run(Slot* ctx, const tsdbhip_sg_desc* d, tsdbhip_sg_out* ou
           // exact integer partials: one allreduce per field (wrapping u64
           // sum, i64 min / max, count sum), no ordering needed
           ReduceArgs mine = loc;
-          partials(mine, "m_", T);
-          dispatch_combine(ctx, agg, mode, loc, mine, T, loc.n_chunks);
-          if (agg == TSDBHIP_AGG_MIN || agg == TSDBHIP_AGG_MAX)
-            hipLaunchKernelGGL(k_neutral_minmax, dim3(grid_for(T, 256)), dim3(256), 0, st, mine.p_cnt, mine.p_i, T,
-                               agg == TSDBHIP_AGG_MIN ? INT64_MAX : INT64_MIN);
+          if (!fap_use) {  // (the aligned group's partials are one slot per t already, every count > 0)
+            partials(mine, "m_", T);
+            dispatch_combine(ctx, agg, mode, loc, mine, T, loc.n_chunks);
+            if (agg == TSDBHIP_AGG_MIN || agg == TSDBHIP_AGG_MAX)
+              hipLaunchKernelGGL(k_neutral_minmax, dim3(grid_for(T, 256)), dim3(256), 0, st, mine.p_cnt, mine.p_i, T,
+                                 agg == TSDBHIP_AGG_MIN ? INT64_MAX : INT64_MIN);
+          }
           HIPCHK(hipEventRecord(ctx->ev[6], st));
           X->group_start(ctx);
           for (const Fld& f : fields(mine, 0)) X->allreduce(ctx, f.p, T, f.t, f.op);

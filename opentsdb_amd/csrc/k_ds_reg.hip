@@ -505,4 +505,23 @@ __global__ void __launch_bounds__(1024) k_fap_final(const int64_t* tmp, uint32_t
   }
 }
 
+// The same, unsharded: the final values straight away (k_finalize_seq's
+// finalize_one on the one-chunk accumulator), one launch instead of two.
+template <int OP, int AGG>
+__global__ void __launch_bounds__(1024) k_fap_final_out(const int64_t* tmp, uint32_t n, uint32_t n_kept,
+                                                        FinalArgs f) {
+  __shared__ int64_t s[16][WAVE];
+  const int lane = lane_id();
+  const uint32_t w = threadIdx.x / WAVE;
+  int64_t acc = fap_rows_wave<OP>(tmp, w, 16, n);
+  acc = fap_block_comb<OP>(acc, s);
+  if (w == 0 && (uint64_t)lane < f.T) {
+    Acc a;
+    acc_init(a);
+    a.cnt = n_kept;
+    a.ia = acc;
+    finalize_one<AGG, MODE_INT, false>(f, (uint64_t)lane, a);
+  }
+}
+
 }  // namespace tsdb

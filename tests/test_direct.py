@@ -152,3 +152,26 @@ def test_many_spans_chunked_reduce(ctx):
         for rate in (False, True):
             g, o = run_both(ctx, ss, agg=agg, rate=rate)
             assert_same(g, o)
+
+
+def test_integer_dev_batches(ctx):
+    """integer dev without rate reduces in one span-ordered pass
+    (Aggregators.java:196-217) over direct spans: 4- and 8-byte cells,
+    staggered starts and ends (lanes where a span is inactive), a batch of 64
+    spans cut by a fallback span, a span count that is not a multiple of 64"""
+    rng = np.random.default_rng(5)
+    spans = []
+    for s in range(333):
+        a = (s * 7) % 40
+        n = 600 - (s * 11) % 50
+        ts = T0 + 10 * (a + np.arange(n))
+        if s % 3 == 0:  # minimal widths: 4-byte cells
+            v = rng.integers(2**20, 2**30, n) * rng.choice([-1, 1], n)  # (every cell 4 bytes wide)
+            spans.append(I([(int(t), int(x)) for t, x in zip(ts, v)]))
+        elif s == 200:  # a phase shift: this batch takes the general path
+            spans.append(long_series(ts + 3, rng.integers(-10**15, 10**15, n)))
+        else:
+            spans.append(long_series(ts, rng.integers(-10**15, 10**15, n)))
+    ss = packing.pack_spans(spans)
+    g, o = run_both(ctx, ss, agg=4)
+    assert_same(g, o)
