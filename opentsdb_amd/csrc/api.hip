@@ -687,8 +687,16 @@ struct LaunchChunks {
     // one wave per span (long rows, C3*): 4 resident blocks per CU (LDS
     // padding) measured faster than the 6 its registers allow; split spans
     // (C2) prefer the full occupancy
+    // (the padding brings the block's LDS to 40 KB whatever the kernel's own
+    // static LDS: a few bytes more would leave room for only 3 blocks)
     static const int pad_env = getenv("TSDBHIP_REG_LDS") ? atoi(getenv("TSDBHIP_REG_LDS")) : -1;
-    const unsigned pad = pad_env >= 0 ? (unsigned)pad_env : (wps_log2 == 0 ? 22000u : 0u);
+    static const unsigned stat_lds = [] {
+      hipFuncAttributes fa = {};
+      return hipFuncGetAttributes(&fa, (const void*)k_ds_reg<AGG>) == hipSuccess ? (unsigned)fa.sharedSizeBytes
+                                                                                 : 18960u;
+    }();
+    const unsigned pad = pad_env >= 0 ? (unsigned)pad_env
+                                      : (wps_log2 == 0 ? (stat_lds < 40960u ? 40960u - stat_lds : 0u) : 0u);
     // the aligned-group reduction (one wave per span): a partial row per block
     FapArgs fa0 = {};
     fa0.op = -1;
