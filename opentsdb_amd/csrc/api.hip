@@ -883,12 +883,13 @@ struct Small {
   // k_ds_reg's aligned-group reduction (FAP): the spans' class keys
   // (t0 << 32 | n, step) as [min, max, min, max], and a span outside it
   unsigned long long fap_key[4];
-  uint32_t fap_broken, fap_pad;
+  uint32_t fap_broken, fap_done;  // (fap_done: the optimistic finish wrote the results)
+  unsigned long long fap_valid;    // this rank's aligned-group partials stand (MIN over ranks when sharded)
   // sharded calls: two 64-bit hashes of the rank's grid bitmap (k_grid_popc /
   // k_grid_scan_blocks), and the agreed header words of the one collective
   // after the local grids (XH_*: MIN, or complemented MAX, over the ranks)
   unsigned long long ghash[2];
-  unsigned long long xh[10];
+  unsigned long long xh[12];  // (XH_N, + the aligned-group validity in an optimistic call)
 };
 // Small.xh slots of the grid-agreement header
 enum { XH_ERR = 0, XH_GF0, XH_GF1, XH_FSTAR, XH_LO, XH_HI, XH_H1MIN, XH_H1MAX, XH_H2MIN, XH_H2MAX, XH_N };
@@ -915,8 +916,9 @@ static Small small_init() {
 // the packed buffer only)
 struct XField { void* p; uint8_t kind; uint64_t imm; };
 constexpr uint32_t XM_MAX = 12;
+struct XExtra { void* p; uint64_t count; XType t; XOp op; };
 static void xchg_minmax(Slot* ctx, Xchg* X, const XField* f, uint32_t n, uint64_t* sum_u64 = nullptr,
-                        uint64_t* buf = nullptr);
+                        uint64_t* buf = nullptr, const XExtra* extra = nullptr, uint32_t n_extra = 0);
 constexpr size_t OUT_HDR = 1024;  // the Small snapshot ahead of the outputs
 static_assert(sizeof(Small) <= OUT_HDR, "Small must fit the output header");
 
@@ -954,7 +956,8 @@ __global__ void k_xmove(XMove m) {
 // (sum_u64: one more field, a u64 SUM, in the same collective group. The
 // pack / unpack kernels stay outside the group: RCCL issues a group's
 // collectives at its end.)
-static void xchg_minmax(Slot* ctx, Xchg* X, const XField* f, uint32_t n, uint64_t* sum_u64, uint64_t* buf) {
+static void xchg_minmax(Slot* ctx, Xchg* X, const XField* f, uint32_t n, uint64_t* sum_u64, uint64_t* buf,
+                        const XExtra* extra, uint32_t n_extra) {
   XMove m = {};
   m.n = n;
   m.buf = buf ? buf : scratch<uint64_t>(ctx, "x_pack", XM_MAX);
@@ -963,6 +966,7 @@ static void xchg_minmax(Slot* ctx, Xchg* X, const XField* f, uint32_t n, uint64_
   X->group_start(ctx);
   X->allreduce(ctx, m.buf, n, X_U64, X_MIN);
   if (sum_u64) X->allreduce(ctx, sum_u64, 1, X_U64, X_SUM);
+  for (uint32_t i = 0; i < n_extra; i++) X->allreduce(ctx, extra[i].p, extra[i].count, extra[i].t, extra[i].op);
   X->group_end(ctx);
   m.out = 1;
   hipLaunchKernelGGL(k_xmove, dim3(1), dim3(1), 0, ctx->stream, m);
@@ -1005,9 +1009,26 @@ __global__ void __launch_bounds__(1024) k_assemble_small(AssembleArgs a, KeptArg
 
 // Small unsharded calls also compute the lazy error index here (block 0,
 // before the snapshot; bad.n_kept = 0: k_bad_index ran).
+// (the optimistic aligned-group finish: `done` null, or the call is over only
+// when *done; otherwise the state is snapshot for the host and left as it is)
 __global__ void __launch_bounds__(256) k_call_end(Small* sm, Small* snap, Small init, uint32_t* bitmap,
-                                                  const uint32_t* grid, uint64_t T, int64_t lo, BadArgs bad) {
+                                                  const uint32_t* grid, uint64_t T, int64_t lo, BadArgs bad,
+                                                  const uint32_t* done = nullptr) {
   __shared__ unsigned long long s_min[4];
+  if (done) {
+    __shared__ uint64_t s_t;
+    __shared__ uint32_t s_over;
+    if (threadIdx.x == 0) {
+      s_over = *(volatile const uint32_t*)done;
+      s_t = sm->T;
+    }
+    __syncthreads();
+    if (!s_over) {
+      if (blockIdx.x == 0 && threadIdx.x == 0) *snap = *sm;
+      return;
+    }
+    T = s_t;
+  }
   if (blockIdx.x == 0) {
     if (bad.n_kept) {
       unsigned long long m = ~0ull;
@@ -1030,6 +1051,44 @@ __global__ void __launch_bounds__(256) k_call_end(Small* sm, Small* snap, Small 
   if (bitmap)
     for (uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x; i < T; i += (uint64_t)gridDim.x * 256)
       bitmap[(uint64_t)((int64_t)grid[i] - lo) >> 5] = 0u;
+}
+
+// ---- the optimistic aligned-group finish (no host round trip after the
+// grid when the group turns out aligned; see spangroup_run) ----
+// this rank's partials stand: every kept span in the one class, G its bucket
+// sequence of at most 64 points, no float, no error
+__global__ void k_fap_valid(Small* sm, uint32_t fap_ran) {
+  const bool v = fap_ran && sm->err == ERR_NONE && !sm->fap_broken && sm->fap_key[0] == sm->fap_key[1] &&
+                 sm->fap_key[2] == sm->fap_key[3] && sm->T > 0 && sm->T <= WAVE && sm->gflags[0] == 0;
+  sm->fap_valid = v ? 1ull : 0ull;
+}
+// a rank without an aligned-group attempt: neutral partials for the exchange
+__global__ void k_fap_neutral64(int64_t* p_i, uint32_t* p_cnt, int op) {
+  p_i[threadIdx.x] = fap_neutral(op);
+  p_cnt[threadIdx.x] = 0;
+}
+// the finalize of the (exchanged) 64-slot partials when the group stands
+// everywhere (sharded: and every rank's grid is the global one); outputs at
+// a fixed stride of 64 (ts | bits | is_int)
+template <int AGG>
+__global__ void __launch_bounds__(64) k_fap_finish(Small* sm, const int64_t* p_i, const uint32_t* p_cnt, FinalArgs f,
+                                                  int32_t sharded, int64_t lo, int64_t hi) {
+  bool ok = sm->fap_valid != 0 && sm->err == ERR_NONE && sm->gflags[0] == 0 && sm->T > 0 && sm->T <= WAVE;
+  if (sharded) {
+    const unsigned long long* xh = sm->xh;
+    ok = ok && xh[XH_LO] == (unsigned long long)lo && (int64_t)~xh[XH_HI] == hi && xh[XH_H1MIN] == ~xh[XH_H1MAX] &&
+         xh[XH_H2MIN] == ~xh[XH_H2MAX] && xh[XH_H1MIN] == sm->ghash[0] && xh[XH_H2MIN] == sm->ghash[1];
+  }
+  if (!ok) return;
+  const uint32_t g = threadIdx.x;
+  if (g < sm->T) {
+    Acc a;
+    acc_init(a);
+    a.cnt = p_cnt[g];
+    a.ia = p_i[g];
+    finalize_one<AGG, MODE_INT, false>(f, g, a);
+  }
+  if (g == 0) sm->fap_done = 1;
 }
 
 // TSDBHIP_CHECK_CLEAN: counts non-zero words of a buffer (debug of the
@@ -1356,6 +1415,11 @@ static int spangroup_run(Slot* ctx, const tsdbhip_sg_desc* d, tsdbhip_sg_out* ou
     }
   };
 
+  // the optimistic aligned-group finish (below): unsharded, when this group
+  // was tried as one; sharded, for every query that allows the attempt (all
+  // ranks must issue the same collectives)
+  const bool fap_query = interval > 0 && !rate && ds_agg <= 3 && agg <= 3 && !exact && !fap_off;
+  const bool fap_opt = !detail && (sharded ? fap_query : (fap_ran && !empty_grid));
   // ---- union grid ----
   uint64_t T = 0;
   uint32_t* word_rank = nullptr;
@@ -1388,7 +1452,112 @@ static int spangroup_run(Slot* ctx, const tsdbhip_sg_desc* d, tsdbhip_sg_out* ou
     if (n_kept)
       hipLaunchKernelGGL(k_grid_mark, dim3(mark_list ? std::min(grid_for(n_kept, 4, 65536), 1024u) : grid_for(n_kept, 4, 65536)),
                          dim3(256), 0, st, ga);
-    grid_ranks(!sharded, sharded);
+    grid_ranks(!sharded && !fap_opt, sharded);
+  }
+  // ---- the optimistic aligned-group finish: when the group is tried as an
+  // aligned group (sharded: every rank does this for a query that allows it,
+  // so that all issue the same collectives), the rest of the call is enqueued
+  // without the second host round trip: G emitted, the block partials reduced
+  // to 64 slots (sharded: exchanged in the agreement's collective group), and
+  // k_fap_finish writes the results iff the group stood (everywhere); the
+  // host then waits once. If it did not stand, the state after the grid (and
+  // the agreement) is intact and the usual path continues from it. ----
+  if (fap_opt) {
+    uint32_t* gridv_o = nullptr;
+    if (!empty_grid) {
+      gridv_o = scratch<uint32_t>(ctx, "grid", nwords * 32);  // (>= |G|)
+      ga.grid = gridv_o;
+      uint32_t* word_rank_f = scratch<uint32_t>(ctx, "word_rank_f", nwords);
+      const uint32_t eb = grid_for(nwords, 256);
+      hipLaunchKernelGGL(k_emit_verify, dim3(eb), dim3(256), 0, st, ga, word_rank_f, dg, 0u, eb);
+    }
+    HIPCHK(hipEventRecord(ctx->ev[4], st));
+    const int fop = agg == TSDBHIP_AGG_MIN ? 1 : (agg == TSDBHIP_AGG_MAX ? 2 : 0);
+    int64_t* o_pi = scratch<int64_t>(ctx, "fo_i", WAVE);
+    uint32_t* o_pc = scratch<uint32_t>(ctx, "fo_cnt", WAVE);
+    const bool mine = fap_ran && !empty_grid;
+    if (mine) {
+      const uint32_t nrows = fap.a.nrows;
+      const unsigned g1 = std::max(1u, std::min(256u, nrows / 128));
+      int64_t* tmp = scratch<int64_t>(ctx, "fap_tmp", (uint64_t)g1 * WAVE);
+      auto go = [&](auto opc) {
+        constexpr int OP = decltype(opc)::value;
+        hipLaunchKernelGGL((k_fap_rows<OP>), dim3(g1), dim3(1024), 0, st, (const int64_t*)fap.a.part, nrows, tmp);
+        hipLaunchKernelGGL((k_fap_final64<OP>), dim3(1), dim3(1024), 0, st, (const int64_t*)tmp, g1,
+                           (const uint64_t*)&sm->T, n_kept, o_pi, o_pc);
+      };
+      if (fop == 1) go(std::integral_constant<int, 1>());
+      else if (fop == 2) go(std::integral_constant<int, 2>());
+      else go(std::integral_constant<int, 0>());
+    } else {
+      hipLaunchKernelGGL(k_fap_neutral64, dim3(1), dim3(WAVE), 0, st, o_pi, o_pc, fop);
+    }
+    hipLaunchKernelGGL(k_fap_valid, dim3(1), dim3(1), 0, st, sm, mine ? 1u : 0u);
+    if (sharded) {  // the agreement, the validity (MIN) and the 64-slot partials: one collective group
+      const uint64_t elo = empty_grid ? ~0ull : (uint64_t)lo, ehi = empty_grid ? 0ull : (uint64_t)hi;
+      if (empty_grid) HIPCHK(hipMemsetAsync(sm->ghash, 0, sizeof sm->ghash, st));
+      const XField fx[XH_N + 1] = {{&sm->err, 0, 0},      {&sm->gflags[0], 2, 0}, {&sm->gflags[1], 2, 0},
+                                   {&sm->fstar, 1, 0},    {nullptr, 3, elo},      {nullptr, 4, ehi},
+                                   {&sm->ghash[0], 5, 0}, {&sm->ghash[0], 6, 0},  {&sm->ghash[1], 5, 0},
+                                   {&sm->ghash[1], 6, 0}, {&sm->fap_valid, 0, 0}};
+      const XExtra ex[2] = {{o_pi, WAVE, fop ? X_I64 : X_U64, fop == 1 ? X_MIN : (fop == 2 ? X_MAX : X_SUM)},
+                            {o_pc, WAVE, X_U32, X_SUM}};
+      xchg_minmax(ctx, X, fx, XH_N + 1, (uint64_t*)&sm->n_input, (uint64_t*)sm->xh, ex, 2);
+    }
+    map_out_reserve(ctx, OUT_HDR + 17 * WAVE);
+    FinalArgs fo;
+    std::memset(&fo, 0, sizeof fo);
+    fo.T = WAVE;
+    fo.n_chunks = 1;
+    fo.grid = gridv_o;
+    fo.out_ts = (int64_t*)(ctx->map_out_dev + OUT_HDR);
+    fo.out_bits = fo.out_ts + WAVE;
+    fo.out_isint = (uint8_t*)(fo.out_bits + WAVE);
+    fo.nan_t = &sm->nan_t;
+    {  // (an empty local grid: never valid; launched anyway, every rank alike)
+      if (agg == TSDBHIP_AGG_MIN)
+        hipLaunchKernelGGL(k_fap_finish<1>, dim3(1), dim3(WAVE), 0, st, sm, (const int64_t*)o_pi, (const uint32_t*)o_pc, fo, (int32_t)sharded, lo, hi);
+      else if (agg == TSDBHIP_AGG_MAX)
+        hipLaunchKernelGGL(k_fap_finish<2>, dim3(1), dim3(WAVE), 0, st, sm, (const int64_t*)o_pi, (const uint32_t*)o_pc, fo, (int32_t)sharded, lo, hi);
+      else if (agg == TSDBHIP_AGG_AVG)
+        hipLaunchKernelGGL(k_fap_finish<3>, dim3(1), dim3(WAVE), 0, st, sm, (const int64_t*)o_pi, (const uint32_t*)o_pc, fo, (int32_t)sharded, lo, hi);
+      else
+        hipLaunchKernelGGL(k_fap_finish<0>, dim3(1), dim3(WAVE), 0, st, sm, (const int64_t*)o_pi, (const uint32_t*)o_pc, fo, (int32_t)sharded, lo, hi);
+    }
+    hipLaunchKernelGGL(k_call_end, dim3(1), dim3(256), 0, st, sm, (Small*)ctx->map_out_dev, small_init(), bitmap,
+                       (const uint32_t*)gridv_o, (uint64_t)0, lo, BadArgs{}, (const uint32_t*)&sm->fap_done);
+    HIPCHK(hipEventRecord(ctx->ev[5], st));
+    HIPCHK(hipStreamSynchronize(st));
+    std::memcpy(&h, ctx->map_out, sizeof h);
+    if (h.fap_done) {  // the call is over (state reset, bitmap clear)
+      ctx->sm_ready = true;
+      ctx->bitmap_clean = true;
+      T = h.T;
+      out->n_input_points = h.n_input;
+      tm.n_grid = T;
+      tm.paths |= TSDBHIP_PATH_ALIGNED_GROUP;
+      if (sharded) tm.n_collectives = X->n_coll;
+      if (ctx->hot_kernel) tm.hot_ms = ev_ms(ctx->ev[8], ctx->ev[9]);
+      tm.hot_kernel = ctx->hot_kernel;
+      tm.reduce_ms = ev_ms(ctx->ev[4], ctx->ev[5]);
+      tm.total_ms = ev_ms(ctx->ev[0], ctx->ev[5]);
+      tm.n_emitted = e_total;
+      ctx->timing = tm;
+      if (T > out->capacity && ctx->want_output) {
+        out->err_code = TSDBHIP_E_CAPACITY;
+        return TSDBHIP_E_CAPACITY;
+      }
+      if (ctx->want_output) {
+        const uint8_t* hb = ctx->map_out;
+        std::memcpy(out->ts, hb + OUT_HDR, T * 8);
+        std::memcpy(out->bits, hb + OUT_HDR + 8 * WAVE, T * 8);
+        std::memcpy(out->is_int, hb + OUT_HDR + 16 * WAVE, T);
+      }
+      out->n_out = T;
+      out->err_code = TSDBHIP_OK;
+      out->err_index = -1;
+      return TSDBHIP_OK;
+    }
   }
   bool grids_agreed = true;  // (sharded: every rank's local grid is the global one)
   if (sharded) {
@@ -1405,10 +1574,12 @@ static int spangroup_run(Slot* ctx, const tsdbhip_sg_desc* d, tsdbhip_sg_out* ou
     const XField fx[XH_N] = {{&sm->err, 0, 0}, {&sm->gflags[0], 2, 0}, {&sm->gflags[1], 2, 0}, {&sm->fstar, 1, 0},
                              {nullptr, 3, elo}, {nullptr, 4, ehi}, {&sm->ghash[0], 5, 0}, {&sm->ghash[0], 6, 0},
                              {&sm->ghash[1], 5, 0}, {&sm->ghash[1], 6, 0}};
-    xchg_minmax(ctx, X, fx, XH_N, (uint64_t*)&sm->n_input, (uint64_t*)sm->xh);
-    const HostPub p2 = next_pub(ctx, sizeof(Small));
-    hipLaunchKernelGGL(k_publish, dim3(1), dim3(64), 0, st, p2, (const uint64_t*)sm);
-    wait_pub(ctx, p2, &h, sizeof h);  // sync 2: agreed error / flags / count, the grids' geometry and hashes
+    if (!fap_opt) {  // (an optimistic call ran the agreement already; h holds it)
+      xchg_minmax(ctx, X, fx, XH_N, (uint64_t*)&sm->n_input, (uint64_t*)sm->xh);
+      const HostPub p2 = next_pub(ctx, sizeof(Small));
+      hipLaunchKernelGGL(k_publish, dim3(1), dim3(64), 0, st, p2, (const uint64_t*)sm);
+      wait_pub(ctx, p2, &h, sizeof h);  // sync 2: agreed error / flags / count, the grids' geometry and hashes
+    }
     after_sync2();
     const int64_t glo = (int64_t)h.xh[XH_LO], ghi = (int64_t)~h.xh[XH_HI];
     const bool all_empty = h.xh[XH_LO] == ~0ull;
@@ -1444,7 +1615,7 @@ static int spangroup_run(Slot* ctx, const tsdbhip_sg_desc* d, tsdbhip_sg_out* ou
     dg.lo = lo;
     dg.hi = hi;
   } else if (!empty_grid) {
-    wait_pub(ctx, ga.pub, &h, sizeof h);  // sync 2: |G|, flags, F*, errors
+    if (!fap_opt) wait_pub(ctx, ga.pub, &h, sizeof h);  // sync 2: |G|, flags, F*, errors
     after_sync2();
   } else {
     readback(ctx, &h, sm, sizeof h);  // sync 2 (no grid)

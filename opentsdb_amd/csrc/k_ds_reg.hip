@@ -505,6 +505,23 @@ __global__ void __launch_bounds__(1024) k_fap_final(const int64_t* tmp, uint32_t
   }
 }
 
+// The same as 64 slots for an exchange (sharded optimistic finish): T read on
+// the device, neutral slots past it.
+template <int OP>
+__global__ void __launch_bounds__(1024) k_fap_final64(const int64_t* tmp, uint32_t n, const uint64_t* Tp,
+                                                      uint32_t n_kept, int64_t* p_i, uint32_t* p_cnt) {
+  __shared__ int64_t s[16][WAVE];
+  const int lane = lane_id();
+  const uint32_t w = threadIdx.x / WAVE;
+  int64_t acc = fap_rows_wave<OP>(tmp, w, 16, n);
+  acc = fap_block_comb<OP>(acc, s);
+  if (w == 0) {
+    const bool in = (uint64_t)lane < *(volatile const uint64_t*)Tp;
+    p_i[lane] = in ? acc : fap_neutral(OP);
+    p_cnt[lane] = in ? n_kept : 0u;
+  }
+}
+
 // The same, unsharded: the final values straight away (k_finalize_seq's
 // finalize_one on the one-chunk accumulator), one launch instead of two.
 template <int OP, int AGG>
