@@ -937,7 +937,7 @@ struct XMove {
   uint64_t imm[XM_MAX];   // kinds 3 / 4
   int32_t out;            // 0: fields -> buf, 1: buf -> fields
 };
-__global__ void k_xmove(XMove m) {
+DEVI void xmove_run(const XMove& m) {
   for (uint32_t i = 0; i < m.n; i++) {
     const uint8_t k = m.kind[i];
     const bool cpl = k == 1 || k == 2 || k == 4 || k == 6;  // MAX kinds travel complemented
@@ -952,10 +952,27 @@ __global__ void k_xmove(XMove m) {
     }
   }
 }
+__global__ void k_xmove(XMove m) { xmove_run(m); }
 
 // (sum_u64: one more field, a u64 SUM, in the same collective group. The
 // pack / unpack kernels stay outside the group: RCCL issues a group's
 // collectives at its end.)
+// the packing descriptor of xchg_minmax, for callers whose own kernels pack
+// before (out = 0) and unpack after (out = 1) the group (xchg_group)
+static XMove xchg_desc(Slot* ctx, const XField* f, uint32_t n, uint64_t* buf) {
+  XMove m = {};
+  m.n = n;
+  m.buf = buf ? buf : scratch<uint64_t>(ctx, "x_pack", XM_MAX);
+  for (uint32_t i = 0; i < n; i++) { m.kind[i] = f[i].kind; m.field[i] = f[i].p; m.imm[i] = f[i].imm; }
+  return m;
+}
+static void xchg_group(Slot* ctx, Xchg* X, const XMove& m, uint64_t* sum_u64, const XExtra* extra, uint32_t n_extra) {
+  X->group_start(ctx);
+  X->allreduce(ctx, m.buf, m.n, X_U64, X_MIN);
+  if (sum_u64) X->allreduce(ctx, sum_u64, 1, X_U64, X_SUM);
+  for (uint32_t i = 0; i < n_extra; i++) X->allreduce(ctx, extra[i].p, extra[i].count, extra[i].t, extra[i].op);
+  X->group_end(ctx);
+}
 static void xchg_minmax(Slot* ctx, Xchg* X, const XField* f, uint32_t n, uint64_t* sum_u64, uint64_t* buf,
                         const XExtra* extra, uint32_t n_extra) {
   XMove m = {};
@@ -1057,23 +1074,48 @@ __global__ void __launch_bounds__(256) k_call_end(Small* sm, Small* snap, Small 
 // grid when the group turns out aligned; see spangroup_run) ----
 // this rank's partials stand: every kept span in the one class, G its bucket
 // sequence of at most 64 points, no float, no error
-__global__ void k_fap_valid(Small* sm, uint32_t fap_ran) {
+// (one thread; then, sharded, the agreement header packed for the group)
+DEVI void fap_valid_pack(Small* sm, uint32_t fap_ran, const XMove& pack) {
   const bool v = fap_ran && sm->err == ERR_NONE && !sm->fap_broken && sm->fap_key[0] == sm->fap_key[1] &&
                  sm->fap_key[2] == sm->fap_key[3] && sm->T > 0 && sm->T <= WAVE && sm->gflags[0] == 0;
   sm->fap_valid = v ? 1ull : 0ull;
+  if (pack.n) xmove_run(pack);
+}
+// this rank's 64-slot partials (k_fap_final64's reduce), its validity, the pack
+template <int OP>
+__global__ void __launch_bounds__(1024) k_fap_final64v(const int64_t* tmp, uint32_t n, uint32_t n_kept, int64_t* p_i,
+                                                       uint32_t* p_cnt, Small* sm, XMove pack) {
+  __shared__ int64_t s[16][WAVE];
+  const int lane = lane_id();
+  const uint32_t w = threadIdx.x / WAVE;
+  int64_t acc = fap_rows_wave<OP>(tmp, w, 16, n);
+  acc = fap_block_comb<OP>(acc, s);
+  if (w == 0) {
+    const bool in = (uint64_t)lane < *(volatile const uint64_t*)&sm->T;
+    p_i[lane] = in ? acc : fap_neutral(OP);
+    p_cnt[lane] = in ? n_kept : 0u;
+    if (lane == 0) fap_valid_pack(sm, 1u, pack);
+  }
 }
 // a rank without an aligned-group attempt: neutral partials for the exchange
-__global__ void k_fap_neutral64(int64_t* p_i, uint32_t* p_cnt, int op) {
+__global__ void k_fap_neutral64(int64_t* p_i, uint32_t* p_cnt, int op, Small* sm, XMove pack) {
   p_i[threadIdx.x] = fap_neutral(op);
   p_cnt[threadIdx.x] = 0;
+  if (threadIdx.x == 0) fap_valid_pack(sm, 0u, pack);
 }
 // the finalize of the (exchanged) 64-slot partials when the group stands
 // everywhere (sharded: and every rank's grid is the global one); outputs at
 // a fixed stride of 64 (ts | bits | is_int)
 template <int AGG>
 __global__ void __launch_bounds__(64) k_fap_finish(Small* sm, const int64_t* p_i, const uint32_t* p_cnt, FinalArgs f,
-                                                  int32_t sharded, int64_t lo, int64_t hi) {
-  bool ok = sm->fap_valid != 0 && sm->err == ERR_NONE && sm->gflags[0] == 0 && sm->T > 0 && sm->T <= WAVE;
+                                                  int32_t sharded, int64_t lo, int64_t hi, XMove unpack) {
+  if (unpack.n) {  // the agreed header back into the call state (sharded)
+    if (threadIdx.x == 0) xmove_run(unpack);
+    __threadfence();
+    __syncthreads();
+  }
+  bool ok = *(volatile unsigned long long*)&sm->fap_valid != 0 && *(volatile unsigned long long*)&sm->err == ERR_NONE &&
+            *(volatile uint32_t*)&sm->gflags[0] == 0 && sm->T > 0 && sm->T <= WAVE;
   if (sharded) {
     const unsigned long long* xh = sm->xh;
     ok = ok && xh[XH_LO] == (unsigned long long)lo && (int64_t)~xh[XH_HI] == hi && xh[XH_H1MIN] == ~xh[XH_H1MAX] &&
@@ -1476,6 +1518,18 @@ static int spangroup_run(Slot* ctx, const tsdbhip_sg_desc* d, tsdbhip_sg_out* ou
     int64_t* o_pi = scratch<int64_t>(ctx, "fo_i", WAVE);
     uint32_t* o_pc = scratch<uint32_t>(ctx, "fo_cnt", WAVE);
     const bool mine = fap_ran && !empty_grid;
+    // (sharded: the agreement header packed by the partial kernel and unpacked
+    // by the finish, no pack / unpack launches of their own)
+    const uint64_t elo = empty_grid ? ~0ull : (uint64_t)lo, ehi = empty_grid ? 0ull : (uint64_t)hi;
+    if (sharded && empty_grid) HIPCHK(hipMemsetAsync(sm->ghash, 0, sizeof sm->ghash, st));
+    const XField fx[XH_N + 1] = {{&sm->err, 0, 0},      {&sm->gflags[0], 2, 0}, {&sm->gflags[1], 2, 0},
+                                 {&sm->fstar, 1, 0},    {nullptr, 3, elo},      {nullptr, 4, ehi},
+                                 {&sm->ghash[0], 5, 0}, {&sm->ghash[0], 6, 0},  {&sm->ghash[1], 5, 0},
+                                 {&sm->ghash[1], 6, 0}, {&sm->fap_valid, 0, 0}};
+    XMove pack = {};
+    if (sharded) pack = xchg_desc(ctx, fx, XH_N + 1, (uint64_t*)sm->xh);
+    XMove unpack = pack;
+    unpack.out = 1;
     if (mine) {
       const uint32_t nrows = fap.a.nrows;
       const unsigned g1 = std::max(1u, std::min(256u, nrows / 128));
@@ -1483,26 +1537,19 @@ static int spangroup_run(Slot* ctx, const tsdbhip_sg_desc* d, tsdbhip_sg_out* ou
       auto go = [&](auto opc) {
         constexpr int OP = decltype(opc)::value;
         hipLaunchKernelGGL((k_fap_rows<OP>), dim3(g1), dim3(1024), 0, st, (const int64_t*)fap.a.part, nrows, tmp);
-        hipLaunchKernelGGL((k_fap_final64<OP>), dim3(1), dim3(1024), 0, st, (const int64_t*)tmp, g1,
-                           (const uint64_t*)&sm->T, n_kept, o_pi, o_pc);
+        hipLaunchKernelGGL((k_fap_final64v<OP>), dim3(1), dim3(1024), 0, st, (const int64_t*)tmp, g1, n_kept, o_pi, o_pc,
+                           sm, pack);
       };
       if (fop == 1) go(std::integral_constant<int, 1>());
       else if (fop == 2) go(std::integral_constant<int, 2>());
       else go(std::integral_constant<int, 0>());
     } else {
-      hipLaunchKernelGGL(k_fap_neutral64, dim3(1), dim3(WAVE), 0, st, o_pi, o_pc, fop);
+      hipLaunchKernelGGL(k_fap_neutral64, dim3(1), dim3(WAVE), 0, st, o_pi, o_pc, fop, sm, pack);
     }
-    hipLaunchKernelGGL(k_fap_valid, dim3(1), dim3(1), 0, st, sm, mine ? 1u : 0u);
     if (sharded) {  // the agreement, the validity (MIN) and the 64-slot partials: one collective group
-      const uint64_t elo = empty_grid ? ~0ull : (uint64_t)lo, ehi = empty_grid ? 0ull : (uint64_t)hi;
-      if (empty_grid) HIPCHK(hipMemsetAsync(sm->ghash, 0, sizeof sm->ghash, st));
-      const XField fx[XH_N + 1] = {{&sm->err, 0, 0},      {&sm->gflags[0], 2, 0}, {&sm->gflags[1], 2, 0},
-                                   {&sm->fstar, 1, 0},    {nullptr, 3, elo},      {nullptr, 4, ehi},
-                                   {&sm->ghash[0], 5, 0}, {&sm->ghash[0], 6, 0},  {&sm->ghash[1], 5, 0},
-                                   {&sm->ghash[1], 6, 0}, {&sm->fap_valid, 0, 0}};
       const XExtra ex[2] = {{o_pi, WAVE, fop ? X_I64 : X_U64, fop == 1 ? X_MIN : (fop == 2 ? X_MAX : X_SUM)},
                             {o_pc, WAVE, X_U32, X_SUM}};
-      xchg_minmax(ctx, X, fx, XH_N + 1, (uint64_t*)&sm->n_input, (uint64_t*)sm->xh, ex, 2);
+      xchg_group(ctx, X, pack, (uint64_t*)&sm->n_input, ex, 2);
     }
     map_out_reserve(ctx, OUT_HDR + 17 * WAVE);
     FinalArgs fo;
@@ -1516,13 +1563,13 @@ static int spangroup_run(Slot* ctx, const tsdbhip_sg_desc* d, tsdbhip_sg_out* ou
     fo.nan_t = &sm->nan_t;
     {  // (an empty local grid: never valid; launched anyway, every rank alike)
       if (agg == TSDBHIP_AGG_MIN)
-        hipLaunchKernelGGL(k_fap_finish<1>, dim3(1), dim3(WAVE), 0, st, sm, (const int64_t*)o_pi, (const uint32_t*)o_pc, fo, (int32_t)sharded, lo, hi);
+        hipLaunchKernelGGL(k_fap_finish<1>, dim3(1), dim3(WAVE), 0, st, sm, (const int64_t*)o_pi, (const uint32_t*)o_pc, fo, (int32_t)sharded, lo, hi, sharded ? unpack : XMove{});
       else if (agg == TSDBHIP_AGG_MAX)
-        hipLaunchKernelGGL(k_fap_finish<2>, dim3(1), dim3(WAVE), 0, st, sm, (const int64_t*)o_pi, (const uint32_t*)o_pc, fo, (int32_t)sharded, lo, hi);
+        hipLaunchKernelGGL(k_fap_finish<2>, dim3(1), dim3(WAVE), 0, st, sm, (const int64_t*)o_pi, (const uint32_t*)o_pc, fo, (int32_t)sharded, lo, hi, sharded ? unpack : XMove{});
       else if (agg == TSDBHIP_AGG_AVG)
-        hipLaunchKernelGGL(k_fap_finish<3>, dim3(1), dim3(WAVE), 0, st, sm, (const int64_t*)o_pi, (const uint32_t*)o_pc, fo, (int32_t)sharded, lo, hi);
+        hipLaunchKernelGGL(k_fap_finish<3>, dim3(1), dim3(WAVE), 0, st, sm, (const int64_t*)o_pi, (const uint32_t*)o_pc, fo, (int32_t)sharded, lo, hi, sharded ? unpack : XMove{});
       else
-        hipLaunchKernelGGL(k_fap_finish<0>, dim3(1), dim3(WAVE), 0, st, sm, (const int64_t*)o_pi, (const uint32_t*)o_pc, fo, (int32_t)sharded, lo, hi);
+        hipLaunchKernelGGL(k_fap_finish<0>, dim3(1), dim3(WAVE), 0, st, sm, (const int64_t*)o_pi, (const uint32_t*)o_pc, fo, (int32_t)sharded, lo, hi, sharded ? unpack : XMove{});
     }
     hipLaunchKernelGGL(k_call_end, dim3(1), dim3(256), 0, st, sm, (Small*)ctx->map_out_dev, small_init(), bitmap,
                        (const uint32_t*)gridv_o, (uint64_t)0, lo, BadArgs{}, (const uint32_t*)&sm->fap_done);
