@@ -739,7 +739,8 @@ static void launch_reduce(Slot* ctx, unsigned blocks, const ReduceArgs& r, const
   if (ctx->time_reduce) HIPCHK(hipEventRecord(ctx->ev[8], ctx->stream));
   if (r.d_info && r.chunk_e)
     hipLaunchKernelGGL((k_reduce<AGG, MODE, RATE, true>), dim3(blocks), dim3(256), 0, ctx->stream, r);
-  hipLaunchKernelGGL((k_reduce<AGG, MODE, RATE, false>), dim3(blocks), dim3(256), 0, ctx->stream, r);
+  hipLaunchKernelGGL((k_reduce<AGG, MODE, RATE, false>), dim3(blocks), dim3(256),
+                     r.lds_state ? 4 * red_lds_stride(r.spans_per_chunk, RATE) : 0, ctx->stream, r);
   if (ctx->time_reduce) HIPCHK(hipEventRecord(ctx->ev[9], ctx->stream));
   if (!finalize) return;
   if (par && f.T >= 1024)  // (large T: coalesced columns)
@@ -824,6 +825,7 @@ static void dispatch_final(Slot* ctx, int agg, int mode, bool rate, const Reduce
 }
 
 // k_reduce launch geometry: (tile group, span chunk) per wave.
+constexpr uint64_t RED_LDS_BLOCK = 40960;  // k_reduce span state: LDS bytes a block at most
 struct ReduceGeom {
   uint32_t spc, n_chunks, tpw, ntg;
   uint64_t n_waves;
@@ -831,7 +833,7 @@ struct ReduceGeom {
 // target: waves in flight over 256 CUs (a group batch splits it over its
 // groups); min_waves: floor for small groups
 static ReduceGeom reduce_geom(uint64_t T, uint32_t n_kept, bool one_chunk, uint64_t target = 16384,
-                              uint64_t min_waves = 2048) {
+                              uint64_t min_waves = 2048, uint32_t spc_cap = 0) {
   ReduceGeom g;
   const uint64_t n_tiles = (T + 63) / 64;
   if (one_chunk || n_kept == 0) {
@@ -844,6 +846,9 @@ static ReduceGeom reduce_geom(uint64_t T, uint32_t n_kept, bool one_chunk, uint6
     const uint64_t by_size = std::max<uint64_t>((n_kept + 255) / 256, (min_waves + n_tiles - 1) / n_tiles);
     want = std::min<uint64_t>(want, by_size);
     want = std::min<uint64_t>(want, std::max<uint32_t>(1, n_kept / 16));
+    // long grids: chunks small enough for the span state to stay in LDS
+    // (read every tile; C4: 180k tiles)
+    if (spc_cap && n_tiles >= 1024) want = std::max<uint64_t>(want, (n_kept + spc_cap - 1) / spc_cap);
     g.n_chunks = (uint32_t)std::max<uint64_t>(1, want);
     g.spc = (n_kept + g.n_chunks - 1) / g.n_chunks;
     g.n_chunks = (n_kept + g.spc - 1) / g.spc;
@@ -1779,7 +1784,11 @@ static int spangroup_run(Slot* ctx, const tsdbhip_sg_desc* d, tsdbhip_sg_out* ou
     // one reduce launch over this rank's kept spans; `init`: the per-t state
     // to continue from (one chunk)
     auto run_reduce = [&](bool one_chunk, bool finalize, const ReduceArgs* init) {
-      const ReduceGeom rg = reduce_geom(T, n_kept, one_chunk || init);
+      static const uint64_t minw_env = getenv("TSDBHIP_REDUCE_MINW") ? atoll(getenv("TSDBHIP_REDUCE_MINW")) : 2048;
+      static const bool lds_env = !(getenv("TSDBHIP_REDUCE_LDS") && !strcmp(getenv("TSDBHIP_REDUCE_LDS"), "0"));
+      // span state in LDS while 4 waves' regions fit 40 KB (4 blocks a CU)
+      const uint32_t spc_cap = lds_env ? (uint32_t)(RED_LDS_BLOCK / 4 / red_lds_span_bytes(rate)) : 0u;
+      const ReduceGeom rg = reduce_geom(T, n_kept, one_chunk || init, 16384, minw_env, spc_cap);
       const uint32_t spc = rg.spc, n_chunks = rg.n_chunks, tpw = rg.tpw, ntg = rg.ntg;
       const uint64_t n_waves = rg.n_waves;
       ReduceArgs r;
@@ -1794,6 +1803,7 @@ static int spangroup_run(Slot* ctx, const tsdbhip_sg_desc* d, tsdbhip_sg_out* ou
       r.chunk_e = nullptr;
       r.fstar = fstar;
       r.exact = exact ? 1 : 0;
+      r.lds_state = lds_env && 4 * red_lds_stride(spc, rate) <= RED_LDS_BLOCK ? 1u : 0u;
       if (init) {
         r.i_cnt = init->p_cnt; r.i_flag = init->p_flag; r.i_i = init->p_i; r.i_d = init->p_d;
         r.i_dhas = init->p_dhas; r.i_wim = init->p_wim; r.i_wiv = init->p_wiv; r.i_wdm = init->p_wdm;

@@ -323,7 +323,7 @@ __global__ void __launch_bounds__(256) k_reduce_seg(ReduceArgs r0, SegReduce s) 
   const SegGroup G = s.sg[s.glist[lo]];
   ReduceArgs r = r0;
   seg_view(r, G);
-  reduce_wave<AGG, MODE, RATE, DONLY>(r, (uint32_t)(wave - s.wv_start[lo]));
+  reduce_wave<AGG, MODE, RATE, DONLY>(r, (uint32_t)(wave - s.wv_start[lo]), nullptr);
 }
 
 // k_finalize_seq over every grid point of the groups of one mode.

@@ -93,7 +93,16 @@ struct ReduceArgs {
   const uint32_t* row_ncells;
   const uint64_t* row_val_off;
   const uint8_t* val;
+  // the span state above (cursors, bracket caches, E offsets / lengths) kept
+  // in each wave's LDS (dynamic, red_lds_stride bytes a wave) instead of the
+  // global st_* arrays: a long grid re-reads it every tile
+  uint32_t lds_state;
 };
+
+// LDS bytes of one span's state (y pair, x pair, E offset, [rate value],
+// cursor, flags, E length); a wave's region, 16-byte aligned
+__host__ __device__ constexpr uint32_t red_lds_span_bytes(bool rate) { return rate ? 52u : 44u; }
+__host__ __device__ inline uint64_t red_lds_stride(uint32_t spc, bool rate) { return ((uint64_t)spc * red_lds_span_bytes(rate) + 15) & ~15ull; }
 
 // value bits of a direct span's cell (width 8: long / double bits; width 4:
 // int or float widened to double, RowSeq.java:194-226)
@@ -354,7 +363,7 @@ DEVI void direct_run(const ReduceArgs& r, Acc& acc, uint32_t run, uint32_t i, ui
 // reduce_wave: the work of one wave (tile group x span chunk) of a group;
 // k_reduce runs one group, k_reduce_seg (k_group.hip) many groups per launch.
 template <int AGG, int MODE, bool RATE, bool DONLY>
-DEVI void reduce_wave(const ReduceArgs& r, const uint32_t wave) {
+DEVI void reduce_wave(const ReduceArgs& r, const uint32_t wave, uint8_t* lds_w) {
   const int lane = lane_id();
   const uint32_t n_waves = r.n_chunks * r.n_tile_groups;
   if (wave >= n_waves) return;
@@ -376,16 +385,39 @@ DEVI void reduce_wave(const ReduceArgs& r, const uint32_t wave) {
     }
     return;
   }
-  uint32_t* ptr = r.ptr + (uint64_t)wave * r.spans_per_chunk;
+  // span state, indexed by k - k0: this wave's LDS region, or global
+  const uint32_t spc = r.spans_per_chunk;
+  const uint64_t so = (uint64_t)wave * spc;
+  uint32_t* ptr = r.ptr + so;
+  uint32_t* S_f = r.st_f + so;
+  uint2* S_x = r.st_x + so;
+  longlong2* S_y = r.st_y + so;
+  double* S_rv = r.st_rv + so;
+  const uint64_t* S_eo = r.e_off + k0;
+  const uint32_t* S_len = r.e_len + k0;
+  uint64_t* L_eo = nullptr;
+  uint32_t* L_len = nullptr;
+  if (lds_w) {
+    S_y = (longlong2*)lds_w;
+    S_x = (uint2*)(S_y + spc);
+    L_eo = (uint64_t*)(S_x + spc);
+    S_rv = (double*)(L_eo + spc);
+    ptr = (uint32_t*)(RATE ? (uint8_t*)(S_rv + spc) : (uint8_t*)S_rv);
+    S_f = ptr + spc;
+    L_len = S_f + spc;
+    S_eo = L_eo;
+    S_len = L_len;
+  }
   const uint32_t base_idx = RATE ? 1u : 0u;
   // cursor init: first point index >= base_idx with ts >= G[tb*64]
   if (!DONLY) {
     const int64_t t0 = r.grid[tb * WAVE];
     for (uint32_t k = k0 + lane; k < k1; k += WAVE) {
-      const uint64_t sl = (uint64_t)wave * r.spans_per_chunk + (k - k0);
-      if (r.d_info && (r.d_info[k] & 1u)) { ptr[k - k0] = 0; r.st_f[sl] = 0; continue; }
+      const uint32_t sl = k - k0;
+      if (r.d_info && (r.d_info[k] & 1u)) { ptr[sl] = 0; S_f[sl] = 0; continue; }
       const uint64_t eo = r.e_off[k];
       const uint32_t len = r.e_len[k];
+      if (L_eo) { L_eo[sl] = eo; L_len[sl] = len; }
       uint32_t lo = base_idx, hi = len;
       if (hi < lo) hi = lo;
       // a span that starts at/after the wave's first grid point (every span
@@ -424,10 +456,10 @@ DEVI void reduce_wave(const ReduceArgs& r, const uint32_t wave) {
           rv = yc / (double)(int64_t)x.x;  // Q5: prev = (0, 0)
         }
       }
-      r.st_x[sl] = x;
-      r.st_y[sl] = y;
-      r.st_rv[sl] = rv;
-      r.st_f[sl] = f;
+      S_x[sl] = x;
+      S_y[sl] = y;
+      if (RATE) S_rv[sl] = rv;
+      S_f[sl] = f;
     }
   }
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
@@ -581,22 +613,22 @@ DEVI void reduce_wave(const ReduceArgs& r, const uint32_t wave) {
       const bool kv = kl < k1;
       const uint32_t dinfo_l = (r.d_info && kv) ? r.d_info[kl] : 0u;
       const bool dl = DONLY || (dinfo_l & 1u) != 0;
-      const uint64_t eo_l = kv && !dl ? r.e_off[kl] : 0;
-      const uint32_t len_l = kv && !dl ? r.e_len[kl] : 0;
+      const uint32_t sl = kl - k0;
+      const uint64_t eo_l = kv && !dl ? S_eo[sl] : 0;
+      const uint32_t len_l = kv && !dl ? S_len[sl] : 0;
       // E spans: cursor and bracket cache, lane = span
-      const uint64_t sl = (uint64_t)wave * r.spans_per_chunk + (kl - k0);
       const bool el = !DONLY && kv && !dl;
       uint32_t j_l = 0, f_l = 0;
       uint2 x_l = make_uint2(0, 0);
       longlong2 y_l = make_longlong2(0, 0);
       double rv_l = 0.0;
       if (el) {
-        j_l = ptr[kl - k0];
-        f_l = r.st_f[sl];
+        j_l = ptr[sl];
+        f_l = S_f[sl];
         if (f_l & 4u) {
-          x_l = r.st_x[sl];
-          y_l = r.st_y[sl];
-          if (RATE) rv_l = r.st_rv[sl];
+          x_l = S_x[sl];
+          y_l = S_y[sl];
+          if (RATE) rv_l = S_rv[sl];
         }
       }
       bool dirty_l = false;
@@ -849,12 +881,12 @@ DEVI void reduce_wave(const ReduceArgs& r, const uint32_t wave) {
       }
       // write back the cursors and caches that changed
       if (dirty_l) {
-        ptr[kl - k0] = j_l;
-        r.st_f[sl] = f_l;
+        ptr[sl] = j_l;
+        S_f[sl] = f_l;
         if (f_l & 4u) {
-          r.st_x[sl] = x_l;
-          r.st_y[sl] = y_l;
-          if (RATE) r.st_rv[sl] = rv_l;
+          S_x[sl] = x_l;
+          S_y[sl] = y_l;
+          if (RATE) S_rv[sl] = rv_l;
         }
       }
     }
@@ -867,7 +899,9 @@ DEVI void reduce_wave(const ReduceArgs& r, const uint32_t wave) {
 
 template <int AGG, int MODE, bool RATE, bool DONLY>
 __global__ void __launch_bounds__(256) k_reduce(ReduceArgs r) {
-  reduce_wave<AGG, MODE, RATE, DONLY>(r, (blockIdx.x * blockDim.x + threadIdx.x) / WAVE);
+  extern __shared__ __align__(16) uint8_t red_lds[];
+  uint8_t* w = (!DONLY && r.lds_state) ? red_lds + (threadIdx.x / WAVE) * red_lds_stride(r.spans_per_chunk, RATE) : nullptr;
+  reduce_wave<AGG, MODE, RATE, DONLY>(r, (blockIdx.x * blockDim.x + threadIdx.x) / WAVE, w);
 }
 
 __global__ void k_chunk_flags(const uint32_t* d_info, uint32_t n_kept, uint32_t spc, uint32_t* chunk_e) {

@@ -132,18 +132,27 @@ DEVI void kept_compact_block(const KeptArgs& A) {
   __shared__ uint64_t s_c[16];
   __shared__ int64_t s_f[16], s_l[16], s_fx[16], s_ln[16];
   const int t = threadIdx.x, lane = lane_id(), w = t / WAVE;
+  const int wu = __builtin_amdgcn_readfirstlane(w);
   uint64_t ck = 0, ce = 0;  // carries: kept spans / E capacity before this round
   uint64_t cnt = 0;
   int64_t f = INT64_MAX, l = INT64_MIN, fx = INT64_MIN, ln = INT64_MAX;
   for (uint64_t base0 = 0; base0 < n; base0 += 4096) {
     const uint64_t base = base0 + 4 * t;
-    uint32_t fk[4];
+    uint32_t fk[4], fn[4];
     uint64_t fe[4], sk = 0, se = 0;
+    int64_t ff[4], fl[4];
 #pragma unroll
-    for (int i = 0; i < 4; i++) {
+    for (int i = 0; i < 4; i++) {  // (branch-free: every load of the round in flight together)
       const uint64_t s = base + i;
-      fk[i] = s < n && kept[s] ? 1u : 0u;
-      fe[i] = s < n ? cap[s] : 0ull;
+      const bool in = s < n;
+      const uint64_t sc = in ? s : n - 1;
+      const uint32_t kb = kept[sc];
+      const uint64_t cb = cap[sc];
+      fn[i] = ncells[sc];
+      ff[i] = sp_first[sc];
+      fl[i] = sp_last[sc];
+      fk[i] = in && kb ? 1u : 0u;
+      fe[i] = in ? cb : 0ull;
       sk += fk[i];
       se += fe[i];
     }
@@ -153,15 +162,11 @@ DEVI void kept_compact_block(const KeptArgs& A) {
       s_we[w] = ie;
     }
     __syncthreads();
-    uint64_t wk = 0, we = 0, tk = 0, te = 0;
-    for (int i = 0; i < 16; i++) {
-      if (i < w) {
-        wk += s_wk[i];
-        we += s_we[i];
-      }
-      tk += s_wk[i];
-      te += s_we[i];
-    }
+    // the 16 wave sums scanned across lanes (not 32 LDS loads per thread)
+    const uint64_t pk = wave_incl_scan_u64_dpp(lane < 16 ? s_wk[lane] : 0ull);
+    const uint64_t pe = wave_incl_scan_u64_dpp(lane < 16 ? s_we[lane] : 0ull);
+    const uint64_t wk = wu ? readlane_u64(pk, wu - 1) : 0ull, we = wu ? readlane_u64(pe, wu - 1) : 0ull;
+    const uint64_t tk = readlane_u64(pk, 15), te = readlane_u64(pe, 15);
     __syncthreads();  // (s_wk reused next round)
     uint64_t rk = ck + wk + ik - sk, re = ce + we + ie - se;
 #pragma unroll
@@ -170,11 +175,11 @@ DEVI void kept_compact_block(const KeptArgs& A) {
       if (fk[i]) {
         kept_list[rk] = (uint32_t)s;
         eoff_k[rk] = re;
-        cnt += ncells[s];
-        f = min(f, sp_first[s]);
-        l = max(l, sp_last[s]);
-        fx = max(fx, sp_first[s]);
-        ln = min(ln, sp_last[s]);
+        cnt += fn[i];
+        f = min(f, ff[i]);
+        l = max(l, fl[i]);
+        fx = max(fx, ff[i]);
+        ln = min(ln, fl[i]);
       }
       rk += fk[i];
       re += fe[i];
