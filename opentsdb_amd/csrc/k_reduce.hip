@@ -608,6 +608,7 @@ DEVI void reduce_wave(const ReduceArgs& r, const uint32_t wave, uint8_t* lds_w) 
       direct_push(info, act, e, raw, rawp, x0, step);
     };
     constexpr bool ALIGNED_OK = !RATE && MODE != MODE_DUAL;
+    constexpr bool LIN_OK = !RATE && MODE != MODE_INT && (AGG == 0 || AGG == 3);
     for (uint32_t kb = k0; kb < k1; kb += WAVE) {
       const uint32_t kl = kb + lane;
       const bool kv = kl < k1;
@@ -644,7 +645,10 @@ DEVI void reduce_wave(const ReduceArgs& r, const uint32_t wave, uint8_t* lds_w) 
       // UINT32_MAX when it is 2^31 - 1 or more (general lerp); |y1 - y0| / d
       uint32_t im_l = UINT32_MAX;
       double magr_l = 0.0;
-      if (!RATE && MODE != MODE_DBL && el && (f_l & 4u) && x_l.y > x_l.x)
+      // dual mode, every lane's t already on the double path: no long lerp of
+      // this batch is read (flags are only ever set), so none is prepared
+      const bool dual_all_dbl = MODE == MODE_DUAL && ballot(gv && !(acc.flag & 1u)) == 0;
+      if (!RATE && MODE != MODE_DBL && !dual_all_dbl && el && (f_l & 4u) && x_l.y > x_l.x)
         lerp_long_prep(y_l.x, y_l.y, x_l.y - x_l.x, im_l, magr_l);
       const uint64_t dmask = ballot(dl);
       uint32_t dga_l = 0, dn_l = 0, dx0_l = 0, dstep_l = 0;
@@ -666,6 +670,36 @@ DEVI void reduce_wave(const ReduceArgs& r, const uint32_t wave, uint8_t* lds_w) 
       // spans with no point in this tile take the cache
       const bool cl_ok = el && !((almask >> lane) & 1) && (f_l & 4u);
       const uint64_t cmask = ballot(cl_ok && (j_l >= len_l || (int64_t)x_l.y > t_last));
+      // Sum / avg of doubles (outside TSDBHIP_EXACT_ORDER): the cached spans
+      // active over the whole tile add up to one line in t, sum_s v_s(t_first)
+      // + (t - t_first) * sum_s slope_s: two wave sums instead of a lerp per
+      // span and lane (C4: ~94% of the span-tiles). Dual mode: int spans only
+      // once every lane's t is on the double path (their long lerps are then
+      // never read). Non-finite brackets keep the per-span path.
+      uint64_t lmask = 0;
+      if (LIN_OK && !r.exact) {
+        const bool all_dbl = MODE != MODE_DUAL || dual_all_dbl;
+        const double sl = dyd_l * rinv_l;
+        const double v0 = y0d_l + ((double)(uint32_t)(t_first - (int64_t)x_l.x) * dyd_l) * rinv_l;
+        const bool lin = ((cmask >> lane) & 1) && j_l > 0 && j_l < len_l && x_l.y > x_l.x &&
+                         (all_dbl || (f_l & 3u)) && __builtin_isfinite(v0) && __builtin_isfinite(sl);
+        lmask = ballot(lin);
+        if (lmask) {
+          double s0 = lin ? v0 : 0.0, s1 = lin ? sl : 0.0;
+#pragma unroll
+          for (int m = 1; m < WAVE; m <<= 1) {  // (xor butterfly: the same sums in every lane)
+            s0 += __longlong_as_double((long long)shfl_xor_u64((uint64_t)__double_as_longlong(s0), m));
+            s1 += __longlong_as_double((long long)shfl_xor_u64((uint64_t)__double_as_longlong(s1), m));
+          }
+          const bool lflt = MODE == MODE_DUAL && ballot(lin && (f_l & 3u)) != 0;
+          if (gv) {
+            const double y = s0 + (double)(tl - t_first) * s1;
+            acc.da = acc.cnt == 0 ? y : acc.da + y;
+            acc.cnt += (uint32_t)__popcll(lmask);
+            if (lflt) acc.flag |= 1u;
+          }
+        }
+      }
       // spans with exactly one point (j) in this tile: point j+1 loaded here,
       // lane-parallel, so the span needs no load of its own
       uint32_t x2_l = UINT32_MAX, f2_l = 0;
@@ -679,7 +713,7 @@ DEVI void reduce_wave(const ReduceArgs& r, const uint32_t wave, uint8_t* lds_w) 
       // (the long lerp of the bracket (j, j+1), prepared as im_l / magr_l)
       uint32_t im2_l = UINT32_MAX;
       double magr2_l = 0.0;
-      if (!RATE && MODE != MODE_DBL && sc && j_l + 1 < len_l && x2_l > x_l.y)
+      if (!RATE && MODE != MODE_DBL && !dual_all_dbl && sc && j_l + 1 < len_l && x2_l > x_l.y)
         lerp_long_prep(y_l.y, y2_l, x2_l - x_l.y, im2_l, magr2_l);
       const uint64_t smask = ballot(sc && (int64_t)x2_l > t_last);
       const uint32_t nb = min((uint32_t)WAVE, k1 - kb);
@@ -729,6 +763,11 @@ DEVI void reduce_wave(const ReduceArgs& r, const uint32_t wave, uint8_t* lds_w) 
         acc_push<AGG, MODE>(acc, yi, yd);
       };
       for (uint32_t i = 0; i < nb;) {
+        if ((lmask >> i) & 1) {  // (added above)
+          const uint64_t m = ~(lmask >> i);
+          i = min(nb, i + (m ? (uint32_t)__builtin_ctzll(m) : 64u));
+          continue;
+        }
         if ((dsingle >> i) & 1) {
           // a run of single-row direct spans with this span's width and type
           const uint32_t info0 = readlane_u32(dinfo_l, (int)i);
