@@ -894,10 +894,20 @@ struct Small {
   // k_grid_scan_blocks), and the agreed header words of the one collective
   // after the local grids (XH_*: MIN, or complemented MAX, over the ranks)
   unsigned long long ghash[2];
-  unsigned long long xh[12];  // (XH_N, + the aligned-group validity in an optimistic call)
+  unsigned long long xh[14];  // (XH_N, + the aligned-group validity in an optimistic call)
 };
-// Small.xh slots of the grid-agreement header
-enum { XH_ERR = 0, XH_GF0, XH_GF1, XH_FSTAR, XH_LO, XH_HI, XH_H1MIN, XH_H1MAX, XH_H2MIN, XH_H2MAX, XH_N };
+// Small.xh slots of the grid-agreement header. Every rank decides from these
+// agreed words alone (never from its own lo / hi against them), so the ranks
+// take the same branch: the grids agree iff min lo == max lo, min hi == max
+// hi and both hashes are equal everywhere (the hashes are over word indices
+// relative to each rank's own lo; equal lo makes them comparable)
+enum { XH_ERR = 0, XH_GF0, XH_GF1, XH_FSTAR, XH_LO, XH_HI, XH_H1MIN, XH_H1MAX, XH_H2MIN, XH_H2MAX, XH_LOMAX, XH_HIMIN, XH_N };
+
+// the agreement test on the agreed header (identical on every rank)
+__host__ __device__ inline bool xh_grids_agree(const unsigned long long* xh) {
+  return xh[XH_LO] == ~xh[XH_LOMAX] && ~xh[XH_HI] == xh[XH_HIMIN] && xh[XH_H1MIN] == ~xh[XH_H1MAX] &&
+         xh[XH_H2MIN] == ~xh[XH_H2MAX];
+}
 
 static Small small_init() {
   Small init = {};
@@ -920,7 +930,7 @@ static Small small_init() {
 // 3 immediate MIN, 4 immediate MAX, 5 u64 field MIN, 6 u64 field MAX (left in
 // the packed buffer only)
 struct XField { void* p; uint8_t kind; uint64_t imm; };
-constexpr uint32_t XM_MAX = 12;
+constexpr uint32_t XM_MAX = 14;
 struct XExtra { void* p; uint64_t count; XType t; XOp op; };
 static void xchg_minmax(Slot* ctx, Xchg* X, const XField* f, uint32_t n, uint64_t* sum_u64 = nullptr,
                         uint64_t* buf = nullptr, const XExtra* extra = nullptr, uint32_t n_extra = 0);
@@ -1113,7 +1123,7 @@ __global__ void k_fap_neutral64(int64_t* p_i, uint32_t* p_cnt, int op, Small* sm
 // a fixed stride of 64 (ts | bits | is_int)
 template <int AGG>
 __global__ void __launch_bounds__(64) k_fap_finish(Small* sm, const int64_t* p_i, const uint32_t* p_cnt, FinalArgs f,
-                                                  int32_t sharded, int64_t lo, int64_t hi, XMove unpack) {
+                                                  int32_t sharded, XMove unpack) {
   if (unpack.n) {  // the agreed header back into the call state (sharded)
     if (threadIdx.x == 0) xmove_run(unpack);
     __threadfence();
@@ -1123,8 +1133,9 @@ __global__ void __launch_bounds__(64) k_fap_finish(Small* sm, const int64_t* p_i
             *(volatile uint32_t*)&sm->gflags[0] == 0 && sm->T > 0 && sm->T <= WAVE;
   if (sharded) {
     const unsigned long long* xh = sm->xh;
-    ok = ok && xh[XH_LO] == (unsigned long long)lo && (int64_t)~xh[XH_HI] == hi && xh[XH_H1MIN] == ~xh[XH_H1MAX] &&
-         xh[XH_H2MIN] == ~xh[XH_H2MAX] && xh[XH_H1MIN] == sm->ghash[0] && xh[XH_H2MIN] == sm->ghash[1];
+    // (rank-independent: an empty grid anywhere makes lo's MIN / MAX differ,
+    // ~0 vs a real lo; all empty fails T > 0 on every rank)
+    ok = ok && xh_grids_agree(xh);
   }
   if (!ok) return;
   const uint32_t g = threadIdx.x;
@@ -1530,7 +1541,8 @@ static int spangroup_run(Slot* ctx, const tsdbhip_sg_desc* d, tsdbhip_sg_out* ou
     const XField fx[XH_N + 1] = {{&sm->err, 0, 0},      {&sm->gflags[0], 2, 0}, {&sm->gflags[1], 2, 0},
                                  {&sm->fstar, 1, 0},    {nullptr, 3, elo},      {nullptr, 4, ehi},
                                  {&sm->ghash[0], 5, 0}, {&sm->ghash[0], 6, 0},  {&sm->ghash[1], 5, 0},
-                                 {&sm->ghash[1], 6, 0}, {&sm->fap_valid, 0, 0}};
+                                 {&sm->ghash[1], 6, 0}, {nullptr, 4, elo},      {nullptr, 3, ehi},
+                                 {&sm->fap_valid, 0, 0}};
     XMove pack = {};
     if (sharded) pack = xchg_desc(ctx, fx, XH_N + 1, (uint64_t*)sm->xh);
     XMove unpack = pack;
@@ -1568,13 +1580,13 @@ static int spangroup_run(Slot* ctx, const tsdbhip_sg_desc* d, tsdbhip_sg_out* ou
     fo.nan_t = &sm->nan_t;
     {  // (an empty local grid: never valid; launched anyway, every rank alike)
       if (agg == TSDBHIP_AGG_MIN)
-        hipLaunchKernelGGL(k_fap_finish<1>, dim3(1), dim3(WAVE), 0, st, sm, (const int64_t*)o_pi, (const uint32_t*)o_pc, fo, (int32_t)sharded, lo, hi, sharded ? unpack : XMove{});
+        hipLaunchKernelGGL(k_fap_finish<1>, dim3(1), dim3(WAVE), 0, st, sm, (const int64_t*)o_pi, (const uint32_t*)o_pc, fo, (int32_t)sharded, sharded ? unpack : XMove{});
       else if (agg == TSDBHIP_AGG_MAX)
-        hipLaunchKernelGGL(k_fap_finish<2>, dim3(1), dim3(WAVE), 0, st, sm, (const int64_t*)o_pi, (const uint32_t*)o_pc, fo, (int32_t)sharded, lo, hi, sharded ? unpack : XMove{});
+        hipLaunchKernelGGL(k_fap_finish<2>, dim3(1), dim3(WAVE), 0, st, sm, (const int64_t*)o_pi, (const uint32_t*)o_pc, fo, (int32_t)sharded, sharded ? unpack : XMove{});
       else if (agg == TSDBHIP_AGG_AVG)
-        hipLaunchKernelGGL(k_fap_finish<3>, dim3(1), dim3(WAVE), 0, st, sm, (const int64_t*)o_pi, (const uint32_t*)o_pc, fo, (int32_t)sharded, lo, hi, sharded ? unpack : XMove{});
+        hipLaunchKernelGGL(k_fap_finish<3>, dim3(1), dim3(WAVE), 0, st, sm, (const int64_t*)o_pi, (const uint32_t*)o_pc, fo, (int32_t)sharded, sharded ? unpack : XMove{});
       else
-        hipLaunchKernelGGL(k_fap_finish<0>, dim3(1), dim3(WAVE), 0, st, sm, (const int64_t*)o_pi, (const uint32_t*)o_pc, fo, (int32_t)sharded, lo, hi, sharded ? unpack : XMove{});
+        hipLaunchKernelGGL(k_fap_finish<0>, dim3(1), dim3(WAVE), 0, st, sm, (const int64_t*)o_pi, (const uint32_t*)o_pc, fo, (int32_t)sharded, sharded ? unpack : XMove{});
     }
     hipLaunchKernelGGL(k_call_end, dim3(1), dim3(256), 0, st, sm, (Small*)ctx->map_out_dev, small_init(), bitmap,
                        (const uint32_t*)gridv_o, (uint64_t)0, lo, BadArgs{}, (const uint32_t*)&sm->fap_done);
@@ -1625,7 +1637,7 @@ static int spangroup_run(Slot* ctx, const tsdbhip_sg_desc* d, tsdbhip_sg_out* ou
     if (empty_grid) HIPCHK(hipMemsetAsync(sm->ghash, 0, sizeof sm->ghash, st));
     const XField fx[XH_N] = {{&sm->err, 0, 0}, {&sm->gflags[0], 2, 0}, {&sm->gflags[1], 2, 0}, {&sm->fstar, 1, 0},
                              {nullptr, 3, elo}, {nullptr, 4, ehi}, {&sm->ghash[0], 5, 0}, {&sm->ghash[0], 6, 0},
-                             {&sm->ghash[1], 5, 0}, {&sm->ghash[1], 6, 0}};
+                             {&sm->ghash[1], 5, 0}, {&sm->ghash[1], 6, 0}, {nullptr, 4, elo}, {nullptr, 3, ehi}};
     if (!fap_opt) {  // (an optimistic call ran the agreement already; h holds it)
       xchg_minmax(ctx, X, fx, XH_N, (uint64_t*)&sm->n_input, (uint64_t*)sm->xh);
       const HostPub p2 = next_pub(ctx, sizeof(Small));
@@ -1635,9 +1647,8 @@ static int spangroup_run(Slot* ctx, const tsdbhip_sg_desc* d, tsdbhip_sg_out* ou
     after_sync2();
     const int64_t glo = (int64_t)h.xh[XH_LO], ghi = (int64_t)~h.xh[XH_HI];
     const bool all_empty = h.xh[XH_LO] == ~0ull;
-    const bool agreed = all_empty || (h.xh[XH_LO] == (uint64_t)lo && ghi == hi && !empty_grid &&
-                                      h.xh[XH_H1MIN] == ~h.xh[XH_H1MAX] && h.xh[XH_H2MIN] == ~h.xh[XH_H2MAX] &&
-                                      h.xh[XH_H1MIN] == h.ghash[0] && h.xh[XH_H2MIN] == h.ghash[1]);
+    // (from the agreed words only: every rank takes the same branch)
+    const bool agreed = all_empty || xh_grids_agree(h.xh);
     grids_agreed = agreed;
     if (!agreed) {
       // the global geometry: this rank's bitmap shifted onto [glo, ghi] (a

@@ -102,21 +102,64 @@ def run_device(ctx, d, agg, rate=False, dsi=0, dsa=0, cap=3600, exact=False):
     return rc, ts[:n], isi[:n], bits[:n], int(out.n_input_points), int(out.err_index)
 
 
-@pytest.mark.gpu
-@pytest.mark.timeout(600)
-@pytest.mark.parametrize("name,agg,rate,dsi,dsa", [
+C3_CASES = [
     ("C3* sum + 1m-avg (the bench line)", _abi.AGG_SUM, False, 60, _abi.AGG_AVG),
     ("C3 sum", _abi.AGG_SUM, False, 0, 0),
     ("C3 rate sum", _abi.AGG_SUM, True, 0, 0),
     ("C3 rate max", _abi.AGG_MAX, True, 0, 0),
     ("C3 rate dev", _abi.AGG_DEV, True, 0, 0),
-])
+]
+_C3_ORACLE = {}
+
+
+def c3_oracle(agg, rate, dsi, dsa):
+    """the 1M-series oracle of one C3 case (host threads, ~1 min), computed
+    once for the unsharded and the 8-rank test"""
+    key = (agg, rate, dsi, dsa)
+    if key not in _C3_ORACLE:
+        o = oracle.regular_sharded(1_000_000, 3600, I64, 3, 1, 0, U32MAX, agg, rate, dsi, dsa, shard_spans=2000)
+        assert o.code == 0 and o.n_input_points == 3_600_000_000
+        assert len(o.ts) == (60 if dsi else 3599 if rate else 3600)
+        _C3_ORACLE[key] = o
+    return _C3_ORACLE[key]
+
+
+@pytest.mark.gpu
+@pytest.mark.timeout(600)
+@pytest.mark.parametrize("name,agg,rate,dsi,dsa", C3_CASES)
 def test_c3_full_size(ctx, c3_desc, name, agg, rate, dsi, dsa):
     g = run_device(ctx, c3_desc, agg, rate, dsi, dsa)
-    o = oracle.regular_sharded(1_000_000, 3600, I64, 3, 1, 0, U32MAX, agg, rate, dsi, dsa, shard_spans=2000)
-    assert o.code == 0 and o.n_input_points == 3_600_000_000
-    assert len(o.ts) == (60 if dsi else 3599 if rate else 3600)
-    assert_same(g, o, rtol=1e-9)
+    assert_same(g, c3_oracle(agg, rate, dsi, dsa), rtol=1e-9)
+
+
+@pytest.fixture(scope="module")
+def ctx8():
+    """8 in-process ranks on the one GPU (LocalXchg): the sharded path of
+    bench.py --gpus 8 with every per-rank kernel, chunking and exchange step
+    at the benchmarked per-rank size (125k spans a rank)"""
+    from opentsdb_amd._lib import Context
+    c = Context(devices=[0] * 8)
+    assert c.ranks == 8
+    yield c
+    c.close()
+
+
+@pytest.mark.gpu
+@pytest.mark.timeout(600)
+@pytest.mark.parametrize("name,agg,rate,dsi,dsa", C3_CASES)
+def test_c3_full_size_8_ranks(ctx8, c3_desc, name, agg, rate, dsi, dsa):
+    """the series-sharded path at the C3 size (1M spans
+    split over 8 ranks) against the same oracle: the per-rank
+    reduce chunking, the optimistic aligned-group finish (C3*: asserted
+    taken, one collective), exact integer partials allreduced, rate doubles
+    gathered and merged in rank order (SpanGroup.java:647-667,736-784) at
+    1e-9 relative, integers bit-exact."""
+    g = run_device(ctx8, c3_desc, agg, rate, dsi, dsa)
+    tm = ctx8.timing()
+    assert_same(g, c3_oracle(agg, rate, dsi, dsa), rtol=1e-9)
+    if dsi:
+        assert tm.paths & _abi.PATH_ALIGNED_GROUP
+        assert tm.n_collectives == 1
 
 
 @pytest.mark.gpu
@@ -191,3 +234,21 @@ def test_c4_full_size(ctx, name):
     assert sha(bits, "<i8") == e["bits"], "value bits (EXACT_ORDER) differ from the oracle"
     assert_same(g, oracle.Result(0, ts, isi, bits, n_in, -1), rtol=1e-9,
                 abs_scale=abs_bound(ctx, e["n_series"], e["n_points"], e["seed"], ff, fc, e["agg"], ts))
+
+
+@pytest.mark.gpu
+@pytest.mark.timeout(600)
+@pytest.mark.parametrize("name", ["c4_sum", "c4i_sum"])
+def test_c4_full_size_8_ranks(ctx8, name):
+    """C4 / C4-int at the bench's size split over 8 in-process ranks: every
+    rank's grid differs (bitmaps exchanged), the double partials are merged in
+    rank order; under EXACT_ORDER the ranks form the span-ordered pipeline,
+    bit-exact against the whole-group oracle's digests (SpanGroup.java:647-667)."""
+    e = json.load(open(DIGESTS))[name]
+    ff, fc = (0.5, 0.01) if e["gen"] == "jitter" else (0.0, 0.0)
+    ss = synth.jittered_packed(e["n_series"], e["n_points"], seed=e["seed"], float_frac=ff, float_cell_frac=fc)
+    rc, ts, isi, bits, n_in, _ = core.run_spanset(ctx8, ss, 0, U32MAX, e["agg"], exact=True)
+    assert rc == e["code"] and n_in == e["n_input"] and len(ts) == e["n_out"]
+    assert sha(ts, "<i8") == e["ts"], "timestamps differ from the oracle"
+    assert sha(isi, "u1") == e["is_int"], "isInteger differs from the oracle"
+    assert sha(bits, "<i8") == e["bits"], "value bits (EXACT_ORDER, 8 ranks) differ from the oracle"

@@ -160,6 +160,27 @@ def test_aligned_grids_skip_the_grid_exchange(mctx, dsi):
 
 
 @pytest.mark.gpu
+@pytest.mark.timeout(120)
+@pytest.mark.parametrize("agg", [0, 2, 4])
+@pytest.mark.parametrize("rate", [False, True])
+def test_equal_bucket_grids_different_last_ts(mctx, agg, rate):
+    """shards whose bucket grids are equal while their raw
+    [first, last] ranges differ (the first half of the spans end one second
+    later than the second half). Each rank's bitmap and hashes match, only hi
+    differs, so a decision that compared a rank's own hi with the agreed max
+    split the ranks (the one holding the max took the agreed branch, its
+    peers the allgather: a deadlock). The decision now reads the agreed words
+    alone. Covers the aligned-group finish (sum / max) and the usual path
+    (dev, rate)."""
+    n = 2 * mctx.ranks
+    length = 120
+    spans = [I([(T0 + i, 1000 * s + i) for i in range(length - (s >= n // 2))]) for s in range(n)]
+    ss = packing.pack_spans(spans)
+    g, o = both(mctx, ss, agg=agg, rate=rate, dsi=60, dsa=3)
+    assert_same(g, o)
+
+
+@pytest.mark.gpu
 def test_error_order_is_global_span_order(mctx, ctx):
     """Two Span.addRow errors at the same base time in different ranks: the
     one in the lower global span wins (the scan's row-key order: base time,
