@@ -149,12 +149,17 @@ def dist_setup(n_gpus):
 
 
 def host_threads():
-    """P = every core this process may run on (independent
-    SpanGroups on nproc threads, TsdbQuery.java:322-362)."""
+    """P = the cores this process may actually use (SURVEY.md §8(d):
+    independent SpanGroups on nproc threads, TsdbQuery.java:322-362): the
+    affinity set, capped by the cgroup's CPU quota (the GPU box shows the
+    whole machine's cores in its affinity mask but grants a share of them;
+    more threads than granted CPUs only time-slice)."""
     try:
-        return max(1, len(os.sched_getaffinity(0)))
+        n = max(1, len(os.sched_getaffinity(0)))
     except AttributeError:
-        return max(1, os.cpu_count() or 1)
+        n = max(1, os.cpu_count() or 1)
+    q = cpu_quota()
+    return max(1, min(n, int(q))) if q else n
 
 
 def cpu_model():
@@ -181,30 +186,46 @@ def cpu_quota():
 def run_pool(fn, probe, seconds):
     """Runs fn() (one independent unit: a SpanGroup or a row batch) on
     host_threads() threads pulling from one work counter, sized so the run
-    takes ~`seconds` wall time at the parallelism the machine grants.
-    Returns (units done, wall seconds, threads, granted CPUs)."""
+    takes ~`seconds` wall time. Returns (units done, wall seconds, threads,
+    granted CPUs, CPU seconds the threads consumed). CPU seconds ~ threads x
+    wall means the threads ran the whole time; per-unit CPU time above the
+    1-thread probe then measures contention for the shared memory system."""
     threads = host_threads()
     quota = cpu_quota()
-    eff = min(threads, quota) if quota else threads
-    total = max(threads, int(seconds * eff / max(probe, 1e-4)))
+    total = max(threads, int(seconds * threads / max(probe, 1e-4)))
     left = [total]
+    cpu = [0.0] * threads
     lock = threading.Lock()
 
-    def work():
+    def work(i):
+        c0 = time.thread_time()
         while True:
             with lock:
                 if left[0] <= 0:
-                    return
+                    break
                 left[0] -= 1
             fn()
+        cpu[i] = time.thread_time() - c0
 
-    ths = [threading.Thread(target=work) for _ in range(threads)]
+    ths = [threading.Thread(target=work, args=(i,)) for i in range(threads)]
     t = time.perf_counter()
     for th in ths:
         th.start()
     for th in ths:
         th.join()
-    return total, time.perf_counter() - t, threads, quota
+    return total, time.perf_counter() - t, threads, quota, sum(cpu)
+
+
+def pool_note(n, wall, threads, cpu_s, probe):
+    """What limited the P-thread run: parallel efficiency against the 1-thread
+    probe, and whether the threads were on a CPU (cpu_s / (threads x wall))
+    or each unit simply took longer (cpu per unit / probe: shared caches and
+    DRAM bandwidth)."""
+    eff = (n * probe / wall) / threads
+    busy = cpu_s / max(threads * wall, 1e-9)
+    slow = (cpu_s / max(n, 1)) / max(probe, 1e-9)
+    return (f"parallel efficiency {eff:.2f} of {threads} x 1-thread; threads on CPU {busy:.0%} of the wall time; "
+            f"CPU time per unit {slow:.2f}x the 1-thread probe")
 
 
 def cpu_baseline(cfg_name, seconds=10.0):
@@ -231,12 +252,13 @@ def cpu_baseline(cfg_name, seconds=10.0):
     t = time.perf_counter()
     r = oracle.spangroup(ss, *args, capacity=cap)
     probe = time.perf_counter() - t
-    n, wall, threads, quota = run_pool(lambda: oracle.spangroup(ss, *args, capacity=cap), probe, seconds)
+    n, wall, threads, quota, cpu_s = run_pool(lambda: oracle.spangroup(ss, *args, capacity=cap), probe, seconds)
     return {
         "value": n * r.n_input_points / wall, "unit": "input points/s", "cores": threads, "kind": "port",
         "cpu_model": cpu_model(), "cgroup_cpus": quota,
         "value_1core": r.n_input_points / probe,
-        "sample": f"{what}, {n} SpanGroups on {threads} threads, {wall:.1f} s wall "
+        "sample": f"{what}, {n} SpanGroups on {threads} threads, {wall:.1f} s wall; "
+                  f"{pool_note(n, wall, threads, cpu_s, probe)} "
                   f"(oracle/oracle.cc: C++ restatement of SpanGroup/Span/RowSeq/Aggregators; "
                   f"no JVM in the image)",
     }
@@ -258,13 +280,13 @@ def cpu_baseline_c5(batch, seconds=10.0):
     t = time.perf_counter()
     oracle.compact_rows(sub)
     probe = time.perf_counter() - t
-    n, wall, threads, quota = run_pool(lambda: oracle.compact_rows(sub), probe, seconds)
+    n, wall, threads, quota, cpu_s = run_pool(lambda: oracle.compact_rows(sub), probe, seconds)
     return {"value": n * cells / wall, "unit": "raw cells/s", "cores": threads, "kind": "port",
             "cpu_model": cpu_model(), "cgroup_cpus": quota,
             "value_1core": cells / probe,
             "sample": f"first {rows} rows ({cells} cells) of the same batch, {n} batches on {threads} threads, "
-                      f"{wall:.1f} s wall (oracle/oracle.cc: C++ restatement of CompactionQueue.compact; "
-                      f"no JVM in the image)"}
+                      f"{wall:.1f} s wall; {pool_note(n, wall, threads, cpu_s, probe)} "
+                      f"(oracle/oracle.cc: C++ restatement of CompactionQueue.compact; no JVM in the image)"}
 
 
 _JSON_OUT = None

@@ -49,7 +49,7 @@
 extern "C" {
 #endif
 
-#define TSDBHIP_ABI_VERSION 5
+#define TSDBHIP_ABI_VERSION 6
 
 /* ---- return codes ---------------------------------------------------- */
 #define TSDBHIP_OK               0
@@ -83,6 +83,7 @@ extern "C" {
 #define TSDBHIP_HOT_DECODE_FAST 2 /* streaming per-span decode(+downsample) */
 #define TSDBHIP_HOT_DECODE_GEN  3 /* general per-span decode(+downsample)   */
 #define TSDBHIP_HOT_REDUCE_DIRECT 5 /* k_reduce over direct spans (no-downsampling path) */
+#define TSDBHIP_HOT_LOCKSTEP    6 /* k_lockstep: one pass over qualifiers + values of a lockstep group */
 #define TSDBHIP_HOT_COMPACT     4 /* k_compact_tiles: classification + single/trivial/short complex
                                      compaction (tsdbhip_compact_rows)      */
 
@@ -165,12 +166,19 @@ typedef struct tsdbhip_timing {
   uint64_t n_emitted;       /* Σ|E_s| (points after downsampling)           */
   uint32_t paths;           /* TSDBHIP_PATH_* bits: which variants ran (ABI v5) */
   uint32_t reserved;
+  uint64_t x_bytes;         /* sharded calls: bytes this rank received in the
+                               call's collectives (ABI v6)                  */
 } tsdbhip_timing;
 /* tsdbhip_timing.paths */
 #define TSDBHIP_PATH_ALIGNED_GROUP 1u  /* k_ds_reg's aligned-group reduction
                                           stood for E + the reduce            */
 #define TSDBHIP_PATH_ALIGNED_RERUN 2u  /* it was tried, a span fell outside the
                                           group: E rewritten, usual reduce    */
+#define TSDBHIP_PATH_LOCKSTEP      4u  /* no downsampling, every span on one
+                                          cadence: k_lockstep's single pass   */
+#define TSDBHIP_PATH_DIRECT_REDO   8u  /* k_lockstep found a qualifier off the
+                                          proposal: the call ran again on the
+                                          proven (scan + reduce) path         */
 
 /* ---- row compaction (CompactionQueue.compact) -------------------------- */
 /*

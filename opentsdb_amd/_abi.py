@@ -6,9 +6,11 @@ and the test harness.
 """
 import ctypes as C
 
-ABI_VERSION = 5
+ABI_VERSION = 6
 PATH_ALIGNED_GROUP = 1  # tsdbhip_timing.paths (include/tsdbhip.h)
 PATH_ALIGNED_RERUN = 2
+PATH_LOCKSTEP = 4  # k_lockstep: one pass over the qualifiers and values of a lockstep group
+PATH_DIRECT_REDO = 8  # its proposal did not hold: the call ran again on the proven path
 
 OK = 0
 E_ILLEGAL_DATA = -1
@@ -90,7 +92,7 @@ class SgOut(C.Structure):
 
 
 HOT_NONE, HOT_DS_CHUNKS, HOT_DECODE_FAST, HOT_DECODE_GEN = 0, 1, 2, 3
-HOT_NAMES = {1: "k_ds_reg+k_ds_spans", 2: "k_decode_fast", 3: "k_decode_general", 4: "k_compact_quals+k_compact_vals", 5: "k_reduce"}
+HOT_NAMES = {1: "k_ds_reg+k_ds_spans", 2: "k_decode_fast", 3: "k_decode_general", 4: "k_compact_quals+k_compact_vals", 5: "k_reduce", 6: "k_lockstep"}
 
 
 class Timing(C.Structure):
@@ -109,6 +111,7 @@ class Timing(C.Structure):
         ("n_emitted", C.c_uint64),
         ("paths", C.c_uint32),
         ("reserved", C.c_uint32),
+        ("x_bytes", C.c_uint64),
     ]
 
 

@@ -37,6 +37,7 @@
 #include "k_ds_reg.hip"
 #include "k_compact.hip"
 #include "k_direct.hip"
+#include "k_lockstep.hip"
 #include "k_group.hip"
 
 using namespace tsdb;
@@ -230,6 +231,7 @@ static void timing_add(tsdbhip_ctx* c, const tsdbhip_timing& t) {  // (c->mu hel
   c->sum.n_grid += t.n_grid;
   c->sum.n_emitted += t.n_emitted;
   c->sum.paths |= t.paths;
+  c->sum.x_bytes += t.x_bytes;
   c->n_sum++;
 }
 
@@ -753,6 +755,54 @@ static void launch_reduce(Slot* ctx, unsigned blocks, const ReduceArgs& r, const
                        r, f);
 }
 
+// k_lockstep over the group (one instantiation per value width and type; the
+// mode follows: rate or float values reduce doubles, int values longs), then
+// the finalize of launch_reduce
+struct LsPlan {
+  LockstepArgs a;
+  bool w8, flt;
+};
+template <int AGG, bool RATE, uint32_t W, bool FLT>
+static void launch_lockstep_wf(Slot* ctx, unsigned blocks, const ReduceArgs& r, const LockstepArgs& a,
+                               const FinalArgs& f, bool finalize) {
+  constexpr int MODE = (RATE || FLT) ? MODE_DBL : MODE_INT;
+  if (AGG == 4 && MODE == MODE_INT) return;  // (integer dev reduces in one span-ordered pass: never lockstep)
+  HIPCHK(hipEventRecord(ctx->ev[8], ctx->stream));
+  hipLaunchKernelGGL((k_lockstep<AGG, MODE, RATE, W, FLT>), dim3(blocks), dim3(256), 0, ctx->stream, r, a);
+  HIPCHK(hipEventRecord(ctx->ev[9], ctx->stream));
+  if (!finalize) return;
+  if (f.n_chunks >= 64 && f.T >= 1024)
+    hipLaunchKernelGGL((k_chunks_cols<AGG, MODE, RATE, true>), dim3((unsigned)((f.T + 63) / 64)), dim3(64 * COLW), 0,
+                       ctx->stream, r, r, f, f.T, f.n_chunks);
+  else if (f.n_chunks >= 64)
+    hipLaunchKernelGGL((k_finalize_par<AGG, MODE, RATE>), dim3((unsigned)f.T), dim3(256), 0, ctx->stream, r, f);
+  else
+    hipLaunchKernelGGL((k_finalize_seq<AGG, MODE, RATE>), dim3(grid_for(f.T, 256)), dim3(256), 0, ctx->stream, r, f);
+}
+template <int AGG>
+static void launch_lockstep(Slot* ctx, bool rate, unsigned blocks, const ReduceArgs& r, const LsPlan& p,
+                            const FinalArgs& f, bool fin) {
+#define LS_GO(RT, W, F) launch_lockstep_wf<AGG, RT, W, F>(ctx, blocks, r, p.a, f, fin)
+  if (rate) {
+    if (p.w8) { if (p.flt) LS_GO(true, 8, true); else LS_GO(true, 8, false); }
+    else { if (p.flt) LS_GO(true, 4, true); else LS_GO(true, 4, false); }
+  } else {
+    if (p.w8) { if (p.flt) LS_GO(false, 8, true); else LS_GO(false, 8, false); }
+    else { if (p.flt) LS_GO(false, 4, true); else LS_GO(false, 4, false); }
+  }
+#undef LS_GO
+}
+static void dispatch_lockstep(Slot* ctx, int agg, bool rate, unsigned blocks, const ReduceArgs& r, const LsPlan& p,
+                              const FinalArgs& f, bool fin) {
+  switch (agg) {
+    case 0: return launch_lockstep<0>(ctx, rate, blocks, r, p, f, fin);
+    case 1: return launch_lockstep<1>(ctx, rate, blocks, r, p, f, fin);
+    case 2: return launch_lockstep<2>(ctx, rate, blocks, r, p, f, fin);
+    case 3: return launch_lockstep<3>(ctx, rate, blocks, r, p, f, fin);
+    default: return launch_lockstep<4>(ctx, rate, blocks, r, p, f, fin);
+  }
+}
+
 template <int AGG>
 static void dispatch_mode(Slot* ctx, int mode, bool rate, unsigned blocks, const ReduceArgs& r,
                           const FinalArgs& f, bool par, bool fin) {
@@ -894,6 +944,10 @@ struct Small {
   // k_grid_scan_blocks), and the agreed header words of the one collective
   // after the local grids (XH_*: MIN, or complemented MAX, over the ranks)
   unsigned long long ghash[2];
+  // the lockstep proposal (k_direct_opt): class keys [min, max, min, max];
+  // ls_broken: k_lockstep found a qualifier off the proposal (MAX over ranks)
+  unsigned long long ls_key[4];
+  uint32_t ls_broken, ls_pad;
   unsigned long long xh[14];  // (XH_N, + the aligned-group validity in an optimistic call)
 };
 // Small.xh slots of the grid-agreement header. Every rank decides from these
@@ -921,6 +975,7 @@ static Small small_init() {
   init.bound[2] = 0;
   init.bound[3] = ~0ull;
   init.fap_key[0] = init.fap_key[2] = ~0ull;
+  init.ls_key[0] = init.ls_key[2] = ~0ull;
   return init;
 }
 // Several MIN / MAX agreements on call-state fields as one MIN allreduce of a
@@ -935,6 +990,9 @@ struct XExtra { void* p; uint64_t count; XType t; XOp op; };
 static void xchg_minmax(Slot* ctx, Xchg* X, const XField* f, uint32_t n, uint64_t* sum_u64 = nullptr,
                         uint64_t* buf = nullptr, const XExtra* extra = nullptr, uint32_t n_extra = 0);
 constexpr size_t OUT_HDR = 1024;  // the Small snapshot ahead of the outputs
+// sharded double partials exchange rank-owned slices of G from this |G| on
+// (below it, one allgather of every rank's partials is the cheaper collective)
+constexpr uint64_t XSLICE_MIN_T = 65536;
 static_assert(sizeof(Small) <= OUT_HDR, "Small must fit the output header");
 
 // End of a call, after the finalize: the call state is snapshot ahead of the
@@ -1172,13 +1230,19 @@ static T* scratch_zero_kept(Slot* ctx, const char* name, size_t count, bool clea
 }
 
 // ------------------------------------------------------- the hot path ----
-static int spangroup_run(Slot* ctx, const tsdbhip_sg_desc* d, tsdbhip_sg_out* out) {
+// ls_allow: the lockstep proposal may be tried (k_direct_opt / k_lockstep);
+// false for the rerun after k_lockstep found a qualifier off the proposal
+constexpr int RC_REDO = 1000;
+static int spangroup_run_once(Slot* ctx, const tsdbhip_sg_desc* d, tsdbhip_sg_out* out, bool ls_allow) {
   const bool dev = (d->flags & TSDBHIP_DESC_DEVICE) != 0;
   const bool exact = (d->flags & TSDBHIP_EXACT_ORDER) != 0;
   // (a 1-rank communicator runs the same exchange code: tests use it)
   Xchg* X = (d->flags & TSDBHIP_SHARDED) ? ctx->x : nullptr;
   const bool sharded = X != nullptr;
-  if (X) X->n_coll = 0;
+  if (X) {
+    X->n_coll = 0;
+    X->x_bytes = 0;
+  }
   const uint32_t S = d->n_spans;
   const uint64_t R = d->n_rows;
   const bool rate = d->rate != 0;
@@ -1358,6 +1422,8 @@ static int spangroup_run(Slot* ctx, const tsdbhip_sg_desc* d, tsdbhip_sg_out* ou
   if (detail) HIPCHK(hipEventRecord(ctx->ev[1], st));
   bool chunk_marked = false;     // k_ds_spans marked G for the spans it took
   bool direct = false;           // k_direct_scan took the no-downsampling path
+  bool ls_try = false;           // k_direct_opt made the lockstep proposal
+  uint64_t* d_qoff = nullptr;    // (its per-span qualifier offsets)
   DirectArgs dg = {};
   const uint32_t* mark_list = nullptr, *mark_count = nullptr;
   if (n_kept) {
@@ -1412,6 +1478,17 @@ static int spangroup_run(Slot* ctx, const tsdbhip_sg_desc* d, tsdbhip_sg_out* ou
         // (spans per wave: 32 for big groups; fewer below ~64k spans, so a
         // small group still spreads over ~2048 waves instead of a handful)
         dg.batch = std::max<uint32_t>(1, std::min<uint32_t>(DIRB, n_kept / 2048));
+        // the lockstep proposal (k_lockstep.hip), where the reduce is not the
+        // span-ordered pass (EXACT_ORDER, integer dev): three qualifiers a
+        // span now, every other one proven by k_lockstep as it reduces
+        ls_try = ls_allow && !exact && (agg != TSDBHIP_AGG_DEV || rate);
+        if (ls_try) {
+          d_qoff = scratch<uint64_t>(ctx, "d_qoff", n_kept);
+          dg.ls_key = sm->ls_key;
+          dg.ls_other = &sm->cnt[5];
+          hipLaunchKernelGGL(k_direct_opt, dim3(grid_for(n_kept, 256)), dim3(256), 0, st, da, dg, row_ncells,
+                             row_val_len, d_qoff, sm->ls_key, &sm->cnt[5]);
+        }
         hipLaunchKernelGGL(k_direct_scan, dim3(grid_for(n_kept, 4 * dg.batch, 1u << 20)), dim3(256), 0, st, da, dg,
                            row_ncells, row_val_len);
         fa.span_list = dg.list;
@@ -1600,7 +1677,10 @@ static int spangroup_run(Slot* ctx, const tsdbhip_sg_desc* d, tsdbhip_sg_out* ou
       out->n_input_points = h.n_input;
       tm.n_grid = T;
       tm.paths |= TSDBHIP_PATH_ALIGNED_GROUP;
-      if (sharded) tm.n_collectives = X->n_coll;
+      if (sharded) {
+        tm.n_collectives = X->n_coll;
+        tm.x_bytes = X->x_bytes;
+      }
       if (ctx->hot_kernel) tm.hot_ms = ev_ms(ctx->ev[8], ctx->ev[9]);
       tm.hot_kernel = ctx->hot_kernel;
       tm.reduce_ms = ev_ms(ctx->ev[4], ctx->ev[5]);
@@ -1684,6 +1764,31 @@ static int spangroup_run(Slot* ctx, const tsdbhip_sg_desc* d, tsdbhip_sg_out* ou
     readback(ctx, &h, sm, sizeof h);  // sync 2 (no grid)
     after_sync2();
   }
+  // lockstep: every kept span proposed the one class key, and the grid is
+  // its pattern (sharded: no other rank put a point elsewhere). A rank whose
+  // proposal stood but whose grid is wider cannot use it: the call is marked
+  // broken and runs again on the proven path (every rank, after the exchange)
+  bool ls_use = false;
+  LsPlan lsp = {};
+  if (ls_try && h.cnt[5] == 0 && h.ls_key[0] != ~0ull && h.ls_key[0] == h.ls_key[1] && h.ls_key[2] == h.ls_key[3]) {
+    const uint32_t ln = (uint32_t)h.ls_key[0];
+    if (h.T == (uint64_t)(rate ? ln - 1 : ln)) {
+      ls_use = true;
+      lsp.a.d_voff = dg.voff;
+      lsp.a.d_qoff = d_qoff;
+      lsp.a.val = val;
+      lsp.a.qual = qual;
+      lsp.a.n = ln;
+      lsp.a.q0 = (uint32_t)(h.ls_key[2] & 0xFFFFu);
+      lsp.a.step = (uint32_t)(h.ls_key[2] >> 32);
+      lsp.a.broken = &sm->ls_broken;
+      lsp.w8 = ((lsp.a.q0 & 7u) == 7u);
+      lsp.flt = (lsp.a.q0 & 8u) != 0;
+      tm.paths |= TSDBHIP_PATH_LOCKSTEP;
+    } else {
+      HIPCHK(hipMemsetD32Async((hipDeviceptr_t)&sm->ls_broken, 1, 1, st));
+    }
+  }
   if (!empty_grid) {
     T = h.T;
     gridv = scratch<uint32_t>(ctx, "grid", T);
@@ -1693,7 +1798,7 @@ static int spangroup_run(Slot* ctx, const tsdbhip_sg_desc* d, tsdbhip_sg_out* ou
     // to the E path (their grid points are already marked; types, F* and
     // errors already counted)
     uint32_t* word_rank_f = scratch<uint32_t>(ctx, "word_rank_f", nwords);
-    const bool verify = direct && n_kept;
+    const bool verify = direct && n_kept && !ls_use;  // (lockstep: every span's points are G itself)
     dg.word_rank = word_rank;  // (block-local ranks + ga.block_sum)
     dg.bitmap = bitmap;
     const uint32_t eb = grid_for(nwords, 256);
@@ -1731,27 +1836,41 @@ static int spangroup_run(Slot* ctx, const tsdbhip_sg_desc* d, tsdbhip_sg_out* ou
   // error index's grid ranks)
   const bool bad_at_end = !sharded && n_kept <= 4096 && T <= 65536;
   // (an aligned group holds no E span, hence no bad cell)
-  if (n_kept && !bad_at_end && !fap_use)
+  // (an aligned or lockstep group holds no E span, hence no bad cell)
+  if (ls_use) bad.n_kept = 0;
+  if (n_kept && !bad_at_end && !fap_use && !ls_use)
     hipLaunchKernelGGL(k_bad_index, dim3(grid_for(n_kept, 256)), dim3(256), 0, st, bad, &sm->bad_at);
 
+  // ---- the reduce's shape: the span-ordered pass (integer dev before the
+  // (long) truncation, Aggregators.java:196-217, or EXACT_ORDER), exact
+  // integer partials, or order-dependent doubles; sharded doubles over a long
+  // grid exchange rank-owned slices of G (below) ----
+  const int mode = rate ? MODE_DBL : (!anyf ? MODE_INT : (!anyi ? MODE_DBL : MODE_DUAL));
+  const bool seq = exact || (agg == TSDBHIP_AGG_DEV && mode != MODE_DBL);
+  const bool int_parts = mode == MODE_INT && agg != TSDBHIP_AGG_DEV;
+  // (per rank (N-1)/N (esz + 17) B a point against (N-1) esz: a gain from 3
+  // ranks on; at 2 it is even, and the slices cost a second collective)
+  const bool sliced = sharded && T > 0 && !seq && !int_parts && X->nranks >= 3 && T >= XSLICE_MIN_T;
+  const uint64_t xs = sliced ? (T + X->nranks - 1) / X->nranks : 0;  // slice length (the last one shorter)
   // ---- output block: [Small snapshot | ts T | bits T | is_int T], written
-  // by the kernels straight into mapped pinned host memory when small ----
-  const bool small_out = T * 17 <= (256u << 10) && ctx->want_output;
-  map_out_reserve(ctx, OUT_HDR + (small_out ? 17 * T : 0));
-  uint8_t* outblk = small_out ? ctx->map_out_dev : scratch<uint8_t>(ctx, "outblk", OUT_HDR + 17 * T);
+  // by the kernels straight into mapped pinned host memory when small (a
+  // sliced exchange gathers the results in device memory: T padded to whole
+  // slices) ----
+  const uint64_t To = sliced ? xs * X->nranks : T;
+  const bool small_out = To * 17 <= (256u << 10) && ctx->want_output && !sliced;
+  map_out_reserve(ctx, OUT_HDR + (small_out ? 17 * To : 0));
+  uint8_t* outblk = small_out ? ctx->map_out_dev : scratch<uint8_t>(ctx, "outblk", OUT_HDR + 17 * To);
   int64_t* o_ts = (int64_t*)(outblk + OUT_HDR);
-  int64_t* o_bits = o_ts + T;
-  uint8_t* o_isint = (uint8_t*)(o_bits + T);
+  int64_t* o_bits = o_ts + To;
+  uint8_t* o_isint = (uint8_t*)(o_bits + To);
 
   // ---- reduce ----
   if (T > 0) {
-    const int mode = rate ? MODE_DBL : (!anyf ? MODE_INT : (!anyi ? MODE_DBL : MODE_DUAL));
     ctx->time_reduce = direct;
-    // integer dev is reduced in one span-ordered pass (and, sharded, in rank
-    // order): the reference's sequential Welford before the (long)
-    // truncation (Aggregators.java:196-217) admits no merge of partial
-    // states; EXACT_ORDER does the same for every aggregator
-    const bool seq = exact || (agg == TSDBHIP_AGG_DEV && mode != MODE_DBL);
+    // (integer dev is reduced in one span-ordered pass, and, sharded, in rank
+    // order: the reference's sequential Welford before the (long)
+    // truncation admits no merge of partial states; EXACT_ORDER does the
+    // same for every aggregator)
     FinalArgs fin;
     std::memset(&fin, 0, sizeof fin);
     fin.T = T; fin.n_chunks = 1; fin.grid = gridv; fin.fstar = fstar; fin.rate = rate;
@@ -1840,6 +1959,30 @@ static int spangroup_run(Slot* ctx, const tsdbhip_sg_desc* d, tsdbhip_sg_out* ou
       dispatch_reduce(ctx, agg, mode, rate, blocks, r, f, n_chunks >= 64, finalize);
       return r;
     };
+    // the lockstep group: tiles of LS_TILE grid points x chunks of spans
+    auto ls_reduce = [&](bool finalize) {
+      const uint32_t n_tiles = (uint32_t)((T + LS_TILE - 1) / LS_TILE);
+      static const uint64_t ls_waves = getenv("TSDBHIP_LS_WAVES") ? atoll(getenv("TSDBHIP_LS_WAVES")) : 16384;  // (TEMP A/B)
+      uint64_t want = std::max<uint64_t>(1, ls_waves / n_tiles);
+      want = std::min<uint64_t>(want, std::max<uint32_t>(1, n_kept / 64));
+      const uint32_t spc = (uint32_t)((n_kept + want - 1) / want);
+      const uint32_t n_chunks = (n_kept + spc - 1) / spc;
+      ReduceArgs r;
+      std::memset(&r, 0, sizeof r);
+      r.T = T;
+      r.n_chunks = n_chunks;
+      r.n_kept = n_kept;
+      partials(r, "p_", (uint64_t)n_chunks * T);
+      LsPlan p = lsp;
+      p.a.spc = spc;
+      p.a.n_tiles = n_tiles;
+      FinalArgs f = fin;
+      f.n_chunks = n_chunks;
+      ctx->hot_kernel = TSDBHIP_HOT_LOCKSTEP;
+      const uint64_t n_waves = (uint64_t)n_tiles * n_chunks;
+      dispatch_lockstep(ctx, agg, rate, (unsigned)((n_waves + 3) / 4), r, p, f, finalize);
+      return r;
+    };
     // the aligned group: its block partials reduced into the 1-chunk layout
     auto fap_reduce = [&](bool finalize) {
       ReduceArgs r;
@@ -1875,6 +2018,7 @@ static int spangroup_run(Slot* ctx, const tsdbhip_sg_desc* d, tsdbhip_sg_out* ou
     };
     if (!sharded) {
       if (fap_use) fap_reduce(true);
+      else if (ls_use) ls_reduce(true);
       else run_reduce(seq, true, nullptr);
     } else {
       const int nr = X->nranks, rk = X->rank;
@@ -1894,15 +2038,18 @@ static int spangroup_run(Slot* ctx, const tsdbhip_sg_desc* d, tsdbhip_sg_out* ou
           const std::vector<Fld> fp = fields(P, 0), fs = fields(S, 0);
           X->group_start(ctx);
           for (size_t i = 0; i < fp.size(); i++) X->broadcast(ctx, fp[i].p, fs[i].p, T * fp[i].esz, step);
-          if (step == 0) X->allreduce(ctx, &sm->bad_at, 1, X_U64, X_MIN);
+          if (step == 0) {
+            X->allreduce(ctx, &sm->bad_at, 1, X_U64, X_MIN);
+            X->allreduce(ctx, &sm->ls_broken, 1, X_U32, X_MAX);
+          }
           X->group_end(ctx);
         }
         HIPCHK(hipEventRecord(ctx->ev[7], st));
         src = S;
       } else {
         // this rank's chunks combined in order into one slot per t
-        ReduceArgs loc = fap_use ? fap_reduce(false) : run_reduce(false, false, nullptr);
-        if (mode == MODE_INT && agg != TSDBHIP_AGG_DEV) {
+        ReduceArgs loc = fap_use ? fap_reduce(false) : ls_use ? ls_reduce(false) : run_reduce(false, false, nullptr);
+        if (int_parts) {
           // exact integer partials: one allreduce per field (wrapping u64
           // sum, i64 min / max, count sum), no ordering needed
           ReduceArgs mine = loc;
@@ -1917,9 +2064,47 @@ static int spangroup_run(Slot* ctx, const tsdbhip_sg_desc* d, tsdbhip_sg_out* ou
           X->group_start(ctx);
           for (const Fld& f : fields(mine, 0)) X->allreduce(ctx, f.p, T, f.t, f.op);
           X->allreduce(ctx, &sm->bad_at, 1, X_U64, X_MIN);
+          X->allreduce(ctx, &sm->ls_broken, 1, X_U32, X_MAX);
           X->group_end(ctx);
           HIPCHK(hipEventRecord(ctx->ev[7], st));
           src = mine;
+        } else if (sliced) {
+          // doubles over a long grid (C4): rank q owns slice q of G (xs
+          // points). Each rank's combined partials of slice q reach rank q
+          // (alltoall), which merges them in rank order (chunk-then-rank, as
+          // unsharded; SpanGroup.java:647-667) and finalizes its slice; the
+          // slices' results are then gathered. Per rank (N-1)/N of the
+          // partials plus the results, instead of N-1 times the partials.
+          ReduceArgs mine = loc, recv = loc;
+          partials(mine, "m_", xs * nr);  // [T] used
+          partials(recv, "x_", xs * nr);  // [rank q][xs]: rank q's partials of this rank's slice
+          dispatch_combine(ctx, agg, mode, loc, mine, T, loc.n_chunks);
+          HIPCHK(hipEventRecord(ctx->ev[6], st));
+          const std::vector<Fld> fm = fields(mine, 0), fr = fields(recv, 0);
+          X->group_start(ctx);
+          for (size_t i = 0; i < fm.size(); i++) X->alltoall(ctx, fm[i].p, fr[i].p, xs * fm[i].esz);
+          X->allreduce(ctx, &sm->bad_at, 1, X_U64, X_MIN);
+          X->allreduce(ctx, &sm->ls_broken, 1, X_U32, X_MAX);
+          X->group_end(ctx);
+          const uint64_t g0 = (uint64_t)rk * xs, ns = g0 < T ? std::min<uint64_t>(xs, T - g0) : 0;
+          FinalArgs f = fin;
+          f.T = ns;
+          f.stride = xs;
+          f.n_chunks = (uint32_t)nr;
+          f.g_base = g0;
+          f.grid = gridv + g0;
+          f.out_ts = o_ts + g0;
+          f.out_bits = o_bits + g0;
+          f.out_isint = o_isint + g0;
+          recv.n_chunks = (uint32_t)nr;
+          if (ns) dispatch_final(ctx, agg, mode, rate, recv, f);
+          X->group_start(ctx);
+          X->allgather(ctx, o_ts + g0, o_ts, xs * 8);
+          X->allgather(ctx, o_bits + g0, o_bits, xs * 8);
+          X->allgather(ctx, o_isint + g0, o_isint, xs);
+          X->allreduce(ctx, &sm->nan_t, 1, X_U64, X_MIN);
+          X->group_end(ctx);
+          HIPCHK(hipEventRecord(ctx->ev[7], st));
         } else {
           // doubles (sums / Welford states depend on the order): every
           // rank's slot gathered, merged in rank order on every rank
@@ -1935,19 +2120,25 @@ static int spangroup_run(Slot* ctx, const tsdbhip_sg_desc* d, tsdbhip_sg_out* ou
           X->group_start(ctx);
           for (size_t i = 0; i < fm.size(); i++) X->allgather(ctx, fm[i].p, fa[i].p, T * fm[i].esz);
           X->allreduce(ctx, &sm->bad_at, 1, X_U64, X_MIN);
+          X->allreduce(ctx, &sm->ls_broken, 1, X_U32, X_MAX);
           X->group_end(ctx);
           HIPCHK(hipEventRecord(ctx->ev[7], st));
           src = all;
           n_src = (uint32_t)nr;
         }
       }
-      FinalArgs f = fin;
-      f.n_chunks = n_src;
-      src.n_chunks = n_src;
-      dispatch_final(ctx, agg, mode, rate, src, f);
+      if (!sliced) {
+        FinalArgs f = fin;
+        f.n_chunks = n_src;
+        src.n_chunks = n_src;
+        dispatch_final(ctx, agg, mode, rate, src, f);
+      }
     }
   } else if (sharded) {
+    X->group_start(ctx);
     X->allreduce(ctx, &sm->bad_at, 1, X_U64, X_MIN);
+    X->allreduce(ctx, &sm->ls_broken, 1, X_U32, X_MAX);
+    X->group_end(ctx);
   }
   // ---- end of call: snapshot + reset of the call state, bitmap cleared ----
   hipLaunchKernelGGL(k_call_end, dim3(bad_at_end ? 1u : grid_for(T, 256, 1024)), dim3(256), 0, st, sm, (Small*)ctx->map_out_dev,
@@ -1959,9 +2150,14 @@ static int spangroup_run(Slot* ctx, const tsdbhip_sg_desc* d, tsdbhip_sg_out* ou
   ctx->sm_ready = true;
   ctx->bitmap_clean = true;
   if (used_bitmap_x) ctx->bitmapx_clean = true;
+  if (ls_try && h.ls_broken) {  // (agreed over the ranks) the proposal did not hold: discard, run again
+    ctx->timing = tm;
+    return RC_REDO;
+  }
   if (sharded) {
     tm.exchange_ms = T > 0 ? ev_ms(ctx->ev[6], ctx->ev[7]) : 0.f;
     tm.n_collectives = X->n_coll;
+    tm.x_bytes = X->x_bytes;
   }
   if (detail) {
     tm.decode_ms = ev_ms(ctx->ev[1], ctx->ev[2]);
@@ -1995,8 +2191,8 @@ static int spangroup_run(Slot* ctx, const tsdbhip_sg_desc* d, tsdbhip_sg_out* ou
     // (a non-zero rank of an in-process sharded call: rank 0 returns the output)
   } else if (n_ok && small_out) {  // (already in the pinned staging with the header)
     std::memcpy(out->ts, hb + OUT_HDR, n_ok * 8);
-    std::memcpy(out->bits, hb + OUT_HDR + 8 * T, n_ok * 8);
-    std::memcpy(out->is_int, hb + OUT_HDR + 16 * T, n_ok);
+    std::memcpy(out->bits, hb + OUT_HDR + 8 * To, n_ok * 8);
+    std::memcpy(out->is_int, hb + OUT_HDR + 16 * To, n_ok);
   } else if (n_ok) {
     HIPCHK(hipMemcpyAsync(out->ts, o_ts, n_ok * 8, hipMemcpyDeviceToHost, st));
     HIPCHK(hipMemcpyAsync(out->is_int, o_isint, n_ok, hipMemcpyDeviceToHost, st));
@@ -2010,6 +2206,17 @@ static int spangroup_run(Slot* ctx, const tsdbhip_sg_desc* d, tsdbhip_sg_out* ou
   tm.alg_bytes = 0;
   ctx->timing = tm;
   return code;
+}
+
+// The call, and its rerun on the proven path when k_lockstep found a
+// qualifier off the lockstep proposal (every rank of a sharded call agrees
+// on that, so all of them rerun)
+static int spangroup_run(Slot* ctx, const tsdbhip_sg_desc* d, tsdbhip_sg_out* out) {
+  const int rc = spangroup_run_once(ctx, d, out, true);
+  if (rc != RC_REDO) return rc;
+  const int rc2 = spangroup_run_once(ctx, d, out, false);
+  ctx->timing.paths |= TSDBHIP_PATH_DIRECT_REDO;
+  return rc2;
 }
 
 // One call on a plain context: a slot of its pool; x = the exchange of a

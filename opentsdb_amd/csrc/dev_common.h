@@ -192,6 +192,13 @@ DEVI uint64_t wave_shr1_u64(uint64_t x, uint64_t old) {
                                                             0xF, 0xF, false);
   return ((uint64_t)hi << 32) | lo;
 }
+// lane l gets lane l+1's x; lane 63 gets `old` (DPP wave_shl:1)
+DEVI uint64_t wave_shl1_u64(uint64_t x, uint64_t old) {
+  const uint32_t lo = (uint32_t)__builtin_amdgcn_update_dpp((int)(uint32_t)old, (int)(uint32_t)x, 0x130, 0xF, 0xF, false);
+  const uint32_t hi = (uint32_t)__builtin_amdgcn_update_dpp((int)(uint32_t)(old >> 32), (int)(uint32_t)(x >> 32), 0x130,
+                                                            0xF, 0xF, false);
+  return ((uint64_t)hi << 32) | lo;
+}
 DEVI uint64_t shfl_up_u64(uint64_t v, int d) {
   uint32_t lo = __shfl_up((uint32_t)v, d), hi = __shfl_up((uint32_t)(v >> 32), d);
   return ((uint64_t)hi << 32) | lo;

@@ -43,7 +43,100 @@ struct DirectArgs {
   int32_t rate;
   uint32_t batch;      // spans per wave batch (<= DIRB): fewer for small groups, so
                        // they spread over more waves
+  // the lockstep proposal of k_direct_opt (null: none made): the spans'
+  // class keys [min, max] of (x0 << 32 | n) and of (step << 32 | q0), and the
+  // count of kept spans outside any class
+  const unsigned long long* ls_key;
+  const uint32_t* ls_other;
 };
+
+// ---- the lockstep proposal (k_lockstep.hip) ----
+// A span of one row with n >= 2 cells of one width W (8 or 4 B) whose
+// qualifiers at cells 0, 1 and n-1 agree with ts = x0 + c*step (same flags),
+// every point inside [start, end], proposes the class key (x0 << 32 | n,
+// step << 32 | q0); k_lockstep proves every other qualifier while it reduces.
+DEVI bool ls_probe(const DecodeArgs& a, const uint32_t* ncells, const uint32_t* vlen, uint32_t k, uint64_t& k1,
+                   uint64_t& k2, uint64_t& r0_out, uint64_t& qo_out, uint64_t& vo_out) {
+  const uint32_t s = a.kept[k];
+  const uint64_t r0 = a.span_row_start[s], r1 = a.span_row_start[s + 1];
+  const uint32_t n = a.sp_ncells[s];
+  if (!(r1 - r0 == 1 && n >= 2 && a.sp_q1[s] < 0 && a.sp_ovf_cell[s] < 0 && a.row_ok[r0] && ncells[r0] == n))
+    return false;
+  const uint32_t vb = vlen[r0] - 1;  // (n >= 2: a compacted row ends with its meta byte)
+  const uint32_t W = vb / n;
+  const uint64_t qo = a.row_qual_off[r0], vo = a.row_val_off[r0];
+  if (!((W == 8 || W == 4) && vb == W * n && (qo & 1) == 0 && (vo & (W - 1)) == 0)) return false;
+  const uint32_t q0 = load_qual(a.qual, qo), q1 = load_qual(a.qual, qo + 2), ql = load_qual(a.qual, qo + 2ull * (n - 1));
+  const uint32_t fl = q0 & 15u;
+  const uint32_t d0 = q0 >> 4, d1 = q1 >> 4, dl = ql >> 4;
+  if (!((fl & 7u) == W - 1 && (q1 & 15u) == fl && (ql & 15u) == fl && d1 > d0 &&
+        (uint64_t)d0 + (uint64_t)(n - 1) * (d1 - d0) == dl))
+    return false;
+  const uint32_t step = d1 - d0;
+  const int64_t first = (int64_t)a.row_base[r0] + d0;
+  const int64_t last = first + (int64_t)(n - 1) * step;
+  if (!(first >= a.start && last <= a.end && last < (1ll << 32))) return false;
+  k1 = ((uint64_t)first << 32) | n;
+  k2 = ((uint64_t)step << 32) | q0;
+  r0_out = r0;
+  qo_out = qo;
+  vo_out = vo;
+  return true;
+}
+
+// Lane per kept span: the proposal, and for a proposing span the direct-path
+// record k_direct_scan would write for it. The group is lockstep iff every
+// span proposes kept span 0's key: each wave compares its spans with that key
+// (span 0's probe, repeated by every wave: the same cached lines) and a wave
+// that finds a span off it stores 1 to n_other; block 0 publishes the key as
+// [min, max] pairs. No atomic, no read of a shared word (every wave polling
+// one word across the XCDs' L2s cost more than the probe itself).
+__global__ void __launch_bounds__(256) k_direct_opt(DecodeArgs a, DirectArgs g, const uint32_t* ncells,
+                                                    const uint32_t* vlen, uint64_t* qoff_out,
+                                                    unsigned long long* key, uint32_t* n_other) {
+  const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
+  if (a.n_kept == 0) return;
+  uint64_t k1 = 0, k2 = 0, r0 = 0, qo = 0, vo = 0;
+  bool cand = false;
+  if (k < a.n_kept) {
+    cand = ls_probe(a, ncells, vlen, k, k1, k2, r0, qo, vo);
+    if (cand) {
+      const uint32_t n = (uint32_t)k1, q0 = (uint32_t)k2 & 0xFFFFu;
+      g.info[k] = DIR_ON | ((q0 & 8u) ? DIR_FLT : 0u) | ((q0 & 7u) == 7u ? DIR_W8 : 0u);
+      g.n[k] = n;
+      g.x0[k] = (uint32_t)(k1 >> 32);
+      g.step[k] = (uint32_t)(k2 >> 32);
+      g.voff[k] = vo;
+      g.c0[k] = 0;
+      g.r0[k] = r0;
+      g.row_cpre[r0] = 0;
+      qoff_out[k] = qo;
+      a.e_len[k] = n;
+      a.e_bad[k] = -1;
+    }
+  }
+  // kept span 0's key (uniform: every lane probes the same span)
+  uint64_t z1 = 0, z2 = 0, zr, zq, zv;
+  const bool zc = ls_probe(a, ncells, vlen, 0u, z1, z2, zr, zq, zv);
+  const bool off = k < a.n_kept && (!cand || k1 != z1 || k2 != z2);
+  const int lane = lane_id();
+  if (zc && ballot(off) && lane == 0) *(volatile uint32_t*)n_other = 1u;
+  if (k == 0) {  // (block 0, lane 0: span 0's own probe decides when it proposes nothing)
+    if (!zc) *(volatile uint32_t*)n_other = 1u;
+    else {
+      key[0] = key[1] = z1;
+      key[2] = key[3] = z2;
+    }
+  }
+}
+
+// The group is lockstep: one class key over every kept span (read after
+// k_direct_opt, the same on every wave).
+DEVI bool ls_lockstep(const DirectArgs& g) {
+  if (!g.ls_key) return false;  // (plain loads: written by the previous kernel)
+  const unsigned long long* k = g.ls_key;
+  return *g.ls_other == 0 && k[0] != ~0ull && k[0] == k[1] && k[2] == k[3];
+}
 
 // Marks {xf + p*step : 0 <= p < np} (all inside [lo, hi]) in the grid bitmap;
 // a word already holding the bits skips the atomic.
@@ -110,6 +203,22 @@ __global__ void __launch_bounds__(256) k_direct_scan(DecodeArgs a, DirectArgs g,
   const int lane = lane_id();
   const uint32_t wave = (blockIdx.x * blockDim.x + threadIdx.x) / WAVE;
   const uint32_t nwaves = gridDim.x * blockDim.x / WAVE;
+  if (ls_lockstep(g)) {
+    // every span proposed the one key: wave 0 marks its pattern and the
+    // group's type (F*: a float series' first point, SpanGroup.java:632-645);
+    // the spans' records are k_direct_opt's, their proof is k_lockstep's
+    if (wave == 0) {
+      const uint64_t k1 = g.ls_key[0], k2 = g.ls_key[2];
+      const uint32_t x0 = (uint32_t)(k1 >> 32), n = (uint32_t)k1, step = (uint32_t)(k2 >> 32);
+      const bool flt = (k2 & 8u) != 0;
+      direct_mark(g, g.rate ? (int64_t)x0 + step : (int64_t)x0, step, g.rate ? n - 1 : n);
+      if (lane == 0) {
+        atomicOr(&a.gflags[flt ? 0 : 1], 1u);
+        if (flt && !a.rate) atomicMax(a.fstar, (unsigned long long)x0 + 1);
+      }
+    }
+    return;
+  }
   Pending pend = {0u, 0u};
   bool any_f = false, any_i = false;
   int64_t fs = 0;

@@ -1,0 +1,208 @@
+// k_lockstep.hip — the no-downsampling reduction of a lockstep group: every
+// kept span one row whose cells sit at x0 + c*step for c = 0..n-1 with the
+// same (x0, n, step), value width and type (C3: 1M counters written at the
+// same 1 s cadence). Then (SpanGroup.java:510-608) the union grid G is that
+// sequence (rate: from its second point), every span is active at every t of
+// G, the SGIterator never interpolates (x == x0 at every emission time,
+// :702-730), and the rate is each span's own constant-step difference
+// (:741-755, no Q5 state: no t lies before a span's second point). The value
+// at G[g] is the cross-series aggregate of cell g (rate: of cells g and g+1),
+// in span order (Aggregators.java:76-243).
+//
+// k_direct_opt (k_direct.hip) proposes the group from three qualifiers a span
+// (cells 0, 1 and n-1: the cadence, width and type); this kernel proves the
+// proposal while it streams: every cell's qualifier is compared with
+// (x0 + c*step - base) << 4 | flags as the values are read, one pass over the
+// reference's bytes (2 B of qualifier + W B of value a point) instead of the
+// direct path's qualifier scan followed by a value pass. A mismatch sets
+// `broken`; the call's results are then discarded and the call runs again on
+// the proven path (spangroup_run, TSDBHIP_PATH_DIRECT_REDO).
+//
+// Work unit: one wave = a tile of 512 grid points (8 consecutive points a
+// lane: one 16-B qualifier load and 2 / 4 16-B value loads a span) x a chunk
+// of spans, the spans streamed in order with the next span's loads in flight
+// while the current one is accumulated; per-t partials [n_chunks][T] in the
+// layout of k_reduce, combined in chunk order by the same finalize / exchange.
+#pragma once
+#include "dev_common.h"
+#include "k_reduce.hip"
+
+namespace tsdb {
+
+constexpr uint32_t LS_TILE = 512;  // grid points a wave (8 a lane)
+
+struct LockstepArgs {
+  const uint64_t* d_voff;  // [n_kept] value byte offset of the span's cell 0
+  const uint64_t* d_qoff;  // [n_kept] qualifier byte offset of the span's cell 0
+  const uint8_t* val;
+  const uint8_t* qual;
+  uint32_t n;              // cells a span
+  uint32_t q0;             // qualifier of cell 0 (delta << 4 | flags), the same in every span
+  uint32_t step;
+  uint32_t spc;            // spans a chunk
+  uint32_t n_tiles;
+  uint32_t* broken;        // [1] set when a qualifier differs from the proposal
+};
+
+template <uint32_t W, bool FLT>
+DEVI int64_t ls_bits(uint64_t raw) {
+  if (W == 8) return (int64_t)bswap64(raw);
+  const uint32_t u = bswap32((uint32_t)raw);
+  if (FLT) return dbits((double)__uint_as_float(u));
+  return (int64_t)(int32_t)u;
+}
+
+// One span's bytes for this lane: cells c0 .. c0+7 (values as 8 raw words,
+// qualifiers as 4 dwords of big-endian pairs) and, rate, the cell after the
+// tile (the last lane's next cell).
+template <uint32_t W>
+struct LsRaw {
+  uint32_t v[2 * W];  // W = 8: 16 dwords; W = 4: 8 dwords
+  uint32_t q[4];
+  uint64_t nxt;
+};
+
+template <uint32_t W, bool RATE>
+DEVI void ls_load(const LockstepArgs& L, uint32_t k, uint32_t c0, uint32_t tile_end, LsRaw<W>& o) {
+  const uint64_t vo = L.d_voff[k], qo = L.d_qoff[k];  // (uniform: scalar loads)
+  const __amdgpu_buffer_rsrc_t rv = __builtin_amdgcn_make_buffer_rsrc((void*)(L.val + vo), 0, (int)(L.n * W), 0x00020000);
+  // (buffer range checks are per dword: a range ending inside a dword would
+  // zero the row's last qualifier with its neighbour's bytes; whole 16-B
+  // groups instead, the bytes past the row are masked)
+  const __amdgpu_buffer_rsrc_t rq =
+      __builtin_amdgcn_make_buffer_rsrc((void*)(L.qual + qo), 0, (int)((2u * L.n + 15u) & ~15u), 0x00020000);
+#pragma unroll
+  for (uint32_t i = 0; i < W / 2; i++) {
+    const auto x = __builtin_amdgcn_raw_buffer_load_b128(rv, (int)(c0 * W + 16u * i), 0, 0);
+    o.v[4 * i] = x[0]; o.v[4 * i + 1] = x[1]; o.v[4 * i + 2] = x[2]; o.v[4 * i + 3] = x[3];
+  }
+  const auto y = __builtin_amdgcn_raw_buffer_load_b128(rq, (int)(2u * c0), 0, 0);
+  o.q[0] = y[0]; o.q[1] = y[1]; o.q[2] = y[2]; o.q[3] = y[3];
+  o.nxt = 0;
+  if (RATE && tile_end < L.n) {  // (uniform) the cell after the tile: the last lane's cur of its 8th point
+    const uint8_t* p = L.val + vo + (uint64_t)W * tile_end;
+    o.nxt = W == 8 ? *(const uint64_t*)p : (uint64_t)*(const uint32_t*)p;
+  }
+}
+
+template <int AGG, int MODE, bool RATE, uint32_t W, bool FLT>
+__global__ void __launch_bounds__(256) k_lockstep(ReduceArgs r, LockstepArgs L) {
+  const int lane = lane_id();
+  // (uniform: the span loop's offsets and buffer descriptors stay scalar)
+  const uint32_t wave = __builtin_amdgcn_readfirstlane((blockIdx.x * blockDim.x + threadIdx.x) / WAVE);
+  if (wave >= L.n_tiles * r.n_chunks) return;
+  const uint32_t tile = wave % L.n_tiles, chunk = wave / L.n_tiles;
+  const uint32_t k0 = chunk * L.spc, k1 = min(r.n_kept, k0 + L.spc);
+  if (k0 >= k1) return;
+  const uint32_t c0 = tile * LS_TILE + 8u * (uint32_t)lane;  // this lane's first grid point (and cell)
+  const uint32_t tile_end = tile * LS_TILE + LS_TILE;
+  const uint32_t n = L.n;
+  // the qualifiers of cells c0 .. c0+7 under the proposal, as loaded (two
+  // big-endian u16 a dword), and the cells of the row (c < n)
+  uint32_t qexp[4], qmask[4];
+  {
+    const uint32_t s16 = L.step << 4;
+#pragma unroll
+    for (int j = 0; j < 4; j++) {
+      const uint32_t ca = c0 + 2u * (uint32_t)j;
+      const uint32_t qa = L.q0 + ca * s16, qb = qa + s16;  // (< 2^16 for every cell of the row)
+      const uint32_t x = (qa & 0xFFFFu) | (qb << 16);
+      qexp[j] = __builtin_amdgcn_perm(x, x, 0x02030001u);  // bytes (1, 0, 3, 2): big-endian halves
+      qmask[j] = (ca < n ? 0x0000FFFFu : 0u) | (ca + 1 < n ? 0xFFFF0000u : 0u);
+    }
+  }
+  const uint64_t T = r.T;
+  const bool full = (uint64_t)tile_end <= T;  // (uniform) every point of the tile is in G
+  bool valid[8];
+#pragma unroll
+  for (int i = 0; i < 8; i++) valid[i] = (uint64_t)(c0 + i) < T;
+  // rate: (y_cur - y_prev) / step; a power-of-two step divides exactly as a
+  // product with its exact reciprocal (same IEEE result)
+  const uint32_t step = L.step;
+  const bool p2 = (step & (step - 1)) == 0;
+  const double rs = __builtin_amdgcn_ldexp(1.0, -(int)__builtin_ctz(step | (1u << 31)));
+  const double sd = (double)step;
+
+  Acc acc[8];
+#pragma unroll
+  for (int i = 0; i < 8; i++) acc_init(acc[i]);
+  uint32_t bad = 0;
+
+  auto process = [&](const LsRaw<W>& cur, uint32_t k) {
+#pragma unroll
+    for (int j = 0; j < 4; j++) bad |= (cur.q[j] ^ qexp[j]) & qmask[j];
+    int64_t b[8];
+#pragma unroll
+    for (int i = 0; i < 8; i++) {
+      const uint64_t raw = W == 8 ? ((uint64_t)cur.v[2 * i + 1] << 32) | cur.v[2 * i] : (uint64_t)cur.v[i];
+      b[i] = ls_bits<W, FLT>(raw);
+    }
+    const uint32_t cnt = k - k0;  // values before this one, in every slot
+    // dev (double path, Aggregators.java:219-238): every span is active at
+    // every t, so the Welford count is the same in all eight slots: one
+    // reciprocal a span (wf_push_rcp's) instead of one a value
+    double wf_r = 0.0;
+    if (AGG == 4 && MODE != MODE_INT && cnt > 0) {
+      const double dn = (double)(cnt + 1);
+      wf_r = __builtin_amdgcn_rcp(dn);
+      wf_r = __builtin_fma(__builtin_fma(-dn, wf_r, 1.0), wf_r, wf_r);  // one Newton step
+    }
+    double y[8];
+    if (RATE) {
+      double d[9];
+#pragma unroll
+      for (int i = 0; i < 8; i++) d[i] = to_double(b[i], FLT);
+      // cell c0 + 8: the next lane's first cell; the last lane's from `nxt`
+      const uint64_t b8 = wave_shl1_u64((uint64_t)b[0], (uint64_t)ls_bits<W, FLT>(cur.nxt));
+      d[8] = to_double((int64_t)b8, FLT);
+      if (p2) {
+#pragma unroll
+        for (int i = 0; i < 8; i++) y[i] = (d[i + 1] - d[i]) * rs;
+      } else {
+#pragma unroll
+        for (int i = 0; i < 8; i++) y[i] = (d[i + 1] - d[i]) / sd;
+      }
+    } else {
+#pragma unroll
+      for (int i = 0; i < 8; i++) y[i] = MODE == MODE_INT ? 0.0 : to_double(b[i], FLT);
+    }
+#pragma unroll
+    for (int i = 0; i < 8; i++) {
+      if (!full && !valid[i]) continue;
+      if (AGG == 4 && MODE != MODE_INT) {
+        Welford& w = acc[i].wd;
+        if (cnt == 0) {
+          w.mean = y[i];
+          w.n = 1;
+        } else {
+          w.n++;
+          const double dd = y[i] - w.mean;
+          const double nm = __builtin_fma(dd, wf_r, w.mean);
+          w.var += dd * (y[i] - nm);
+          w.mean = nm;
+        }
+        acc[i].cnt++;
+      } else {
+        acc_push<AGG, MODE>(acc[i], RATE ? 0 : b[i], y[i]);
+      }
+    }
+  };
+  // two register sets: the next span's loads are in flight while one is
+  // accumulated (the last span reloads itself, so the loads stay straight-line)
+  LsRaw<W> ra, rb;
+  ls_load<W, RATE>(L, k0, c0, tile_end, ra);
+  for (uint32_t k = k0;;) {
+    ls_load<W, RATE>(L, min(k + 1, k1 - 1), c0, tile_end, rb);
+    process(ra, k);
+    if (++k >= k1) break;
+    ls_load<W, RATE>(L, min(k + 1, k1 - 1), c0, tile_end, ra);
+    process(rb, k);
+    if (++k >= k1) break;
+  }
+  if (ballot(bad != 0) && lane == 0) atomicOr(L.broken, 1u);
+#pragma unroll
+  for (int i = 0; i < 8; i++)
+    if (valid[i]) acc_store<AGG, MODE>(r, (uint64_t)chunk * T + c0 + i, acc[i]);
+}
+
+}  // namespace tsdb

@@ -959,6 +959,8 @@ struct FinalArgs {
   uint8_t* out_isint;
   int64_t* out_bits;
   unsigned long long* nan_t; // [1] min t index with NaN/Inf double
+  uint64_t g_base;           // global index of point 0 (a rank's slice of G; nan_t is global)
+  uint64_t stride;           // partials' stride between chunks (0: T)
 };
 
 template <int AGG, int MODE, bool RATE>
@@ -972,7 +974,7 @@ DEVI void finalize_one(const FinalArgs& f, uint64_t g, const Acc& a) {
     else if (AGG == 3) d = a.da / (double)(int32_t)a.cnt;
     else if (AGG == 4) d = wf_result(a.wd);
     else d = (a.flag & 2u) ? __longlong_as_double(0x7ff8000000000000LL) : a.da;
-    if (d != d || isinf(d)) atomicMin(f.nan_t, (unsigned long long)g);
+    if (d != d || isinf(d)) atomicMin(f.nan_t, (unsigned long long)(f.g_base + g));
     bits = dbits(d);
   } else {
     if (AGG == 3) bits = ldiv(a.ia, (int64_t)(int32_t)a.cnt);
@@ -991,11 +993,12 @@ template <int AGG, int MODE, bool RATE>
 __global__ void __launch_bounds__(256) k_finalize_seq(ReduceArgs r, FinalArgs f) {
   const uint64_t g = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (g >= f.T) return;
+  const uint64_t st = f.stride ? f.stride : f.T;
   Acc a;
   acc_load<AGG, MODE>(r, g, a);
   for (uint32_t c = 1; c < f.n_chunks; c++) {
     Acc b;
-    acc_load<AGG, MODE>(r, (uint64_t)c * f.T + g, b);
+    acc_load<AGG, MODE>(r, (uint64_t)c * st + g, b);
     acc_merge<AGG, MODE>(a, b);
   }
   finalize_one<AGG, MODE, RATE>(f, g, a);
@@ -1047,7 +1050,17 @@ __global__ void __launch_bounds__(64 * COLW) k_chunks_cols(ReduceArgs r, ReduceA
   Acc a;
   acc_init(a);
   if (g < T) {
-    for (uint32_t c = c0; c < c1; c++) {
+    // 8 chunks' partials loaded before they are merged (in order): one memory
+    // round trip per 8 chunks instead of one per chunk (C3: ~128 a wave)
+    uint32_t c = c0;
+    for (; c + 8 <= c1; c += 8) {
+      Acc b[8];
+#pragma unroll
+      for (int u = 0; u < 8; u++) acc_load<AGG, MODE>(r, (uint64_t)(c + u) * T + g, b[u]);
+#pragma unroll
+      for (int u = 0; u < 8; u++) acc_merge<AGG, MODE>(a, b[u]);
+    }
+    for (; c < c1; c++) {
       Acc b;
       acc_load<AGG, MODE>(r, (uint64_t)c * T + g, b);
       acc_merge<AGG, MODE>(a, b);

@@ -35,6 +35,10 @@ struct Xchg {
   // collective launches of the current call: one per group (RCCL issues a
   // group's operations as one launch at its end) or ungrouped operation
   uint32_t n_coll = 0;
+  // bytes this rank receives in the current call's collectives (algorithmic:
+  // a ring allreduce 2(N-1)/N of the buffer, an allgather (N-1) blocks, a
+  // broadcast one buffer off the root, an alltoall (N-1) blocks)
+  uint64_t x_bytes = 0;
   int depth = 0;
   virtual ~Xchg() {}
   void group_start(Slot* ctx) {
@@ -48,15 +52,24 @@ struct Xchg {
   }
   void allreduce(Slot* ctx, void* buf, size_t count, XType t, XOp op) {
     if (!depth) n_coll++;
+    x_bytes += 2 * (uint64_t)(nranks - 1) * count * xsize(t) / nranks;
     do_allreduce(ctx, buf, count, t, op);
   }
   void allgather(Slot* ctx, const void* send, void* recv, size_t bytes) {
     if (!depth) n_coll++;
+    x_bytes += (uint64_t)(nranks - 1) * bytes;
     do_allgather(ctx, send, recv, bytes);
   }
   void broadcast(Slot* ctx, const void* send, void* recv, size_t bytes, int root) {
     if (!depth) n_coll++;
+    if (rank != root) x_bytes += bytes;
     do_broadcast(ctx, send, recv, bytes, root);
+  }
+  // recv[q * bytes, (q+1) * bytes) = rank q's send[rank * bytes, (rank+1) * bytes)
+  void alltoall(Slot* ctx, const void* send, void* recv, size_t bytes) {
+    if (!depth) n_coll++;
+    x_bytes += (uint64_t)(nranks - 1) * bytes;
+    do_alltoall(ctx, send, recv, bytes);
   }
 
  protected:
@@ -68,6 +81,7 @@ struct Xchg {
   virtual void do_allgather(Slot* ctx, const void* send, void* recv, size_t bytes) = 0;
   // every rank's recv = root's send (the root's recv too)
   virtual void do_broadcast(Slot* ctx, const void* send, void* recv, size_t bytes, int root) = 0;
+  virtual void do_alltoall(Slot* ctx, const void* send, void* recv, size_t bytes) = 0;
 };
 
 // ---------------------------------------------------------------- RCCL ----
@@ -95,6 +109,15 @@ struct RcclXchg : Xchg {
   }
   void do_broadcast(Slot* ctx, const void* send, void* recv, size_t bytes, int root) override {
     NCCLCHK(ncclBroadcast(send, recv, bytes, ncclUint8, root, comm, ctx->stream));
+  }
+  // point-to-point pairs in one group (a nested group inside a caller's)
+  void do_alltoall(Slot* ctx, const void* send, void* recv, size_t bytes) override {
+    NCCLCHK(ncclGroupStart());
+    for (int q = 0; q < nranks; q++) {
+      NCCLCHK(ncclSend((const char*)send + (size_t)q * bytes, bytes, ncclUint8, q, comm, ctx->stream));
+      NCCLCHK(ncclRecv((char*)recv + (size_t)q * bytes, bytes, ncclUint8, q, comm, ctx->stream));
+    }
+    NCCLCHK(ncclGroupEnd());
   }
 };
 
@@ -182,7 +205,17 @@ struct LocalXchg : Xchg {
     publish(ctx, send);
     for (int q = 0; q < nranks; q++) {
       if (q != rank) HIPCHK(hipStreamWaitEvent(ctx->stream, G->ready[q], 0));
-      copy_from(ctx, (char*)recv + (size_t)q * bytes, q, G->ptr[q], bytes);
+      char* dst = (char*)recv + (size_t)q * bytes;
+      if (q == rank && dst == (const char*)send) continue;  // (in place)
+      copy_from(ctx, dst, q, G->ptr[q], bytes);
+    }
+    retire(ctx);
+  }
+  void do_alltoall(Slot* ctx, const void* send, void* recv, size_t bytes) override {
+    publish(ctx, send);
+    for (int q = 0; q < nranks; q++) {
+      if (q != rank) HIPCHK(hipStreamWaitEvent(ctx->stream, G->ready[q], 0));
+      copy_from(ctx, (char*)recv + (size_t)q * bytes, q, (const char*)G->ptr[q] + (size_t)rank * bytes, bytes);
     }
     retire(ctx);
   }

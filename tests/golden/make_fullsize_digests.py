@@ -12,7 +12,14 @@ doubles bit-exactly under TSDBHIP_EXACT_ORDER, whose span-ordered sums are
 the reference's order). The inputs are bench.py's own generator
 (synth.jittered_packed, seed 4), deterministic across machines.
 
-Usage: python tests/golden/make_fullsize_digests.py   (from the repo root)
+The "_abs" cases run the same groups on |value| (synth.jittered_packed
+absval=True): their aggregate is the sum of |terms| the default-order
+(chunk-parallel) double sums are checked against, so the
+GPU's run of them is first matched bit-exactly (EXACT_ORDER) to these
+digests and only then used as the tolerance scale.
+
+Usage: python tests/golden/make_fullsize_digests.py [--force]   (from the repo root;
+existing entries are kept unless --force)
 """
 import hashlib
 import json
@@ -25,15 +32,17 @@ ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)
 sys.path.insert(0, ROOT)
 sys.path.insert(0, os.path.join(ROOT, "oracle"))
 
-# (name, generator, aggregator): bench.py's C4 lines
-CASES = [("c4_sum", "jitter", 0), ("c4i_sum", "jitter_int", 0), ("c4_avg", "jitter", 3)]
+# (name, generator, aggregator, |values|): bench.py's C4 lines, and the |terms| scales of
+# the double-path ones
+CASES = [("c4_sum", "jitter", 0, False), ("c4i_sum", "jitter_int", 0, False), ("c4_avg", "jitter", 3, False),
+         ("c4_sum_abs", "jitter", 0, True), ("c4_avg_abs", "jitter", 3, True)]
 N_SERIES, N_POINTS, SEED = 1000, 11500, 4
 
 
-def spanset(gen):
+def spanset(gen, absval=False):
     from opentsdb_amd import synth
     ff, fc = (0.5, 0.01) if gen == "jitter" else (0.0, 0.0)
-    return synth.jittered_packed(N_SERIES, N_POINTS, seed=SEED, float_frac=ff, float_cell_frac=fc)
+    return synth.jittered_packed(N_SERIES, N_POINTS, seed=SEED, float_frac=ff, float_cell_frac=fc, absval=absval)
 
 
 def digest(ts, isi, bits):
@@ -46,24 +55,28 @@ def digest(ts, isi, bits):
 def one(case):
     import oracle
     from opentsdb_amd import _abi
-    name, gen, agg = case
-    ss = spanset(gen)
+    name, gen, agg, absval = case
+    ss = spanset(gen, absval)
     t = time.time()
     o = oracle.spangroup(ss, 0, (1 << 32) - 1, agg, capacity=ss.n_cells() + 16)
     d = digest(o.ts, o.is_int, o.bits)
     d.update(code=int(o.code), n_input=int(o.n_input_points), gen=gen, agg=agg, n_series=N_SERIES,
-             n_points=N_POINTS, seed=SEED, oracle_s=round(time.time() - t, 1))
+             n_points=N_POINTS, seed=SEED, oracle_s=round(time.time() - t, 1), absval=absval)
     return name, d
 
 
 def main():
-    out = {"about": "sha256 of the oracle's (ts int64 LE, is_int u8, bits int64 LE) arrays on bench.py's C4 "
-                    "workloads at full size; made by tests/golden/make_fullsize_digests.py"}
-    with ProcessPoolExecutor(max_workers=len(CASES)) as ex:
-        for name, d in ex.map(one, CASES):
+    path = os.path.join(os.path.dirname(os.path.abspath(__file__)), "fullsize_digests.json")
+    out = {}
+    if os.path.exists(path) and "--force" not in sys.argv:
+        out = json.load(open(path))
+    out["about"] = ("sha256 of the oracle's (ts int64 LE, is_int u8, bits int64 LE) arrays on bench.py's C4 "
+                    "workloads at full size (_abs: on |values|); made by tests/golden/make_fullsize_digests.py")
+    todo = [c for c in CASES if c[0] not in out]
+    with ProcessPoolExecutor(max_workers=max(1, len(todo))) as ex:
+        for name, d in ex.map(one, todo):
             out[name] = d
             print(name, d, flush=True)
-    path = os.path.join(os.path.dirname(os.path.abspath(__file__)), "fullsize_digests.json")
     with open(path, "w") as f:
         json.dump(out, f, indent=1, sort_keys=True)
 

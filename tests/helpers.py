@@ -61,3 +61,16 @@ def assert_same(g, o, rtol=1e-9, exact_double=False, check_err_index=True, abs_s
                                f"{int(np.nonzero(bad)[0][0])}: err {err[bad][0]!r}, sum|terms| {sc[bad][0]!r}")
     else:
         np.testing.assert_allclose(gd, od, rtol=rtol, atol=0, err_msg="double values")
+
+
+def corrupt_qual(ss, span, cell, fn):
+    """A copy of the SpanSet with one qualifier (cell `cell` of span `span`'s
+    first row) rewritten by fn(q) -> q' (16-bit host-order values)."""
+    qb = ss.qual_bytes.copy()
+    r = int(ss.span_row_start[span])
+    off = int(ss.row_qual_off[r]) + 2 * cell
+    q = (int(qb[off]) << 8) | int(qb[off + 1])
+    q2 = fn(q) & 0xFFFF
+    qb[off], qb[off + 1] = q2 >> 8, q2 & 0xFF
+    return packing.SpanSet(ss.span_row_start, ss.row_base, ss.row_ncells, ss.row_qual_off, ss.row_val_off,
+                           ss.row_val_len, qb, ss.val_bytes)

@@ -175,19 +175,40 @@ def test_c4_million_point_union(ctx, gen, agg):
     g = core.run_spanset(ctx, ss, 0, U32MAX, agg)
     o = oracle.spangroup(ss, 0, U32MAX, agg, capacity=ss.n_cells() + 16)
     assert o.code == 0 and len(o.ts) > 1_000_000
-    assert_same(g, o, abs_scale=abs_bound(ctx, 100, 11500, 4, ff, fc, agg, o.ts))
+    assert_same(g, o, abs_scale=abs_bound(100, 11500, 4, ff, fc, agg, o.ts))
 
 
-def abs_bound(ctx, n_series, n_points, seed, ff, fc, agg, ts):
-    """Per output point, the same aggregation over the |values| of the same
-    series (synth.jittered_packed(absval=True)): an upper bound of the
+def as_values(isi, bits):
+    return np.where(isi.astype(bool), bits.astype(np.float64), bits.view(np.float64))
+
+
+def abs_bound(n_series, n_points, seed, ff, fc, agg, ts):
+    """Per output point, the oracle's aggregation over the |values| of the
+    same series (synth.jittered_packed(absval=True)): an upper bound of the
     aggregated |terms| a mixed-sign double sum is rounded against (SURVEY.md
     §8(d): C4's tolerance is relative to sum|x|, not to a result that can
-    cancel to ~0)."""
+    cancel to ~0). From the CPU oracle, so no GPU result sets its own
+    tolerance."""
     sa = synth.jittered_packed(n_series, n_points, seed=seed, float_frac=ff, float_cell_frac=fc, absval=True)
-    rc, ts_a, isi_a, bits_a, _, _ = core.run_spanset(ctx, sa, 0, U32MAX, agg)
-    assert rc == 0 and np.array_equal(ts_a, ts)
-    return np.where(isi_a.astype(bool), bits_a.astype(np.float64), bits_a.view(np.float64))
+    o = oracle.spangroup(sa, 0, U32MAX, agg, capacity=sa.n_cells() + 16)
+    assert o.code == 0 and np.array_equal(o.ts, ts)
+    return as_values(o.is_int, o.bits)
+
+
+def abs_bound_full(ctx, e, name):
+    """abs_bound at the bench's own size (1000 series, where the oracle takes
+    ~3 min): the GPU's EXACT_ORDER run of the |values| group, accepted only
+    once it matches the oracle's digest of that run bit for bit
+    (tests/golden/fullsize_digests.json, "<name>_abs")."""
+    d = json.load(open(DIGESTS))[name + "_abs"]
+    ff, fc = (0.5, 0.01) if e["gen"] == "jitter" else (0.0, 0.0)
+    sa = synth.jittered_packed(e["n_series"], e["n_points"], seed=e["seed"], float_frac=ff, float_cell_frac=fc,
+                               absval=True)
+    rc, ts, isi, bits, _, _ = core.run_spanset(ctx, sa, 0, U32MAX, e["agg"], exact=True)
+    assert rc == d["code"] and len(ts) == d["n_out"]
+    assert sha(ts, "<i8") == d["ts"] and sha(isi, "u1") == d["is_int"] and sha(bits, "<i8") == d["bits"], \
+        "the |values| run differs from the oracle's digest"
+    return as_values(isi, bits)
 
 
 @pytest.mark.gpu
@@ -232,8 +253,39 @@ def test_c4_full_size(ctx, name):
     assert sha(ts, "<i8") == e["ts"], "timestamps differ from the oracle"
     assert sha(isi, "u1") == e["is_int"], "isInteger differs from the oracle"
     assert sha(bits, "<i8") == e["bits"], "value bits (EXACT_ORDER) differ from the oracle"
-    assert_same(g, oracle.Result(0, ts, isi, bits, n_in, -1), rtol=1e-9,
-                abs_scale=abs_bound(ctx, e["n_series"], e["n_points"], e["seed"], ff, fc, e["agg"], ts))
+    sc = abs_bound_full(ctx, e, name) if e["gen"] == "jitter" else None
+    assert_same(g, oracle.Result(0, ts, isi, bits, n_in, -1), rtol=1e-9, abs_scale=sc)
+
+
+@pytest.mark.gpu
+@pytest.mark.timeout(600)
+@pytest.mark.parametrize("name", ["c4_sum", "c4_avg"])
+def test_c4_full_size_8_ranks_sliced(ctx, ctx8, name):
+    """C4 at the bench's size over 8 ranks in the default order: the double
+    partials travel as rank-owned slices of the ~10.5M-point grid (alltoall,
+    rank-ordered merge, gathered results; SpanGroup.java:647-667). Timestamps
+    and isInteger against the oracle's digests; values within 1e-9 of the
+    oracle-verified sum of |terms|; the bytes each rank received against the
+    slice exchange's size."""
+    e = json.load(open(DIGESTS))[name]
+    ss = synth.jittered_packed(e["n_series"], e["n_points"], seed=e["seed"], float_frac=0.5, float_cell_frac=0.01)
+    g = core.run_spanset(ctx8, ss, 0, U32MAX, e["agg"])
+    x_bytes = ctx8.timing().x_bytes
+    rc, ts, isi, bits, n_in, _ = g
+    assert rc == e["code"] and n_in == e["n_input"] and len(ts) == e["n_out"]
+    assert sha(ts, "<i8") == e["ts"] and sha(isi, "u1") == e["is_int"]
+    gx = core.run_spanset(ctx, ss, 0, U32MAX, e["agg"], exact=True)
+    assert sha(gx[3], "<i8") == e["bits"]
+    assert_same(g, oracle.Result(0, gx[1], gx[2], gx[3], gx[4], -1), rtol=1e-9, abs_scale=abs_bound_full(ctx, e, name))
+    T = len(ts)
+    # partials (cnt 4 + flag 1 + long 8 + double 8 B a point) once over the
+    # slices, the 17-B results once, the grid bitmaps (1 bit a second of the
+    # group's range) gathered; the allgather of every rank's partials would
+    # be 7 x T x 21 B
+    bitmap = 7 * ((int(ss.row_base.max()) + 3600 - int(ss.row_base.min())) // 32 + 2) * 4
+    lo_x = 7 * ((T + 7) // 8) * (21 + 17)
+    assert lo_x <= x_bytes <= lo_x + bitmap + 65536, (x_bytes, lo_x, bitmap)
+    assert x_bytes < 7 * T * 21 / 3
 
 
 @pytest.mark.gpu

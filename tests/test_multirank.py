@@ -16,7 +16,7 @@ import numpy as np
 import pytest
 
 import oracle
-from helpers import I, F, T0, U32MAX, assert_same
+from helpers import I, F, T0, U32MAX, assert_same, corrupt_qual
 from opentsdb_amd import _abi, core, packing, synth
 
 AGGS = [0, 1, 2, 3, 4]
@@ -178,6 +178,73 @@ def test_equal_bucket_grids_different_last_ts(mctx, agg, rate):
     ss = packing.pack_spans(spans)
     g, o = both(mctx, ss, agg=agg, rate=rate, dsi=60, dsa=3)
     assert_same(g, o)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("agg", [0, 2, 4])
+@pytest.mark.parametrize("rate", [False, True])
+def test_lockstep_sharded(mctx, agg, rate):
+    """every rank's shard lockstep on the same cadence (C3's shape): each rank
+    reduces its spans with k_lockstep, the partials travel as usual"""
+    ss = synth.regular(64, 900, _abi.SYN_INT64_COUNTER, seed=4, step=1)
+    g, o = both(mctx, ss, agg=agg, rate=rate)
+    assert_same(g, o)
+    p = mctx.timing().paths
+    assert bool(p & _abi.PATH_LOCKSTEP) == (agg != 4 or rate) and not p & _abi.PATH_DIRECT_REDO
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("rate", [False, True])
+def test_lockstep_sharded_broken_in_last_rank(mctx, rate):
+    """a qualifier off the cadence in the last rank's shard: that rank's
+    k_lockstep flags it, the flag is agreed in the partials' collective group
+    and every rank runs the call again on the proven path"""
+    ss = corrupt_qual(synth.regular(64, 900, _abi.SYN_INT64_COUNTER, seed=4, step=2), 63, 400, lambda q: q + 16)
+    g, o = both(mctx, ss, agg=0, rate=rate)
+    assert_same(g, o)
+    p = mctx.timing().paths
+    assert p & _abi.PATH_DIRECT_REDO and not p & _abi.PATH_LOCKSTEP
+
+
+@pytest.mark.gpu
+def test_lockstep_sharded_ranks_disagree(mctx):
+    """each rank lockstep on its own, but on different phases: the global
+    grid is wider than every rank's pattern, so no rank may use its proposal
+    (unproven spans): broken everywhere, rerun"""
+    n = 4 * mctx.ranks
+    spans = [I([(T0 + (s >= n // 2) + 2 * i, s * 7 + i) for i in range(800)], minimal=False) for s in range(n)]
+    ss = packing.pack_spans(spans)
+    for agg, rate in ((0, False), (2, True)):
+        g, o = both(mctx, ss, agg=agg, rate=rate)
+        assert_same(g, o)
+        assert mctx.timing().paths & _abi.PATH_DIRECT_REDO
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("agg", AGGS)
+@pytest.mark.parametrize("rate", [False, True])
+def test_long_grid_sliced_exchange(mctx, agg, rate):
+    """a union grid of > 64k points with double partials
+    (mixed int/float jittered series): each rank owns 1/N of G, receives the
+    ranks' partials of its slice only (alltoall), merges them in rank order
+    (SpanGroup.java:647-667) and finalizes it; the slices' results are
+    gathered. Compared with the whole-group oracle; the sum case also checks
+    the bytes a rank received: (N-1)/N of its 21-B dual-mode partials plus the
+    17-B results, instead of N-1 times all of them (from 3 ranks on)."""
+    ss = synth.jittered(60, 2000, seed=8, span_range=3_000_000, max_gap=3000)
+    g, o = both(mctx, ss, agg=agg, rate=rate)
+    assert_same(g, o)
+    T, N = len(o.ts), mctx.ranks
+    assert T >= 65536
+    if agg == 0 and not rate:
+        bitmap = (N - 1) * ((int(ss.row_base.max()) + 3600 - int(ss.row_base.min())) // 32 + 2) * 4
+        x = mctx.timing().x_bytes
+        if N == 2:  # (no gain from slices at 2 ranks: every partial gathered)
+            assert (N - 1) * T * 21 <= x <= (N - 1) * T * 21 + bitmap + 4096, (x, T, bitmap)
+        else:
+            xs = (T + N - 1) // N
+            lo_x = (N - 1) * xs * (21 + 17)
+            assert lo_x <= x <= lo_x + bitmap + 4096, (x, lo_x, bitmap)
 
 
 @pytest.mark.gpu
