@@ -292,6 +292,12 @@ def cpu_baseline_c5(batch, seconds=10.0):
 _JSON_OUT = None
 
 
+def set_options(ctx, opts):
+    for o in opts:
+        name, _, value = o.partition("=")
+        ctx.set_option(name, value)
+
+
 def emit(res):
     """The one JSON line, on the process's original stdout. main() points fd 1
     at stderr first, so banners native libraries print to stdout (RCCL's
@@ -314,6 +320,7 @@ def bench_c5(args):
     b = compaction.synth_rows(args.series or 1_000_000, seed=5, **mix)
     gen_s = time.perf_counter() - t0
     ctx = Context(0)
+    set_options(ctx, args.option)
     L = lib()
     dev = torch.device("cuda", 0)
     keep = []
@@ -375,9 +382,8 @@ def bench_c5(args):
     hot_ms = float(np.mean(hot))
     achieved = alg_all / (call_ms * 1e-3) / 1e9
     kname = "tsdbhip_compact_rows (whole call)"
-    call_kernels = ("k_compact_tiles+k_compact_complex+k_compact_dups" if os.environ.get("TSDBHIP_COMPACT") == "tiles"
-                    else "k_compact_quals+k_compact_classify+k_compact_vals+k_compact_rows+k_compact_complex"
-                         "+k_compact_dups")
+    call_kernels = ("k_compact_quals+k_compact_classify+k_compact_vals+k_compact_rows+k_compact_complex"
+                    "+k_compact_dups")
     traffic, traffic_src = pmc_traffic("c5", call_kernels, 1)
     res = {
         "metric": "raw cells/sec compacted (CompactionQueue.compact) + % HBM roofline, 1 MI355X",
@@ -524,6 +530,9 @@ def main():
                     help="diagnostic at N=1: run rank 0's shard of an N-way series split through the sharded "
                          "path on a 1-rank RCCL communicator (per-rank work and exchange code of an N-GPU run; "
                          "the line says so and its value is that one shard's rate)")
+    ap.add_argument("--option", action="append", default=[], metavar="NAME=VALUE",
+                    help="a context option (tsdbhip_set_option: decode, aligned_group, lockstep, compact, "
+                         "timing_detail) for A/B runs; results never depend on it")
     ap.add_argument("--dry-run", action="store_true",
                     help="harness check without a GPU: the multi-rank timing/barrier/report path with a "
                          "no-op step (its value is meaningless and says so)")
@@ -586,6 +595,7 @@ def main():
     import torch
     torch.cuda.set_device(local_rank)
     ctx = Context(local_rank)
+    set_options(ctx, args.option)
     L = lib()
     if world > 1:
         uid = [Context.unique_id() if rank == 0 else None]

@@ -307,6 +307,17 @@ int         tsdbhip_open(int32_t device, tsdbhip_ctx** out);
  * Compaction, group-by batches, synthetic inputs and probes of a
  * multi-device context run on its first device. */
 int         tsdbhip_open_devices(const int32_t* devices, uint32_t n, tsdbhip_ctx** out);
+/* Path / diagnostic options of a context and of its member contexts (ABI v6;
+ * results never depend on them: the tests use them to run every kernel
+ * variant, A/B runs to compare; no environment variable is read):
+ *   "decode"        "auto" | "general" | "fast" | "chunks" | "spans" | "direct"
+ *   "aligned_group" "on" | "off"   k_ds_reg's aligned-group reduction
+ *   "lockstep"      "on" | "off"   the lockstep proposal (k_lockstep)
+ *   "compact"       "auto" | "tiles"  (tiles: every row through k_compact_tiles)
+ *   "timing_detail" "on" | "off"   decode / grid event pairs in tsdbhip_timing
+ *   "check_clean"   "on" | "off"   check the zero-on-entry invariants (stderr)
+ * Unknown names or values: TSDBHIP_E_INVALID_ARG. */
+int         tsdbhip_set_option(tsdbhip_ctx* ctx, const char* name, const char* value);
 int         tsdbhip_open_mask(uint32_t gpu_mask, tsdbhip_ctx** out);
 int         tsdbhip_ranks(tsdbhip_ctx* ctx);  /* shards per SpanGroup (1: one device) */
 void        tsdbhip_close(tsdbhip_ctx* ctx);

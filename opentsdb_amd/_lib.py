@@ -24,7 +24,7 @@ EXPORTS = [
     "tsdbhip_comm_init", "tsdbhip_synth_generate", "tsdbhip_synth_free",
     "tsdbhip_desc_download", "tsdbhip_bw_probe", "tsdbhip_spangroup_run_batch",
     "tsdbhip_format_points", "tsdbhip_open_devices", "tsdbhip_open_mask", "tsdbhip_ranks",
-    "tsdbhip_timing_totals",
+    "tsdbhip_timing_totals", "tsdbhip_set_option",
 ]
 
 
@@ -60,6 +60,8 @@ def lib():
     L.tsdbhip_open_devices.restype = C.c_int
     L.tsdbhip_open_mask.argtypes = [C.c_uint32, P(C.c_void_p)]
     L.tsdbhip_open_mask.restype = C.c_int
+    L.tsdbhip_set_option.argtypes = [C.c_void_p, C.c_char_p, C.c_char_p]
+    L.tsdbhip_set_option.restype = C.c_int
     L.tsdbhip_ranks.argtypes = [C.c_void_p]
     L.tsdbhip_ranks.restype = C.c_int
     L.tsdbhip_close.argtypes = [C.c_void_p]
@@ -124,6 +126,11 @@ class Context:
     def check(self, rc):
         if rc:
             raise TsdbHipError(rc, self.last_error())
+
+    def set_option(self, name, value):
+        """tsdbhip_set_option: a path / diagnostic option of this context
+        (include/tsdbhip.h); results never depend on it"""
+        self.check(self._lib.tsdbhip_set_option(self._h, name.encode(), value.encode()))
 
     def timing(self):
         t = _abi.Timing()

@@ -55,6 +55,19 @@ struct Fail {
 
 }  // namespace
 
+// Path / diagnostic options of a context (tsdbhip_set_option): which kernel
+// variant takes a span or a row. Results never depend on them; the tests set
+// them to run every variant. No environment variable is read.
+enum { DEC_AUTO = 0, DEC_GENERAL, DEC_FAST, DEC_CHUNKS, DEC_SPANS, DEC_DIRECT };
+struct Options {
+  int decode = DEC_AUTO;       // "decode": the decode / downsample path forced
+  bool aligned_group = true;   // "aligned_group": k_ds_reg's aligned-group reduction may be tried
+  bool lockstep = true;        // "lockstep": the lockstep proposal may be made
+  bool compact_tiles = false;  // "compact": "tiles" sends every row through k_compact_tiles
+  bool timing_detail = false;  // "timing_detail": decode / grid event pairs (tsdbhip_timing)
+  bool check_clean = false;    // "check_clean": verify the zero-on-entry invariants (stderr)
+};
+
 // Per-call resources. A call takes a free slot of its context (or a new
 // one), so calls from several host threads on one context run concurrently,
 // each on its own stream with its own scratch (the reference's Netty workers
@@ -81,6 +94,7 @@ struct Slot {
   uint32_t hot_kernel = 0;
   tsdbhip_timing timing = {};
   Xchg* x = nullptr;  // the exchange of a sharded call (its rank / nranks)
+  Options opt;        // the context's options, copied at the lease
   bool want_output = true;  // false: a non-zero rank of an in-process sharded call
   // left by the previous spangroup_run that completed: its call state reset
   // to the initial values, its grid bitmap all zero (k_call_end)
@@ -97,6 +111,7 @@ struct tsdbhip_ctx {
   std::map<std::string, Buf> owned;  // tsdbhip_synth_generate datasets
   tsdbhip_timing last = {};
   tsdbhip_timing sum = {};  // tsdbhip_timing_totals
+  Options opt;              // tsdbhip_set_option
   uint64_t n_sum = 0;
   // one process per GPU (tsdbhip_comm_init): sharded calls serialise on the
   // communicator (every rank must issue its collectives in the same order)
@@ -257,6 +272,10 @@ struct Lease {
     }
     s->x = nullptr;
     s->want_output = true;
+    {
+      std::lock_guard<std::mutex> lk(c->mu);
+      s->opt = c->opt;
+    }
     if (hipSetDevice(c->device) != hipSuccess) {  // (the destructor will not run: hand the slot back here)
       set_error(c, "hipSetDevice(%d) failed", c->device);
       std::lock_guard<std::mutex> lk(c->mu);
@@ -380,8 +399,7 @@ extern "C" int tsdbhip_open_devices(const int32_t* devs, uint32_t n, tsdbhip_ctx
   bool distinct = true;
   for (uint32_t a = 0; a < n; a++)
     for (uint32_t b = a + 1; b < n; b++) distinct = distinct && devs[a] != devs[b];
-  const char* xe = getenv("TSDBHIP_XCHG");
-  m->rccl = distinct && !(xe && !strcmp(xe, "local"));
+  m->rccl = distinct;
   try {
     if (rc) throw Fail{rc};
     if (m->rccl) {
@@ -440,6 +458,50 @@ extern "C" int tsdbhip_open_mask(uint32_t gpu_mask, tsdbhip_ctx** out) {
     if (gpu_mask & (1u << d)) devs[n++] = d;
   if (!n) return TSDBHIP_E_INVALID_ARG;
   return tsdbhip_open_devices(devs, n, out);
+}
+
+extern "C" int tsdbhip_set_option(tsdbhip_ctx* ctx, const char* name, const char* value) {
+  if (!ctx || !name || !value) return TSDBHIP_E_INVALID_ARG;
+  const std::string n(name), v(value);
+  auto on_off = [&](bool& f) {
+    if (v == "on") f = true;
+    else if (v == "off") f = false;
+    else return false;
+    return true;
+  };
+  Options o;
+  {
+    std::lock_guard<std::mutex> lk(ctx->mu);
+    o = ctx->opt;
+  }
+  bool ok = true;
+  if (n == "decode") {
+    static const char* names[] = {"auto", "general", "fast", "chunks", "spans", "direct"};
+    ok = false;
+    for (int i = 0; i < 6; i++)
+      if (v == names[i]) { o.decode = i; ok = true; }
+  } else if (n == "aligned_group") ok = on_off(o.aligned_group);
+  else if (n == "lockstep") ok = on_off(o.lockstep);
+  else if (n == "compact") {
+    ok = v == "auto" || v == "tiles";
+    o.compact_tiles = v == "tiles";
+  } else if (n == "timing_detail") ok = on_off(o.timing_detail);
+  else if (n == "check_clean") ok = on_off(o.check_clean);
+  else ok = false;
+  if (!ok) {
+    set_error(ctx, "tsdbhip_set_option: unknown option %s=%s", name, value);
+    return TSDBHIP_E_INVALID_ARG;
+  }
+  {
+    std::lock_guard<std::mutex> lk(ctx->mu);
+    ctx->opt = o;
+  }
+  if (ctx->multi)  // (every rank's member context runs with them)
+    for (tsdbhip_ctx* m : ctx->multi->members) {
+      std::lock_guard<std::mutex> lk(m->mu);
+      m->opt = o;
+    }
+  return TSDBHIP_OK;
 }
 
 extern "C" int tsdbhip_ranks(tsdbhip_ctx* ctx) {
@@ -691,14 +753,12 @@ struct LaunchChunks {
     // (C2) prefer the full occupancy
     // (the padding brings the block's LDS to 40 KB whatever the kernel's own
     // static LDS: a few bytes more would leave room for only 3 blocks)
-    static const int pad_env = getenv("TSDBHIP_REG_LDS") ? atoi(getenv("TSDBHIP_REG_LDS")) : -1;
     static const unsigned stat_lds = [] {
       hipFuncAttributes fa = {};
       return hipFuncGetAttributes(&fa, (const void*)k_ds_reg<AGG>) == hipSuccess ? (unsigned)fa.sharedSizeBytes
                                                                                  : 18960u;
     }();
-    const unsigned pad = pad_env >= 0 ? (unsigned)pad_env
-                                      : (wps_log2 == 0 ? (stat_lds < 40960u ? 40960u - stat_lds : 0u) : 0u);
+    const unsigned pad = wps_log2 == 0 ? (stat_lds < 40960u ? 40960u - stat_lds : 0u) : 0u;
     // the aligned-group reduction (one wave per span): a partial row per block
     FapArgs fa0 = {};
     fa0.op = -1;
@@ -1176,35 +1236,47 @@ __global__ void k_fap_neutral64(int64_t* p_i, uint32_t* p_cnt, int op, Small* sm
   p_cnt[threadIdx.x] = 0;
   if (threadIdx.x == 0) fap_valid_pack(sm, 0u, pack);
 }
-// the finalize of the (exchanged) 64-slot partials when the group stands
-// everywhere (sharded: and every rank's grid is the global one); outputs at
-// a fixed stride of 64 (ts | bits | is_int)
+// The finalize of the (exchanged) 64-slot partials when the group stands
+// everywhere (sharded: and every rank's grid is the global one; outputs at a
+// fixed stride of 64: ts | bits | is_int), then k_call_end's `done` variant,
+// in one block of 256 threads: the call state is snapshot, and reset with
+// the bitmap cleared iff the group stood
 template <int AGG>
-__global__ void __launch_bounds__(64) k_fap_finish(Small* sm, const int64_t* p_i, const uint32_t* p_cnt, FinalArgs f,
-                                                  int32_t sharded, XMove unpack) {
-  if (unpack.n) {  // the agreed header back into the call state (sharded)
-    if (threadIdx.x == 0) xmove_run(unpack);
-    __threadfence();
-    __syncthreads();
+__global__ void __launch_bounds__(256) k_fap_finish_end(Small* sm, const int64_t* p_i, const uint32_t* p_cnt,
+                                                        FinalArgs f, int32_t sharded, XMove unpack, Small* snap,
+                                                        Small init, uint32_t* bitmap, const uint32_t* grid, int64_t lo) {
+  __shared__ uint32_t s_ok, s_T;
+  const uint32_t t = threadIdx.x;
+  if (t == 0) {
+    if (unpack.n) xmove_run(unpack);  // the agreed header back into the call state (sharded)
+    bool ok = sm->fap_valid != 0 && sm->err == ERR_NONE && sm->gflags[0] == 0 && sm->T > 0 && sm->T <= WAVE;
+    // (sharded: rank-independent: an empty grid anywhere makes lo's MIN / MAX
+    // differ, ~0 vs a real lo; all empty fails T > 0 on every rank)
+    if (sharded) ok = ok && xh_grids_agree(sm->xh);
+    s_ok = ok ? 1u : 0u;
+    s_T = (uint32_t)sm->T;
   }
-  bool ok = *(volatile unsigned long long*)&sm->fap_valid != 0 && *(volatile unsigned long long*)&sm->err == ERR_NONE &&
-            *(volatile uint32_t*)&sm->gflags[0] == 0 && sm->T > 0 && sm->T <= WAVE;
-  if (sharded) {
-    const unsigned long long* xh = sm->xh;
-    // (rank-independent: an empty grid anywhere makes lo's MIN / MAX differ,
-    // ~0 vs a real lo; all empty fails T > 0 on every rank)
-    ok = ok && xh_grids_agree(xh);
+  __syncthreads();
+  if (!s_ok) {  // the group did not stand: the state stays for the usual path
+    if (t == 0) *snap = *sm;
+    return;
   }
-  if (!ok) return;
-  const uint32_t g = threadIdx.x;
-  if (g < sm->T) {
+  if (t < s_T) {
     Acc a;
     acc_init(a);
-    a.cnt = p_cnt[g];
-    a.ia = p_i[g];
-    finalize_one<AGG, MODE_INT, false>(f, g, a);
+    a.cnt = p_cnt[t];
+    a.ia = p_i[t];
+    finalize_one<AGG, MODE_INT, false>(f, t, a);
   }
-  if (g == 0) sm->fap_done = 1;
+  __syncthreads();
+  if (t == 0) {
+    sm->fap_done = 1;
+    __threadfence();
+    *snap = *sm;
+    *sm = init;
+  }
+  __syncthreads();  // (the grid read below is this block's own)
+  if (bitmap && t < s_T) bitmap[(uint64_t)((int64_t)grid[t] - lo) >> 5] = 0u;
 }
 
 // TSDBHIP_CHECK_CLEAN: counts non-zero words of a buffer (debug of the
@@ -1269,7 +1341,7 @@ static int spangroup_run_once(Slot* ctx, const tsdbhip_sg_desc* d, tsdbhip_sg_ou
   const uint8_t* val = stage(ctx, "in_val", d->val_bytes, d->val_nbytes, dev, 16);
 
   Small* sm = scratch<Small>(ctx, "small", 1);
-  static const bool check_clean = getenv("TSDBHIP_CHECK_CLEAN") != nullptr;
+  const bool check_clean = ctx->opt.check_clean;
   if (check_clean && ctx->sm_ready) {  // (debug) the reset state must equal small_init()
     Small cur, ini = small_init();
     readback(ctx, &cur, sm, sizeof cur);
@@ -1288,7 +1360,7 @@ static int spangroup_run_once(Slot* ctx, const tsdbhip_sg_desc* d, tsdbhip_sg_ou
   ctx->sm_ready = false;
   const bool bm_clean = ctx->bitmap_clean;
   ctx->bitmap_clean = false;
-  static const bool detail = getenv("TSDBHIP_TIMING_DETAIL") != nullptr;  // decode / grid event pairs
+  const bool detail = ctx->opt.timing_detail;  // decode / grid event pairs
   HIPCHK(hipEventRecord(ctx->ev[0], st));
 
   // ---- assemble ----
@@ -1393,7 +1465,7 @@ static int spangroup_run_once(Slot* ctx, const tsdbhip_sg_desc* d, tsdbhip_sg_ou
   // downsamples, and the aggregation is exact integer (no rate, no dev) ----
   FapPlan fap;
   fap.a.op = -1;
-  static const bool fap_off = getenv("TSDBHIP_FAP") && !strcmp(getenv("TSDBHIP_FAP"), "0");  // (tests / A/B)
+  const bool fap_off = !ctx->opt.aligned_group;
   if (!fap_off && interval > 0 && !rate && ds_agg <= 3 && agg <= 3 && !(sharded && exact) && n_kept > 0 &&
       h.bound[0] == h.bound[2] && h.bound[1] == h.bound[3] && h.bound[1] - h.bound[0] <= 62ull * (uint64_t)interval) {
     // (at most 64 buckets a span: a partial row holds them)
@@ -1431,17 +1503,17 @@ static int spangroup_run_once(Slot* ctx, const tsdbhip_sg_desc* d, tsdbhip_sg_ou
     // wide rows (the reference's hourly compacted rows) take the streaming
     // kernels; rows of a few cells (sparse series) the general one. With
     // downsampling, regular-cadence integer spans go chunk-parallel first.
-    const char* force = getenv("TSDBHIP_DECODE");
+    const int force = ctx->opt.decode;
     bool fast = R > 0 && h.n_input / R >= 64;
     bool chunks = fast;
     direct = fast && interval == 0 && bitmap != nullptr;
-    if (force && !strcmp(force, "general")) fast = chunks = direct = false;
-    if (force && !strcmp(force, "fast")) { fast = true; chunks = direct = false; }
-    if (force && !strcmp(force, "chunks")) { fast = chunks = true; direct = false; }
+    if (force == DEC_GENERAL) fast = chunks = direct = false;
+    if (force == DEC_FAST) { fast = true; chunks = direct = false; }
+    if (force == DEC_CHUNKS) { fast = chunks = true; direct = false; }
     // "spans": the chain-proved downsampler alone (k_ds_spans, no k_ds_reg first)
-    const bool use_reg = !(force && !strcmp(force, "spans"));
+    const bool use_reg = force != DEC_SPANS;
     if (!use_reg) { fast = chunks = true; direct = false; }
-    if (force && !strcmp(force, "direct")) { fast = chunks = true; direct = interval == 0 && bitmap != nullptr; }
+    if (force == DEC_DIRECT) { fast = chunks = true; direct = interval == 0 && bitmap != nullptr; }
     da.fb_list = scratch<uint32_t>(ctx, "fb_list", n_kept);
     da.fb_count = &sm->cnt[1];
     da.use_fb = 0;
@@ -1481,7 +1553,7 @@ static int spangroup_run_once(Slot* ctx, const tsdbhip_sg_desc* d, tsdbhip_sg_ou
         // the lockstep proposal (k_lockstep.hip), where the reduce is not the
         // span-ordered pass (EXACT_ORDER, integer dev): three qualifiers a
         // span now, every other one proven by k_lockstep as it reduces
-        ls_try = ls_allow && !exact && (agg != TSDBHIP_AGG_DEV || rate);
+        ls_try = ls_allow && ctx->opt.lockstep && !exact && (agg != TSDBHIP_AGG_DEV || rate);
         if (ls_try) {
           d_qoff = scratch<uint64_t>(ctx, "d_qoff", n_kept);
           dg.ls_key = sm->ls_key;
@@ -1577,6 +1649,8 @@ static int spangroup_run_once(Slot* ctx, const tsdbhip_sg_desc* d, tsdbhip_sg_ou
     ga.lo = lo; ga.hi = hi; ga.bitmap = bitmap; ga.nwords = nwords; ga.word_rank = word_rank;
     ga.block_sum = scratch<uint32_t>(ctx, "grid_bsum", nb);
     ga.hash = hash ? sm->ghash : nullptr;
+    // (the optimistic aligned-group finish reads G right after: one block emits it)
+    ga.emit1 = fap_opt && nb == 1 ? scratch<uint32_t>(ctx, "grid", nwords * 32) : nullptr;
     ga.block_hash = hash && nb > 1 ? scratch<unsigned long long>(ctx, "grid_bhash", 2 * nb) : nullptr;
     ga.pub = pub ? next_pub(ctx, sizeof(Small)) : HostPub{};
     hipLaunchKernelGGL(k_grid_popc, dim3((unsigned)nb), dim3(256), 0, st, ga);
@@ -1602,9 +1676,11 @@ static int spangroup_run_once(Slot* ctx, const tsdbhip_sg_desc* d, tsdbhip_sg_ou
     if (!empty_grid) {
       gridv_o = scratch<uint32_t>(ctx, "grid", nwords * 32);  // (>= |G|)
       ga.grid = gridv_o;
-      uint32_t* word_rank_f = scratch<uint32_t>(ctx, "word_rank_f", nwords);
-      const uint32_t eb = grid_for(nwords, 256);
-      hipLaunchKernelGGL(k_emit_verify, dim3(eb), dim3(256), 0, st, ga, word_rank_f, dg, 0u, eb);
+      if (!ga.emit1) {  // (a single-block k_grid_popc emitted it)
+        uint32_t* word_rank_f = scratch<uint32_t>(ctx, "word_rank_f", nwords);
+        const uint32_t eb = grid_for(nwords, 256);
+        hipLaunchKernelGGL(k_emit_verify, dim3(eb), dim3(256), 0, st, ga, word_rank_f, dg, 0u, eb);
+      }
     }
     HIPCHK(hipEventRecord(ctx->ev[4], st));
     const int fop = agg == TSDBHIP_AGG_MIN ? 1 : (agg == TSDBHIP_AGG_MAX ? 2 : 0);
@@ -1656,17 +1732,19 @@ static int spangroup_run_once(Slot* ctx, const tsdbhip_sg_desc* d, tsdbhip_sg_ou
     fo.out_isint = (uint8_t*)(fo.out_bits + WAVE);
     fo.nan_t = &sm->nan_t;
     {  // (an empty local grid: never valid; launched anyway, every rank alike)
+      // the finish and the end of the call in one single-block launch
+      const XMove um = sharded ? unpack : XMove{};
+      Small* snap = (Small*)ctx->map_out_dev;
+      const Small ini = small_init();
       if (agg == TSDBHIP_AGG_MIN)
-        hipLaunchKernelGGL(k_fap_finish<1>, dim3(1), dim3(WAVE), 0, st, sm, (const int64_t*)o_pi, (const uint32_t*)o_pc, fo, (int32_t)sharded, sharded ? unpack : XMove{});
+        hipLaunchKernelGGL(k_fap_finish_end<1>, dim3(1), dim3(256), 0, st, sm, (const int64_t*)o_pi, (const uint32_t*)o_pc, fo, (int32_t)sharded, um, snap, ini, bitmap, (const uint32_t*)gridv_o, lo);
       else if (agg == TSDBHIP_AGG_MAX)
-        hipLaunchKernelGGL(k_fap_finish<2>, dim3(1), dim3(WAVE), 0, st, sm, (const int64_t*)o_pi, (const uint32_t*)o_pc, fo, (int32_t)sharded, sharded ? unpack : XMove{});
+        hipLaunchKernelGGL(k_fap_finish_end<2>, dim3(1), dim3(256), 0, st, sm, (const int64_t*)o_pi, (const uint32_t*)o_pc, fo, (int32_t)sharded, um, snap, ini, bitmap, (const uint32_t*)gridv_o, lo);
       else if (agg == TSDBHIP_AGG_AVG)
-        hipLaunchKernelGGL(k_fap_finish<3>, dim3(1), dim3(WAVE), 0, st, sm, (const int64_t*)o_pi, (const uint32_t*)o_pc, fo, (int32_t)sharded, sharded ? unpack : XMove{});
+        hipLaunchKernelGGL(k_fap_finish_end<3>, dim3(1), dim3(256), 0, st, sm, (const int64_t*)o_pi, (const uint32_t*)o_pc, fo, (int32_t)sharded, um, snap, ini, bitmap, (const uint32_t*)gridv_o, lo);
       else
-        hipLaunchKernelGGL(k_fap_finish<0>, dim3(1), dim3(WAVE), 0, st, sm, (const int64_t*)o_pi, (const uint32_t*)o_pc, fo, (int32_t)sharded, sharded ? unpack : XMove{});
+        hipLaunchKernelGGL(k_fap_finish_end<0>, dim3(1), dim3(256), 0, st, sm, (const int64_t*)o_pi, (const uint32_t*)o_pc, fo, (int32_t)sharded, um, snap, ini, bitmap, (const uint32_t*)gridv_o, lo);
     }
-    hipLaunchKernelGGL(k_call_end, dim3(1), dim3(256), 0, st, sm, (Small*)ctx->map_out_dev, small_init(), bitmap,
-                       (const uint32_t*)gridv_o, (uint64_t)0, lo, BadArgs{}, (const uint32_t*)&sm->fap_done);
     HIPCHK(hipEventRecord(ctx->ev[5], st));
     HIPCHK(hipStreamSynchronize(st));
     std::memcpy(&h, ctx->map_out, sizeof h);
@@ -1914,11 +1992,9 @@ static int spangroup_run_once(Slot* ctx, const tsdbhip_sg_desc* d, tsdbhip_sg_ou
     // one reduce launch over this rank's kept spans; `init`: the per-t state
     // to continue from (one chunk)
     auto run_reduce = [&](bool one_chunk, bool finalize, const ReduceArgs* init) {
-      static const uint64_t minw_env = getenv("TSDBHIP_REDUCE_MINW") ? atoll(getenv("TSDBHIP_REDUCE_MINW")) : 2048;
-      static const bool lds_env = !(getenv("TSDBHIP_REDUCE_LDS") && !strcmp(getenv("TSDBHIP_REDUCE_LDS"), "0"));
       // span state in LDS while 4 waves' regions fit 40 KB (4 blocks a CU)
-      const uint32_t spc_cap = lds_env ? (uint32_t)(RED_LDS_BLOCK / 4 / red_lds_span_bytes(rate)) : 0u;
-      const ReduceGeom rg = reduce_geom(T, n_kept, one_chunk || init, 16384, minw_env, spc_cap);
+      const uint32_t spc_cap = (uint32_t)(RED_LDS_BLOCK / 4 / red_lds_span_bytes(rate));
+      const ReduceGeom rg = reduce_geom(T, n_kept, one_chunk || init, 16384, 2048, spc_cap);
       const uint32_t spc = rg.spc, n_chunks = rg.n_chunks, tpw = rg.tpw, ntg = rg.ntg;
       const uint64_t n_waves = rg.n_waves;
       ReduceArgs r;
@@ -1933,7 +2009,7 @@ static int spangroup_run_once(Slot* ctx, const tsdbhip_sg_desc* d, tsdbhip_sg_ou
       r.chunk_e = nullptr;
       r.fstar = fstar;
       r.exact = exact ? 1 : 0;
-      r.lds_state = lds_env && 4 * red_lds_stride(spc, rate) <= RED_LDS_BLOCK ? 1u : 0u;
+      r.lds_state = 4 * red_lds_stride(spc, rate) <= RED_LDS_BLOCK ? 1u : 0u;
       if (init) {
         r.i_cnt = init->p_cnt; r.i_flag = init->p_flag; r.i_i = init->p_i; r.i_d = init->p_d;
         r.i_dhas = init->p_dhas; r.i_wim = init->p_wim; r.i_wiv = init->p_wiv; r.i_wdm = init->p_wdm;
@@ -1962,8 +2038,7 @@ static int spangroup_run_once(Slot* ctx, const tsdbhip_sg_desc* d, tsdbhip_sg_ou
     // the lockstep group: tiles of LS_TILE grid points x chunks of spans
     auto ls_reduce = [&](bool finalize) {
       const uint32_t n_tiles = (uint32_t)((T + LS_TILE - 1) / LS_TILE);
-      static const uint64_t ls_waves = getenv("TSDBHIP_LS_WAVES") ? atoll(getenv("TSDBHIP_LS_WAVES")) : 16384;  // (TEMP A/B)
-      uint64_t want = std::max<uint64_t>(1, ls_waves / n_tiles);
+      uint64_t want = std::max<uint64_t>(1, 16384 / n_tiles);
       want = std::min<uint64_t>(want, std::max<uint32_t>(1, n_kept / 64));
       const uint32_t spc = (uint32_t)((n_kept + want - 1) / want);
       const uint32_t n_chunks = (n_kept + spc - 1) / spc;
@@ -2638,8 +2713,7 @@ static int compact_rows(Slot* ctx, const tsdbhip_rows_desc* d, tsdbhip_rows_out*
     a.big_cells = scratch<uint64_t>(ctx, "c_cells", qext / 2 + R + 1);
     hipStream_t st = ctx->stream;
     HIPCHK(hipEventRecord(ctx->ev[0], st));
-    const char* cm = getenv("TSDBHIP_COMPACT");
-    if (cm && !strcmp(cm, "tiles")) {  // (every row through the LDS tiles: the A/B reference)
+    if (ctx->opt.compact_tiles) {  // (every row through the LDS tiles: the A/B reference)
       HIPCHK(hipEventRecord(ctx->ev[8], st));
       HIPCHK(hipEventRecord(ctx->ev[4], st));
       HIPCHK(hipEventRecord(ctx->ev[2], st));

@@ -246,7 +246,7 @@ static int spangroup_run_batch(Slot* ctx, const tsdbhip_sg_desc* d, uint32_t G, 
   DirectArgs dg = {};
   if (n_kept) {
     const unsigned blocks = grid_for(n_kept, 4, 65536);
-    const char* force = getenv("TSDBHIP_DECODE");  // "fast": no direct path (tests)
+    const bool no_direct = ctx->opt.decode == DEC_FAST;  // (tests: the E path for every span)
     const bool fast = R > 0 && h.n_input / R >= 64;  // wide (hourly compacted) rows
     da.fb_list = scratch<uint32_t>(ctx, "fb_list", n_kept);
     da.fb_count = scratch<uint32_t>(ctx, "fb_count", 1, true);
@@ -263,7 +263,7 @@ static int spangroup_run_batch(Slot* ctx, const tsdbhip_sg_desc* d, uint32_t G, 
       HIPCHK(hipEventRecord(ctx->ev[9], st));
     } else if (interval == 0) {
       DecodeArgs fa = da;
-      direct = !(force && !strcmp(force, "fast"));
+      direct = !no_direct;
       if (direct) {
         // regular-cadence spans on consecutive grid ranks of their group skip E
         // (k_direct.hip); the scan only proves the cadence here, the group

@@ -41,6 +41,9 @@ struct GridArgs {
   // local grids agree; null: not computed
   unsigned long long* hash;        // [2]
   unsigned long long* block_hash;  // [2 nblocks] (more than one block)
+  // k_grid_popc over a single block (nwords <= 1024): also emits G here
+  // (its ranks are final), one launch fewer (null: k_grid_emit / k_emit_verify do)
+  uint32_t* emit1;
 };
 
 // the per-word terms of the two grid hashes (splitmix64 finalisers of the
@@ -128,7 +131,16 @@ __global__ void __launch_bounds__(256) k_grid_popc(GridArgs g) {
 #pragma unroll
   for (int i = 0; i < 4; i++) {
     const uint64_t w = base + t * 4 + i;
-    if (w < g.nwords) g.word_rank[w] = run;
+    if (w < g.nwords) {
+      g.word_rank[w] = run;
+      if (g.emit1 && gridDim.x == 1) {  // (one block: run is the final rank)
+        uint32_t bits = g.bitmap[w], j = run;
+        while (bits) {
+          g.emit1[j++] = (uint32_t)(g.lo + (int64_t)(w * 32 + __builtin_ctz(bits)));
+          bits &= bits - 1;
+        }
+      }
+    }
     run += c[i];
   }
   if (t == 0 && blockIdx.x == 0 && g.zero2) {  // (their last readers ran before this kernel)

@@ -74,3 +74,17 @@ def corrupt_qual(ss, span, cell, fn):
     qb[off], qb[off + 1] = q2 >> 8, q2 & 0xFF
     return packing.SpanSet(ss.span_row_start, ss.row_base, ss.row_ncells, ss.row_qual_off, ss.row_val_off,
                            ss.row_val_len, qb, ss.val_bytes)
+
+
+def with_option(request, name, value, default):
+    """Fixture body: set a context option (tsdbhip_set_option) for a GPU test
+    and restore its default after it; CPU tests open no context."""
+    if request.node.get_closest_marker("gpu") is None:
+        yield value
+        return
+    c = request.getfixturevalue("ctx")
+    c.set_option(name, value)
+    try:
+        yield value
+    finally:
+        c.set_option(name, default)

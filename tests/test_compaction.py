@@ -8,6 +8,8 @@ import struct
 import numpy as np
 import pytest
 
+from helpers import with_option
+
 import closed_form_compaction as cfc
 import oracle
 from opentsdb_amd import _abi, compaction
@@ -189,14 +191,10 @@ def test_pack_rejects_long_kv():
 
 # ------------------------------------------------------------------ GPU ----
 @pytest.fixture(autouse=True, params=["plain", "tiles"])
-def compact_path(request, monkeypatch):
+def compact_path(request):
     """every GPU test twice: the plain-row path (classify / shifted copy /
     LDS row kernel, the default) and all rows through the LDS tiles"""
-    if request.param == "tiles":
-        monkeypatch.setenv("TSDBHIP_COMPACT", "tiles")
-    else:
-        monkeypatch.delenv("TSDBHIP_COMPACT", raising=False)
-    return request.param
+    yield from with_option(request, "compact", "tiles" if request.param == "tiles" else "auto", "auto")
 
 
 def assert_same(g, o):

@@ -1,14 +1,14 @@
 """The no-downsampling direct path (opentsdb_amd/csrc/k_direct.hip): spans on a
 regular cadence whose points are consecutive union-grid ranks are reduced
 straight from the reference's value bytes. Each case is checked against the
-oracle with the path forced on (TSDBHIP_DECODE=direct) and in auto mode;
+oracle with the path forced on (ctx option decode=direct) and in auto mode;
 cases that break a precondition (phase shift, mixed cadences, points after
 end, mixed types, start at a row boundary) check that the fallback to the E
 path is exact too. Integers bit-exact, doubles 1e-9 rel. (helpers.py)."""
 import numpy as np
 import pytest
 
-from helpers import I, F, T0, U32MAX, run_both, assert_same
+from helpers import with_option, I, F, T0, U32MAX, run_both, assert_same
 from opentsdb_amd import _abi, packing, synth
 
 pytestmark = pytest.mark.gpu
@@ -17,12 +17,8 @@ AGGS = [0, 1, 2, 3, 4]
 
 
 @pytest.fixture(autouse=True, params=["auto", "direct"])
-def path(request, monkeypatch):
-    if request.param == "direct":
-        monkeypatch.setenv("TSDBHIP_DECODE", "direct")
-    else:
-        monkeypatch.delenv("TSDBHIP_DECODE", raising=False)
-    return request.param
+def path(request):
+    yield from with_option(request, "decode", request.param, "auto")
 
 
 def long_series(ts, vals):

@@ -6,7 +6,7 @@ reference's summation order)."""
 import numpy as np
 import pytest
 
-from helpers import I, F, M, T0, U32MAX, run_both, assert_same
+from helpers import with_option, I, F, M, T0, U32MAX, run_both, assert_same
 from opentsdb_amd import _abi, core, packing, synth
 
 pytestmark = pytest.mark.gpu
@@ -15,17 +15,13 @@ AGGS = [0, 1, 2, 3, 4]
 
 
 @pytest.fixture(autouse=True, params=["auto", "general", "fast", "chunks", "spans", "direct"])
-def decode_path(request, monkeypatch):
+def decode_path(request):
     """Run every case through the streaming downsamplers (chunks: the
     constant-step k_ds_reg first, then the chain-proved k_ds_spans; spans:
     k_ds_spans alone), the streaming decode kernel (each with its fallback
     queue), the general per-span kernel, and (no downsampling) the direct
     path of k_direct.hip forced on whatever the row sizes."""
-    if request.param != "auto":
-        monkeypatch.setenv("TSDBHIP_DECODE", request.param)
-    else:
-        monkeypatch.delenv("TSDBHIP_DECODE", raising=False)
-    return request.param
+    yield from with_option(request, "decode", request.param, "auto")
 
 
 def ka_groups():

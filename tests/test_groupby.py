@@ -229,12 +229,12 @@ def groups_direct():
 @pytest.mark.parametrize("agg", AGGS)
 @pytest.mark.parametrize("rate", [False, True])
 @pytest.mark.parametrize("decode", ["auto", "fast"])
-def test_batch_direct_groups(ctx, agg, rate, decode, monkeypatch):
-    if decode == "fast":
-        monkeypatch.setenv("TSDBHIP_DECODE", "fast")  # the E path for every span
-    else:
-        monkeypatch.delenv("TSDBHIP_DECODE", raising=False)
-    ss, gss = pack_groups(groups_direct())
-    check_batch(ctx, ss, gss, agg=agg, rate=rate)
-    check_batch(ctx, ss, gss, agg=agg, rate=rate, start=T0 + 1234, end=T0 + 7000)
-    check_batch(ctx, ss, gss, agg=agg, rate=rate, exact=True)
+def test_batch_direct_groups(ctx, agg, rate, decode):
+    ctx.set_option("decode", decode)  # fast: the E path for every span
+    try:
+        ss, gss = pack_groups(groups_direct())
+        check_batch(ctx, ss, gss, agg=agg, rate=rate)
+        check_batch(ctx, ss, gss, agg=agg, rate=rate, start=T0 + 1234, end=T0 + 7000)
+        check_batch(ctx, ss, gss, agg=agg, rate=rate, exact=True)
+    finally:
+        ctx.set_option("decode", "auto")
