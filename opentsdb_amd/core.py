@@ -128,10 +128,12 @@ class Span:
 
 
 def run_spanset(ctx, spanset: SpanSet, start, end, agg, rate=False, ds_interval=0, ds_agg=0,
-                exact=False, capacity=None, device_desc=None, sharded=False, span0=0):
+                exact=False, capacity=None, device_desc=None, sharded=False, span0=0, register_out=False):
     """Low-level: one tsdbhip_spangroup_run. Returns (code, ts, is_int, bits,
     n_input_points, err_index). sharded: this rank's shard of a group whose
-    first span has global index span0."""
+    first span has global index span0. register_out: the result buffers
+    registered (tsdbhip_host_register, as the JNI bridge registers its
+    DirectByteBuffers) for the call."""
     desc = _abi.SgDesc()
     if device_desc is not None:
         C.pointer(desc)[0] = device_desc
@@ -157,7 +159,16 @@ def run_spanset(ctx, spanset: SpanSet, start, end, agg, rate=False, ds_interval=
     out.ts = _abi.ptr(ts, C.c_int64)
     out.is_int = _abi.ptr(isi, C.c_uint8)
     out.bits = _abi.ptr(bits, C.c_int64)
-    rc = ctx._lib.tsdbhip_spangroup_run(ctx.handle, C.byref(desc), C.byref(out))
+    regs = []
+    try:
+        if register_out:
+            for a in (ts, isi, bits):
+                ctx.check(ctx._lib.tsdbhip_host_register(ctx.handle, a.ctypes.data_as(C.c_void_p), a.nbytes))
+                regs.append(a)
+        rc = ctx._lib.tsdbhip_spangroup_run(ctx.handle, C.byref(desc), C.byref(out))
+    finally:
+        for a in regs:
+            ctx._lib.tsdbhip_host_unregister(ctx.handle, a.ctypes.data_as(C.c_void_p))
     n = int(out.n_out)
     return rc, ts[:n], isi[:n], bits[:n], int(out.n_input_points), int(out.err_index)
 

@@ -100,6 +100,7 @@ struct Slot {
   // to the initial values, its grid bitmap all zero (k_call_end)
   bool sm_ready = false, bitmap_clean = false;
   bool bitmapx_clean = false;  // the same for "gbitmap_x" (sharded calls whose grids differ)
+  bool tgdone_clean = false;   // the same for k_reduce's tile-group counters ("tg_done")
   std::map<std::string, Buf> zeroed;  // scratch_zero_kept: allocation last zeroed whole (not owned)
 };
 
@@ -514,7 +515,8 @@ extern "C" int tsdbhip_host_register(tsdbhip_ctx* ctx, void* p, size_t n) {
   try {
     HIPCHK(hipSetDevice(ctx->device));
     // (portable: pinned for every device of a multi-device context)
-    HIPCHK(hipHostRegister(p, n, ctx->multi ? hipHostRegisterPortable : hipHostRegisterDefault));
+    // (mapped: a long result is then written by the reduce straight into it)
+    HIPCHK(hipHostRegister(p, n, hipHostRegisterMapped | (ctx->multi ? hipHostRegisterPortable : 0u)));
   } catch (Fail& f) {
     return f.code;
   }
@@ -1286,6 +1288,17 @@ __global__ void k_count_nonzero(const uint32_t* p, uint64_t n, unsigned long lon
     if (p[i]) atomicAdd(out, 1ull);
 }
 
+// The device address of a host buffer registered mapped (tsdbhip_host_register),
+// or null for unregistered memory.
+static void* mapped_dev_ptr(void* h) {
+  void* d = nullptr;
+  if (!h || hipHostGetDevicePointer(&d, h, 0) != hipSuccess) {
+    (void)hipGetLastError();
+    return nullptr;
+  }
+  return d;
+}
+
 // grow-only scratch whose whole allocation is zero when `clean` (a new
 // allocation, or a buffer the last call left dirty, is zeroed once, all of it)
 template <typename T>
@@ -1360,6 +1373,9 @@ static int spangroup_run_once(Slot* ctx, const tsdbhip_sg_desc* d, tsdbhip_sg_ou
   ctx->sm_ready = false;
   const bool bm_clean = ctx->bitmap_clean;
   ctx->bitmap_clean = false;
+  const bool tgd_clean = ctx->tgdone_clean;
+  ctx->tgdone_clean = false;
+  bool tgd_used = false;
   const bool detail = ctx->opt.timing_detail;  // decode / grid event pairs
   HIPCHK(hipEventRecord(ctx->ev[0], st));
 
@@ -1490,7 +1506,7 @@ static int spangroup_run_once(Slot* ctx, const tsdbhip_sg_desc* d, tsdbhip_sg_ou
   da.sp_ovf_cell = sp_ovf; da.sp_cap = sp_cap; da.e_off = eoff; da.e_ts = e_ts; da.e_val = e_val;
   da.e_flt = e_flt; da.e_len = e_len; da.e_bad = e_bad; da.start = d->start_time; da.end = d->end_time;
   da.interval = interval; da.ds_agg = ds_agg; da.rate = rate; da.err = &sm->err; da.gflags = sm->gflags;
-  da.range = sm->range; da.fstar = &sm->fstar; da.span0 = sharded ? d->span0 : 0;
+  da.range = sm->range; da.fstar = &sm->fstar; da.span0 = sharded ? d->span0 : 0; da.sp_first = sp_first;
   if (detail) HIPCHK(hipEventRecord(ctx->ev[1], st));
   bool chunk_marked = false;     // k_ds_spans marked G for the spans it took
   bool direct = false;           // k_direct_scan took the no-downsampling path
@@ -1524,7 +1540,10 @@ static int spangroup_run_once(Slot* ctx, const tsdbhip_sg_desc* d, tsdbhip_sg_ou
     ctx->hot_kernel = fast ? TSDBHIP_HOT_DECODE_FAST : TSDBHIP_HOT_DECODE_GEN;
     if (!direct) HIPCHK(hipEventRecord(ctx->ev[8], st));
     if (!fast) {
-      if (interval == 0) hipLaunchKernelGGL(k_decode_nods, dim3(blocks), dim3(256), 0, st, da);
+      // (spans of many short rows, C4: a block per span decodes its rows in
+      // parallel; else a wave per span walks them)
+      if (interval == 0 && R >= 64ull * n_kept) hipLaunchKernelGGL(k_decode_rows, dim3(n_kept), dim3(256), 0, st, da);
+      else if (interval == 0) hipLaunchKernelGGL(k_decode_nods, dim3(blocks), dim3(256), 0, st, da);
       else launch_agg<LaunchGeneralDs>(ds_agg, ctx, blocks, da);
       HIPCHK(hipEventRecord(ctx->ev[9], st));
     } else if (interval == 0) {
@@ -1658,9 +1677,18 @@ static int spangroup_run_once(Slot* ctx, const tsdbhip_sg_desc* d, tsdbhip_sg_ou
   };
   if (!empty_grid) {
     ga.lo = lo; ga.hi = hi; ga.bitmap = bitmap; ga.nwords = nwords;
-    if (n_kept)
+    // (a bitmap of many slices marked by few spans each, C4: sliced through
+    // LDS; else an atomic a point)
+    const uint32_t n_sl = (uint32_t)((nwords + GM_WORDS - 1) >> GM_SHIFT);
+    if (n_kept && n_sl >= 8 && (uint64_t)(n_sl + 1) * n_kept <= (64ull << 20)) {
+      uint32_t* B = scratch<uint32_t>(ctx, "gm_bounds", (uint64_t)(n_sl + 1) * n_kept);
+      hipLaunchKernelGGL(k_grid_bounds, dim3(mark_list ? std::min(grid_for(n_kept, 4, 65536), 1024u) : grid_for(n_kept, 4, 65536)),
+                         dim3(256), 0, st, ga, B, n_sl);
+      hipLaunchKernelGGL(k_grid_mark_slices, dim3(n_sl), dim3(256), 0, st, ga, (const uint32_t*)B, n_sl);
+    } else if (n_kept) {
       hipLaunchKernelGGL(k_grid_mark, dim3(mark_list ? std::min(grid_for(n_kept, 4, 65536), 1024u) : grid_for(n_kept, 4, 65536)),
                          dim3(256), 0, st, ga);
+    }
     grid_ranks(!sharded && !fap_opt, sharded);
   }
   // ---- the optimistic aligned-group finish: when the group is tried as an
@@ -1941,6 +1969,19 @@ static int spangroup_run_once(Slot* ctx, const tsdbhip_sg_desc* d, tsdbhip_sg_ou
   int64_t* o_ts = (int64_t*)(outblk + OUT_HDR);
   int64_t* o_bits = o_ts + To;
   uint8_t* o_isint = (uint8_t*)(o_bits + To);
+  // a long unsharded result into registered (mapped) caller buffers: the
+  // reduce finalizes each tile group into them as soon as its last chunk is
+  // done, so the results cross PCIe while the reduce still runs (no D2H copy
+  // after it; C4: 178 MB)
+  FinalArgs fin_map;
+  std::memset(&fin_map, 0, sizeof fin_map);
+  if (!sharded && !small_out && ctx->want_output && T >= 65536 && out->capacity >= T) {
+    fin_map.out_ts = (int64_t*)mapped_dev_ptr(out->ts);
+    fin_map.out_bits = (int64_t*)mapped_dev_ptr(out->bits);
+    fin_map.out_isint = (uint8_t*)mapped_dev_ptr(out->is_int);
+    if (!fin_map.out_ts || !fin_map.out_bits || !fin_map.out_isint) fin_map.out_ts = nullptr;
+  }
+  bool out_direct = false;  // the results are already in the caller's buffers
 
   // ---- reduce ----
   if (T > 0) {
@@ -2022,6 +2063,19 @@ static int spangroup_run_once(Slot* ctx, const tsdbhip_sg_desc* d, tsdbhip_sg_ou
         hipLaunchKernelGGL(k_chunk_flags_w, dim3(grid_for(n_chunks, 4)), dim3(256), 0, st, dg.info, n_kept, spc,
                            n_chunks, ce);
         r.chunk_e = ce;
+      }
+      // the in-kernel finalize into the mapped result (unsharded, one pass,
+      // no direct spans, few chunks: the last chunk-wave merges them)
+      if (finalize && !init && !one_chunk && !direct && fin_map.out_ts && n_chunks > 1 && n_chunks < 64) {
+        r.tg_done = scratch_zero_kept<uint32_t>(ctx, "tg_done", ntg, tgd_clean);
+        tgd_used = true;
+        r.fin = fin;
+        r.fin.n_chunks = n_chunks;
+        r.fin.out_ts = fin_map.out_ts;
+        r.fin.out_bits = fin_map.out_bits;
+        r.fin.out_isint = fin_map.out_isint;
+        out_direct = true;
+        finalize = false;
       }
       r.ptr = scratch<uint32_t>(ctx, "cursor", n_waves * spc);
       r.st_x = scratch<uint2>(ctx, "st_x", n_waves * spc);
@@ -2225,6 +2279,7 @@ static int spangroup_run_once(Slot* ctx, const tsdbhip_sg_desc* d, tsdbhip_sg_ou
   ctx->sm_ready = true;
   ctx->bitmap_clean = true;
   if (used_bitmap_x) ctx->bitmapx_clean = true;
+  if (tgd_used) ctx->tgdone_clean = true;  // (every counter reset by its group's last wave)
   if (ls_try && h.ls_broken) {  // (agreed over the ranks) the proposal did not hold: discard, run again
     ctx->timing = tm;
     return RC_REDO;
@@ -2262,8 +2317,9 @@ static int spangroup_run_once(Slot* ctx, const tsdbhip_sg_desc* d, tsdbhip_sg_ou
     out->err_code = TSDBHIP_E_CAPACITY;
     return TSDBHIP_E_CAPACITY;
   }
-  if (!ctx->want_output) {
-    // (a non-zero rank of an in-process sharded call: rank 0 returns the output)
+  if (!ctx->want_output || out_direct) {
+    // (a non-zero rank of an in-process sharded call: rank 0 returns the
+    // output; or the reduce wrote it into the mapped caller buffers)
   } else if (n_ok && small_out) {  // (already in the pinned staging with the header)
     std::memcpy(out->ts, hb + OUT_HDR, n_ok * 8);
     std::memcpy(out->bits, hb + OUT_HDR + 8 * To, n_ok * 8);

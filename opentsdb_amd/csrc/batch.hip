@@ -239,7 +239,7 @@ static int spangroup_run_batch(Slot* ctx, const tsdbhip_sg_desc* d, uint32_t G, 
   da.sp_q1_shift = sp_q1s; da.sp_q1_rs = sp_q1rs; da.sp_ovf_cell = sp_ovf; da.sp_cap = sp_cap; da.e_off = eoff; da.e_ts = e_ts;
   da.e_val = e_val; da.e_flt = e_flt; da.e_len = e_len; da.e_bad = e_bad; da.start = d->start_time;
   da.end = d->end_time; da.interval = interval; da.ds_agg = ds_agg; da.rate = rate; da.err = &sm->err;
-  da.gflags = sm->gflags; da.range = sm->range; da.fstar = &sm->fstar; da.span0 = 0;
+  da.gflags = sm->gflags; da.range = sm->range; da.fstar = &sm->fstar; da.span0 = 0; da.sp_first = sp_first;
   da.row_ncells = dd.row_ncells; da.row_val_len = dd.row_val_len;
   HIPCHK(hipEventRecord(ctx->ev[1], st));
   bool direct = false;  // k_direct_scan took the no-downsampling path

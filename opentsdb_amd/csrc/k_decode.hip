@@ -63,6 +63,7 @@ struct DecodeArgs {
   int32_t use_fb;
   const uint32_t* span_list;  // k_decode_fast: spans to take (null = all kept)
   const uint32_t* span_count;
+  const int64_t* sp_first;    // [n_spans] first accepted ts (k_decode_rows)
 };
 
 #define BAD_ILLEGAL 1
@@ -216,6 +217,82 @@ __device__ void span_nods_general(const DecodeArgs& a, uint32_t k) {
       if (anyf) atomicOr(&a.gflags[0], 1u);
       if (anyi) atomicOr(&a.gflags[1], 1u);
     }
+  }
+}
+
+// Block (256 threads) per kept span, no downsampling: spans of many short
+// rows (C4: ~11k one-cell hourly rows a span) decoded row-parallel, a thread
+// per row, instead of the wave walk whose every 64 cells each binary-search
+// their row (k_decode_nods). Taken when the span's E is its accepted cells
+// in order (first point >= start, no Q1 seek, no `short` overflow): cell c
+// of the span (row_cell0 prefix) is E[c]. Otherwise wave 0 runs the general
+// walk. RowSeq.java:360-497 (ts = base + delta, values at the running
+// offset of the row), :194-226 (widths); unsorted cells: E_UNSORTED, as the
+// walk raises it.
+__global__ void __launch_bounds__(256) k_decode_rows(DecodeArgs a) {
+  __shared__ unsigned long long s_bad[4];
+  __shared__ uint32_t s_f[4], s_i[4], s_uns[4];
+  const uint32_t k = blockIdx.x;
+  if (k >= a.n_kept) return;
+  const uint32_t s = a.kept[k];
+  const bool rowpar = a.sp_q1[s] < 0 && a.sp_ovf_cell[s] < 0 && a.sp_first[s] >= a.start;
+  const uint32_t t = threadIdx.x, lane = t & 63, w = t >> 6;
+  if (!rowpar) {
+    if (w == 0) span_nods_general(a, k);
+    return;
+  }
+  const uint64_t r0 = a.span_row_start[s], r1 = a.span_row_start[s + 1];
+  const uint64_t eo = a.e_off[k];
+  unsigned long long bad = ~0ull;
+  bool anyf = false, anyi = false, uns = false;
+  for (uint64_t r = r0 + t; r < r1; r += 256) {
+    if (!a.row_ok[r]) continue;
+    const uint32_t n = a.row_ncells[r], c0 = a.row_cell0[r];
+    const uint64_t qo = a.row_qual_off[r], vo = a.row_val_off[r];
+    const int64_t base = a.row_base[r];
+    uint64_t off = 0;
+    int64_t prev = -1;
+    for (uint32_t i = 0; i < n; i++) {
+      const uint32_t q = load_qual(a.qual, qo + 2ull * i);
+      const uint32_t fl = q & 15;
+      const int64_t ts = base + (q >> 4);
+      int64_t bits = 0;
+      const bool ok = decode_value(a.val, vo + off, fl, &bits);
+      off += (fl & 7) + 1;
+      const uint64_t e = (uint64_t)c0 + i;
+      a.e_ts[eo + e] = (uint32_t)ts;
+      a.e_val[eo + e] = bits;
+      a.e_flt[eo + e] = (fl & 8) ? 1 : 0;
+      if (!ok) bad = min(bad, (unsigned long long)((e << 4) | BAD_ILLEGAL));
+      if (fl & 8) anyf = true; else anyi = true;
+      if (i && ts <= prev) uns = true;
+      prev = ts;
+    }
+  }
+  __syncthreads();  // (every E point of the span written by this block)
+  __threadfence_block();
+  // a row's first cell against the cell before it (the previous accepted row's last)
+  for (uint64_t r = r0 + t; r < r1; r += 256) {
+    if (!a.row_ok[r] || a.row_ncells[r] == 0) continue;
+    const uint32_t c0 = a.row_cell0[r];
+    if (c0 > 0 && a.e_ts[eo + c0] <= a.e_ts[eo + c0 - 1]) uns = true;
+  }
+  for (int o = 1; o < WAVE; o <<= 1) bad = min(bad, (unsigned long long)shfl_xor_u64(bad, o));
+  const uint64_t fm = ballot(anyf), im = ballot(anyi), um = ballot(uns);
+  if (lane == 0) {
+    s_bad[w] = bad;
+    s_f[w] = fm != 0;
+    s_i[w] = im != 0;
+    s_uns[w] = um != 0;
+  }
+  __syncthreads();
+  if (t == 0) {
+    const unsigned long long b = min(min(s_bad[0], s_bad[1]), min(s_bad[2], s_bad[3]));
+    a.e_len[k] = a.sp_ncells[s];
+    a.e_bad[k] = b == ~0ull ? -1 : (int64_t)b;
+    if (s_uns[0] | s_uns[1] | s_uns[2] | s_uns[3]) err_raise(a.err, 2, a.span0 + s, -8 /*E_UNSORTED*/);
+    if (s_f[0] | s_f[1] | s_f[2] | s_f[3]) atomicOr(&a.gflags[0], 1u);
+    if (s_i[0] | s_i[1] | s_i[2] | s_i[3]) atomicOr(&a.gflags[1], 1u);
   }
 }
 

@@ -92,6 +92,94 @@ __global__ void __launch_bounds__(256) k_grid_mark(GridArgs g) {
   }
 }
 
+// ---- the sliced grid marking (long grids of sparse spans, C4) ----
+// k_grid_mark's one atomic a point lands on a random word of a bitmap far
+// larger than an XCD's L2 (C4: 11.7M points over ~2.5M words: ~140 B of
+// fabric traffic a point). Instead the bitmap is cut into slices of GM_WORDS
+// words a block owns: k_grid_bounds records, for every marked span, the
+// first E index of each slice (one pass over E, coalesced); k_grid_mark_slices
+// then marks a slice in LDS from every span's points inside it and ORs the
+// slice into the bitmap with plain stores (one read, one write a word).
+constexpr uint32_t GM_SHIFT = 13, GM_WORDS = 1u << GM_SHIFT;  // 32 KB of LDS a slice
+
+DEVI int64_t gm_slice(const GridArgs& g, int64_t t) { return (t - g.lo) >> (5 + GM_SHIFT); }
+
+// wave per marked span w (k = list[w] or w): B[sl * nm + w] = the first of
+// the span's marked points (E indices [i0, iend): i0 = 1 with rate, iend the
+// first point past hi) in slice sl or later, iend if none, for sl in [0,
+// n_sl]; also the empty-span / F* work of k_grid_mark
+__global__ void __launch_bounds__(256) k_grid_bounds(GridArgs g, uint32_t* B, uint32_t n_sl) {
+  const int lane = lane_id();
+  const uint32_t wave = (blockIdx.x * blockDim.x + threadIdx.x) / WAVE;
+  const uint32_t nwaves = gridDim.x * blockDim.x / WAVE;
+  const uint32_t nm = g.list ? *g.list_count : g.n_kept;
+  int64_t fs = 0;
+  bool empty = false;
+  for (uint32_t w = wave; w < nm; w += nwaves) {
+    const uint32_t k = g.list ? g.list[w] : w;
+    const uint64_t eo = g.e_off[k];
+    const uint32_t len = g.e_len[k];
+    if (g.err) {
+      empty |= len == 0;
+      if (len && !g.rate && g.e_flt[eo]) fs = max(fs, (int64_t)g.e_ts[eo] + 1);
+    }
+    const uint32_t i0 = g.rate ? 1u : 0u;
+    uint32_t iend = max(len, i0);
+    int64_t last_sl = -1;  // slice of the last marked point so far
+    for (uint32_t b = i0; b < iend; b += WAVE) {
+      const uint32_t i = b + lane;
+      const bool valid = i < iend;
+      const int64_t t = valid ? (int64_t)g.e_ts[eo + i] : 0;
+      const uint64_t past = ballot(valid && t > g.hi);
+      const uint32_t lim = past ? b + (uint32_t)__builtin_ctzll(past) : iend;
+      const bool mine = i < lim;
+      const int64_t sl = mine ? gm_slice(g, t) : 0;
+      int64_t sp = (int64_t)shfl_up_u64((uint64_t)sl, 1);
+      if (lane == 0) sp = last_sl;
+      if (mine)
+        for (int64_t s2 = sp + 1; s2 <= sl; s2++) B[(uint64_t)s2 * nm + w] = i;
+      if (lim > b) last_sl = (int64_t)readlane_u64((uint64_t)sl, (int)min(lim - b, (uint32_t)WAVE) - 1);
+      if (past) {
+        iend = lim;
+        break;
+      }
+    }
+    for (int64_t sl = last_sl + 1 + lane; sl <= (int64_t)n_sl; sl += WAVE) B[(uint64_t)sl * nm + w] = iend;
+  }
+  if (g.err && lane == 0) {
+    if (empty) err_raise(g.err, 2, 0, -3 /*E_EMPTY_SPAN*/);
+    if (fs && (unsigned long long)fs > *(volatile unsigned long long*)g.fstar)
+      atomicMax(g.fstar, (unsigned long long)fs);
+  }
+}
+
+// block per slice: the marked spans' points inside it set in LDS, then OR-ed
+// into the bitmap's words of the slice
+__global__ void __launch_bounds__(256) k_grid_mark_slices(GridArgs g, const uint32_t* B, uint32_t n_sl) {
+  __shared__ uint32_t s_w[GM_WORDS];
+  const uint32_t sl = blockIdx.x;
+  for (uint32_t i = threadIdx.x; i < GM_WORDS; i += 256) s_w[i] = 0;
+  __syncthreads();
+  const uint32_t nm = g.list ? *g.list_count : g.n_kept;
+  const int lane = lane_id();
+  const uint64_t wbase = (uint64_t)sl << GM_SHIFT;
+  for (uint32_t w = threadIdx.x / WAVE; w < nm; w += 4) {
+    const uint32_t k = g.list ? g.list[w] : w;
+    const uint32_t a = B[(uint64_t)sl * nm + w], b = B[(uint64_t)(sl + 1) * nm + w];
+    if (a >= b) continue;
+    const uint64_t eo = g.e_off[k];
+    for (uint32_t i = a + lane; i < b; i += WAVE) {
+      const uint64_t bit = (uint64_t)((int64_t)g.e_ts[eo + i] - g.lo);
+      atomicOr(&s_w[(bit >> 5) - wbase], 1u << (bit & 31));
+    }
+  }
+  __syncthreads();
+  for (uint32_t i = threadIdx.x; i < GM_WORDS; i += 256) {
+    const uint64_t wd = wbase + i;
+    if (wd < g.nwords && s_w[i]) g.bitmap[wd] |= s_w[i];
+  }
+}
+
 // Per-block (1024 words) exclusive popcount prefix.
 __global__ void __launch_bounds__(256) k_grid_popc(GridArgs g) {
   __shared__ uint32_t s_wave[4];

@@ -26,6 +26,20 @@ namespace tsdb {
 
 enum { MODE_INT = 0, MODE_DBL = 1, MODE_DUAL = 2 };
 
+struct FinalArgs {
+  uint64_t T;
+  uint32_t n_chunks;
+  const uint32_t* grid;
+  uint64_t fstar;            // max float-first ts + 1 (0: none)
+  int32_t rate;
+  int64_t* out_ts;
+  uint8_t* out_isint;
+  int64_t* out_bits;
+  unsigned long long* nan_t; // [1] min t index with NaN/Inf double
+  uint64_t g_base;           // global index of point 0 (a rank's slice of G; nan_t is global)
+  uint64_t stride;           // partials' stride between chunks (0: T)
+};
+
 struct ReduceArgs {
   const uint64_t* e_off;
   const uint32_t* e_len;
@@ -97,6 +111,13 @@ struct ReduceArgs {
   // in each wave's LDS (dynamic, red_lds_stride bytes a wave) instead of the
   // global st_* arrays: a long grid re-reads it every tile
   uint32_t lds_state;
+  // in-kernel finalize (k_reduce only; null: the finalize kernels run after):
+  // the last of a tile group's n_chunks waves to finish (tg_done[tg] counts
+  // them, and is reset to 0 by that wave) merges the chunks in order and
+  // finalizes the group's points into `fin` (the caller's mapped result
+  // buffers: the results cross PCIe while the other waves still compute)
+  uint32_t* tg_done;
+  FinalArgs fin;
 };
 
 // LDS bytes of one span's state (y pair, x pair, E offset, [rate value],
@@ -239,6 +260,32 @@ DEVI void acc_load(const ReduceArgs& r, uint64_t p, Acc& a) {
   }
 }
 
+
+template <int AGG, int MODE, bool RATE>
+DEVI void finalize_one(const FinalArgs& f, uint64_t g, const Acc& a) {
+  const int64_t t = f.grid[g];
+  const bool isflt = RATE || MODE == MODE_DBL || (a.flag & 1u) || ((uint64_t)t + 1 < f.fstar);
+  int64_t bits;
+  if (isflt) {
+    double d;
+    if (AGG == 0) d = a.da;
+    else if (AGG == 3) d = a.da / (double)(int32_t)a.cnt;
+    else if (AGG == 4) d = wf_result(a.wd);
+    else d = (a.flag & 2u) ? __longlong_as_double(0x7ff8000000000000LL) : a.da;
+    if (d != d || isinf(d)) atomicMin(f.nan_t, (unsigned long long)(f.g_base + g));
+    bits = dbits(d);
+  } else {
+    if (AGG == 3) bits = ldiv(a.ia, (int64_t)(int32_t)a.cnt);
+    // (integer dev: the caller reduces in one span-ordered pass, so this is
+    // the reference's sequential Welford, :196-217)
+    else if (AGG == 4) bits = d2l(wf_result(a.wi));
+    else bits = a.ia;
+  }
+  f.out_ts[g] = t;
+  f.out_isint[g] = isflt ? 0 : 1;
+  f.out_bits[g] = bits;
+}
+
 // Java long lerp: y0 + (x - x0) * (y1 - y0) / (x1 - x0), 0 < x1 - x0 < 2^32.
 DEVI int64_t lerp_long(int64_t x, int64_t x0, int64_t y0, int64_t x1, int64_t y1) {
   const int64_t num = lmul(x - x0, lsub(y1, y0));
@@ -363,8 +410,10 @@ DEVI void direct_run(const ReduceArgs& r, Acc& acc, uint32_t run, uint32_t i, ui
 // reduce_wave: the work of one wave (tile group x span chunk) of a group;
 // k_reduce runs one group, k_reduce_seg (k_group.hip) many groups per launch.
 template <int AGG, int MODE, bool RATE, bool DONLY>
+DEVI void reduce_wave_body(const ReduceArgs& r, const uint32_t wave, uint8_t* lds_w, const uint32_t chunk,
+                           const uint32_t tg);
+template <int AGG, int MODE, bool RATE, bool DONLY>
 DEVI void reduce_wave(const ReduceArgs& r, const uint32_t wave, uint8_t* lds_w) {
-  const int lane = lane_id();
   const uint32_t n_waves = r.n_chunks * r.n_tile_groups;
   if (wave >= n_waves) return;
   const uint32_t chunk = wave % r.n_chunks;
@@ -372,6 +421,38 @@ DEVI void reduce_wave(const ReduceArgs& r, const uint32_t wave, uint8_t* lds_w) 
   // (no chunk flags: the general instantiation takes every chunk)
   if (r.d_info && r.chunk_e && (r.chunk_e[chunk] != 0) == DONLY) return;  // the other instantiation's chunk
   if ((!r.d_info || !r.chunk_e) && DONLY) return;
+  reduce_wave_body<AGG, MODE, RATE, DONLY>(r, wave, lds_w, chunk, tg);
+  if (!r.tg_done) return;
+  // this chunk's partials of tile group tg are stored: release them; the
+  // group's last wave acquires every chunk's and finalizes the group
+  const int lane = lane_id();
+  __threadfence();
+  uint32_t prev = 0;
+  if (lane == 0) prev = atomicAdd(&r.tg_done[tg], 1u);
+  prev = __builtin_amdgcn_readfirstlane(prev);
+  if (prev != r.n_chunks - 1) return;
+  __threadfence();
+  if (lane == 0) r.tg_done[tg] = 0u;  // (zero for the next call)
+  const uint64_t n_tiles = (r.T + WAVE - 1) / WAVE;
+  const uint64_t tb = (uint64_t)tg * r.tiles_per_wave, te = min(n_tiles, tb + r.tiles_per_wave);
+  for (uint64_t t = tb; t < te; t++) {
+    const uint64_t g = t * WAVE + lane;
+    if (g >= r.T) break;
+    Acc a;
+    acc_load<AGG, MODE>(r, g, a);
+    for (uint32_t c = 1; c < r.n_chunks; c++) {
+      Acc b;
+      acc_load<AGG, MODE>(r, (uint64_t)c * r.T + g, b);
+      acc_merge<AGG, MODE>(a, b);
+    }
+    finalize_one<AGG, MODE, RATE>(r.fin, g, a);
+  }
+}
+
+template <int AGG, int MODE, bool RATE, bool DONLY>
+DEVI void reduce_wave_body(const ReduceArgs& r, const uint32_t wave, uint8_t* lds_w, const uint32_t chunk,
+                           const uint32_t tg) {
+  const int lane = lane_id();
   const uint32_t k0 = chunk * r.spans_per_chunk;
   const uint32_t k1 = min(r.n_kept, k0 + r.spans_per_chunk);
   const uint64_t n_tiles = (r.T + WAVE - 1) / WAVE;
@@ -715,6 +796,15 @@ DEVI void reduce_wave(const ReduceArgs& r, const uint32_t wave, uint8_t* lds_w) 
       double magr2_l = 0.0;
       if (!RATE && MODE != MODE_DBL && !dual_all_dbl && sc && j_l + 1 < len_l && x2_l > x_l.y)
         lerp_long_prep(y_l.y, y2_l, x2_l - x_l.y, im2_l, magr2_l);
+      // ... and its double lerp's y0, y1 - y0 and 1 / (x1 - x0) (outside
+      // EXACT_ORDER the lanes after point j then lerp as the cached path does:
+      // a product with the reciprocal, no division a lane)
+      double y0d2_l = 0.0, dyd2_l = 0.0, rinv2_l = 0.0;
+      if (!RATE && MODE != MODE_INT && !r.exact && sc && j_l + 1 < len_l && x2_l > x_l.y) {
+        y0d2_l = to_double(y_l.y, MODE == MODE_DBL || (f_l & 2u));
+        dyd2_l = to_double(y2_l, MODE == MODE_DBL || f2_l != 0) - y0d2_l;
+        rinv2_l = 1.0 / (double)(x2_l - x_l.y);
+      }
       const uint64_t smask = ballot(sc && (int64_t)x2_l > t_last);
       const uint32_t nb = min((uint32_t)WAVE, k1 - kb);
       // A span with no point in this tile (its next point j lies past t_last):
@@ -843,8 +933,15 @@ DEVI void reduce_wave(const ReduceArgs& r, const uint32_t wave, uint8_t* lds_w) 
                   else
                     yi = lerp_long(tl, xc, yc, xn, yn);
                 }
-                if (MODE != MODE_INT)
-                  yd = lerp_double(tl, xc, to_double(yc, MODE == MODE_DBL || fc), xn, to_double(yn, MODE == MODE_DBL || fn));
+                if (MODE != MODE_INT) {
+                  if (r.exact)
+                    yd = lerp_double(tl, xc, to_double(yc, MODE == MODE_DBL || fc), xn, to_double(yn, MODE == MODE_DBL || fn));
+                  else  // (the cached bracket's prepared doubles, as `cached`)
+                    yd = __longlong_as_double((long long)readlane_u64((uint64_t)__double_as_longlong(y0d_l), (int)i)) +
+                         ((double)(uint32_t)(tl - xc) *
+                          __longlong_as_double((long long)readlane_u64((uint64_t)__double_as_longlong(dyd_l), (int)i))) *
+                             __longlong_as_double((long long)readlane_u64((uint64_t)__double_as_longlong(rinv_l), (int)i));
+                }
                 acc_push<AGG, MODE>(acc, yi, yd);
               }
             } else if (tl == xn) {
@@ -862,8 +959,15 @@ DEVI void reduce_wave(const ReduceArgs& r, const uint32_t wave, uint8_t* lds_w) 
                 else
                   yi = lerp_long(tl, xn, yn, x2, y2);
               }
-              if (MODE != MODE_INT)
-                yd = lerp_double(tl, xn, to_double(yn, MODE == MODE_DBL || fn), x2, to_double(y2, MODE == MODE_DBL || ff));
+              if (MODE != MODE_INT) {
+                if (r.exact)
+                  yd = lerp_double(tl, xn, to_double(yn, MODE == MODE_DBL || fn), x2, to_double(y2, MODE == MODE_DBL || ff));
+                else
+                  yd = __longlong_as_double((long long)readlane_u64((uint64_t)__double_as_longlong(y0d2_l), (int)i)) +
+                       ((double)(uint32_t)(tl - xn) *
+                        __longlong_as_double((long long)readlane_u64((uint64_t)__double_as_longlong(dyd2_l), (int)i))) *
+                           __longlong_as_double((long long)readlane_u64((uint64_t)__double_as_longlong(rinv2_l), (int)i));
+              }
               acc_push<AGG, MODE>(acc, yi, yd);
             }
           }
@@ -949,45 +1053,6 @@ __global__ void k_chunk_flags(const uint32_t* d_info, uint32_t n_kept, uint32_t 
 }
 
 // ------------------------------------------------------------- finalize ---
-struct FinalArgs {
-  uint64_t T;
-  uint32_t n_chunks;
-  const uint32_t* grid;
-  uint64_t fstar;            // max float-first ts + 1 (0: none)
-  int32_t rate;
-  int64_t* out_ts;
-  uint8_t* out_isint;
-  int64_t* out_bits;
-  unsigned long long* nan_t; // [1] min t index with NaN/Inf double
-  uint64_t g_base;           // global index of point 0 (a rank's slice of G; nan_t is global)
-  uint64_t stride;           // partials' stride between chunks (0: T)
-};
-
-template <int AGG, int MODE, bool RATE>
-DEVI void finalize_one(const FinalArgs& f, uint64_t g, const Acc& a) {
-  const int64_t t = f.grid[g];
-  const bool isflt = RATE || MODE == MODE_DBL || (a.flag & 1u) || ((uint64_t)t + 1 < f.fstar);
-  int64_t bits;
-  if (isflt) {
-    double d;
-    if (AGG == 0) d = a.da;
-    else if (AGG == 3) d = a.da / (double)(int32_t)a.cnt;
-    else if (AGG == 4) d = wf_result(a.wd);
-    else d = (a.flag & 2u) ? __longlong_as_double(0x7ff8000000000000LL) : a.da;
-    if (d != d || isinf(d)) atomicMin(f.nan_t, (unsigned long long)(f.g_base + g));
-    bits = dbits(d);
-  } else {
-    if (AGG == 3) bits = ldiv(a.ia, (int64_t)(int32_t)a.cnt);
-    // (integer dev: the caller reduces in one span-ordered pass, so this is
-    // the reference's sequential Welford, :196-217)
-    else if (AGG == 4) bits = d2l(wf_result(a.wi));
-    else bits = a.ia;
-  }
-  f.out_ts[g] = t;
-  f.out_isint[g] = isflt ? 0 : 1;
-  f.out_bits[g] = bits;
-}
-
 // few chunks: one thread per t, chunks in order
 template <int AGG, int MODE, bool RATE>
 __global__ void __launch_bounds__(256) k_finalize_seq(ReduceArgs r, FinalArgs f) {

@@ -63,11 +63,11 @@ def assert_same(g, o, rtol=1e-9, exact_double=False, check_err_index=True, abs_s
         np.testing.assert_allclose(gd, od, rtol=rtol, atol=0, err_msg="double values")
 
 
-def corrupt_qual(ss, span, cell, fn):
-    """A copy of the SpanSet with one qualifier (cell `cell` of span `span`'s
-    first row) rewritten by fn(q) -> q' (16-bit host-order values)."""
+def corrupt_qual(ss, span, cell, fn, row=0):
+    """A copy of the SpanSet with one qualifier (cell `cell` of row `row` of
+    span `span`) rewritten by fn(q) -> q' (16-bit host-order values)."""
     qb = ss.qual_bytes.copy()
-    r = int(ss.span_row_start[span])
+    r = int(ss.span_row_start[span]) + row
     off = int(ss.row_qual_off[r]) + 2 * cell
     q = (int(qb[off]) << 8) | int(qb[off + 1])
     q2 = fn(q) & 0xFFFF

@@ -19,6 +19,10 @@ from opentsdb_amd import _abi, core, packing
 
 
 def groups(seed, absval=False):
+    return packing.pack_spans(groups_list(seed, absval))
+
+
+def groups_list(seed, absval=False):
     rng = np.random.default_rng(seed)
     spans = []
     for s in range(100):  # sparse double series: long brackets over many tiles
@@ -32,7 +36,7 @@ def groups(seed, absval=False):
     # lie inside the sparse series' brackets
     drv = [(T0 + 7 * i, (1000 + i) if absval else (1000 + i) * (1 if i % 3 else -1)) for i in range(150_000)]
     spans.append(I(drv, minimal=False))
-    return packing.pack_spans(spans)
+    return spans
 
 
 @pytest.mark.gpu
@@ -49,5 +53,23 @@ def test_opposite_slopes_line_in_t(ctx, seed, agg):
     assert np.median(np.abs(res[dbl]) / scale[dbl]) < 0.5  # (the sums cancel)
     g = core.run_spanset(ctx, ss, 0, U32MAX, agg)
     assert_same(g, o, abs_scale=scale)
+    # (registered result buffers: each tile group finalized by the reduce into them)
+    g = core.run_spanset(ctx, ss, 0, U32MAX, agg, register_out=True)
+    assert_same(g, o, abs_scale=scale)
     gx = core.run_spanset(ctx, ss, 0, U32MAX, agg, exact=True)
     assert_same(gx, o, exact_double=True)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("register_out", [False, True])
+def test_nan_in_a_long_grid(ctx, register_out):
+    """a NaN value mid-way through a long grid: IllegalStateException at the
+    first NaN output (SpanGroup.java:660-663), also when the reduce finalizes
+    into the caller's registered buffers"""
+    spans = [F([(T0 + 7 * i + 3, float("nan") if i == 60_000 else 1.5) for i in range(100_000)], double=True)]
+    base = groups_list(3) + spans
+    ss = packing.pack_spans(base)
+    o = oracle.spangroup(ss, 0, U32MAX, _abi.AGG_SUM)
+    assert o.code == _abi.E_NAN_INF and o.err_index > 100_000
+    g = core.run_spanset(ctx, ss, 0, U32MAX, _abi.AGG_SUM, register_out=register_out)
+    assert_same(g, o)

@@ -172,7 +172,8 @@ def test_c4_million_point_union(ctx, gen, agg):
     ~11.5k points: a union grid of > 1M points, general (bitmap + E) path."""
     ff, fc = (0.5, 0.01) if gen == "c4" else (0.0, 0.0)
     ss = synth.jittered_packed(100, 11500, seed=4, float_frac=ff, float_cell_frac=fc)
-    g = core.run_spanset(ctx, ss, 0, U32MAX, agg)
+    # (registered result buffers: the reduce writes the results into them)
+    g = core.run_spanset(ctx, ss, 0, U32MAX, agg, register_out=True)
     o = oracle.spangroup(ss, 0, U32MAX, agg, capacity=ss.n_cells() + 16)
     assert o.code == 0 and len(o.ts) > 1_000_000
     assert_same(g, o, abs_scale=abs_bound(100, 11500, 4, ff, fc, agg, o.ts))
@@ -247,7 +248,7 @@ def test_c4_full_size(ctx, name):
     ff, fc = (0.5, 0.01) if e["gen"] == "jitter" else (0.0, 0.0)
     ss = synth.jittered_packed(e["n_series"], e["n_points"], seed=e["seed"], float_frac=ff, float_cell_frac=fc)
     gx = core.run_spanset(ctx, ss, 0, U32MAX, e["agg"], exact=True)
-    g = core.run_spanset(ctx, ss, 0, U32MAX, e["agg"])
+    g = core.run_spanset(ctx, ss, 0, U32MAX, e["agg"], register_out=True)
     rc, ts, isi, bits, n_in, _ = gx
     assert rc == e["code"] and n_in == e["n_input"] and len(ts) == e["n_out"]
     assert sha(ts, "<i8") == e["ts"], "timestamps differ from the oracle"
