@@ -269,6 +269,37 @@ def test_error_order_is_global_span_order(mctx, ctx):
 
 
 @pytest.mark.gpu
+def test_error_stages_across_ranks_vs_oracle(mctx):
+    """Errors in different ranks and stages, against the oracle:
+    the reference throws the first it meets -- Span.addRow while the rows
+    are scanned (an empty KeyValue: ArrayIndexOutOfBounds), then SpanGroup
+    construction (an empty span: AssertionError, SpanGroup.java:452-455),
+    then the lazy iteration (an illegal cell width, RowSeq.java:203, at its
+    output index) -- whichever rank holds each. Rows sorted within spans (the
+    header's contract)."""
+    n = 3 * mctx.ranks
+    good = lambda s: I([(T0 + 5 * i, 100 * s + i) for i in range(40)])  # noqa: E731
+    bad_cell = packing.KeyValue(T0 + 3600, bytes([0x00, 0x02, 0x00, 0x12]), bytes([1, 2, 3, 4, 5, 6, 0]))
+    spans = [good(s) for s in range(n)]
+    spans[0] = spans[0] + [bad_cell]                       # lazy, rank 0
+    spans[n - 1] = [packing.KeyValue(T0, b"", b"")] + spans[n - 1]  # scan, last rank
+    for drop_scan in (False, True):
+        sp = list(spans)
+        if drop_scan:
+            sp[n - 1] = good(n - 1)
+        ss = packing.pack_spans(sp)
+        # an empty span in rank 0 (SpanGroup construction)
+        ss.span_row_start = np.concatenate([ss.span_row_start[:2], ss.span_row_start[1:]]).astype(np.uint64)
+        g, o = both(mctx, ss)
+        assert o.code == (_abi.E_EMPTY_SPAN if drop_scan else _abi.E_OUT_OF_BOUNDS)
+        assert_same(g, o)
+    ss = packing.pack_spans([good(s) for s in range(n - 1)] + [spans[0]])  # the bad cell in the last rank only
+    g, o = both(mctx, ss)
+    assert o.code == _abi.E_ILLEGAL_DATA and o.err_index > 0
+    assert_same(g, o)
+
+
+@pytest.mark.gpu
 def test_device_desc_sharded(mctx):
     """device-resident input (tsdbhip_synth_generate) split by span count"""
     import ctypes as C
