@@ -35,8 +35,13 @@ def test_many_short_rows(ctx, seed, agg, rate):
 @pytest.mark.gpu
 @pytest.mark.parametrize("agg", [0, 4])
 def test_many_short_rows_int(ctx, agg):
+    """integer spans: the long outputs bit-exact; the double ones (dev, and
+    the lerped-to-double points) at 1e-9 in the default merge order, bit-exact
+    under EXACT_ORDER"""
     ss = sparse(3, float_frac=0.0)
     g, o = run_both(ctx, ss, agg=agg)
+    assert_same(g, o)
+    g, o = run_both(ctx, ss, agg=agg, exact=True)
     assert_same(g, o, exact_double=True)
 
 
