@@ -380,7 +380,7 @@ def bench_c5(args):
     # first and last HIP event (the copies alone overstate it)
     call_ms = float(np.mean(tot))
     hot_ms = float(np.mean(hot))
-    achieved = alg_all / (call_ms * 1e-3) / 1e9
+    achieved = alg_all / (max(call_ms, 1e-9) * 1e-3) / 1e9
     kname = "tsdbhip_compact_rows (whole call)"
     call_kernels = ("k_compact_quals+k_compact_classify+k_compact_vals+k_compact_rows+k_compact_complex"
                     "+k_compact_dups")
@@ -398,7 +398,7 @@ def bench_c5(args):
                      "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                      "traffic_source": traffic_src, "traffic_kernels": call_kernels,
                      "alg_bytes_per_launch": alg_all, "kernel_ms": call_ms,
-                     "copy_kernels_ms": hot_ms, "copy_kernels_achieved": alg_all / (hot_ms * 1e-3) / 1e9,
+                     "copy_kernels_ms": hot_ms, "copy_kernels_achieved": alg_all / (max(hot_ms, 1e-9) * 1e-3) / 1e9,
                      "complex_kernel_ms": float(np.mean(cx)), "classify_kernel_ms": float(np.mean(cls)),
                      "rows_kernel_ms": float(np.mean(rows_k))},
     }
@@ -531,7 +531,7 @@ def main():
                          "path on a 1-rank RCCL communicator (per-rank work and exchange code of an N-GPU run; "
                          "the line says so and its value is that one shard's rate)")
     ap.add_argument("--option", action="append", default=[], metavar="NAME=VALUE",
-                    help="a context option (tsdbhip_set_option: decode, aligned_group, lockstep, compact, "
+                    help="a context option (tsdbhip_set_option: decode, aligned_group, lockstep, compact, events, "
                          "timing_detail) for A/B runs; results never depend on it")
     ap.add_argument("--dry-run", action="store_true",
                     help="harness check without a GPU: the multi-rank timing/barrier/report path with a "
@@ -733,7 +733,7 @@ def main():
         kname, hot = "k_reduce", reduce_ms
         hot_bytes = emitted[0] * 13 + emitted[1] * 17
         valu_bound = True
-    achieved = hot_bytes / (hot * 1e-3) / 1e9
+    achieved = hot_bytes / (max(hot, 1e-9) * 1e-3) / 1e9
     traffic, traffic_src = pmc_traffic(args.config, kname, world)
     if rank == 0:
         res = {
@@ -776,7 +776,7 @@ def main():
                 "kernel_ms": hot,
                 "step_device_ms": float(np.mean(total_ms)),
                 "path_alg_bytes": local_bytes,
-                "path_GBs": local_bytes / (float(np.mean(total_ms)) * 1e-3) / 1e9,
+                "path_GBs": local_bytes / (max(float(np.mean(total_ms)), 1e-9) * 1e-3) / 1e9,
                 "achievable_GBs": {k: round(v, 1) for k, v in probe.items()},
                 "frac_of_read_stream": achieved / probe["read_stream"] if probe else None,
             },
@@ -794,7 +794,7 @@ def main():
             rl["peak"] = VALU_PEAK_WIPS
             rl["valu_insts_per_launch"] = vi
             rl["valu_source"] = vsrc
-            rl["achieved"] = vi / (hot * 1e-3) if vi else None
+            rl["achieved"] = vi / (hot * 1e-3) if vi and hot > 0 else None
             rl["frac"] = rl["achieved"] / VALU_PEAK_WIPS if vi else None
         # which variants ran (tsdbhip_timing.paths): the aligned-group reduction
         # (k_ds_reg's block partials instead of E + k_reduce) or its rerun

@@ -155,7 +155,7 @@ typedef struct tsdbhip_timing {
   float    decode_ms;       /* decode(+downsample) kernel — dominant, HBM   */
   float    grid_ms;         /* union-grid construction                      */
   float    reduce_ms;       /* cross-span reduction + combine               */
-  float    exchange_ms;     /* RCCL exchange (sharded runs)                 */
+  float    exchange_ms;     /* RCCL exchange (sharded runs, "timing_detail") */
   float    hot_ms;          /* the dominant HBM-streaming kernel alone      */
   uint32_t hot_kernel;      /* TSDBHIP_HOT_*: which kernel hot_ms timed      */
   uint32_t n_collectives;   /* sharded calls: collective launches this rank
@@ -312,10 +312,16 @@ int         tsdbhip_open_devices(const int32_t* devices, uint32_t n, tsdbhip_ctx
  * variant, A/B runs to compare; no environment variable is read):
  *   "decode"        "auto" | "general" | "fast" | "chunks" | "spans" | "direct"
  *   "aligned_group" "on" | "off"   k_ds_reg's aligned-group reduction
- *   "lockstep"      "on" | "off"   the lockstep proposal (k_lockstep)
+ *   "lockstep"      "on" | "off" | "always"   the lockstep proposal (k_lockstep):
+ *                   "on" for groups of >= 2048 lockstep waves (and sharded
+ *                   groups), "always" for any group
  *   "compact"       "auto" | "tiles"  (tiles: every row through k_compact_tiles)
  *   "timing_detail" "on" | "off"   decode / grid event pairs in tsdbhip_timing
  *   "check_clean"   "on" | "off"   check the zero-on-entry invariants (stderr)
+ *   "events"        "kernel" | "marker" | "none"   how tsdbhip_timing is measured:
+ *                   HIP events carried by the kernel launches (default), event
+ *                   markers between kernels (each can idle the GPU a few us),
+ *                   or not at all (timings 0)
  * Unknown names or values: TSDBHIP_E_INVALID_ARG. */
 int         tsdbhip_set_option(tsdbhip_ctx* ctx, const char* name, const char* value);
 int         tsdbhip_open_mask(uint32_t gpu_mask, tsdbhip_ctx** out);

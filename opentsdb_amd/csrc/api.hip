@@ -12,6 +12,7 @@
 // With TSDBHIP_SHARDED the grid bitmap and the per-t partials are exchanged
 // over RCCL (allgather, then a rank-ordered combine on every rank).
 #include <hip/hip_runtime.h>
+#include <hip/hip_ext.h>
 #include <rccl/rccl.h>
 
 #include <algorithm>
@@ -62,10 +63,11 @@ enum { DEC_AUTO = 0, DEC_GENERAL, DEC_FAST, DEC_CHUNKS, DEC_SPANS, DEC_DIRECT };
 struct Options {
   int decode = DEC_AUTO;       // "decode": the decode / downsample path forced
   bool aligned_group = true;   // "aligned_group": k_ds_reg's aligned-group reduction may be tried
-  bool lockstep = true;        // "lockstep": the lockstep proposal may be made
+  int lockstep = 1;            // "lockstep": "off" (0), "on" (1: groups big enough), "always" (2)
   bool compact_tiles = false;  // "compact": "tiles" sends every row through k_compact_tiles
   bool timing_detail = false;  // "timing_detail": decode / grid event pairs (tsdbhip_timing)
   bool check_clean = false;    // "check_clean": verify the zero-on-entry invariants (stderr)
+  int events = 0;              // "events": timing events on kernel launches (0), marker packets (1), none (2)
 };
 
 // Per-call resources. A call takes a free slot of its context (or a new
@@ -180,6 +182,43 @@ static unsigned grid_for(uint64_t work, unsigned per_block, unsigned cap = 1u <<
   return (unsigned)g;
 }
 
+// Timing events (tsdbhip_timing). "kernel" (the default): a start event rides
+// on the next kernel launched through LAUNCH (hipExtLaunchKernel's start
+// event) and a stop event on the kernel it follows (LAUNCH_STOP), so no
+// marker packet stands between two kernels: in the C3* shard trace each
+// hipEventRecord between kernels left the GPU idle ~5 us. "marker": events
+// recorded in the stream (hipEventRecord). "none": no events (timings 0).
+static thread_local hipEvent_t g_ev_pend = nullptr;
+static inline hipEvent_t ev_take() {
+  hipEvent_t e = g_ev_pend;
+  g_ev_pend = nullptr;
+  return e;
+}
+static void EV_START(Slot* ctx, int i) {
+  if (ctx->opt.events == 0) {
+    if (g_ev_pend) HIPCHK(hipEventRecord(ev_take(), ctx->stream));  // (no kernel took the last one)
+    g_ev_pend = ctx->ev[i];
+  } else if (ctx->opt.events == 1) {
+    HIPCHK(hipEventRecord(ctx->ev[i], ctx->stream));
+  }
+}
+// the stop event for LAUNCH_STOP ("kernel"), then EV_STOP_M after it ("marker")
+#define EV_STOP_K(ctx, i) ((ctx)->opt.events == 0 ? (ctx)->ev[i] : (hipEvent_t) nullptr)
+#define EV_STOP_M(ctx, i)                                                             \
+  do {                                                                                \
+    if ((ctx)->opt.events == 1) HIPCHK(hipEventRecord((ctx)->ev[i], (ctx)->stream)); \
+  } while (0)
+#define LAUNCH(k, g, b, sh, st, ...) hipExtLaunchKernelGGL(k, g, b, sh, st, ev_take(), nullptr, 0, ##__VA_ARGS__)
+#define LAUNCH_STOP(ev, k, g, b, sh, st, ...) hipExtLaunchKernelGGL(k, g, b, sh, st, ev_take(), ev, 0, ##__VA_ARGS__)
+static float ev_ms(Slot* ctx, int a, int b) {
+  float ms = 0;
+  if (ctx->opt.events == 2 || hipEventElapsedTime(&ms, ctx->ev[a], ctx->ev[b]) != hipSuccess) {
+    (void)hipGetLastError();
+    return ctx->opt.events == 2 ? 0.f : -1.f;
+  }
+  return ms;
+}
+
 #include "xchg.hip"
 
 static void dscan_u64(Slot* ctx, const uint64_t* in, uint64_t* out, uint64_t n, uint64_t* d_total,
@@ -191,9 +230,9 @@ static void dscan_u64(Slot* ctx, const uint64_t* in, uint64_t* out, uint64_t n, 
     HIPCHK(hipMemsetAsync(d_total, 0, 8, ctx->stream));
     return;
   }
-  hipLaunchKernelGGL(k_scan_block_u64, dim3((unsigned)nb), dim3(256), 0, ctx->stream, in, out, n, bs);
-  hipLaunchKernelGGL(k_scan_blocks_u64, dim3(1), dim3(256), 0, ctx->stream, bs, nb, d_total);
-  hipLaunchKernelGGL(k_scan_add_u64, dim3(grid_for(n, 256)), dim3(256), 0, ctx->stream, out, n, bs);
+  LAUNCH(k_scan_block_u64, dim3((unsigned)nb), dim3(256), 0, ctx->stream, in, out, n, bs);
+  LAUNCH(k_scan_blocks_u64, dim3(1), dim3(256), 0, ctx->stream, bs, nb, d_total);
+  LAUNCH(k_scan_add_u64, dim3(grid_for(n, 256)), dim3(256), 0, ctx->stream, out, n, bs);
 }
 
 // ------------------------------------------------------------ slot pool ----
@@ -223,7 +262,10 @@ static Slot* slot_new(int device) {
     HIPCHK(hipHostMalloc((void**)&ctx->map_state, 8 * 520, hipHostMallocMapped | hipHostMallocCoherent));
     HIPCHK(hipHostGetDevicePointer((void**)&ctx->map_state_dev, ctx->map_state, 0));
     std::memset(ctx->map_state, 0, 8 * 520);
-    for (auto& e : ctx->ev) HIPCHK(hipEventCreate(&e));
+    // (timing only: no system-scope fence, i.e. no L2 writeback / invalidate
+    // when an event is recorded; results reach the host through coherent
+    // mapped memory and stream syncs, never through these events)
+    for (auto& e : ctx->ev) HIPCHK(hipEventCreateWithFlags(&e, hipEventDisableSystemFence));
   } catch (Fail&) {
     slot_free(ctx);
     throw;
@@ -482,13 +524,21 @@ extern "C" int tsdbhip_set_option(tsdbhip_ctx* ctx, const char* name, const char
     for (int i = 0; i < 6; i++)
       if (v == names[i]) { o.decode = i; ok = true; }
   } else if (n == "aligned_group") ok = on_off(o.aligned_group);
-  else if (n == "lockstep") ok = on_off(o.lockstep);
+  else if (n == "lockstep") {
+    ok = v == "on" || v == "off" || v == "always";
+    o.lockstep = v == "off" ? 0 : (v == "on" ? 1 : 2);
+  }
   else if (n == "compact") {
     ok = v == "auto" || v == "tiles";
     o.compact_tiles = v == "tiles";
   } else if (n == "timing_detail") ok = on_off(o.timing_detail);
   else if (n == "check_clean") ok = on_off(o.check_clean);
-  else ok = false;
+  else if (n == "events") {
+    static const char* names[] = {"kernel", "marker", "none"};
+    ok = false;
+    for (int i = 0; i < 3; i++)
+      if (v == names[i]) { o.events = i; ok = true; }
+  } else ok = false;
   if (!ok) {
     set_error(ctx, "tsdbhip_set_option: unknown option %s=%s", name, value);
     return TSDBHIP_E_INVALID_ARG;
@@ -684,7 +734,7 @@ static void launch_agg(int agg, A&&... args) {
 struct LaunchGeneralDs {
   template <int AGG>
   static void run(Slot* ctx, unsigned blocks, const DecodeArgs& a) {
-    hipLaunchKernelGGL(k_decode_ds<AGG>, dim3(blocks), dim3(256), 0, ctx->stream, a);
+    LAUNCH(k_decode_ds<AGG>, dim3(blocks), dim3(256), 0, ctx->stream, a);
   }
 };
 
@@ -692,7 +742,7 @@ struct LaunchFastDs {
   template <int AGG>
   static void run(Slot* ctx, unsigned blocks, const DecodeArgs& a, const uint32_t* ncells,
                   const uint32_t* vlen) {
-    hipLaunchKernelGGL((k_decode_fast<AGG, true>), dim3(blocks), dim3(256), 0, ctx->stream, a, ncells, vlen);
+    LAUNCH((k_decode_fast<AGG, true>), dim3(blocks), dim3(256), 0, ctx->stream, a, ncells, vlen);
   }
 };
 // (a leftover list: the general code inline, one launch)
@@ -700,7 +750,7 @@ struct LaunchFastDsInl {
   template <int AGG>
   static void run(Slot* ctx, unsigned blocks, const DecodeArgs& a, const uint32_t* ncells,
                   const uint32_t* vlen) {
-    hipLaunchKernelGGL((k_decode_fast<AGG, true, true>), dim3(blocks), dim3(256), 0, ctx->stream, a, ncells, vlen);
+    LAUNCH((k_decode_fast<AGG, true, true>), dim3(blocks), dim3(256), 0, ctx->stream, a, ncells, vlen);
   }
 };
 
@@ -749,7 +799,7 @@ struct LaunchChunks {
     g.nseg = g.seg_cap = 0;
     g.list = scratch<uint32_t>(ctx, "ck_list2", n_kept);
     g.list_count = zeroed2 ? zeroed2 + 1 : scratch<uint32_t>(ctx, "ck_list2_count", 1, true);
-    HIPCHK(hipEventRecord(ctx->ev[8], st));
+    EV_START(ctx, 8);
     // one wave per span (long rows, C3*): 4 resident blocks per CU (LDS
     // padding) measured faster than the 6 its registers allow; split spans
     // (C2) prefer the full occupancy
@@ -773,10 +823,10 @@ struct LaunchChunks {
       fp->pad = pad;
     }
     if (use_reg)
-      hipLaunchKernelGGL((k_ds_reg<AGG>), dim3(rblocks), dim3(256), pad, st, da, gr, ncells, vlen, wps_log2,
+      LAUNCH((k_ds_reg<AGG>), dim3(rblocks), dim3(256), pad, st, da, gr, ncells, vlen, wps_log2,
                          fp ? fp->a : fa0);
-    hipLaunchKernelGGL((k_ds_spans<AGG, 2>), dim3(iblocks), dim3(256), 0, st, da, g, ncells, vlen);
-    HIPCHK(hipEventRecord(ctx->ev[9], st));
+    LAUNCH_STOP(EV_STOP_K(ctx, 9), (k_ds_spans<AGG, 2>), dim3(iblocks), dim3(256), 0, st, da, g, ncells, vlen);
+    EV_STOP_M(ctx, 9);
     ctx->hot_kernel = TSDBHIP_HOT_DS_CHUNKS;
     fa.span_list = g.list;
     fa.span_count = g.list_count;
@@ -792,7 +842,7 @@ struct LaunchRegRerun {
     FapArgs a = fp.a;
     a.op = -1;
     a.rewrite = 1;
-    hipLaunchKernelGGL((k_ds_reg<AGG>), dim3(fp.blocks), dim3(256), fp.pad, ctx->stream, da, fp.g, ncells, vlen, 0u,
+    LAUNCH((k_ds_reg<AGG>), dim3(fp.blocks), dim3(256), fp.pad, ctx->stream, da, fp.g, ncells, vlen, 0u,
                        a);
   }
 };
@@ -800,20 +850,20 @@ struct LaunchRegRerun {
 template <int AGG, int MODE, bool RATE>
 static void launch_reduce(Slot* ctx, unsigned blocks, const ReduceArgs& r, const FinalArgs& f,
                           bool par, bool finalize) {
-  if (ctx->time_reduce) HIPCHK(hipEventRecord(ctx->ev[8], ctx->stream));
+  if (ctx->time_reduce) EV_START(ctx, 8);
   if (r.d_info && r.chunk_e)
-    hipLaunchKernelGGL((k_reduce<AGG, MODE, RATE, true>), dim3(blocks), dim3(256), 0, ctx->stream, r);
-  hipLaunchKernelGGL((k_reduce<AGG, MODE, RATE, false>), dim3(blocks), dim3(256),
-                     r.lds_state ? 4 * red_lds_stride(r.spans_per_chunk, RATE) : 0, ctx->stream, r);
-  if (ctx->time_reduce) HIPCHK(hipEventRecord(ctx->ev[9], ctx->stream));
+    LAUNCH((k_reduce<AGG, MODE, RATE, true>), dim3(blocks), dim3(256), 0, ctx->stream, r);
+  LAUNCH_STOP(ctx->time_reduce ? EV_STOP_K(ctx, 9) : nullptr, (k_reduce<AGG, MODE, RATE, false>), dim3(blocks),
+              dim3(256), r.lds_state ? 4 * red_lds_stride(r.spans_per_chunk, RATE) : 0, ctx->stream, r);
+  if (ctx->time_reduce) EV_STOP_M(ctx, 9);
   if (!finalize) return;
   if (par && f.T >= 1024)  // (large T: coalesced columns)
-    hipLaunchKernelGGL((k_chunks_cols<AGG, MODE, RATE, true>), dim3((unsigned)((f.T + 63) / 64)), dim3(64 * COLW), 0,
+    LAUNCH((k_chunks_cols<AGG, MODE, RATE, true>), dim3((unsigned)((f.T + 63) / 64)), dim3(64 * COLW), 0,
                        ctx->stream, r, r, f, f.T, f.n_chunks);
   else if (par)
-    hipLaunchKernelGGL((k_finalize_par<AGG, MODE, RATE>), dim3((unsigned)f.T), dim3(256), 0, ctx->stream, r, f);
+    LAUNCH((k_finalize_par<AGG, MODE, RATE>), dim3((unsigned)f.T), dim3(256), 0, ctx->stream, r, f);
   else
-    hipLaunchKernelGGL((k_finalize_seq<AGG, MODE, RATE>), dim3(grid_for(f.T, 256)), dim3(256), 0, ctx->stream,
+    LAUNCH((k_finalize_seq<AGG, MODE, RATE>), dim3(grid_for(f.T, 256)), dim3(256), 0, ctx->stream,
                        r, f);
 }
 
@@ -829,17 +879,17 @@ static void launch_lockstep_wf(Slot* ctx, unsigned blocks, const ReduceArgs& r, 
                                const FinalArgs& f, bool finalize) {
   constexpr int MODE = (RATE || FLT) ? MODE_DBL : MODE_INT;
   if (AGG == 4 && MODE == MODE_INT) return;  // (integer dev reduces in one span-ordered pass: never lockstep)
-  HIPCHK(hipEventRecord(ctx->ev[8], ctx->stream));
-  hipLaunchKernelGGL((k_lockstep<AGG, MODE, RATE, W, FLT>), dim3(blocks), dim3(256), 0, ctx->stream, r, a);
-  HIPCHK(hipEventRecord(ctx->ev[9], ctx->stream));
+  EV_START(ctx, 8);
+  LAUNCH_STOP(EV_STOP_K(ctx, 9), (k_lockstep<AGG, MODE, RATE, W, FLT>), dim3(blocks), dim3(256), 0, ctx->stream, r, a);
+  EV_STOP_M(ctx, 9);
   if (!finalize) return;
   if (f.n_chunks >= 64 && f.T >= 1024)
-    hipLaunchKernelGGL((k_chunks_cols<AGG, MODE, RATE, true>), dim3((unsigned)((f.T + 63) / 64)), dim3(64 * COLW), 0,
+    LAUNCH((k_chunks_cols<AGG, MODE, RATE, true>), dim3((unsigned)((f.T + 63) / 64)), dim3(64 * COLW), 0,
                        ctx->stream, r, r, f, f.T, f.n_chunks);
   else if (f.n_chunks >= 64)
-    hipLaunchKernelGGL((k_finalize_par<AGG, MODE, RATE>), dim3((unsigned)f.T), dim3(256), 0, ctx->stream, r, f);
+    LAUNCH((k_finalize_par<AGG, MODE, RATE>), dim3((unsigned)f.T), dim3(256), 0, ctx->stream, r, f);
   else
-    hipLaunchKernelGGL((k_finalize_seq<AGG, MODE, RATE>), dim3(grid_for(f.T, 256)), dim3(256), 0, ctx->stream, r, f);
+    LAUNCH((k_finalize_seq<AGG, MODE, RATE>), dim3(grid_for(f.T, 256)), dim3(256), 0, ctx->stream, r, f);
 }
 template <int AGG>
 static void launch_lockstep(Slot* ctx, bool rate, unsigned blocks, const ReduceArgs& r, const LsPlan& p,
@@ -890,13 +940,13 @@ static void launch_combine(Slot* ctx, const ReduceArgs& src, const ReduceArgs& d
                            uint32_t n_chunks) {
   if (n_chunks >= 64 && T >= 1024) {  // (large T: coalesced columns)
     FinalArgs nf = {};
-    hipLaunchKernelGGL((k_chunks_cols<AGG, MODE, false, false>), dim3((unsigned)((T + 63) / 64)), dim3(64 * COLW), 0,
+    LAUNCH((k_chunks_cols<AGG, MODE, false, false>), dim3((unsigned)((T + 63) / 64)), dim3(64 * COLW), 0,
                        ctx->stream, src, dst, nf, T, n_chunks);
   } else if (n_chunks >= 64)  // (as the finalize: serial chunk loops are latency-bound)
-    hipLaunchKernelGGL((k_combine_par<AGG, MODE>), dim3((unsigned)T), dim3(256), 0, ctx->stream, src, dst, T,
+    LAUNCH((k_combine_par<AGG, MODE>), dim3((unsigned)T), dim3(256), 0, ctx->stream, src, dst, T,
                        n_chunks);
   else
-    hipLaunchKernelGGL((k_combine_chunks<AGG, MODE>), dim3(grid_for(T, 256)), dim3(256), 0, ctx->stream, src,
+    LAUNCH((k_combine_chunks<AGG, MODE>), dim3(grid_for(T, 256)), dim3(256), 0, ctx->stream, src,
                        dst, T, n_chunks);
 }
 template <int AGG>
@@ -920,10 +970,10 @@ static void dispatch_combine(Slot* ctx, int agg, int mode, const ReduceArgs& s, 
 template <int AGG>
 static void final_mode(Slot* ctx, int mode, bool rate, const ReduceArgs& r, const FinalArgs& f) {
   const dim3 g(grid_for(f.T, 256)), b(256);
-  if (rate) hipLaunchKernelGGL((k_finalize_seq<AGG, MODE_DBL, true>), g, b, 0, ctx->stream, r, f);
-  else if (mode == MODE_INT) hipLaunchKernelGGL((k_finalize_seq<AGG, MODE_INT, false>), g, b, 0, ctx->stream, r, f);
-  else if (mode == MODE_DBL) hipLaunchKernelGGL((k_finalize_seq<AGG, MODE_DBL, false>), g, b, 0, ctx->stream, r, f);
-  else hipLaunchKernelGGL((k_finalize_seq<AGG, MODE_DUAL, false>), g, b, 0, ctx->stream, r, f);
+  if (rate) LAUNCH((k_finalize_seq<AGG, MODE_DBL, true>), g, b, 0, ctx->stream, r, f);
+  else if (mode == MODE_INT) LAUNCH((k_finalize_seq<AGG, MODE_INT, false>), g, b, 0, ctx->stream, r, f);
+  else if (mode == MODE_DBL) LAUNCH((k_finalize_seq<AGG, MODE_DBL, false>), g, b, 0, ctx->stream, r, f);
+  else LAUNCH((k_finalize_seq<AGG, MODE_DUAL, false>), g, b, 0, ctx->stream, r, f);
 }
 static void dispatch_final(Slot* ctx, int agg, int mode, bool rate, const ReduceArgs& r,
                            const FinalArgs& f) {
@@ -971,11 +1021,6 @@ static ReduceGeom reduce_geom(uint64_t T, uint32_t n_kept, bool one_chunk, uint6
   return g;
 }
 
-static float ev_ms(hipEvent_t a, hipEvent_t b) {
-  float ms = 0;
-  if (hipEventElapsedTime(&ms, a, b) != hipSuccess) return -1.f;
-  return ms;
-}
 
 // Device state of one spangroup_run call (err_raise keys, grid range, flags,
 // counters); read back at the call's host round trips.
@@ -1114,14 +1159,14 @@ static void xchg_minmax(Slot* ctx, Xchg* X, const XField* f, uint32_t n, uint64_
   m.n = n;
   m.buf = buf ? buf : scratch<uint64_t>(ctx, "x_pack", XM_MAX);
   for (uint32_t i = 0; i < n; i++) { m.kind[i] = f[i].kind; m.field[i] = f[i].p; m.imm[i] = f[i].imm; }
-  hipLaunchKernelGGL(k_xmove, dim3(1), dim3(1), 0, ctx->stream, m);
+  LAUNCH(k_xmove, dim3(1), dim3(1), 0, ctx->stream, m);
   X->group_start(ctx);
   X->allreduce(ctx, m.buf, n, X_U64, X_MIN);
   if (sum_u64) X->allreduce(ctx, sum_u64, 1, X_U64, X_SUM);
   for (uint32_t i = 0; i < n_extra; i++) X->allreduce(ctx, extra[i].p, extra[i].count, extra[i].t, extra[i].op);
   X->group_end(ctx);
   m.out = 1;
-  hipLaunchKernelGGL(k_xmove, dim3(1), dim3(1), 0, ctx->stream, m);
+  LAUNCH(k_xmove, dim3(1), dim3(1), 0, ctx->stream, m);
 }
 
 // dst (global geometry [dst_lo, ...]) = src (a rank's bitmap over [src_lo,
@@ -1377,7 +1422,8 @@ static int spangroup_run_once(Slot* ctx, const tsdbhip_sg_desc* d, tsdbhip_sg_ou
   ctx->tgdone_clean = false;
   bool tgd_used = false;
   const bool detail = ctx->opt.timing_detail;  // decode / grid event pairs
-  HIPCHK(hipEventRecord(ctx->ev[0], st));
+  g_ev_pend = nullptr;
+  EV_START(ctx, 0);
 
   // ---- assemble ----
   uint8_t* row_ok = scratch<uint8_t>(ctx, "row_ok", R);
@@ -1418,20 +1464,20 @@ static int spangroup_run_once(Slot* ctx, const tsdbhip_sg_desc* d, tsdbhip_sg_ou
     // (the block's 16 waves walk the deferred spans: a group of long spans of
     // many rows, C4's, needs the wave-per-span kernel's whole grid)
     if (S && S <= 1024 && R <= 8192) {
-      hipLaunchKernelGGL(k_assemble_small, dim3(1), dim3(1024), 0, st, a, K);
+      LAUNCH(k_assemble_small, dim3(1), dim3(1024), 0, st, a, K);
     } else if (S) {  // thread per span, then a wave per span for the ones it queued
       uint32_t* alist = scratch<uint32_t>(ctx, "asm_list", S);
       uint32_t* acount = &sm->cnt[0];
-      hipLaunchKernelGGL(k_assemble_fast, dim3(grid_for(S, 256)), dim3(256), 0, st, a, alist, acount);
-      hipLaunchKernelGGL(k_assemble, dim3(grid_for(S, 4, 4096)), dim3(256), 0, st, a, (const uint32_t*)alist,
+      LAUNCH(k_assemble_fast, dim3(grid_for(S, 256)), dim3(256), 0, st, a, alist, acount);
+      LAUNCH(k_assemble, dim3(grid_for(S, 4, 4096)), dim3(256), 0, st, a, (const uint32_t*)alist,
                          (const uint32_t*)acount);
       if (S <= KC_MAX) {
-        hipLaunchKernelGGL(k_kept_compact, dim3(1), dim3(1024), 0, st, K);
+        LAUNCH(k_kept_compact, dim3(1), dim3(1024), 0, st, K);
       } else {  // bigger groups: tile sums, then per-tile offsets + scatter
         const uint32_t nt = (S + 1023) / 1024;
         ulonglong2* ts = scratch<ulonglong2>(ctx, "kept_tiles", nt);
-        hipLaunchKernelGGL(k_kept_tiles, dim3(nt), dim3(256), 0, st, sp_kept, sp_cap, S, ts);
-        hipLaunchKernelGGL(k_kept_scatter_tiles, dim3(nt), dim3(256), 0, st, sp_kept, sp_cap, sp_ncells, S,
+        LAUNCH(k_kept_tiles, dim3(nt), dim3(256), 0, st, sp_kept, sp_cap, S, ts);
+        LAUNCH(k_kept_scatter_tiles, dim3(nt), dim3(256), 0, st, sp_kept, sp_cap, sp_ncells, S,
                            (const ulonglong2*)ts, kept, eoff, &sm->n_input, sp_first, sp_last, sm->bound,
                            &sm->n_kept, &sm->e_total);
       }
@@ -1443,7 +1489,7 @@ static int spangroup_run_once(Slot* ctx, const tsdbhip_sg_desc* d, tsdbhip_sg_ou
   Small h;
   if (!pub1) {  // (the state's last writer cannot publish it: a one-wave kernel does)
     p1 = next_pub(ctx, sizeof(Small));
-    hipLaunchKernelGGL(k_publish, dim3(1), dim3(64), 0, st, p1, (const uint64_t*)sm);
+    LAUNCH(k_publish, dim3(1), dim3(64), 0, st, p1, (const uint64_t*)sm);
   }
   wait_pub(ctx, p1, &h, sizeof h);  // sync 1
   // a rank whose own scan failed still takes part in the agreement below (its
@@ -1469,7 +1515,7 @@ static int spangroup_run_once(Slot* ctx, const tsdbhip_sg_desc* d, tsdbhip_sg_ou
   if (check_clean && bitmap) {  // (debug) the bitmap must be zero on entry
     unsigned long long* cnt = scratch<unsigned long long>(ctx, "chk_cnt", 1, true);
     const uint64_t nall = ctx->bufs["gbitmap"].n / 4;
-    hipLaunchKernelGGL(k_count_nonzero, dim3(grid_for(nall, 256, 1024)), dim3(256), 0, st, bitmap, nall, cnt);
+    LAUNCH(k_count_nonzero, dim3(grid_for(nall, 256, 1024)), dim3(256), 0, st, bitmap, nall, cnt);
     unsigned long long nz = 0;
     readback(ctx, &nz, cnt, 8);
     if (nz) fprintf(stderr, "TSDBHIP_CHECK_CLEAN: %llu non-zero bitmap words on entry (clean=%d, nwords=%llu)\n", nz,
@@ -1538,12 +1584,12 @@ static int spangroup_run_once(Slot* ctx, const tsdbhip_sg_desc* d, tsdbhip_sg_ou
     DecodeArgs ga = da;  // spans the streaming kernels hand to the general ones
     ga.use_fb = 1;
     ctx->hot_kernel = fast ? TSDBHIP_HOT_DECODE_FAST : TSDBHIP_HOT_DECODE_GEN;
-    if (!direct) HIPCHK(hipEventRecord(ctx->ev[8], st));
+    if (!direct) EV_START(ctx, 8);
     if (!fast) {
       // (spans of many short rows, C4: a block per span decodes its rows in
       // parallel; else a wave per span walks them)
-      if (interval == 0 && R >= 64ull * n_kept) hipLaunchKernelGGL(k_decode_rows, dim3(n_kept), dim3(256), 0, st, da);
-      else if (interval == 0) hipLaunchKernelGGL(k_decode_nods, dim3(blocks), dim3(256), 0, st, da);
+      if (interval == 0 && R >= 64ull * n_kept) LAUNCH(k_decode_rows, dim3(n_kept), dim3(256), 0, st, da);
+      else if (interval == 0) LAUNCH(k_decode_nods, dim3(blocks), dim3(256), 0, st, da);
       else launch_agg<LaunchGeneralDs>(ds_agg, ctx, blocks, da);
       HIPCHK(hipEventRecord(ctx->ev[9], st));
     } else if (interval == 0) {
@@ -1572,15 +1618,21 @@ static int spangroup_run_once(Slot* ctx, const tsdbhip_sg_desc* d, tsdbhip_sg_ou
         // the lockstep proposal (k_lockstep.hip), where the reduce is not the
         // span-ordered pass (EXACT_ORDER, integer dev): three qualifiers a
         // span now, every other one proven by k_lockstep as it reduces
-        ls_try = ls_allow && ctx->opt.lockstep && !exact && (agg != TSDBHIP_AGG_DEV || rate);
+        // Unsharded, only when k_lockstep gets >= 2048 waves (LS_TILE grid
+        // points x >= 64 spans each, the points per span estimated from the
+        // input): C1's 100 spans made 8 waves (38 us) where k_reduce takes
+        // 11 us. (Sharded: every rank alike, whatever its shard.)
+        const uint64_t ls_waves = (h.n_input / n_kept + LS_TILE - 1) / LS_TILE * std::max<uint64_t>(1, n_kept / 64);
+        ls_try = ls_allow && ctx->opt.lockstep && !exact && (agg != TSDBHIP_AGG_DEV || rate) &&
+                 (ctx->opt.lockstep == 2 || sharded || ls_waves >= 2048);
         if (ls_try) {
           d_qoff = scratch<uint64_t>(ctx, "d_qoff", n_kept);
           dg.ls_key = sm->ls_key;
           dg.ls_other = &sm->cnt[5];
-          hipLaunchKernelGGL(k_direct_opt, dim3(grid_for(n_kept, 256)), dim3(256), 0, st, da, dg, row_ncells,
+          LAUNCH(k_direct_opt, dim3(grid_for(n_kept, 256)), dim3(256), 0, st, da, dg, row_ncells,
                              row_val_len, d_qoff, sm->ls_key, &sm->cnt[5]);
         }
-        hipLaunchKernelGGL(k_direct_scan, dim3(grid_for(n_kept, 4 * dg.batch, 1u << 20)), dim3(256), 0, st, da, dg,
+        LAUNCH(k_direct_scan, dim3(grid_for(n_kept, 4 * dg.batch, 1u << 20)), dim3(256), 0, st, da, dg,
                            row_ncells, row_val_len);
         fa.span_list = dg.list;
         fa.span_count = dg.list_count;
@@ -1588,12 +1640,12 @@ static int spangroup_run_once(Slot* ctx, const tsdbhip_sg_desc* d, tsdbhip_sg_ou
         mark_count = dg.list_count;
       }
       if (fa.span_list) {  // (the direct scan's leftovers: general code inline)
-        hipLaunchKernelGGL((k_decode_fast<0, false, true>), dim3(std::min(blocks, 1024u)), dim3(256), 0, st, fa,
+        LAUNCH((k_decode_fast<0, false, true>), dim3(std::min(blocks, 1024u)), dim3(256), 0, st, fa,
                            row_ncells, row_val_len);
       } else {
-        hipLaunchKernelGGL((k_decode_fast<0, false>), dim3(blocks), dim3(256), 0, st, fa, row_ncells, row_val_len);
+        LAUNCH((k_decode_fast<0, false>), dim3(blocks), dim3(256), 0, st, fa, row_ncells, row_val_len);
         HIPCHK(hipEventRecord(ctx->ev[9], st));
-        hipLaunchKernelGGL(k_decode_nods, dim3(std::min(blocks, 1024u)), dim3(256), 0, st, ga);
+        LAUNCH(k_decode_nods, dim3(std::min(blocks, 1024u)), dim3(256), 0, st, ga);
       }
     } else {
       DecodeArgs fa = da;
@@ -1672,8 +1724,8 @@ static int spangroup_run_once(Slot* ctx, const tsdbhip_sg_desc* d, tsdbhip_sg_ou
     ga.emit1 = fap_opt && nb == 1 ? scratch<uint32_t>(ctx, "grid", nwords * 32) : nullptr;
     ga.block_hash = hash && nb > 1 ? scratch<unsigned long long>(ctx, "grid_bhash", 2 * nb) : nullptr;
     ga.pub = pub ? next_pub(ctx, sizeof(Small)) : HostPub{};
-    hipLaunchKernelGGL(k_grid_popc, dim3((unsigned)nb), dim3(256), 0, st, ga);
-    if (nb > 1) hipLaunchKernelGGL(k_grid_scan_blocks, dim3(1), dim3(256), 0, st, ga, (uint32_t)nb);
+    LAUNCH(k_grid_popc, dim3((unsigned)nb), dim3(256), 0, st, ga);
+    if (nb > 1) LAUNCH(k_grid_scan_blocks, dim3(1), dim3(256), 0, st, ga, (uint32_t)nb);
   };
   if (!empty_grid) {
     ga.lo = lo; ga.hi = hi; ga.bitmap = bitmap; ga.nwords = nwords;
@@ -1682,11 +1734,11 @@ static int spangroup_run_once(Slot* ctx, const tsdbhip_sg_desc* d, tsdbhip_sg_ou
     const uint32_t n_sl = (uint32_t)((nwords + GM_WORDS - 1) >> GM_SHIFT);
     if (n_kept && n_sl >= 8 && (uint64_t)(n_sl + 1) * n_kept <= (64ull << 20)) {
       uint32_t* B = scratch<uint32_t>(ctx, "gm_bounds", (uint64_t)(n_sl + 1) * n_kept);
-      hipLaunchKernelGGL(k_grid_bounds, dim3(mark_list ? std::min(grid_for(n_kept, 4, 65536), 1024u) : grid_for(n_kept, 4, 65536)),
+      LAUNCH(k_grid_bounds, dim3(mark_list ? std::min(grid_for(n_kept, 4, 65536), 1024u) : grid_for(n_kept, 4, 65536)),
                          dim3(256), 0, st, ga, B, n_sl);
-      hipLaunchKernelGGL(k_grid_mark_slices, dim3(n_sl), dim3(256), 0, st, ga, (const uint32_t*)B, n_sl);
+      LAUNCH(k_grid_mark_slices, dim3(n_sl), dim3(256), 0, st, ga, (const uint32_t*)B, n_sl);
     } else if (n_kept) {
-      hipLaunchKernelGGL(k_grid_mark, dim3(mark_list ? std::min(grid_for(n_kept, 4, 65536), 1024u) : grid_for(n_kept, 4, 65536)),
+      LAUNCH(k_grid_mark, dim3(mark_list ? std::min(grid_for(n_kept, 4, 65536), 1024u) : grid_for(n_kept, 4, 65536)),
                          dim3(256), 0, st, ga);
     }
     grid_ranks(!sharded && !fap_opt, sharded);
@@ -1707,10 +1759,10 @@ static int spangroup_run_once(Slot* ctx, const tsdbhip_sg_desc* d, tsdbhip_sg_ou
       if (!ga.emit1) {  // (a single-block k_grid_popc emitted it)
         uint32_t* word_rank_f = scratch<uint32_t>(ctx, "word_rank_f", nwords);
         const uint32_t eb = grid_for(nwords, 256);
-        hipLaunchKernelGGL(k_emit_verify, dim3(eb), dim3(256), 0, st, ga, word_rank_f, dg, 0u, eb);
+        LAUNCH(k_emit_verify, dim3(eb), dim3(256), 0, st, ga, word_rank_f, dg, 0u, eb);
       }
     }
-    HIPCHK(hipEventRecord(ctx->ev[4], st));
+    EV_START(ctx, 4);
     const int fop = agg == TSDBHIP_AGG_MIN ? 1 : (agg == TSDBHIP_AGG_MAX ? 2 : 0);
     int64_t* o_pi = scratch<int64_t>(ctx, "fo_i", WAVE);
     uint32_t* o_pc = scratch<uint32_t>(ctx, "fo_cnt", WAVE);
@@ -1734,15 +1786,15 @@ static int spangroup_run_once(Slot* ctx, const tsdbhip_sg_desc* d, tsdbhip_sg_ou
       int64_t* tmp = scratch<int64_t>(ctx, "fap_tmp", (uint64_t)g1 * WAVE);
       auto go = [&](auto opc) {
         constexpr int OP = decltype(opc)::value;
-        hipLaunchKernelGGL((k_fap_rows<OP>), dim3(g1), dim3(1024), 0, st, (const int64_t*)fap.a.part, nrows, tmp);
-        hipLaunchKernelGGL((k_fap_final64v<OP>), dim3(1), dim3(1024), 0, st, (const int64_t*)tmp, g1, n_kept, o_pi, o_pc,
+        LAUNCH((k_fap_rows<OP>), dim3(g1), dim3(1024), 0, st, (const int64_t*)fap.a.part, nrows, tmp);
+        LAUNCH((k_fap_final64v<OP>), dim3(1), dim3(1024), 0, st, (const int64_t*)tmp, g1, n_kept, o_pi, o_pc,
                            sm, pack);
       };
       if (fop == 1) go(std::integral_constant<int, 1>());
       else if (fop == 2) go(std::integral_constant<int, 2>());
       else go(std::integral_constant<int, 0>());
     } else {
-      hipLaunchKernelGGL(k_fap_neutral64, dim3(1), dim3(WAVE), 0, st, o_pi, o_pc, fop, sm, pack);
+      LAUNCH(k_fap_neutral64, dim3(1), dim3(WAVE), 0, st, o_pi, o_pc, fop, sm, pack);
     }
     if (sharded) {  // the agreement, the validity (MIN) and the 64-slot partials: one collective group
       const XExtra ex[2] = {{o_pi, WAVE, fop ? X_I64 : X_U64, fop == 1 ? X_MIN : (fop == 2 ? X_MAX : X_SUM)},
@@ -1765,15 +1817,15 @@ static int spangroup_run_once(Slot* ctx, const tsdbhip_sg_desc* d, tsdbhip_sg_ou
       Small* snap = (Small*)ctx->map_out_dev;
       const Small ini = small_init();
       if (agg == TSDBHIP_AGG_MIN)
-        hipLaunchKernelGGL(k_fap_finish_end<1>, dim3(1), dim3(256), 0, st, sm, (const int64_t*)o_pi, (const uint32_t*)o_pc, fo, (int32_t)sharded, um, snap, ini, bitmap, (const uint32_t*)gridv_o, lo);
+        LAUNCH_STOP(EV_STOP_K(ctx, 5), k_fap_finish_end<1>, dim3(1), dim3(256), 0, st, sm, (const int64_t*)o_pi, (const uint32_t*)o_pc, fo, (int32_t)sharded, um, snap, ini, bitmap, (const uint32_t*)gridv_o, lo);
       else if (agg == TSDBHIP_AGG_MAX)
-        hipLaunchKernelGGL(k_fap_finish_end<2>, dim3(1), dim3(256), 0, st, sm, (const int64_t*)o_pi, (const uint32_t*)o_pc, fo, (int32_t)sharded, um, snap, ini, bitmap, (const uint32_t*)gridv_o, lo);
+        LAUNCH_STOP(EV_STOP_K(ctx, 5), k_fap_finish_end<2>, dim3(1), dim3(256), 0, st, sm, (const int64_t*)o_pi, (const uint32_t*)o_pc, fo, (int32_t)sharded, um, snap, ini, bitmap, (const uint32_t*)gridv_o, lo);
       else if (agg == TSDBHIP_AGG_AVG)
-        hipLaunchKernelGGL(k_fap_finish_end<3>, dim3(1), dim3(256), 0, st, sm, (const int64_t*)o_pi, (const uint32_t*)o_pc, fo, (int32_t)sharded, um, snap, ini, bitmap, (const uint32_t*)gridv_o, lo);
+        LAUNCH_STOP(EV_STOP_K(ctx, 5), k_fap_finish_end<3>, dim3(1), dim3(256), 0, st, sm, (const int64_t*)o_pi, (const uint32_t*)o_pc, fo, (int32_t)sharded, um, snap, ini, bitmap, (const uint32_t*)gridv_o, lo);
       else
-        hipLaunchKernelGGL(k_fap_finish_end<0>, dim3(1), dim3(256), 0, st, sm, (const int64_t*)o_pi, (const uint32_t*)o_pc, fo, (int32_t)sharded, um, snap, ini, bitmap, (const uint32_t*)gridv_o, lo);
+        LAUNCH_STOP(EV_STOP_K(ctx, 5), k_fap_finish_end<0>, dim3(1), dim3(256), 0, st, sm, (const int64_t*)o_pi, (const uint32_t*)o_pc, fo, (int32_t)sharded, um, snap, ini, bitmap, (const uint32_t*)gridv_o, lo);
     }
-    HIPCHK(hipEventRecord(ctx->ev[5], st));
+    EV_STOP_M(ctx, 5);
     HIPCHK(hipStreamSynchronize(st));
     std::memcpy(&h, ctx->map_out, sizeof h);
     if (h.fap_done) {  // the call is over (state reset, bitmap clear)
@@ -1787,10 +1839,10 @@ static int spangroup_run_once(Slot* ctx, const tsdbhip_sg_desc* d, tsdbhip_sg_ou
         tm.n_collectives = X->n_coll;
         tm.x_bytes = X->x_bytes;
       }
-      if (ctx->hot_kernel) tm.hot_ms = ev_ms(ctx->ev[8], ctx->ev[9]);
+      if (ctx->hot_kernel) tm.hot_ms = ev_ms(ctx, 8, 9);
       tm.hot_kernel = ctx->hot_kernel;
-      tm.reduce_ms = ev_ms(ctx->ev[4], ctx->ev[5]);
-      tm.total_ms = ev_ms(ctx->ev[0], ctx->ev[5]);
+      tm.reduce_ms = ev_ms(ctx, 4, 5);
+      tm.total_ms = ev_ms(ctx, 0, 5);
       tm.n_emitted = e_total;
       ctx->timing = tm;
       if (T > out->capacity && ctx->want_output) {
@@ -1827,7 +1879,7 @@ static int spangroup_run_once(Slot* ctx, const tsdbhip_sg_desc* d, tsdbhip_sg_ou
     if (!fap_opt) {  // (an optimistic call ran the agreement already; h holds it)
       xchg_minmax(ctx, X, fx, XH_N, (uint64_t*)&sm->n_input, (uint64_t*)sm->xh);
       const HostPub p2 = next_pub(ctx, sizeof(Small));
-      hipLaunchKernelGGL(k_publish, dim3(1), dim3(64), 0, st, p2, (const uint64_t*)sm);
+      LAUNCH(k_publish, dim3(1), dim3(64), 0, st, p2, (const uint64_t*)sm);
       wait_pub(ctx, p2, &h, sizeof h);  // sync 2: agreed error / flags / count, the grids' geometry and hashes
     }
     after_sync2();
@@ -1844,7 +1896,7 @@ static int spangroup_run_once(Slot* ctx, const tsdbhip_sg_desc* d, tsdbhip_sg_ou
       ctx->bitmapx_clean = false;
       uint32_t* gbm = scratch_zero_kept<uint32_t>(ctx, "gbitmap_x", gw, clean_x);
       if (!empty_grid) {
-        hipLaunchKernelGGL(k_bitmap_remap, dim3(grid_for(gw, 256)), dim3(256), 0, st, (const uint32_t*)bitmap, nwords,
+        LAUNCH(k_bitmap_remap, dim3(grid_for(gw, 256)), dim3(256), 0, st, (const uint32_t*)bitmap, nwords,
                            lo, gbm, gw, glo);
         HIPCHK(hipMemsetAsync(bitmap, 0, nwords * 4, st));
       }
@@ -1856,7 +1908,7 @@ static int spangroup_run_once(Slot* ctx, const tsdbhip_sg_desc* d, tsdbhip_sg_ou
       used_bitmap_x = true;
       uint32_t* all = scratch<uint32_t>(ctx, "bitmap_all", nwords * X->nranks);
       X->allgather(ctx, bitmap, all, nwords * 4);
-      hipLaunchKernelGGL(k_bitmap_or, dim3(grid_for(nwords, 256)), dim3(256), 0, st, all, (uint32_t)X->nranks,
+      LAUNCH(k_bitmap_or, dim3(grid_for(nwords, 256)), dim3(256), 0, st, all, (uint32_t)X->nranks,
                          nwords, bitmap);
       grid_ranks(true, false);
       wait_pub(ctx, ga.pub, &h, sizeof h);  // sync 3: |G| of the global grid
@@ -1908,7 +1960,7 @@ static int spangroup_run_once(Slot* ctx, const tsdbhip_sg_desc* d, tsdbhip_sg_ou
     dg.word_rank = word_rank;  // (block-local ranks + ga.block_sum)
     dg.bitmap = bitmap;
     const uint32_t eb = grid_for(nwords, 256);
-    hipLaunchKernelGGL(k_emit_verify, dim3(eb + (verify ? grid_for(n_kept, 256) : 0)), dim3(256), 0, st, ga,
+    LAUNCH(k_emit_verify, dim3(eb + (verify ? grid_for(n_kept, 256) : 0)), dim3(256), 0, st, ga,
                        word_rank_f, dg, verify ? n_kept : 0u, eb);
     word_rank = word_rank_f;
     dg.word_rank = word_rank_f;
@@ -1916,7 +1968,7 @@ static int spangroup_run_once(Slot* ctx, const tsdbhip_sg_desc* d, tsdbhip_sg_ou
       DecodeArgs fa = da;
       fa.span_list = dg.list;
       fa.span_count = dg.list_count;
-      hipLaunchKernelGGL((k_decode_fast<0, false, true>), dim3(std::min(grid_for(n_kept, 4, 65536), 1024u)), dim3(256),
+      LAUNCH((k_decode_fast<0, false, true>), dim3(std::min(grid_for(n_kept, 4, 65536), 1024u)), dim3(256),
                          0, st, fa, row_ncells, row_val_len);
     }
   }
@@ -1930,7 +1982,7 @@ static int spangroup_run_once(Slot* ctx, const tsdbhip_sg_desc* d, tsdbhip_sg_ou
                        !anyf && T > 0 && T <= WAVE && grids_agreed;
   if (fap_ran && !fap_use) launch_agg<LaunchRegRerun>(ds_agg, ctx, da, fap, row_ncells, row_val_len);
   tm.paths |= fap_use ? TSDBHIP_PATH_ALIGNED_GROUP : (fap_ran ? TSDBHIP_PATH_ALIGNED_RERUN : 0u);
-  HIPCHK(hipEventRecord(ctx->ev[4], st));
+  EV_START(ctx, 4);
   tm.n_grid = T;
   // lazy error index for illegal cells (every span's E and e_bad are final
   // here; sharded: a rank of the global grid, reduced with the exchange)
@@ -1945,7 +1997,7 @@ static int spangroup_run_once(Slot* ctx, const tsdbhip_sg_desc* d, tsdbhip_sg_ou
   // (an aligned or lockstep group holds no E span, hence no bad cell)
   if (ls_use) bad.n_kept = 0;
   if (n_kept && !bad_at_end && !fap_use && !ls_use)
-    hipLaunchKernelGGL(k_bad_index, dim3(grid_for(n_kept, 256)), dim3(256), 0, st, bad, &sm->bad_at);
+    LAUNCH(k_bad_index, dim3(grid_for(n_kept, 256)), dim3(256), 0, st, bad, &sm->bad_at);
 
   // ---- the reduce's shape: the span-ordered pass (integer dev before the
   // (long) truncation, Aggregators.java:196-217, or EXACT_ORDER), exact
@@ -2060,7 +2112,7 @@ static int spangroup_run_once(Slot* ctx, const tsdbhip_sg_desc* d, tsdbhip_sg_ou
       // spans included; no flags, one launch)
       if (direct && n_waves > 4096) {
         uint32_t* ce = scratch<uint32_t>(ctx, "chunk_e", n_chunks);
-        hipLaunchKernelGGL(k_chunk_flags_w, dim3(grid_for(n_chunks, 4)), dim3(256), 0, st, dg.info, n_kept, spc,
+        LAUNCH(k_chunk_flags_w, dim3(grid_for(n_chunks, 4)), dim3(256), 0, st, dg.info, n_kept, spc,
                            n_chunks, ce);
         r.chunk_e = ce;
       }
@@ -2128,17 +2180,17 @@ static int spangroup_run_once(Slot* ctx, const tsdbhip_sg_desc* d, tsdbhip_sg_ou
       f.n_chunks = 1;
       auto go = [&](auto opc) {
         constexpr int OP = decltype(opc)::value;
-        hipLaunchKernelGGL((k_fap_rows<OP>), dim3(g1), dim3(1024), 0, st, (const int64_t*)fap.a.part, nrows, tmp);
+        LAUNCH((k_fap_rows<OP>), dim3(g1), dim3(1024), 0, st, (const int64_t*)fap.a.part, nrows, tmp);
         if (!finalize) {
-          hipLaunchKernelGGL((k_fap_final<OP>), dim3(1), dim3(1024), 0, st, (const int64_t*)tmp, g1, T, n_kept, r.p_i,
+          LAUNCH((k_fap_final<OP>), dim3(1), dim3(1024), 0, st, (const int64_t*)tmp, g1, T, n_kept, r.p_i,
                              r.p_cnt, r.p_flag);
           return;
         }
         // (the cross-series aggregator: OP 0 is sum or avg)
-        if (OP == 1) hipLaunchKernelGGL((k_fap_final_out<OP, 1>), dim3(1), dim3(1024), 0, st, (const int64_t*)tmp, g1, n_kept, f);
-        else if (OP == 2) hipLaunchKernelGGL((k_fap_final_out<OP, 2>), dim3(1), dim3(1024), 0, st, (const int64_t*)tmp, g1, n_kept, f);
-        else if (agg == TSDBHIP_AGG_AVG) hipLaunchKernelGGL((k_fap_final_out<0, 3>), dim3(1), dim3(1024), 0, st, (const int64_t*)tmp, g1, n_kept, f);
-        else hipLaunchKernelGGL((k_fap_final_out<0, 0>), dim3(1), dim3(1024), 0, st, (const int64_t*)tmp, g1, n_kept, f);
+        if (OP == 1) LAUNCH((k_fap_final_out<OP, 1>), dim3(1), dim3(1024), 0, st, (const int64_t*)tmp, g1, n_kept, f);
+        else if (OP == 2) LAUNCH((k_fap_final_out<OP, 2>), dim3(1), dim3(1024), 0, st, (const int64_t*)tmp, g1, n_kept, f);
+        else if (agg == TSDBHIP_AGG_AVG) LAUNCH((k_fap_final_out<0, 3>), dim3(1), dim3(1024), 0, st, (const int64_t*)tmp, g1, n_kept, f);
+        else LAUNCH((k_fap_final_out<0, 0>), dim3(1), dim3(1024), 0, st, (const int64_t*)tmp, g1, n_kept, f);
       };
       if (fap.a.op == 1) go(std::integral_constant<int, 1>());
       else if (fap.a.op == 2) go(std::integral_constant<int, 2>());
@@ -2160,7 +2212,7 @@ static int spangroup_run_once(Slot* ctx, const tsdbhip_sg_desc* d, tsdbhip_sg_ou
         ReduceArgs S;
         std::memset(&S, 0, sizeof S);
         partials(S, "s_", T);
-        HIPCHK(hipEventRecord(ctx->ev[6], st));
+        if (detail) HIPCHK(hipEventRecord(ctx->ev[6], st));
         for (int step = 0; step < nr; step++) {
           ReduceArgs P = S;  // (non-roots: the send side of the broadcast is unused)
           if (rk == step) P = run_reduce(true, false, step ? &S : nullptr);
@@ -2173,7 +2225,7 @@ static int spangroup_run_once(Slot* ctx, const tsdbhip_sg_desc* d, tsdbhip_sg_ou
           }
           X->group_end(ctx);
         }
-        HIPCHK(hipEventRecord(ctx->ev[7], st));
+        if (detail) HIPCHK(hipEventRecord(ctx->ev[7], st));
         src = S;
       } else {
         // this rank's chunks combined in order into one slot per t
@@ -2186,16 +2238,16 @@ static int spangroup_run_once(Slot* ctx, const tsdbhip_sg_desc* d, tsdbhip_sg_ou
             partials(mine, "m_", T);
             dispatch_combine(ctx, agg, mode, loc, mine, T, loc.n_chunks);
             if (agg == TSDBHIP_AGG_MIN || agg == TSDBHIP_AGG_MAX)
-              hipLaunchKernelGGL(k_neutral_minmax, dim3(grid_for(T, 256)), dim3(256), 0, st, mine.p_cnt, mine.p_i, T,
+              LAUNCH(k_neutral_minmax, dim3(grid_for(T, 256)), dim3(256), 0, st, mine.p_cnt, mine.p_i, T,
                                  agg == TSDBHIP_AGG_MIN ? INT64_MAX : INT64_MIN);
           }
-          HIPCHK(hipEventRecord(ctx->ev[6], st));
+          if (detail) HIPCHK(hipEventRecord(ctx->ev[6], st));
           X->group_start(ctx);
           for (const Fld& f : fields(mine, 0)) X->allreduce(ctx, f.p, T, f.t, f.op);
           X->allreduce(ctx, &sm->bad_at, 1, X_U64, X_MIN);
           X->allreduce(ctx, &sm->ls_broken, 1, X_U32, X_MAX);
           X->group_end(ctx);
-          HIPCHK(hipEventRecord(ctx->ev[7], st));
+          if (detail) HIPCHK(hipEventRecord(ctx->ev[7], st));
           src = mine;
         } else if (sliced) {
           // doubles over a long grid (C4): rank q owns slice q of G (xs
@@ -2208,7 +2260,7 @@ static int spangroup_run_once(Slot* ctx, const tsdbhip_sg_desc* d, tsdbhip_sg_ou
           partials(mine, "m_", xs * nr);  // [T] used
           partials(recv, "x_", xs * nr);  // [rank q][xs]: rank q's partials of this rank's slice
           dispatch_combine(ctx, agg, mode, loc, mine, T, loc.n_chunks);
-          HIPCHK(hipEventRecord(ctx->ev[6], st));
+          if (detail) HIPCHK(hipEventRecord(ctx->ev[6], st));
           const std::vector<Fld> fm = fields(mine, 0), fr = fields(recv, 0);
           X->group_start(ctx);
           for (size_t i = 0; i < fm.size(); i++) X->alltoall(ctx, fm[i].p, fr[i].p, xs * fm[i].esz);
@@ -2233,7 +2285,7 @@ static int spangroup_run_once(Slot* ctx, const tsdbhip_sg_desc* d, tsdbhip_sg_ou
           X->allgather(ctx, o_isint + g0, o_isint, xs);
           X->allreduce(ctx, &sm->nan_t, 1, X_U64, X_MIN);
           X->group_end(ctx);
-          HIPCHK(hipEventRecord(ctx->ev[7], st));
+          if (detail) HIPCHK(hipEventRecord(ctx->ev[7], st));
         } else {
           // doubles (sums / Welford states depend on the order): every
           // rank's slot gathered, merged in rank order on every rank
@@ -2244,14 +2296,14 @@ static int spangroup_run_once(Slot* ctx, const tsdbhip_sg_desc* d, tsdbhip_sg_ou
           mine.p_cnt += off; mine.p_flag += off; mine.p_i += off; mine.p_d += off; mine.p_dhas += off;
           if (agg == TSDBHIP_AGG_DEV) { mine.p_wim += off; mine.p_wiv += off; mine.p_wdm += off; mine.p_wdv += off; }
           dispatch_combine(ctx, agg, mode, loc, mine, T, loc.n_chunks);
-          HIPCHK(hipEventRecord(ctx->ev[6], st));
+          if (detail) HIPCHK(hipEventRecord(ctx->ev[6], st));
           const std::vector<Fld> fm = fields(mine, 0), fa = fields(all, 0);
           X->group_start(ctx);
           for (size_t i = 0; i < fm.size(); i++) X->allgather(ctx, fm[i].p, fa[i].p, T * fm[i].esz);
           X->allreduce(ctx, &sm->bad_at, 1, X_U64, X_MIN);
           X->allreduce(ctx, &sm->ls_broken, 1, X_U32, X_MAX);
           X->group_end(ctx);
-          HIPCHK(hipEventRecord(ctx->ev[7], st));
+          if (detail) HIPCHK(hipEventRecord(ctx->ev[7], st));
           src = all;
           n_src = (uint32_t)nr;
         }
@@ -2270,9 +2322,10 @@ static int spangroup_run_once(Slot* ctx, const tsdbhip_sg_desc* d, tsdbhip_sg_ou
     X->group_end(ctx);
   }
   // ---- end of call: snapshot + reset of the call state, bitmap cleared ----
-  hipLaunchKernelGGL(k_call_end, dim3(bad_at_end ? 1u : grid_for(T, 256, 1024)), dim3(256), 0, st, sm, (Small*)ctx->map_out_dev,
-                     small_init(), bitmap, (const uint32_t*)gridv, T, lo, bad_at_end ? bad : BadArgs{});
-  HIPCHK(hipEventRecord(ctx->ev[5], st));
+  LAUNCH_STOP(EV_STOP_K(ctx, 5), k_call_end, dim3(bad_at_end ? 1u : grid_for(T, 256, 1024)), dim3(256), 0, st, sm,
+              (Small*)ctx->map_out_dev, small_init(), bitmap, (const uint32_t*)gridv, T, lo, bad_at_end ? bad : BadArgs{},
+              (const uint32_t*)nullptr);
+  EV_STOP_M(ctx, 5);
   HIPCHK(hipStreamSynchronize(st));  // (the header and small results are already in host memory)
   const uint8_t* hb = ctx->map_out;
   std::memcpy(&h, hb, sizeof h);
@@ -2285,18 +2338,18 @@ static int spangroup_run_once(Slot* ctx, const tsdbhip_sg_desc* d, tsdbhip_sg_ou
     return RC_REDO;
   }
   if (sharded) {
-    tm.exchange_ms = T > 0 ? ev_ms(ctx->ev[6], ctx->ev[7]) : 0.f;
+    tm.exchange_ms = T > 0 && detail ? ev_ms(ctx, 6, 7) : 0.f;  // (timing_detail only)
     tm.n_collectives = X->n_coll;
     tm.x_bytes = X->x_bytes;
   }
   if (detail) {
-    tm.decode_ms = ev_ms(ctx->ev[1], ctx->ev[2]);
-    tm.grid_ms = ev_ms(ctx->ev[3], ctx->ev[4]);
+    tm.decode_ms = ev_ms(ctx, 1, 2);
+    tm.grid_ms = ev_ms(ctx, 3, 4);
   }
-  if (ctx->hot_kernel) tm.hot_ms = ev_ms(ctx->ev[8], ctx->ev[9]);
+  if (ctx->hot_kernel) tm.hot_ms = ev_ms(ctx, 8, 9);
   tm.hot_kernel = ctx->hot_kernel;
-  tm.reduce_ms = ev_ms(ctx->ev[4], ctx->ev[5]);
-  tm.total_ms = ev_ms(ctx->ev[0], ctx->ev[5]);
+  tm.reduce_ms = ev_ms(ctx, 4, 5);
+  tm.total_ms = ev_ms(ctx, 0, 5);
   tm.n_emitted = e_total;
   ctx->timing = tm;
 
@@ -2606,9 +2659,9 @@ extern "C" int tsdbhip_synth_generate(tsdbhip_ctx* c, const tsdbhip_synth_params
     a.row_val_len = (uint32_t*)al("vlen", 4ull * n_rows);
     a.qual = (uint8_t*)al("qual", n_rows * a.qstride);
     a.val = (uint8_t*)al("val", n_rows * a.vstride);
-    hipLaunchKernelGGL(k_synth_rows, dim3(grid_for(n_rows, 256)), dim3(256), 0, ctx->stream, a);
+    LAUNCH(k_synth_rows, dim3(grid_for(n_rows, 256)), dim3(256), 0, ctx->stream, a);
     const uint64_t cells = (uint64_t)p->n_spans * p->n_points;
-    hipLaunchKernelGGL(k_synth_cells, dim3(grid_for(cells, 256, 0x7fffffff)), dim3(256), 0, ctx->stream, a);
+    LAUNCH(k_synth_cells, dim3(grid_for(cells, 256, 0x7fffffff)), dim3(256), 0, ctx->stream, a);
     HIPCHK(hipGetLastError());
     HIPCHK(hipStreamSynchronize(ctx->stream));
     d->flags |= TSDBHIP_DESC_DEVICE;
@@ -2768,7 +2821,7 @@ static int compact_rows(Slot* ctx, const tsdbhip_rows_desc* d, tsdbhip_rows_out*
     a.list_big = scratch<uint32_t>(ctx, "c_lbig", R);
     a.big_cells = scratch<uint64_t>(ctx, "c_cells", qext / 2 + R + 1);
     hipStream_t st = ctx->stream;
-    HIPCHK(hipEventRecord(ctx->ev[0], st));
+    g_ev_pend = nullptr;
     if (ctx->opt.compact_tiles) {  // (every row through the LDS tiles: the A/B reference)
       HIPCHK(hipEventRecord(ctx->ev[8], st));
       HIPCHK(hipEventRecord(ctx->ev[4], st));
@@ -2782,22 +2835,25 @@ static int compact_rows(Slot* ctx, const tsdbhip_rows_desc* d, tsdbhip_rows_out*
       // around the holes; the other rows through the LDS row kernel
       a.tile_bad = scratch<uint8_t>(ctx, "c_tbad", R / CC_ROWS + 1);
       a.row_holes = scratch<uint2>(ctx, "c_holes", R);
-      HIPCHK(hipEventRecord(ctx->ev[8], st));
-      hipLaunchKernelGGL(k_compact_quals, dim3(grid_for(R, CC_ROWS, 1u << 16)), dim3(256), 0, st, a);
-      HIPCHK(hipEventRecord(ctx->ev[4], st));
-      hipLaunchKernelGGL(k_compact_classify, dim3(grid_for(R, 16, 1u << 16)), dim3(256), 0, st, a);
-      HIPCHK(hipEventRecord(ctx->ev[2], st));
-      hipLaunchKernelGGL(k_compact_vals, dim3(grid_for(R, 16, 1u << 16)), dim3(256), 0, st, a);
-      HIPCHK(hipEventRecord(ctx->ev[9], st));
-      hipLaunchKernelGGL(k_compact_rows, dim3(grid_for(R, CR_RANGE, 1u << 14)), dim3(256), 0, st, a);
-      HIPCHK(hipEventRecord(ctx->ev[3], st));
+      // (each boundary event the stop of the kernel before it)
+      EV_START(ctx, 8);
+      LAUNCH_STOP(EV_STOP_K(ctx, 4), k_compact_quals, dim3(grid_for(R, CC_ROWS, 1u << 16)), dim3(256), 0, st, a);
+      EV_STOP_M(ctx, 4);
+      LAUNCH_STOP(EV_STOP_K(ctx, 2), k_compact_classify, dim3(grid_for(R, 16, 1u << 16)), dim3(256), 0, st, a);
+      EV_STOP_M(ctx, 2);
+      LAUNCH_STOP(EV_STOP_K(ctx, 9), k_compact_vals, dim3(grid_for(R, 16, 1u << 16)), dim3(256), 0, st, a);
+      EV_STOP_M(ctx, 9);
+      LAUNCH_STOP(EV_STOP_K(ctx, 3), k_compact_rows, dim3(grid_for(R, CR_RANGE, 1u << 14)), dim3(256), 0, st, a);
+      EV_STOP_M(ctx, 3);
     }
     HIPCHK(hipGetLastError());
-    hipLaunchKernelGGL(k_compact_complex<true>, dim3(1024), dim3(256), 0, ctx->stream, a);
-    hipLaunchKernelGGL(k_compact_complex<false>, dim3(256), dim3(256), 0, ctx->stream, a);
-    if (a.out_write) hipLaunchKernelGGL(k_compact_dups, dim3(grid_for(R, 4 * WAVE, 4096)), dim3(256), 0, ctx->stream, a);
+    LAUNCH(k_compact_complex<true>, dim3(1024), dim3(256), 0, ctx->stream, a);
+    LAUNCH_STOP(a.out_write ? nullptr : EV_STOP_K(ctx, 1), k_compact_complex<false>, dim3(256), dim3(256), 0,
+                ctx->stream, a);
+    if (a.out_write)
+      LAUNCH_STOP(EV_STOP_K(ctx, 1), k_compact_dups, dim3(grid_for(R, 4 * WAVE, 4096)), dim3(256), 0, ctx->stream, a);
     HIPCHK(hipGetLastError());
-    HIPCHK(hipEventRecord(ctx->ev[1], ctx->stream));
+    EV_STOP_M(ctx, 1);
     uint32_t cnt[4];
     readback(ctx, cnt, a.counters, sizeof cnt);
     if (cnt[2]) {
@@ -2819,12 +2875,12 @@ static int compact_rows(Slot* ctx, const tsdbhip_rows_desc* d, tsdbhip_rows_out*
       HIPCHK(hipStreamSynchronize(ctx->stream));
     }
     tsdbhip_timing t = {};
-    t.total_ms = ev_ms(ctx->ev[0], ctx->ev[1]);
-    t.hot_ms = ev_ms(ctx->ev[8], ctx->ev[4]) + ev_ms(ctx->ev[2], ctx->ev[9]);  // k_compact_quals + k_compact_vals (tiles: k_compact_tiles)
+    t.total_ms = ev_ms(ctx, 8, 1);
+    t.hot_ms = ev_ms(ctx, 8, 4) + ev_ms(ctx, 2, 9);  // k_compact_quals + k_compact_vals (tiles: k_compact_tiles)
     t.hot_kernel = TSDBHIP_HOT_COMPACT;
-    t.decode_ms = ev_ms(ctx->ev[4], ctx->ev[2]);  // k_compact_classify
-    t.grid_ms = ev_ms(ctx->ev[9], ctx->ev[3]);    // k_compact_rows
-    t.reduce_ms = ev_ms(ctx->ev[3], ctx->ev[1]);  // k_compact_complex + k_compact_dups
+    t.decode_ms = ev_ms(ctx, 4, 2);  // k_compact_classify
+    t.grid_ms = ev_ms(ctx, 9, 3);    // k_compact_rows
+    t.reduce_ms = ev_ms(ctx, 3, 1);  // k_compact_complex + k_compact_dups
     ctx->timing = t;
     out->qual_used = qext;
     out->val_used = vext + R;
@@ -2850,31 +2906,31 @@ extern "C" int tsdbhip_bw_probe(tsdbhip_ctx* c, const tsdbhip_sg_desc* d, int32_
     uint32_t* sink = scratch<uint32_t>(ctx, "probe_sink", 1);
     HIPCHK(hipEventRecord(ctx->ev[0], st));
     if (mode == 0) {
-      hipLaunchKernelGGL(k_probe_read, dim3(grid_for(d->n_spans, 4, 1u << 20)), dim3(256), 0, st, d->span_row_start,
+      LAUNCH(k_probe_read, dim3(grid_for(d->n_spans, 4, 1u << 20)), dim3(256), 0, st, d->span_row_start,
                          d->row_ncells, d->row_qual_off, d->row_val_off, d->qual_bytes, d->val_bytes, d->n_spans,
                          width, sink);
       *bytes = d->qual_nbytes + d->val_nbytes;
     } else if (mode == 2) {
       const uint64_t n16 = d->val_nbytes / 16;
-      hipLaunchKernelGGL(k_probe_flat, dim3(grid_for(n16, 1024, 1u << 16)), dim3(256), 0, st,
+      LAUNCH(k_probe_flat, dim3(grid_for(n16, 1024, 1u << 16)), dim3(256), 0, st,
                          (const uint4*)d->val_bytes, n16, sink);
       *bytes = n16 * 16;
     } else if (mode == 3) {
-      hipLaunchKernelGGL(k_probe_read2, dim3(grid_for(d->n_spans, 4, 1u << 20)), dim3(256), 0, st,
+      LAUNCH(k_probe_read2, dim3(grid_for(d->n_spans, 4, 1u << 20)), dim3(256), 0, st,
                          d->span_row_start, d->row_ncells, d->row_qual_off, d->row_val_off, d->qual_bytes,
                          d->val_bytes, d->n_spans, sink);
       *bytes = d->qual_nbytes + d->val_nbytes;
     } else {
       const uint64_t n16 = d->val_nbytes / 16;
       uint4* dst = scratch<uint4>(ctx, "probe_dst", n16);
-      hipLaunchKernelGGL(k_probe_copy, dim3(grid_for(n16, 256, 1u << 16)), dim3(256), 0, st,
+      LAUNCH(k_probe_copy, dim3(grid_for(n16, 256, 1u << 16)), dim3(256), 0, st,
                          (const uint4*)d->val_bytes, dst, n16);
       *bytes = 2 * n16 * 16;
     }
     HIPCHK(hipGetLastError());
     HIPCHK(hipEventRecord(ctx->ev[1], st));
     HIPCHK(hipStreamSynchronize(st));
-    *ms = ev_ms(ctx->ev[0], ctx->ev[1]);
+    HIPCHK(hipEventElapsedTime(ms, ctx->ev[0], ctx->ev[1]));  // (markers whatever the "events" option)
   } catch (Fail& f) {
     return f.code;
   }

@@ -24,13 +24,13 @@ static void launch_seg(Slot* ctx, const ReduceArgs& r0, const FinalArgs& f0, con
                        uint64_t waves, const SegGroup* sg, const uint64_t* goff, uint32_t G, uint64_t T_all,
                        GroupDev* gd) {
   if (waves && r0.d_info)  // span chunks without E spans (k_reduce's DONLY instantiation)
-    hipLaunchKernelGGL((k_reduce_seg<AGG, MODE, RATE, true>), dim3((unsigned)((waves + 3) / 4)), dim3(256), 0,
+    LAUNCH((k_reduce_seg<AGG, MODE, RATE, true>), dim3((unsigned)((waves + 3) / 4)), dim3(256), 0,
                        ctx->stream, r0, sr);
   if (waves)
-    hipLaunchKernelGGL((k_reduce_seg<AGG, MODE, RATE, false>), dim3((unsigned)((waves + 3) / 4)), dim3(256), 0,
+    LAUNCH((k_reduce_seg<AGG, MODE, RATE, false>), dim3((unsigned)((waves + 3) / 4)), dim3(256), 0,
                        ctx->stream, r0, sr);
   if (T_all)
-    hipLaunchKernelGGL((k_finalize_seg<AGG, MODE, RATE>), dim3(grid_for(T_all, 256)), dim3(256), 0, ctx->stream,
+    LAUNCH((k_finalize_seg<AGG, MODE, RATE>), dim3(grid_for(T_all, 256)), dim3(256), 0, ctx->stream,
                        r0, f0, sg, goff, G, T_all, gd);
 }
 
@@ -164,8 +164,8 @@ static int spangroup_run_batch(Slot* ctx, const tsdbhip_sg_desc* d, uint32_t G, 
     a.span0 = 0;
     uint32_t* alist = scratch<uint32_t>(ctx, "asm_list", S);
     uint32_t* acount = scratch<uint32_t>(ctx, "asm_count", 1, true);
-    hipLaunchKernelGGL(k_assemble_fast, dim3(grid_for(S, 256)), dim3(256), 0, st, a, alist, acount);
-    hipLaunchKernelGGL(k_assemble, dim3(grid_for(S, 4, 4096)), dim3(256), 0, st, a, (const uint32_t*)alist,
+    LAUNCH(k_assemble_fast, dim3(grid_for(S, 256)), dim3(256), 0, st, a, alist, acount);
+    LAUNCH(k_assemble, dim3(grid_for(S, 4, 4096)), dim3(256), 0, st, a, (const uint32_t*)alist,
                        (const uint32_t*)acount);
   }
   uint64_t* kflag = scratch<uint64_t>(ctx, "kflag", S);
@@ -177,17 +177,17 @@ static int spangroup_run_batch(Slot* ctx, const tsdbhip_sg_desc* d, uint32_t G, 
   GroupStat* stat = scratch<GroupStat>(ctx, "b_stat", G);
   const uint32_t* gss_d = upload(ctx, "b_gss", std::vector<uint32_t>(gss, gss + G + 1));
   if (S) {
-    hipLaunchKernelGGL(k_kept_flags, dim3(grid_for(S, 256)), dim3(256), 0, st, sp_kept, kflag, S);
+    LAUNCH(k_kept_flags, dim3(grid_for(S, 256)), dim3(256), 0, st, sp_kept, kflag, S);
     dscan_u64(ctx, kflag, kidx, S, &sm->n_kept, "k");
     dscan_u64(ctx, sp_cap, eoff_s, S, &sm->e_total, "e");
-    hipLaunchKernelGGL(k_kept_scatter, dim3(grid_for(S, 256, 1024)), dim3(256), 0, st, sp_kept, kidx, eoff_s,
+    LAUNCH(k_kept_scatter, dim3(grid_for(S, 256, 1024)), dim3(256), 0, st, sp_kept, kidx, eoff_s,
                        sp_ncells, S, kept, eoff, &sm->n_input, sp_first, sp_last, sm->bound);
   }
   Small h;
   readback(ctx, &h, sm, sizeof h);
   if (h.err != ERR_NONE) return batch_one_by_one(ctx, dd, G, gss, outs);
   const uint32_t n_kept = (uint32_t)h.n_kept;
-  hipLaunchKernelGGL(k_group_stats, dim3(std::min<uint32_t>(std::max<uint32_t>(G, 1), 65536)), dim3(256), 0, st,
+  LAUNCH(k_group_stats, dim3(std::min<uint32_t>(std::max<uint32_t>(G, 1), 65536)), dim3(256), 0, st,
                      gss_d, G, S, n_kept, sp_kept, kidx, sp_ncells, sp_first, sp_last, kgrp, stat);
   std::vector<GroupStat> gs(G);
   {
@@ -258,7 +258,7 @@ static int spangroup_run_batch(Slot* ctx, const tsdbhip_sg_desc* d, uint32_t G, 
     ctx->hot_kernel = fast ? TSDBHIP_HOT_DECODE_FAST : TSDBHIP_HOT_DECODE_GEN;
     HIPCHK(hipEventRecord(ctx->ev[8], st));
     if (!fast) {
-      if (interval == 0) hipLaunchKernelGGL(k_decode_nods, dim3(blocks), dim3(256), 0, st, da);
+      if (interval == 0) LAUNCH(k_decode_nods, dim3(blocks), dim3(256), 0, st, da);
       else launch_agg<LaunchGeneralDs>(ds_agg, ctx, blocks, da);
       HIPCHK(hipEventRecord(ctx->ev[9], st));
     } else if (interval == 0) {
@@ -287,15 +287,15 @@ static int spangroup_run_batch(Slot* ctx, const tsdbhip_sg_desc* d, uint32_t G, 
         // (spans per wave: 32 for big groups; fewer below ~64k spans, so a
         // small group still spreads over ~2048 waves instead of a handful)
         dg.batch = std::max<uint32_t>(1, std::min<uint32_t>(DIRB, n_kept / 2048));
-        hipLaunchKernelGGL(k_direct_scan, dim3(grid_for(n_kept, 4 * dg.batch, 1u << 20)), dim3(256), 0, st, da, dg,
+        LAUNCH(k_direct_scan, dim3(grid_for(n_kept, 4 * dg.batch, 1u << 20)), dim3(256), 0, st, da, dg,
                            row_ncells, row_val_len);
         fa.span_list = dg.list;
         fa.span_count = dg.list_count;
       }
       const unsigned lblocks = fa.span_list ? std::min(blocks, 1024u) : blocks;
-      hipLaunchKernelGGL((k_decode_fast<0, false>), dim3(lblocks), dim3(256), 0, st, fa, row_ncells, row_val_len);
+      LAUNCH((k_decode_fast<0, false>), dim3(lblocks), dim3(256), 0, st, fa, row_ncells, row_val_len);
       if (!direct) HIPCHK(hipEventRecord(ctx->ev[9], st));
-      hipLaunchKernelGGL(k_decode_nods, dim3(std::min(blocks, 1024u)), dim3(256), 0, st, ga);
+      LAUNCH(k_decode_nods, dim3(std::min(blocks, 1024u)), dim3(256), 0, st, ga);
     } else {
       DecodeArgs fa = da;
       if (ds_agg != 4) {
@@ -317,53 +317,53 @@ static int spangroup_run_batch(Slot* ctx, const tsdbhip_sg_desc* d, uint32_t G, 
 
   // ---- per-group summary and segmented union grids ----
   GroupDev* gd = scratch<GroupDev>(ctx, "b_gd", G);
-  hipLaunchKernelGGL(k_group_init, dim3(grid_for(G, 256)), dim3(256), 0, st, gd, G);
+  LAUNCH(k_group_init, dim3(grid_for(G, 256)), dim3(256), 0, st, gd, G);
   HIPCHK(hipEventRecord(ctx->ev[3], st));
   const uint32_t* d_info = direct ? dg.info : nullptr;
   uint32_t* bitmap = scratch<uint32_t>(ctx, "bitmap", W, true);
   uint32_t* word_rank = scratch<uint32_t>(ctx, "word_rank", W);
   const uint64_t nb = (W + 1023) / 1024;
   uint32_t* bsum = scratch<uint32_t>(ctx, "grid_bsum", nb);
-  hipLaunchKernelGGL(k_group_words, dim3(std::min<uint32_t>(std::max<uint32_t>(G, 1), 65536)), dim3(256), 0, st, q,
+  LAUNCH(k_group_words, dim3(std::min<uint32_t>(std::max<uint32_t>(G, 1), 65536)), dim3(256), 0, st, q,
                      G, wgrp);
   if (n_kept)
-    hipLaunchKernelGGL(k_grid_mark_seg, dim3(grid_for(n_kept, 4, 65536)), dim3(256), 0, st, eoff, e_len, e_ts,
+    LAUNCH(k_grid_mark_seg, dim3(grid_for(n_kept, 4, 65536)), dim3(256), 0, st, eoff, e_len, e_ts,
                        n_kept, (int32_t)rate, kgrp, q, bitmap, d_info);
   if (direct && n_kept)
-    hipLaunchKernelGGL(k_direct_mark_seg, dim3(grid_for(n_kept, 4 * WAVE, 16384)), dim3(256), 0, st, dg, n_kept,
+    LAUNCH(k_direct_mark_seg, dim3(grid_for(n_kept, 4 * WAVE, 16384)), dim3(256), 0, st, dg, n_kept,
                        kgrp, q, bitmap);
   GridArgs ga = {};
   std::memset(&ga, 0, sizeof ga);
   ga.bitmap = bitmap; ga.nwords = W; ga.word_rank = word_rank; ga.block_sum = bsum; ga.total = &sm->T;
-  hipLaunchKernelGGL(k_grid_popc, dim3((unsigned)nb), dim3(256), 0, st, ga);
-  if (nb > 1) hipLaunchKernelGGL(k_grid_scan_blocks, dim3(1), dim3(256), 0, st, ga, (uint32_t)nb);
+  LAUNCH(k_grid_popc, dim3((unsigned)nb), dim3(256), 0, st, ga);
+  if (nb > 1) LAUNCH(k_grid_scan_blocks, dim3(1), dim3(256), 0, st, ga, (uint32_t)nb);
   readback(ctx, &h, sm, sizeof h);  // total |G| over the groups (grid buffer size)
   const uint64_t T_all = h.T;
   uint32_t* gridv = scratch<uint32_t>(ctx, "grid", T_all);
-  hipLaunchKernelGGL(k_grid_emit_seg, dim3(grid_for(W, 256)), dim3(256), 0, st, bitmap, word_rank,
+  LAUNCH(k_grid_emit_seg, dim3(grid_for(W, 256)), dim3(256), 0, st, bitmap, word_rank,
                      (const uint32_t*)bsum, W, q, gridv);
-  hipLaunchKernelGGL(k_group_T, dim3(grid_for(G, 256)), dim3(256), 0, st, q, G, (const uint32_t*)word_rank, gd);
-  hipLaunchKernelGGL(k_group_rebase, dim3(grid_for(W, 256)), dim3(256), 0, st, q, W, (const GroupDev*)gd,
+  LAUNCH(k_group_T, dim3(grid_for(G, 256)), dim3(256), 0, st, q, G, (const uint32_t*)word_rank, gd);
+  LAUNCH(k_group_rebase, dim3(grid_for(W, 256)), dim3(256), 0, st, q, W, (const GroupDev*)gd,
                      word_rank);
   if (direct && n_kept) {
     // candidates whose points are not consecutive ranks of their group grid
     // need E (their grid points are already marked)
     HIPCHK(hipMemsetAsync(dg.list_count, 0, 4, st));
     HIPCHK(hipMemsetAsync(da.fb_count, 0, 4, st));
-    hipLaunchKernelGGL(k_direct_verify_seg, dim3(grid_for(n_kept, 256)), dim3(256), 0, st, dg, n_kept, kgrp, q,
+    LAUNCH(k_direct_verify_seg, dim3(grid_for(n_kept, 256)), dim3(256), 0, st, dg, n_kept, kgrp, q,
                        (const uint32_t*)bitmap, (const uint32_t*)word_rank);
     DecodeArgs fa = da;
     fa.span_list = dg.list;
     fa.span_count = dg.list_count;
     const unsigned vb = std::min(grid_for(n_kept, 4, 65536), 1024u);
-    hipLaunchKernelGGL((k_decode_fast<0, false>), dim3(vb), dim3(256), 0, st, fa, row_ncells, row_val_len);
+    LAUNCH((k_decode_fast<0, false>), dim3(vb), dim3(256), 0, st, fa, row_ncells, row_val_len);
     DecodeArgs gfa = da;
     gfa.use_fb = 1;
-    hipLaunchKernelGGL(k_decode_nods, dim3(vb), dim3(256), 0, st, gfa);
+    LAUNCH(k_decode_nods, dim3(vb), dim3(256), 0, st, gfa);
   }
   // E_EMPTY_SPAN, F*_g and the group's int/float flags, over final E / direct spans
   if (n_kept)
-    hipLaunchKernelGGL(k_group_summary, dim3(grid_for(n_kept, 4, 65536)), dim3(256), 0, st, eoff, e_len, e_ts,
+    LAUNCH(k_group_summary, dim3(grid_for(n_kept, 4, 65536)), dim3(256), 0, st, eoff, e_len, e_ts,
                        e_flt, n_kept, (int32_t)rate, (int32_t)(!rate && anyf && anyi), kgrp, d_info,
                        (const uint32_t*)dg.x0, gd, &sm->err);
   HIPCHK(hipEventRecord(ctx->ev[4], st));
@@ -464,7 +464,7 @@ static int spangroup_run_batch(Slot* ctx, const tsdbhip_sg_desc* d, uint32_t G, 
     uint32_t* ce = scratch<uint32_t>(ctx, "chunk_e", std::max<uint64_t>(choff, 1), true);
     const uint64_t* choff_d = upload(ctx, "b_choff", choffv);
     if (n_kept)
-      hipLaunchKernelGGL(k_chunk_flags_seg, dim3(grid_for(n_kept, 256)), dim3(256), 0, st, (const uint32_t*)dg.info,
+      LAUNCH(k_chunk_flags_seg, dim3(grid_for(n_kept, 256)), dim3(256), 0, st, (const uint32_t*)dg.info,
                          n_kept, (const uint32_t*)kgrp, sg_d, choff_d, ce);
     r0.chunk_e = ce;
     HIPCHK(hipEventRecord(ctx->ev[8], st));
@@ -480,17 +480,17 @@ static int spangroup_run_batch(Slot* ctx, const tsdbhip_sg_desc* d, uint32_t G, 
   }
   if (direct) HIPCHK(hipEventRecord(ctx->ev[9], st));  // (finalize included: small next to the reduce)
   if (n_kept)
-    hipLaunchKernelGGL(k_bad_index_seg, dim3(grid_for(n_kept, 256)), dim3(256), 0, st, e_bad, eoff, e_ts, n_kept,
+    LAUNCH(k_bad_index_seg, dim3(grid_for(n_kept, 256)), dim3(256), 0, st, e_bad, eoff, e_ts, n_kept,
                        (int32_t)rate, kgrp, q, bitmap, word_rank, gd);
   HIPCHK(hipEventRecord(ctx->ev[5], st));
   read_groups();  // sync 4
   HIPCHK(hipStreamSynchronize(st));
-  tm.decode_ms = ev_ms(ctx->ev[1], ctx->ev[2]);
-  if (ctx->hot_kernel) tm.hot_ms = ev_ms(ctx->ev[8], ctx->ev[9]);
+  tm.decode_ms = ev_ms(ctx, 1, 2);
+  if (ctx->hot_kernel) tm.hot_ms = ev_ms(ctx, 8, 9);
   tm.hot_kernel = ctx->hot_kernel;
-  tm.grid_ms = ev_ms(ctx->ev[3], ctx->ev[4]);
-  tm.reduce_ms = ev_ms(ctx->ev[4], ctx->ev[5]);
-  tm.total_ms = ev_ms(ctx->ev[0], ctx->ev[5]);
+  tm.grid_ms = ev_ms(ctx, 3, 4);
+  tm.reduce_ms = ev_ms(ctx, 4, 5);
+  tm.total_ms = ev_ms(ctx, 0, 5);
   tm.n_emitted = e_total;
   ctx->timing = tm;
 

@@ -10,11 +10,18 @@ check that the rerun reproduces the reference's results and errors."""
 import numpy as np
 import pytest
 
-from helpers import I, F, T0, U32MAX, assert_same, corrupt_qual as corrupt, run_both
+from helpers import I, F, T0, U32MAX, assert_same, corrupt_qual as corrupt, run_both, with_option
 from opentsdb_amd import _abi, packing, synth
 
 I64, F32, F64 = _abi.SYN_INT64_COUNTER, _abi.SYN_FLOAT32, _abi.SYN_FLOAT64
 AGGS = [0, 1, 2, 3, 4]
+
+
+@pytest.fixture(autouse=True)
+def always(request):
+    """these groups are small: "always" makes the proposal whatever the size
+    ("on", the default, leaves groups of < 2048 lockstep waves to k_reduce)"""
+    yield from with_option(request, "lockstep", "always", "on")
 
 
 def tried(agg, rate):
@@ -138,5 +145,24 @@ def test_lockstep_nan_result(ctx):
     ss = packing.pack_spans(spans)
     g, o = run_both(ctx, ss, agg=0)
     assert o.code == _abi.E_NAN_INF
+    assert_same(g, o)
+    check_paths(ctx, True)
+
+
+@pytest.mark.gpu
+def test_lockstep_auto_skips_small_groups(ctx):
+    """the default ("on"): C1's shape (100 spans x 3600) takes k_reduce, no
+    proposal; a group of >= 2048 lockstep waves takes k_lockstep"""
+    ss = synth.regular(100, 3600, I64, seed=1, step=1)
+    ctx.set_option("lockstep", "on")
+    g, o = run_both(ctx, ss, agg=0)
+    assert_same(g, o)
+    check_paths(ctx, False)
+    ss = synth.regular(20_000, 600, I64, seed=1, step=1)  # 2 tiles x 312 chunks of 64 spans
+    g, o = run_both(ctx, ss, agg=0)
+    assert_same(g, o)
+    check_paths(ctx, False)
+    ss = synth.regular(70_000, 600, I64, seed=1, step=1)  # 2 x 1093
+    g, o = run_both(ctx, ss, agg=0)
     assert_same(g, o)
     check_paths(ctx, True)
