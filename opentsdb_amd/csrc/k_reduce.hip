@@ -807,6 +807,97 @@ DEVI void reduce_wave_body(const ReduceArgs& r, const uint32_t wave, uint8_t* ld
       }
       const uint64_t smask = ballot(sc && (int64_t)x2_l > t_last);
       const uint32_t nb = min((uint32_t)WAVE, k1 - kb);
+      // Integer sum / min / max / avg are order-free (wrapping sums, exact
+      // min / max), so the cached spans whose long lerp is prepared (C4-int:
+      // ~93% of the span-tiles) go first, in a loop of their own: five
+      // readlanes, the prepared lerp and the push, instead of the ordered
+      // loop's dispatch over six masks and the generic cached(). Sum / avg add
+      // the y0s on the scalar unit and the signed quotients per lane.
+      constexpr bool INT_FAST = MODE == MODE_INT && !RATE && AGG != 4;
+      uint64_t skip = lmask;
+      if (INT_FAST) {
+        const bool fc_l = ((cmask >> lane) & 1) && (j_l == 0 || j_l >= len_l || im_l != UINT32_MAX);
+        skip |= ballot(fc_l);
+        const uint64_t work = ballot(fc_l && j_l > 0 && j_l < len_l);
+        if (work) {
+          const uint32_t d_l = x_l.y - x_l.x;
+          const uint32_t tl32 = gv ? (uint32_t)tl : (uint32_t)t_first;  // (x0 < t_first <= t < x1)
+          if (AGG == 0 || AGG == 3) {
+            uint64_t ysum = 0, qsum = 0;
+            for (uint64_t m = work; m; m &= m - 1) {
+              const int i = (int)__builtin_ctzll(m);
+              const uint32_t x0 = readlane_u32(x_l.x, i), d = readlane_u32(d_l, i), im = readlane_u32(im_l, i);
+              const double magr = __longlong_as_double((long long)readlane_u64((uint64_t)__double_as_longlong(magr_l), i));
+              ysum += readlane_u64((uint64_t)y_l.x, i);
+              const uint32_t u = tl32 - x0, mag = im & 0x7fffffffu;
+              uint32_t q = (uint32_t)((double)u * magr);
+              const int64_t rem = (int64_t)((uint64_t)u * mag) - (int64_t)((uint64_t)q * d);
+              q = rem < 0 ? q - 1u : (rem >= (int64_t)d ? q + 1u : q);
+              qsum = (im >> 31) ? qsum - q : qsum + q;
+            }
+            acc.ia = (int64_t)((acc.cnt == 0 ? 0ull : (uint64_t)acc.ia) + ysum + qsum);
+            acc.cnt += (uint32_t)__popcll(work);
+          } else {
+            for (uint64_t m = work; m; m &= m - 1) {
+              const int i = (int)__builtin_ctzll(m);
+              const uint32_t x0 = readlane_u32(x_l.x, i), d = readlane_u32(d_l, i), im = readlane_u32(im_l, i);
+              const double magr = __longlong_as_double((long long)readlane_u64((uint64_t)__double_as_longlong(magr_l), i));
+              const int64_t y0 = (int64_t)readlane_u64((uint64_t)y_l.x, i);
+              acc_push<AGG, MODE>(acc, lerp_long_prepped(tl32 - x0, d, y0, im, magr), 0.0);
+            }
+          }
+        }
+        // ... and the spans with one point x_n in the tile (smask), their
+        // brackets prepared: each lane picks its bracket, (j-1, j) before x_n
+        // or (j, j+1) after it (y_n on it), so one lerp a lane instead of the
+        // ordered loop's divergent branches; the cursors move past x_n
+        // lane-parallel afterwards (SpanGroup.java:702-784)
+        const bool sf_l = ((smask >> lane) & 1) && (j_l == 0 || im_l != UINT32_MAX) &&
+                          (j_l + 1 >= len_l || im2_l != UINT32_MAX);
+        const uint64_t sfm = ballot(sf_l);
+        if (sfm) {
+          skip |= sfm;
+          const uint32_t tl32 = gv ? (uint32_t)tl : (uint32_t)t_first;
+          uint64_t lsum = 0;
+          uint32_t lcnt = 0;
+          for (uint64_t m = sfm; m; m &= m - 1) {
+            const int i = (int)__builtin_ctzll(m);
+            const uint32_t j = readlane_u32(j_l, i), len = readlane_u32(len_l, i);
+            const uint32_t xc = readlane_u32(x_l.x, i), xn = readlane_u32(x_l.y, i), x2 = readlane_u32(x2_l, i);
+            const uint32_t im = readlane_u32(im_l, i), im2 = readlane_u32(im2_l, i);
+            const int64_t yc = (int64_t)readlane_u64((uint64_t)y_l.x, i), yn = (int64_t)readlane_u64((uint64_t)y_l.y, i);
+            const double mr = __longlong_as_double((long long)readlane_u64((uint64_t)__double_as_longlong(magr_l), i));
+            const double mr2 = __longlong_as_double((long long)readlane_u64((uint64_t)__double_as_longlong(magr2_l), i));
+            const bool before = tl32 < xn, at = tl32 == xn;
+            const bool act = gv && (before ? j > 0 : (at || j + 1 < len));
+            const bool lerp = act && !at;
+            const uint32_t a = before ? xc : xn, d = before ? xn - xc : x2 - xn, imv = before ? im : im2;
+            const double mrv = lerp ? (before ? mr : mr2) : 0.0;
+            const uint32_t u = lerp ? tl32 - a : 0u, mag = imv & 0x7fffffffu;
+            uint32_t q = (uint32_t)((double)u * mrv);
+            const int64_t rem = (int64_t)((uint64_t)u * mag) - (int64_t)((uint64_t)q * d);
+            q = rem < 0 ? q - 1u : (rem >= (int64_t)d ? q + 1u : q);
+            const int64_t v = at ? yn : ladd(before ? yc : yn, (imv >> 31) ? -(int64_t)q : (int64_t)q);
+            if (AGG == 0 || AGG == 3) {
+              lsum += act ? (uint64_t)v : 0ull;
+              lcnt += act ? 1u : 0u;
+            } else {
+              acc_push_if<AGG, MODE>(acc, act, v, 0.0);
+            }
+          }
+          if (AGG == 0 || AGG == 3) {
+            acc.ia = (int64_t)((acc.cnt == 0 ? 0ull : (uint64_t)acc.ia) + lsum);
+            acc.cnt += lcnt;
+          }
+          if (sf_l) {  // the cursor past point j
+            j_l = j_l + 1;
+            x_l = make_uint2(x_l.y, x2_l);
+            y_l = make_longlong2(y_l.y, y2_l);
+            f_l = 4u | ((f_l & 2u) ? 1u : 0u) | (f2_l ? 2u : 0u);
+            dirty_l = true;
+          }
+        }
+      }
       // A span with no point in this tile (its next point j lies past t_last):
       // every lane's bracket is (j-1, j), all from the cache (the span's lane
       // i of the batch registers above; only what the lerp reads is broadcast).
@@ -853,8 +944,8 @@ DEVI void reduce_wave_body(const ReduceArgs& r, const uint32_t wave, uint8_t* ld
         acc_push<AGG, MODE>(acc, yi, yd);
       };
       for (uint32_t i = 0; i < nb;) {
-        if ((lmask >> i) & 1) {  // (added above)
-          const uint64_t m = ~(lmask >> i);
+        if ((skip >> i) & 1) {  // (added above)
+          const uint64_t m = ~(skip >> i);
           i = min(nb, i + (m ? (uint32_t)__builtin_ctzll(m) : 64u));
           continue;
         }
