@@ -814,7 +814,11 @@ DEVI void reduce_wave_body(const ReduceArgs& r, const uint32_t wave, uint8_t* ld
       // loop's dispatch over six masks and the generic cached(). Sum / avg add
       // the y0s on the scalar unit and the signed quotients per lane.
       constexpr bool INT_FAST = MODE == MODE_INT && !RATE && AGG != 4;
-      uint64_t skip = lmask;
+      // cached spans that contribute nothing to this tile (expired; not
+      // started, outside rate mode): cached() would return at once, so the
+      // ordered loop skips them in runs instead of visiting each (C4: the
+      // spans outside their time range at a tile)
+      uint64_t skip = lmask | ballot(((cmask >> lane) & 1) && (j_l >= len_l || (!RATE && j_l == 0)));
       if (INT_FAST) {
         const bool fc_l = ((cmask >> lane) & 1) && (j_l == 0 || j_l >= len_l || im_l != UINT32_MAX);
         skip |= ballot(fc_l);
@@ -887,6 +891,53 @@ DEVI void reduce_wave_body(const ReduceArgs& r, const uint32_t wave, uint8_t* ld
           }
           if (AGG == 0 || AGG == 3) {
             acc.ia = (int64_t)((acc.cnt == 0 ? 0ull : (uint64_t)acc.ia) + lsum);
+            acc.cnt += lcnt;
+          }
+          if (sf_l) {  // the cursor past point j
+            j_l = j_l + 1;
+            x_l = make_uint2(x_l.y, x2_l);
+            y_l = make_longlong2(y_l.y, y2_l);
+            f_l = 4u | ((f_l & 2u) ? 1u : 0u) | (f2_l ? 2u : 0u);
+            dirty_l = true;
+          }
+        }
+      }
+      // Double sum / avg outside EXACT_ORDER, every lane's t on the double
+      // path (dual mode: no long lerp is read): the one-point-in-tile spans
+      // (C4: the bulk of what LIN leaves) the same way, from their prepared
+      // doubles (y0, y1 - y0, 1 / (x1 - x0)) and the double of y_n; finite
+      // brackets only. The order of the adds changes as LIN's does.
+      constexpr bool DBL_FAST = (MODE == MODE_DBL || MODE == MODE_DUAL) && !RATE && (AGG == 0 || AGG == 3);
+      if (DBL_FAST && !r.exact && (MODE == MODE_DBL || dual_all_dbl)) {
+        const bool more_l = j_l + 1 < len_l;
+        const double ynd_l = to_double(y_l.y, MODE == MODE_DBL || (f_l & 2u));
+        const bool sf_l = ((smask >> lane) & 1) && (j_l == 0 || (x_l.y > x_l.x && __builtin_isfinite(y0d_l) &&
+                                                                 __builtin_isfinite(dyd_l))) &&
+                          __builtin_isfinite(ynd_l) &&
+                          (!more_l || (__builtin_isfinite(y0d2_l) && __builtin_isfinite(dyd2_l)));
+        const uint64_t sfm = ballot(sf_l);
+        if (sfm) {
+          skip |= sfm;
+          const uint32_t tl32 = gv ? (uint32_t)tl : (uint32_t)t_first;
+          double lsum = 0.0;
+          uint32_t lcnt = 0;
+          for (uint64_t m = sfm; m; m &= m - 1) {
+            const int i = (int)__builtin_ctzll(m);
+            const uint32_t j = readlane_u32(j_l, i), len = readlane_u32(len_l, i);
+            const uint32_t xc = readlane_u32(x_l.x, i), xn = readlane_u32(x_l.y, i);
+            const bool before = tl32 < xn, at = tl32 == xn;
+            const bool act = gv && (before ? j > 0 : (at || j + 1 < len));
+            auto rl = [&](double x) { return __longlong_as_double((long long)readlane_u64((uint64_t)__double_as_longlong(x), i)); };
+            const double y0a = rl(y0d_l), dya = rl(dyd_l), ria = rl(rinv_l);
+            const double y0b = rl(y0d2_l), dyb = rl(dyd2_l), rib = rl(rinv2_l), yn = rl(ynd_l);
+            const double v = at ? yn
+                                : (before ? y0a + ((double)(tl32 - xc) * dya) * ria
+                                          : y0b + ((double)(tl32 - xn) * dyb) * rib);
+            lsum += act ? v : 0.0;
+            lcnt += act ? 1u : 0u;
+          }
+          if (gv && lcnt) {
+            acc.da = acc.cnt == 0 ? lsum : acc.da + lsum;
             acc.cnt += lcnt;
           }
           if (sf_l) {  // the cursor past point j
