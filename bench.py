@@ -107,6 +107,13 @@ def ref_row_bytes(n_series, n_points, step, kind):
     return n_series * per_span
 
 
+def kbase(name):
+    """a profiled kernel's base name: template arguments and the occupancy
+    variant's suffix dropped (k_reduce_w4<0, 2, ...> -> k_reduce)"""
+    b = name.split("<")[0]
+    return b[:-3] if b.endswith("_w4") else b
+
+
 def pmc_traffic(config, kernel, world):
     """HBM bytes per launch of `kernel` from the committed rocprofv3 PMC
     summary of this config (profiles/pmc_<config>.json, made by
@@ -119,7 +126,7 @@ def pmc_traffic(config, kernel, world):
     # integer and float k_ds_spans), and the timed region covers them all
     names = kernel.split("+")  # (a "+"-joined name: the kernels the timed bracket covers)
     tot = sum(e["hbm_bytes_per_launch"] for name, e in ks.items()
-              if name.split("<")[0] in names and e.get("hbm_bytes_per_launch"))
+              if kbase(name) in names and e.get("hbm_bytes_per_launch"))
     return (tot, os.path.relpath(path, ROOT)) if tot else (None, None)
 
 
@@ -135,7 +142,7 @@ def pmc_valu(config, kernel):
     if not os.path.exists(path):
         return None, None
     ks = json.load(open(path)).get("kernels", {})
-    tot = sum(e.get("valu_insts_per_launch") or 0 for name, e in ks.items() if name.split("<")[0] == kernel)
+    tot = sum(e.get("valu_insts_per_launch") or 0 for name, e in ks.items() if kbase(name) == kernel)
     return (tot, os.path.relpath(path, ROOT)) if tot else (None, None)
 
 

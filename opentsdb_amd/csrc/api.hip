@@ -853,8 +853,12 @@ static void launch_reduce(Slot* ctx, unsigned blocks, const ReduceArgs& r, const
   if (ctx->time_reduce) EV_START(ctx, 8);
   if (r.d_info && r.chunk_e)
     LAUNCH((k_reduce<AGG, MODE, RATE, true>), dim3(blocks), dim3(256), 0, ctx->stream, r);
-  LAUNCH_STOP(ctx->time_reduce ? EV_STOP_K(ctx, 9) : nullptr, (k_reduce<AGG, MODE, RATE, false>), dim3(blocks),
-              dim3(256), r.lds_state ? 4 * red_lds_stride(r.spans_per_chunk, RATE) : 0, ctx->stream, r);
+  const unsigned lds = r.lds_state ? 4 * red_lds_stride(r.spans_per_chunk, RATE) : 0;
+  const hipEvent_t stop = ctx->time_reduce ? EV_STOP_K(ctx, 9) : nullptr;
+  if constexpr (AGG == TSDBHIP_AGG_DEV)
+    LAUNCH_STOP(stop, (k_reduce<AGG, MODE, RATE, false>), dim3(blocks), dim3(256), lds, ctx->stream, r);
+  else
+    LAUNCH_STOP(stop, (k_reduce_w4<AGG, MODE, RATE, false>), dim3(blocks), dim3(256), lds, ctx->stream, r);
   if (ctx->time_reduce) EV_STOP_M(ctx, 9);
   if (!finalize) return;
   if (par && f.T >= 1024)  // (large T: coalesced columns)
@@ -1039,7 +1043,8 @@ struct Small {
   unsigned long long bound[4];  // [min first ts, max last ts, max first ts, min last ts] of the kept spans
   uint32_t cnt[6];  // list counters, zero at the start of a call (no memsets):
                     // [0] assembly queue, [1] decode fallback, [2] direct list,
-                    // [3] [4] k_ds_spans int / float leftovers
+                    // [3] [4] k_ds_spans int / float leftovers, [5] lockstep
+                    // proposal
   uint32_t seg[CK_NSEG];  // k_ds_spans integer leftovers, per segment
   uint32_t seg2[CK_NSEG];  // k_ds_reg leftovers, per segment
   // k_ds_reg's aligned-group reduction (FAP): the spans' class keys
@@ -1469,17 +1474,19 @@ static int spangroup_run_once(Slot* ctx, const tsdbhip_sg_desc* d, tsdbhip_sg_ou
       uint32_t* alist = scratch<uint32_t>(ctx, "asm_list", S);
       uint32_t* acount = &sm->cnt[0];
       LAUNCH(k_assemble_fast, dim3(grid_for(S, 256)), dim3(256), 0, st, a, alist, acount);
-      LAUNCH(k_assemble, dim3(grid_for(S, 4, 4096)), dim3(256), 0, st, a, (const uint32_t*)alist,
+      LAUNCH(k_assemble, dim3(grid_for(S, 4, 1024)), dim3(256), 0, st, a, (const uint32_t*)alist,
                          (const uint32_t*)acount);
       if (S <= KC_MAX) {
         LAUNCH(k_kept_compact, dim3(1), dim3(1024), 0, st, K);
       } else {  // bigger groups: tile sums, then per-tile offsets + scatter
         const uint32_t nt = (S + 1023) / 1024;
-        ulonglong2* ts = scratch<ulonglong2>(ctx, "kept_tiles", nt);
-        LAUNCH(k_kept_tiles, dim3(nt), dim3(256), 0, st, sp_kept, sp_cap, S, ts);
-        LAUNCH(k_kept_scatter_tiles, dim3(nt), dim3(256), 0, st, sp_kept, sp_cap, sp_ncells, S,
-                           (const ulonglong2*)ts, kept, eoff, &sm->n_input, sp_first, sp_last, sm->bound,
-                           &sm->n_kept, &sm->e_total);
+        KeptTile* ts = scratch<KeptTile>(ctx, "kept_tiles", nt);
+        LAUNCH(k_kept_tiles, dim3(nt), dim3(256), 0, st, sp_kept, sp_cap, sp_ncells, sp_first, sp_last, S, ts);
+        // (its last block publishes the call state)
+        pub1 = true;
+        p1 = next_pub(ctx, sizeof(Small));
+        LAUNCH(k_kept_scatter_tiles, dim3(nt), dim3(256), 0, st, sp_kept, sp_cap, S, (const KeptTile*)ts, kept,
+               eoff, &sm->n_input, sm->bound, &sm->n_kept, &sm->e_total, p1, (const uint64_t*)sm);
       }
     }
   }
@@ -1786,9 +1793,11 @@ static int spangroup_run_once(Slot* ctx, const tsdbhip_sg_desc* d, tsdbhip_sg_ou
       int64_t* tmp = scratch<int64_t>(ctx, "fap_tmp", (uint64_t)g1 * WAVE);
       auto go = [&](auto opc) {
         constexpr int OP = decltype(opc)::value;
+        // (two launches: a last-block-done fusion of the two measured slower,
+        // 20.3 us against 4.6 + 9.3, its 244 blocks' counter atomics contended)
         LAUNCH((k_fap_rows<OP>), dim3(g1), dim3(1024), 0, st, (const int64_t*)fap.a.part, nrows, tmp);
-        LAUNCH((k_fap_final64v<OP>), dim3(1), dim3(1024), 0, st, (const int64_t*)tmp, g1, n_kept, o_pi, o_pc,
-                           sm, pack);
+        LAUNCH((k_fap_final64v<OP>), dim3(1), dim3(1024), 0, st, (const int64_t*)tmp, g1, n_kept, o_pi, o_pc, sm,
+               pack);
       };
       if (fop == 1) go(std::integral_constant<int, 1>());
       else if (fop == 2) go(std::integral_constant<int, 2>());

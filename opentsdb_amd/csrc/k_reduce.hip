@@ -1188,6 +1188,16 @@ __global__ void __launch_bounds__(256) k_reduce(ReduceArgs r) {
   uint8_t* w = (!DONLY && r.lds_state) ? red_lds + (threadIdx.x / WAVE) * red_lds_stride(r.spans_per_chunk, RATE) : nullptr;
   reduce_wave<AGG, MODE, RATE, DONLY>(r, (blockIdx.x * blockDim.x + threadIdx.x) / WAVE, w);
 }
+// The same for sum / min / max / avg held to 128 VGPRs (4 waves a SIMD
+// instead of 3 for the dual / double modes' 137): C4's reduce 9.66 -> 8.69
+// ms, same box; dev, which would spill, and a 5-wave cap (12.7 ms, spills)
+// keep the plain kernel.
+template <int AGG, int MODE, bool RATE, bool DONLY>
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) k_reduce_w4(ReduceArgs r) {
+  extern __shared__ __align__(16) uint8_t red_lds[];
+  uint8_t* w = (!DONLY && r.lds_state) ? red_lds + (threadIdx.x / WAVE) * red_lds_stride(r.spans_per_chunk, RATE) : nullptr;
+  reduce_wave<AGG, MODE, RATE, DONLY>(r, (blockIdx.x * blockDim.x + threadIdx.x) / WAVE, w);
+}
 
 __global__ void k_chunk_flags(const uint32_t* d_info, uint32_t n_kept, uint32_t spc, uint32_t* chunk_e) {
   const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;

@@ -230,50 +230,90 @@ DEVI void kept_compact_block(const KeptArgs& A) {
 }
 __global__ void __launch_bounds__(1024) k_kept_compact(KeptArgs A) { kept_compact_block(A); }
 
-// Bigger groups in two launches: per tile of 1024 spans its (kept, capacity)
-// sums; then each tile adds up its predecessors' sums itself (at most a few
-// thousand tiles: no serial chain across tiles) and scatters.
-__global__ void __launch_bounds__(256) k_kept_tiles(const uint8_t* kept, const uint64_t* cap, uint32_t n,
-                                                    ulonglong2* tile_sum) {
-  __shared__ uint64_t sh_k[4], sh_e[4];
+// Bigger groups in two launches: per tile of 1024 spans its sums (kept,
+// capacity, cells) and bounds; then each tile adds up its predecessors' sums
+// itself (at most a few thousand tiles: no serial chain across tiles) and
+// scatters, and the last tile's block, which reads every tile's sums anyway,
+// writes the group's totals and bounds (no atomics from every block) and
+// hands the call state to the host (no k_publish launch).
+struct KeptTile {
+  uint64_t k, e, cnt;
+  int64_t f, l, fx, ln;  // over the tile's kept spans with cells (neutral otherwise)
+  uint64_t pad;
+};
+__global__ void __launch_bounds__(256) k_kept_tiles(const uint8_t* kept, const uint64_t* cap, const uint32_t* ncells,
+                                                    const int64_t* sp_first, const int64_t* sp_last, uint32_t n,
+                                                    KeptTile* tile_sum) {
+  __shared__ uint64_t sh_k[4], sh_e[4], sh_c[4];
+  __shared__ int64_t sh_f[4], sh_l[4];
   const uint64_t base = (uint64_t)blockIdx.x * 1024 + 4 * threadIdx.x;
-  uint64_t sk = 0, se = 0;
+  uint64_t sk = 0, se = 0, cnt = 0;
+  int64_t f = INT64_MAX, l = INT64_MIN, fx = INT64_MIN, ln = INT64_MAX;
 #pragma unroll
   for (int i = 0; i < 4; i++) {
     const uint64_t s = base + i;
     if (s < n) {
-      sk += kept[s] ? 1u : 0u;
       se += cap[s];
+      if (kept[s]) {
+        sk++;
+        cnt += ncells[s];
+        f = min(f, sp_first[s]);
+        l = max(l, sp_last[s]);
+        fx = max(fx, sp_first[s]);
+        ln = min(ln, sp_last[s]);
+      }
     }
   }
   sk = block_reduce_256(sk, [](uint64_t x, uint64_t y) { return x + y; }, sh_k);
   se = block_reduce_256(se, [](uint64_t x, uint64_t y) { return x + y; }, sh_e);
-  if (threadIdx.x == 0) tile_sum[blockIdx.x] = make_ulonglong2(sk, se);
+  cnt = block_reduce_256(cnt, [](uint64_t x, uint64_t y) { return x + y; }, sh_c);
+  f = block_reduce_256(f, [](int64_t x, int64_t y) { return min(x, y); }, sh_f);
+  l = block_reduce_256(l, [](int64_t x, int64_t y) { return max(x, y); }, sh_l);
+  __syncthreads();
+  fx = block_reduce_256(fx, [](int64_t x, int64_t y) { return max(x, y); }, sh_f);
+  ln = block_reduce_256(ln, [](int64_t x, int64_t y) { return min(x, y); }, sh_l);
+  if (threadIdx.x == 0) {
+    KeptTile o;
+    o.k = sk; o.e = se; o.cnt = cnt; o.pad = 0;
+    // (a tile whose kept spans hold no cell leaves the bounds alone, as the
+    // per-block atomics of the single-block path do)
+    o.f = cnt ? f : INT64_MAX; o.l = cnt ? l : INT64_MIN; o.fx = cnt ? fx : INT64_MIN; o.ln = cnt ? ln : INT64_MAX;
+    tile_sum[blockIdx.x] = o;
+  }
 }
 
-__global__ void __launch_bounds__(256) k_kept_scatter_tiles(const uint8_t* kept, const uint64_t* cap,
-                                                            const uint32_t* ncells, uint32_t n,
-                                                            const ulonglong2* tile_sum, uint32_t* kept_list,
+__global__ void __launch_bounds__(256) k_kept_scatter_tiles(const uint8_t* kept, const uint64_t* cap, uint32_t n,
+                                                            const KeptTile* tile_sum, uint32_t* kept_list,
                                                             uint64_t* eoff_k, unsigned long long* n_input,
-                                                            const int64_t* sp_first, const int64_t* sp_last,
                                                             unsigned long long* bound, uint64_t* n_kept_out,
-                                                            uint64_t* e_total_out) {
+                                                            uint64_t* e_total_out, HostPub pub,
+                                                            const uint64_t* pub_src) {
   __shared__ uint64_t s_wk[4], s_we[4];
   __shared__ uint64_t sh_c[4];
   __shared__ int64_t sh_f[4], sh_l[4];
+  __shared__ uint64_t s_pk, s_pe;
   const int t = threadIdx.x, lane = lane_id(), w = t / WAVE;
   const uint32_t tile = blockIdx.x;
-  // this tile's offset: the sum of its predecessors' sums
-  uint64_t pk = 0, pe = 0;
-  for (uint32_t q = t; q < tile; q += 256) {
-    const ulonglong2 v = tile_sum[q];
-    pk += v.x;
-    pe += v.y;
+  const bool last = tile == gridDim.x - 1;
+  // this tile's offset: the sum of its predecessors' sums (the last tile: and
+  // the totals of every tile)
+  uint64_t pk = 0, pe = 0, cnt = 0;
+  int64_t f = INT64_MAX, l = INT64_MIN, fx = INT64_MIN, ln = INT64_MAX;
+  for (uint32_t q = t; q < (last ? gridDim.x : tile); q += 256) {
+    const KeptTile v = tile_sum[q];
+    if (q < tile) {
+      pk += v.k;
+      pe += v.e;
+    }
+    cnt += v.cnt;
+    f = min(f, v.f);
+    l = max(l, v.l);
+    fx = max(fx, v.fx);
+    ln = min(ln, v.ln);
   }
   pk = block_reduce_256(pk, [](uint64_t x, uint64_t y) { return x + y; }, sh_c);
   __syncthreads();
   pe = block_reduce_256(pe, [](uint64_t x, uint64_t y) { return x + y; }, sh_c);
-  __shared__ uint64_t s_pk, s_pe;
   if (t == 0) {
     s_pk = pk;
     s_pe = pe;
@@ -300,27 +340,22 @@ __global__ void __launch_bounds__(256) k_kept_scatter_tiles(const uint8_t* kept,
     rk += s_wk[i];
     re += s_we[i];
   }
-  if (t == 255 && (uint64_t)tile * 1024 + 1024 >= n) {  // the last tile: totals
+  if (t == 255 && last) {  // the totals
     *n_kept_out = rk + sk;
     *e_total_out = re + se;
   }
-  uint64_t cnt = 0;
-  int64_t f = INT64_MAX, l = INT64_MIN, fx = INT64_MIN, ln = INT64_MAX;
 #pragma unroll
   for (int i = 0; i < 4; i++) {
     const uint64_t s = base + i;
     if (fk[i]) {
       kept_list[rk] = (uint32_t)s;
       eoff_k[rk] = re;
-      cnt += ncells[s];
-      f = min(f, sp_first[s]);
-      l = max(l, sp_last[s]);
-      fx = max(fx, sp_first[s]);
-      ln = min(ln, sp_last[s]);
     }
     rk += fk[i];
     re += fe[i];
   }
+  if (!last) return;
+  __syncthreads();
   cnt = block_reduce_256(cnt, [](uint64_t x, uint64_t y) { return x + y; }, sh_c);
   f = block_reduce_256(f, [](int64_t x, int64_t y) { return min(x, y); }, sh_f);
   l = block_reduce_256(l, [](int64_t x, int64_t y) { return max(x, y); }, sh_l);
@@ -329,11 +364,17 @@ __global__ void __launch_bounds__(256) k_kept_scatter_tiles(const uint8_t* kept,
   __syncthreads();
   ln = block_reduce_256(ln, [](int64_t x, int64_t y) { return min(x, y); }, sh_l);
   if (t == 0 && cnt) {
-    atomicAdd(n_input, (unsigned long long)cnt);
-    atomicMin(&bound[0], (unsigned long long)f);
-    atomicMax(&bound[1], (unsigned long long)l);
-    atomicMax(&bound[2], (unsigned long long)fx);
-    atomicMin(&bound[3], (unsigned long long)ln);
+    *n_input += cnt;
+    bound[0] = min(bound[0], (unsigned long long)f);
+    bound[1] = max(bound[1], (unsigned long long)l);
+    bound[2] = max(bound[2], (unsigned long long)fx);
+    bound[3] = min(bound[3], (unsigned long long)ln);
+  }
+  __syncthreads();
+  if (pub.dst && t < WAVE) {  // the call state, final here, to the host (wave 0)
+    __threadfence();
+    __builtin_amdgcn_wave_barrier();
+    host_publish(pub, pub_src);
   }
 }
 
