@@ -92,6 +92,7 @@ struct Slot {
   void* host_big = nullptr;         // grow-only pinned staging (group-by batches)
   size_t host_big_n = 0;
   hipEvent_t ev[10] = {};  // [8],[9] bracket the dominant kernel
+  int8_t ev_alias[10] = {-1, -1, -1, -1, -1, -1, -1, -1, -1, -1};  // "kernel" events: a start no kernel carried reads as this one (-1: none)
   bool time_reduce = false;  // the dominant kernel is k_reduce (direct path)
   uint32_t hot_kernel = 0;
   tsdbhip_timing timing = {};
@@ -189,15 +190,20 @@ static unsigned grid_for(uint64_t work, unsigned per_block, unsigned cap = 1u <<
 // hipEventRecord between kernels left the GPU idle ~5 us. "marker": events
 // recorded in the stream (hipEventRecord). "none": no events (timings 0).
 static thread_local hipEvent_t g_ev_pend = nullptr;
+static thread_local int g_ev_pend_i = -1;
 static inline hipEvent_t ev_take() {
   hipEvent_t e = g_ev_pend;
   g_ev_pend = nullptr;
+  g_ev_pend_i = -1;
   return e;
 }
 static void EV_START(Slot* ctx, int i) {
   if (ctx->opt.events == 0) {
-    if (g_ev_pend) HIPCHK(hipEventRecord(ev_take(), ctx->stream));  // (no kernel took the last one)
+    // (a start no kernel took reads as this one: both mark the next kernel's
+    // start, and a marker would cost a host call and a GPU-side gap)
+    if (g_ev_pend && g_ev_pend_i >= 0) ctx->ev_alias[g_ev_pend_i] = (int8_t)i;
     g_ev_pend = ctx->ev[i];
+    g_ev_pend_i = i;
   } else if (ctx->opt.events == 1) {
     HIPCHK(hipEventRecord(ctx->ev[i], ctx->stream));
   }
@@ -212,6 +218,8 @@ static void EV_START(Slot* ctx, int i) {
 #define LAUNCH_STOP(ev, k, g, b, sh, st, ...) hipExtLaunchKernelGGL(k, g, b, sh, st, ev_take(), ev, 0, ##__VA_ARGS__)
 static float ev_ms(Slot* ctx, int a, int b) {
   float ms = 0;
+  for (int n = 0; n < 10 && ctx->ev_alias[a] >= 0; n++) a = ctx->ev_alias[a];
+  for (int n = 0; n < 10 && ctx->ev_alias[b] >= 0; n++) b = ctx->ev_alias[b];
   if (ctx->opt.events == 2 || hipEventElapsedTime(&ms, ctx->ev[a], ctx->ev[b]) != hipSuccess) {
     (void)hipGetLastError();
     return ctx->opt.events == 2 ? 0.f : -1.f;
@@ -1428,6 +1436,8 @@ static int spangroup_run_once(Slot* ctx, const tsdbhip_sg_desc* d, tsdbhip_sg_ou
   bool tgd_used = false;
   const bool detail = ctx->opt.timing_detail;  // decode / grid event pairs
   g_ev_pend = nullptr;
+  g_ev_pend_i = -1;
+  std::memset(ctx->ev_alias, 0xff, sizeof ctx->ev_alias);
   EV_START(ctx, 0);
 
   // ---- assemble ----
@@ -2151,10 +2161,13 @@ static int spangroup_run_once(Slot* ctx, const tsdbhip_sg_desc* d, tsdbhip_sg_ou
       return r;
     };
     // the lockstep group: tiles of LS_TILE grid points x chunks of spans
+#ifndef LS_MIN_SPC
+#define LS_MIN_SPC 64  // fewest spans a lockstep chunk (the n_chunks x T partials the combine reads)
+#endif
     auto ls_reduce = [&](bool finalize) {
       const uint32_t n_tiles = (uint32_t)((T + LS_TILE - 1) / LS_TILE);
       uint64_t want = std::max<uint64_t>(1, 16384 / n_tiles);
-      want = std::min<uint64_t>(want, std::max<uint32_t>(1, n_kept / 64));
+      want = std::min<uint64_t>(want, std::max<uint32_t>(1, n_kept / LS_MIN_SPC));
       const uint32_t spc = (uint32_t)((n_kept + want - 1) / want);
       const uint32_t n_chunks = (n_kept + spc - 1) / spc;
       ReduceArgs r;
@@ -2831,6 +2844,8 @@ static int compact_rows(Slot* ctx, const tsdbhip_rows_desc* d, tsdbhip_rows_out*
     a.big_cells = scratch<uint64_t>(ctx, "c_cells", qext / 2 + R + 1);
     hipStream_t st = ctx->stream;
     g_ev_pend = nullptr;
+    g_ev_pend_i = -1;
+    std::memset(ctx->ev_alias, 0xff, sizeof ctx->ev_alias);
     if (ctx->opt.compact_tiles) {  // (every row through the LDS tiles: the A/B reference)
       HIPCHK(hipEventRecord(ctx->ev[8], st));
       HIPCHK(hipEventRecord(ctx->ev[4], st));

@@ -139,6 +139,7 @@ static int spangroup_run_batch(Slot* ctx, const tsdbhip_sg_desc* d, uint32_t G, 
     std::memcpy(ctx->host_small, &init, sizeof init);
     HIPCHK(hipMemcpyAsync(sm, ctx->host_small, sizeof init, hipMemcpyHostToDevice, st));
   }
+  std::memset(ctx->ev_alias, 0xff, sizeof ctx->ev_alias);  // (markers only here)
   HIPCHK(hipEventRecord(ctx->ev[0], st));
 
   // ---- assemble (every span of every group) ----
