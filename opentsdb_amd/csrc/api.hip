@@ -1221,6 +1221,22 @@ __global__ void __launch_bounds__(1024) k_assemble_small(AssembleArgs a, KeptArg
 // before the snapshot; bad.n_kept = 0: k_bad_index ran).
 // (the optimistic aligned-group finish: `done` null, or the call is over only
 // when *done; otherwise the state is snapshot for the host and left as it is)
+// The call state's snapshot into mapped host memory and, with `init`, its
+// reset: word by word over the block's threads, every thread of the block
+// calling (one thread copying the ~1 KB across PCIe took most of a 10-12 us
+// single-block launch)
+static_assert(sizeof(Small) % 8 == 0, "Small is copied in 8-byte words");
+DEVI void small_snap(Small* sm, Small* snap, const Small* init) {
+  constexpr uint32_t NW = sizeof(Small) / 8;
+  const volatile uint64_t* s = (const volatile uint64_t*)sm;
+  uint64_t* d = (uint64_t*)snap;
+  for (uint32_t i = threadIdx.x; i < NW; i += blockDim.x) d[i] = s[i];
+  if (!init) return;
+  __syncthreads();  // (every word read before any is reset)
+  const uint64_t* in = (const uint64_t*)init;
+  uint64_t* w = (uint64_t*)sm;
+  for (uint32_t i = threadIdx.x; i < NW; i += blockDim.x) w[i] = in[i];
+}
 __global__ void __launch_bounds__(256) k_call_end(Small* sm, Small* snap, Small init, uint32_t* bitmap,
                                                   const uint32_t* grid, uint64_t T, int64_t lo, BadArgs bad,
                                                   const uint32_t* done = nullptr) {
@@ -1234,7 +1250,7 @@ __global__ void __launch_bounds__(256) k_call_end(Small* sm, Small* snap, Small 
     }
     __syncthreads();
     if (!s_over) {
-      if (blockIdx.x == 0 && threadIdx.x == 0) *snap = *sm;
+      if (blockIdx.x == 0) small_snap(sm, snap, nullptr);
       return;
     }
     T = s_t;
@@ -1252,10 +1268,8 @@ __global__ void __launch_bounds__(256) k_call_end(Small* sm, Small* snap, Small 
         __threadfence();
       }
     }
-    if (threadIdx.x == 0) {
-      *snap = *sm;
-      *sm = init;
-    }
+    __syncthreads();  // (bad_at final)
+    small_snap(sm, snap, &init);
     __syncthreads();  // (the ranks above read the bitmap cleared below)
   }
   if (bitmap)
@@ -1318,7 +1332,7 @@ __global__ void __launch_bounds__(256) k_fap_finish_end(Small* sm, const int64_t
   }
   __syncthreads();
   if (!s_ok) {  // the group did not stand: the state stays for the usual path
-    if (t == 0) *snap = *sm;
+    small_snap(sm, snap, nullptr);
     return;
   }
   if (t < s_T) {
@@ -1329,12 +1343,9 @@ __global__ void __launch_bounds__(256) k_fap_finish_end(Small* sm, const int64_t
     finalize_one<AGG, MODE_INT, false>(f, t, a);
   }
   __syncthreads();
-  if (t == 0) {
-    sm->fap_done = 1;
-    __threadfence();
-    *snap = *sm;
-    *sm = init;
-  }
+  if (t == 0) sm->fap_done = 1;
+  __syncthreads();
+  small_snap(sm, snap, &init);
   __syncthreads();  // (the grid read below is this block's own)
   if (bitmap && t < s_T) bitmap[(uint64_t)((int64_t)grid[t] - lo) >> 5] = 0u;
 }
