@@ -1495,7 +1495,7 @@ static int spangroup_run_once(Slot* ctx, const tsdbhip_sg_desc* d, tsdbhip_sg_ou
       uint32_t* alist = scratch<uint32_t>(ctx, "asm_list", S);
       uint32_t* acount = &sm->cnt[0];
       LAUNCH(k_assemble_fast, dim3(grid_for(S, 256)), dim3(256), 0, st, a, alist, acount);
-      LAUNCH(k_assemble, dim3(grid_for(S, 4, 1024)), dim3(256), 0, st, a, (const uint32_t*)alist,
+      LAUNCH(k_assemble, dim3(grid_for(S, 4, 4096)), dim3(256), 0, st, a, (const uint32_t*)alist,
                          (const uint32_t*)acount);
       if (S <= KC_MAX) {
         LAUNCH(k_kept_compact, dim3(1), dim3(1024), 0, st, K);

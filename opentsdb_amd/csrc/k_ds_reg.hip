@@ -462,6 +462,15 @@ template <int OP>
 DEVI int64_t fap_rows_wave(const int64_t* rows, uint32_t r, uint32_t stride, uint32_t nrows) {
   const int lane = lane_id();
   int64_t acc = fap_neutral(OP);
+  // (8 rows in flight a wave: the single-block final reduce of ~250 rows is
+  // a chain of round trips)
+  for (; r + 7 * stride < nrows; r += 8 * stride) {
+    int64_t v[8];
+#pragma unroll
+    for (int u = 0; u < 8; u++) v[u] = rows[(uint64_t)(r + u * stride) * WAVE + lane];
+#pragma unroll
+    for (int u = 0; u < 8; u++) acc = fap_comb<OP>(acc, v[u]);
+  }
   for (; r + 3 * stride < nrows; r += 4 * stride) {
     const int64_t v0 = rows[(uint64_t)r * WAVE + lane], v1 = rows[(uint64_t)(r + stride) * WAVE + lane];
     const int64_t v2 = rows[(uint64_t)(r + 2 * stride) * WAVE + lane], v3 = rows[(uint64_t)(r + 3 * stride) * WAVE + lane];
