@@ -214,6 +214,10 @@ static void EV_START(Slot* ctx, int i) {
   do {                                                                                \
     if ((ctx)->opt.events == 1) HIPCHK(hipEventRecord((ctx)->ev[i], (ctx)->stream)); \
   } while (0)
+// The call's last event, a marker in every mode: its system-scope release
+// makes the call-end kernels' writes into mapped host memory (the state
+// snapshot, small results) visible to the host after the stream sync.
+#define EV_FINAL(ctx, i) HIPCHK(hipEventRecord((ctx)->ev[i], (ctx)->stream))
 #define LAUNCH(k, g, b, sh, st, ...) hipExtLaunchKernelGGL(k, g, b, sh, st, ev_take(), nullptr, 0, ##__VA_ARGS__)
 #define LAUNCH_STOP(ev, k, g, b, sh, st, ...) hipExtLaunchKernelGGL(k, g, b, sh, st, ev_take(), ev, 0, ##__VA_ARGS__)
 static float ev_ms(Slot* ctx, int a, int b) {
@@ -270,10 +274,14 @@ static Slot* slot_new(int device) {
     HIPCHK(hipHostMalloc((void**)&ctx->map_state, 8 * 520, hipHostMallocMapped | hipHostMallocCoherent));
     HIPCHK(hipHostGetDevicePointer((void**)&ctx->map_state_dev, ctx->map_state, 0));
     std::memset(ctx->map_state, 0, 8 * 520);
-    // (timing only: no system-scope fence, i.e. no L2 writeback / invalidate
-    // when an event is recorded; results reach the host through coherent
-    // mapped memory and stream syncs, never through these events)
-    for (auto& e : ctx->ev) HIPCHK(hipEventCreateWithFlags(&e, hipEventDisableSystemFence));
+    // Timing events inside a call: no system-scope fence (no L2 writeback /
+    // invalidate between kernels). The call's last events ([5] spangroup,
+    // [1] compaction) keep it: the call-end kernels write the state snapshot
+    // and small results into mapped host memory, and that release is what
+    // makes them visible to the host after the stream sync (without it a
+    // host read of the snapshot came back stale about once in five suites).
+    for (int i = 0; i < 10; i++)
+      HIPCHK(hipEventCreateWithFlags(&ctx->ev[i], (i == 5 || i == 1) ? hipEventDefault : hipEventDisableSystemFence));
   } catch (Fail&) {
     slot_free(ctx);
     throw;
@@ -1231,6 +1239,7 @@ DEVI void small_snap(Small* sm, Small* snap, const Small* init) {
   const volatile uint64_t* s = (const volatile uint64_t*)sm;
   uint64_t* d = (uint64_t*)snap;
   for (uint32_t i = threadIdx.x; i < NW; i += blockDim.x) d[i] = s[i];
+  __threadfence_system();  // (the snapshot's host writes complete before this kernel does)
   if (!init) return;
   __syncthreads();  // (every word read before any is reset)
   const uint64_t* in = (const uint64_t*)init;
@@ -1616,7 +1625,7 @@ static int spangroup_run_once(Slot* ctx, const tsdbhip_sg_desc* d, tsdbhip_sg_ou
     if (!fast) {
       // (spans of many short rows, C4: a block per span decodes its rows in
       // parallel; else a wave per span walks them)
-      if (interval == 0 && R >= 64ull * n_kept) LAUNCH(k_decode_rows, dim3(n_kept), dim3(256), 0, st, da);
+      if (interval == 0 && R >= 64ull * n_kept) LAUNCH(k_decode_rows, dim3(n_kept), dim3(DR_THREADS), 0, st, da);
       else if (interval == 0) LAUNCH(k_decode_nods, dim3(blocks), dim3(256), 0, st, da);
       else launch_agg<LaunchGeneralDs>(ds_agg, ctx, blocks, da);
       HIPCHK(hipEventRecord(ctx->ev[9], st));
@@ -1847,15 +1856,15 @@ static int spangroup_run_once(Slot* ctx, const tsdbhip_sg_desc* d, tsdbhip_sg_ou
       Small* snap = (Small*)ctx->map_out_dev;
       const Small ini = small_init();
       if (agg == TSDBHIP_AGG_MIN)
-        LAUNCH_STOP(EV_STOP_K(ctx, 5), k_fap_finish_end<1>, dim3(1), dim3(256), 0, st, sm, (const int64_t*)o_pi, (const uint32_t*)o_pc, fo, (int32_t)sharded, um, snap, ini, bitmap, (const uint32_t*)gridv_o, lo);
+        LAUNCH(k_fap_finish_end<1>, dim3(1), dim3(256), 0, st, sm, (const int64_t*)o_pi, (const uint32_t*)o_pc, fo, (int32_t)sharded, um, snap, ini, bitmap, (const uint32_t*)gridv_o, lo);
       else if (agg == TSDBHIP_AGG_MAX)
-        LAUNCH_STOP(EV_STOP_K(ctx, 5), k_fap_finish_end<2>, dim3(1), dim3(256), 0, st, sm, (const int64_t*)o_pi, (const uint32_t*)o_pc, fo, (int32_t)sharded, um, snap, ini, bitmap, (const uint32_t*)gridv_o, lo);
+        LAUNCH(k_fap_finish_end<2>, dim3(1), dim3(256), 0, st, sm, (const int64_t*)o_pi, (const uint32_t*)o_pc, fo, (int32_t)sharded, um, snap, ini, bitmap, (const uint32_t*)gridv_o, lo);
       else if (agg == TSDBHIP_AGG_AVG)
-        LAUNCH_STOP(EV_STOP_K(ctx, 5), k_fap_finish_end<3>, dim3(1), dim3(256), 0, st, sm, (const int64_t*)o_pi, (const uint32_t*)o_pc, fo, (int32_t)sharded, um, snap, ini, bitmap, (const uint32_t*)gridv_o, lo);
+        LAUNCH(k_fap_finish_end<3>, dim3(1), dim3(256), 0, st, sm, (const int64_t*)o_pi, (const uint32_t*)o_pc, fo, (int32_t)sharded, um, snap, ini, bitmap, (const uint32_t*)gridv_o, lo);
       else
-        LAUNCH_STOP(EV_STOP_K(ctx, 5), k_fap_finish_end<0>, dim3(1), dim3(256), 0, st, sm, (const int64_t*)o_pi, (const uint32_t*)o_pc, fo, (int32_t)sharded, um, snap, ini, bitmap, (const uint32_t*)gridv_o, lo);
+        LAUNCH(k_fap_finish_end<0>, dim3(1), dim3(256), 0, st, sm, (const int64_t*)o_pi, (const uint32_t*)o_pc, fo, (int32_t)sharded, um, snap, ini, bitmap, (const uint32_t*)gridv_o, lo);
     }
-    EV_STOP_M(ctx, 5);
+    EV_FINAL(ctx, 5);
     HIPCHK(hipStreamSynchronize(st));
     std::memcpy(&h, ctx->map_out, sizeof h);
     if (h.fap_done) {  // the call is over (state reset, bitmap clear)
@@ -2355,10 +2364,10 @@ static int spangroup_run_once(Slot* ctx, const tsdbhip_sg_desc* d, tsdbhip_sg_ou
     X->group_end(ctx);
   }
   // ---- end of call: snapshot + reset of the call state, bitmap cleared ----
-  LAUNCH_STOP(EV_STOP_K(ctx, 5), k_call_end, dim3(bad_at_end ? 1u : grid_for(T, 256, 1024)), dim3(256), 0, st, sm,
+  LAUNCH(k_call_end, dim3(bad_at_end ? 1u : grid_for(T, 256, 1024)), dim3(256), 0, st, sm,
               (Small*)ctx->map_out_dev, small_init(), bitmap, (const uint32_t*)gridv, T, lo, bad_at_end ? bad : BadArgs{},
               (const uint32_t*)nullptr);
-  EV_STOP_M(ctx, 5);
+  EV_FINAL(ctx, 5);
   HIPCHK(hipStreamSynchronize(st));  // (the header and small results are already in host memory)
   const uint8_t* hb = ctx->map_out;
   std::memcpy(&h, hb, sizeof h);
@@ -2883,12 +2892,10 @@ static int compact_rows(Slot* ctx, const tsdbhip_rows_desc* d, tsdbhip_rows_out*
     }
     HIPCHK(hipGetLastError());
     LAUNCH(k_compact_complex<true>, dim3(1024), dim3(256), 0, ctx->stream, a);
-    LAUNCH_STOP(a.out_write ? nullptr : EV_STOP_K(ctx, 1), k_compact_complex<false>, dim3(256), dim3(256), 0,
-                ctx->stream, a);
-    if (a.out_write)
-      LAUNCH_STOP(EV_STOP_K(ctx, 1), k_compact_dups, dim3(grid_for(R, 4 * WAVE, 4096)), dim3(256), 0, ctx->stream, a);
+    LAUNCH(k_compact_complex<false>, dim3(256), dim3(256), 0, ctx->stream, a);
+    if (a.out_write) LAUNCH(k_compact_dups, dim3(grid_for(R, 4 * WAVE, 4096)), dim3(256), 0, ctx->stream, a);
     HIPCHK(hipGetLastError());
-    EV_STOP_M(ctx, 1);
+    EV_FINAL(ctx, 1);
     uint32_t cnt[4];
     readback(ctx, cnt, a.counters, sizeof cnt);
     if (cnt[2]) {

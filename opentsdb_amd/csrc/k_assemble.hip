@@ -338,20 +338,38 @@ DEVI bool assemble_walk_pairs(const AssembleArgs& a, uint32_t s, uint64_t r0, ui
   bool pm1 = false;                      // row r-1 merged
   uint32_t cell = 0;
   int64_t first_ts = -1, last_all = 0;
+  // the next batch's row fields are loaded while this batch's qualifiers are
+  // (the walk is a chain of batches, two dependent loads each otherwise)
+  uint32_t n_n = 0, vl_n = 0;
+  int64_t base_n = 0;
+  uint64_t qo_n = 0;
+  auto load_rows = [&](uint64_t rb) {
+    const uint64_t r = rb + lane;
+    n_n = vl_n = 0;
+    base_n = 0;
+    qo_n = 0;
+    if (r < r1) {
+      n_n = a.row_ncells[r];
+      vl_n = a.row_val_len[r];
+      base_n = a.row_base[r];
+      qo_n = a.row_qual_off[r];
+    }
+  };
+  load_rows(r0);
   for (uint64_t rb = r0; rb < r1; rb += WAVE) {
     const uint64_t r = rb + lane;
     const bool valid = r < r1;
-    uint32_t n = 0, vb = 0;
-    int64_t base = 0, first = 0, last = 0;
-    if (valid) {
-      n = a.row_ncells[r];
-      base = a.row_base[r];
-      if (n > 0) {
-        first = base + (load_qual(a.qual, a.row_qual_off[r]) >> 4);
-        last = base + (load_qual(a.qual, a.row_qual_off[r] + 2ull * (n - 1)) >> 4);
-        vb = row_value_bytes(a, r);
-      }
+    const uint32_t n = n_n;
+    const int64_t base = base_n;
+    const uint64_t qo = qo_n;
+    // (row_value_bytes: without the compacted meta byte, CompactionQueue.java:469-470)
+    const uint32_t vb = valid && n > 0 ? (n > 1 && vl_n > 0 ? vl_n - 1 : vl_n) : 0u;
+    int64_t first = 0, last = 0;
+    if (valid && n > 0) {
+      first = base + (load_qual(a.qual, qo) >> 4);
+      last = base + (load_qual(a.qual, qo + 2ull * (n - 1)) >> 4);
     }
+    if (rb + WAVE < r1) load_rows(rb + WAVE);
     if (ballot(valid && n == 0)) return false;
     const uint32_t nb = (uint32_t)min((uint64_t)WAVE, r1 - rb);
     int64_t b1 = (int64_t)shfl_up_u64((uint64_t)base, 1);

@@ -229,9 +229,13 @@ __device__ void span_nods_general(const DecodeArgs& a, uint32_t k) {
 // walk. RowSeq.java:360-497 (ts = base + delta, values at the running
 // offset of the row), :194-226 (widths); unsorted cells: E_UNSORTED, as the
 // walk raises it.
-__global__ void __launch_bounds__(256) k_decode_rows(DecodeArgs a) {
-  __shared__ unsigned long long s_bad[4];
-  __shared__ uint32_t s_f[4], s_i[4], s_uns[4];
+#ifndef DR_THREADS
+#define DR_THREADS 512  // threads a span (C4 step: 256 9.98 ms, 512 9.93, 1024 9.96)
+#endif
+__global__ void __launch_bounds__(DR_THREADS) k_decode_rows(DecodeArgs a) {
+  constexpr uint32_t NW = DR_THREADS / WAVE;
+  __shared__ unsigned long long s_bad[NW];
+  __shared__ uint32_t s_f[NW], s_i[NW], s_uns[NW];
   const uint32_t k = blockIdx.x;
   if (k >= a.n_kept) return;
   const uint32_t s = a.kept[k];
@@ -245,7 +249,7 @@ __global__ void __launch_bounds__(256) k_decode_rows(DecodeArgs a) {
   const uint64_t eo = a.e_off[k];
   unsigned long long bad = ~0ull;
   bool anyf = false, anyi = false, uns = false;
-  for (uint64_t r = r0 + t; r < r1; r += 256) {
+  for (uint64_t r = r0 + t; r < r1; r += DR_THREADS) {
     if (!a.row_ok[r]) continue;
     const uint32_t n = a.row_ncells[r], c0 = a.row_cell0[r];
     const uint64_t qo = a.row_qual_off[r], vo = a.row_val_off[r];
@@ -272,7 +276,7 @@ __global__ void __launch_bounds__(256) k_decode_rows(DecodeArgs a) {
   __syncthreads();  // (every E point of the span written by this block)
   __threadfence_block();
   // a row's first cell against the cell before it (the previous accepted row's last)
-  for (uint64_t r = r0 + t; r < r1; r += 256) {
+  for (uint64_t r = r0 + t; r < r1; r += DR_THREADS) {
     if (!a.row_ok[r] || a.row_ncells[r] == 0) continue;
     const uint32_t c0 = a.row_cell0[r];
     if (c0 > 0 && a.e_ts[eo + c0] <= a.e_ts[eo + c0 - 1]) uns = true;
@@ -287,12 +291,19 @@ __global__ void __launch_bounds__(256) k_decode_rows(DecodeArgs a) {
   }
   __syncthreads();
   if (t == 0) {
-    const unsigned long long b = min(min(s_bad[0], s_bad[1]), min(s_bad[2], s_bad[3]));
+    unsigned long long b = ~0ull;
+    uint32_t fu = 0, ff = 0, fi = 0;
+    for (uint32_t i = 0; i < NW; i++) {
+      b = min(b, s_bad[i]);
+      fu |= s_uns[i];
+      ff |= s_f[i];
+      fi |= s_i[i];
+    }
     a.e_len[k] = a.sp_ncells[s];
     a.e_bad[k] = b == ~0ull ? -1 : (int64_t)b;
-    if (s_uns[0] | s_uns[1] | s_uns[2] | s_uns[3]) err_raise(a.err, 2, a.span0 + s, -8 /*E_UNSORTED*/);
-    if (s_f[0] | s_f[1] | s_f[2] | s_f[3]) atomicOr(&a.gflags[0], 1u);
-    if (s_i[0] | s_i[1] | s_i[2] | s_i[3]) atomicOr(&a.gflags[1], 1u);
+    if (fu) err_raise(a.err, 2, a.span0 + s, -8 /*E_UNSORTED*/);
+    if (ff) atomicOr(&a.gflags[0], 1u);
+    if (fi) atomicOr(&a.gflags[1], 1u);
   }
 }
 
