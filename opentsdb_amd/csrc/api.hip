@@ -65,6 +65,7 @@ struct Options {
   bool aligned_group = true;   // "aligned_group": k_ds_reg's aligned-group reduction may be tried
   int lockstep = 1;            // "lockstep": "off" (0), "on" (1: groups big enough), "always" (2)
   bool compact_tiles = false;  // "compact": "tiles" sends every row through k_compact_tiles
+  bool compact_rows_vals = true;  // "compact_vals": "rows" (a quarter wave per row) or "flat" (runs of rows)
   bool timing_detail = false;  // "timing_detail": decode / grid event pairs (tsdbhip_timing)
   bool check_clean = false;    // "check_clean": verify the zero-on-entry invariants (stderr)
   int events = 0;              // "events": timing events on kernel launches (0), marker packets (1), none (2)
@@ -549,6 +550,10 @@ extern "C" int tsdbhip_set_option(tsdbhip_ctx* ctx, const char* name, const char
     o.compact_tiles = v == "tiles";
   } else if (n == "timing_detail") ok = on_off(o.timing_detail);
   else if (n == "check_clean") ok = on_off(o.check_clean);
+  else if (n == "compact_vals") {
+    ok = v == "flat" || v == "rows";
+    o.compact_rows_vals = v == "rows";
+  }
   else if (n == "events") {
     static const char* names[] = {"kernel", "marker", "none"};
     ok = false;
@@ -2885,7 +2890,10 @@ static int compact_rows(Slot* ctx, const tsdbhip_rows_desc* d, tsdbhip_rows_out*
       EV_STOP_M(ctx, 4);
       LAUNCH_STOP(EV_STOP_K(ctx, 2), k_compact_classify, dim3(grid_for(R, 16, 1u << 16)), dim3(256), 0, st, a);
       EV_STOP_M(ctx, 2);
-      LAUNCH_STOP(EV_STOP_K(ctx, 9), k_compact_vals, dim3(grid_for(R, 16, 1u << 16)), dim3(256), 0, st, a);
+      if (ctx->opt.compact_rows_vals)
+        LAUNCH_STOP(EV_STOP_K(ctx, 9), k_compact_vals, dim3(grid_for(R, 16, 1u << 16)), dim3(256), 0, st, a);
+      else
+        LAUNCH_STOP(EV_STOP_K(ctx, 9), k_compact_vals_flat, dim3(grid_for(R, CV_ROWS, 1u << 16)), dim3(256), 0, st, a);
       EV_STOP_M(ctx, 9);
       LAUNCH_STOP(EV_STOP_K(ctx, 3), k_compact_rows, dim3(grid_for(R, CR_RANGE, 1u << 14)), dim3(256), 0, st, a);
       EV_STOP_M(ctx, 3);

@@ -1291,6 +1291,50 @@ DEVI CvRow cv_row(const CompactArgs& a, uint64_t r, uint64_t V0) {
 }
 DEVI uint64_t cv_meta(const CvRow& w) { return w.e - 1 - 4ull * ((w.h0 != ~0u) + (w.h1 != ~0u)); }
 
+// One aligned 16-B output chunk c (absolute address) whose first byte lies in
+// row r (w; n = row r + 1, when there is one): one source, one hole or the
+// row end inside (two sources selected by byte), or byte by byte.
+DEVI void cv_chunk(const CompactArgs& a, uint64_t r, const CvRow& w, const CvRow& n, uintptr_t c,
+                   uintptr_t ov_abs, uint64_t V0, bool act) {
+  const uint64_t m = cv_meta(w);
+  const uint64_t o = c - ov_abs, y0 = o - w.s, x = w.in + y0;
+  const uint64_t xa = x + 4 * ((w.h0 <= y0) + (w.h1 <= y0));
+  const bool in0 = w.h0 > y0 && w.h0 < y0 + 16, in1 = w.h1 > y0 && w.h1 < y0 + 16;  // holes inside
+  // one source, or one hole inside (from it on, 4 bytes further down the input)
+  const bool c1 = o + 16 <= m && !(in0 && in1);
+  // the meta byte at m - o; then the unused bytes; then the next row (one
+  // byte further down the input; 4 more when its first KV is a legacy
+  // float), which must have no hole and no end inside the chunk
+  uint64_t xb = x - 1;
+  bool ok = true;
+  if (w.e < o + 16) {
+    const uint64_t L = o + 16 - w.e;
+    ok = r + 1 < a.n_rows && n.ok && !(n.h0 > 0 && n.h0 < L) && !(n.h1 > 0 && n.h1 < L) && cv_meta(n) >= o + 16;
+    if (n.h0 == 0) xb += 4;
+  }
+  const bool c2 = !c1 && m < o + 16 && !in0 && !in1 && ok && xb + 1 != 0;  // (B inside the buffer)
+  if (act && (c1 || c2)) {
+    const uint64_t xB = c1 ? xa + 4 : xb;
+    const int pos = c1 ? (in0 ? (int)(w.h0 - y0) : in1 ? (int)(w.h1 - y0) : 16) : (int)(m - o);
+    *(uint4*)c = cq_funnel(ld16_any(a.val, xa), ld16_any(a.val, xB), pos, !c1);
+  } else if (act) {  // byte by byte, walking the rows (two boundaries in the chunk)
+    CvRow u = w;
+    uint64_t ru = r;
+    for (int b = 0; b < 16; b++) {
+      const uint64_t ob = o + b;
+      while (ob >= u.e && u.ok) {
+        if (++ru >= a.n_rows) u.ok = false;
+        else u = cv_row(a, ru, V0);
+      }
+      if (!u.ok) break;
+      const uint64_t mu = cv_meta(u);
+      if (ob > mu) continue;  // (unused)
+      const uint64_t y = ob - u.s;
+      *(uint8_t*)(c + b) = ob == mu ? (uint8_t)0 : a.val[u.in + y + 4 * ((u.h0 <= y) + (u.h1 <= y))];
+    }
+  }
+}
+
 __global__ void __launch_bounds__(256) k_compact_vals(CompactArgs a) {
   const int lane = lane_id(), sub = lane & 15, qtr = lane >> 4;
   const uint64_t nw = (uint64_t)gridDim.x * 4;
@@ -1317,42 +1361,64 @@ __global__ void __launch_bounds__(256) k_compact_vals(CompactArgs a) {
       const uint64_t k = i0 + sub;
       const bool act = k < nch;
       const uintptr_t c = c0 + 16 * k;
-      const uint64_t o = c - ov_abs, y0 = o - w.s, x = w.in + y0;
-      const uint64_t xa = x + 4 * ((w.h0 <= y0) + (w.h1 <= y0));
-      const bool in0 = w.h0 > y0 && w.h0 < y0 + 16, in1 = w.h1 > y0 && w.h1 < y0 + 16;  // holes inside
-      // one source, or one hole inside (from it on, 4 bytes further down the input)
-      const bool c1 = o + 16 <= m && !(in0 && in1);
-      // the meta byte at m - o; then the unused bytes; then the next row (one
-      // byte further down the input; 4 more when its first KV is a legacy
-      // float), which must have no hole and no end inside the chunk
-      uint64_t xb = x - 1;
-      bool ok = true;
-      if (w.e < o + 16) {
-        const uint64_t L = o + 16 - w.e;
-        ok = r + 1 < a.n_rows && n.ok && !(n.h0 > 0 && n.h0 < L) && !(n.h1 > 0 && n.h1 < L) && cv_meta(n) >= o + 16;
-        if (n.h0 == 0) xb += 4;
+      cv_chunk(a, r, w, n, c, ov_abs, V0, act);
+    }
+  }
+}
+
+// The same copy, flat: a block per run of CV_ROWS rows writes the aligned
+// 16-B chunks whose first byte lies in those rows (their output is one
+// contiguous range), a thread per chunk, its row found by a binary search
+// over the rows' output starts in LDS — instead of a quarter wave per row
+// looping over its ~19 chunks (two rounds, the second mostly idle lanes).
+// A run holding a row with offsets out of bounds goes row by row.
+#ifndef CV_ROWS
+#define CV_ROWS 64
+#endif
+__global__ void __launch_bounds__(256) k_compact_vals_flat(CompactArgs a) {
+  __shared__ CvRow s_w[CV_ROWS + 1];
+  __shared__ uint32_t s_bad;
+  const uint64_t V0 = a.row_val_off[0];
+  const uintptr_t ov_abs = (uintptr_t)a.ov;
+  const uint64_t nrun = (a.n_rows + CV_ROWS - 1) / CV_ROWS;
+  const uint32_t t = threadIdx.x;
+  for (uint64_t run = blockIdx.x; run < nrun; run += gridDim.x) {
+    const uint64_t r0 = run * CV_ROWS;
+    const uint32_t nr = (uint32_t)min((uint64_t)CV_ROWS, a.n_rows - r0);
+    __syncthreads();  // (the previous run's rows consumed)
+    if (t == 0) s_bad = 0;
+    __syncthreads();
+    if (t <= nr && r0 + t < a.n_rows) {  // the run's rows and the one after it
+      const CvRow w = cv_row(a, r0 + t, V0);
+      s_w[t] = w;
+      if (t < nr && !w.ok) s_bad = 1;
+    }
+    __syncthreads();
+    if (s_bad) {  // row by row: a wave a row, a lane a chunk
+      for (uint32_t i = t / WAVE; i < nr; i += 256 / WAVE) {
+        const CvRow w = s_w[i];
+        if (!w.ok) continue;
+        CvRow n = {};
+        if (r0 + i + 1 < a.n_rows) n = s_w[i + 1];
+        const uintptr_t c0 = (ov_abs + w.s + 15) & ~(uintptr_t)15;
+        const uint64_t nch = ov_abs + w.e > c0 ? (ov_abs + w.e - c0 + 15) / 16 : 0;
+        for (uint64_t k = lane_id(); k < nch; k += WAVE) cv_chunk(a, r0 + i, w, n, c0 + 16 * k, ov_abs, V0, true);
       }
-      const bool c2 = !c1 && m < o + 16 && !in0 && !in1 && ok && xb + 1 != 0;  // (B inside the buffer)
-      if (act && (c1 || c2)) {
-        const uint64_t xB = c1 ? xa + 4 : xb;
-        const int pos = c1 ? (in0 ? (int)(w.h0 - y0) : in1 ? (int)(w.h1 - y0) : 16) : (int)(m - o);
-        *(uint4*)c = cq_funnel(ld16_any(a.val, xa), ld16_any(a.val, xB), pos, !c1);
-      } else if (act) {  // byte by byte, walking the rows (two boundaries in the chunk)
-        CvRow u = w;
-        uint64_t ru = r;
-        for (int b = 0; b < 16; b++) {
-          const uint64_t ob = o + b;
-          while (ob >= u.e && u.ok) {
-            if (++ru >= a.n_rows) u.ok = false;
-            else u = cv_row(a, ru, V0);
-          }
-          if (!u.ok) break;
-          const uint64_t mu = cv_meta(u);
-          if (ob > mu) continue;  // (unused)
-          const uint64_t y = ob - u.s;
-          *(uint8_t*)(c + b) = ob == mu ? (uint8_t)0 : a.val[u.in + y + 4 * ((u.h0 <= y) + (u.h1 <= y))];
-        }
+      continue;
+    }
+    // every row of the run in bounds: consecutive rows' output ranges abut
+    const uintptr_t cb = (ov_abs + s_w[0].s + 15) & ~(uintptr_t)15;
+    const uintptr_t ce = ov_abs + s_w[nr - 1].e;
+    for (uintptr_t c = cb + 16ull * t; c < ce; c += 16ull * 256) {
+      const uint64_t o = c - ov_abs;
+      uint32_t lo = 0, hi = nr - 1;  // the last row whose output starts at or before o
+      while (lo < hi) {
+        const uint32_t mid = (lo + hi + 1) >> 1;
+        if (s_w[mid].s <= o) lo = mid; else hi = mid - 1;
       }
+      CvRow n = {};
+      if (r0 + lo + 1 < a.n_rows) n = s_w[lo + 1];
+      cv_chunk(a, r0 + lo, s_w[lo], n, c, ov_abs, V0, true);
     }
   }
 }
