@@ -3,9 +3,11 @@ the reference's TestCompactionQueue vectors (test_oracle.py) and an
 independent Python restatement on edge cases and random C5-style batches
 (CPU), then the GPU path (tsdbhip_compact_rows) against the oracle,
 byte-exact (-m gpu)."""
+import os
 import struct
 
 import numpy as np
+
 import pytest
 
 from helpers import with_option
@@ -190,11 +192,16 @@ def test_pack_rejects_long_kv():
 
 
 # ------------------------------------------------------------------ GPU ----
-@pytest.fixture(autouse=True, params=["plain", "tiles"])
+# (TSDBHIP_TEST_FLAT=1: also the value copy over runs of rows, option
+# compact_vals=flat, while it is opt-in)
+@pytest.fixture(autouse=True, params=["plain", "tiles"] + (["plain_flat"] if os.environ.get("TSDBHIP_TEST_FLAT") else []))
 def compact_path(request):
     """every GPU test twice: the plain-row path (classify / shifted copy /
     LDS row kernel, the default) and all rows through the LDS tiles"""
-    yield from with_option(request, "compact", "tiles" if request.param == "tiles" else "auto", "auto")
+    if request.param == "plain_flat":
+        yield from with_option(request, "compact_vals", "flat", "rows")
+    else:
+        yield from with_option(request, "compact", "tiles" if request.param == "tiles" else "auto", "auto")
 
 
 def assert_same(g, o):
