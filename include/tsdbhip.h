@@ -316,9 +316,9 @@ int         tsdbhip_open_devices(const int32_t* devices, uint32_t n, tsdbhip_ctx
  *                   "on" for groups of >= 2048 lockstep waves (and sharded
  *                   groups), "always" for any group
  *   "compact"       "auto" | "tiles"  (tiles: every row through k_compact_tiles)
- *   "compact_vals"  "rows" | "flat"  plain rows' value copy: a quarter wave
- *                   per row (default), or a block per run of rows with a
- *                   thread per 16-B chunk
+ *   "compact_vals"  "flat" | "rows"  plain rows' value copy: a block per run
+ *                   of rows with a thread per 16-B chunk (default), or a
+ *                   quarter wave per row
  *   "timing_detail" "on" | "off"   decode / grid event pairs in tsdbhip_timing
  *   "check_clean"   "on" | "off"   check the zero-on-entry invariants (stderr)
  *   "events"        "kernel" | "marker" | "none"   how tsdbhip_timing is measured:

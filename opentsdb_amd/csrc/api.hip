@@ -65,7 +65,7 @@ struct Options {
   bool aligned_group = true;   // "aligned_group": k_ds_reg's aligned-group reduction may be tried
   int lockstep = 1;            // "lockstep": "off" (0), "on" (1: groups big enough), "always" (2)
   bool compact_tiles = false;  // "compact": "tiles" sends every row through k_compact_tiles
-  bool compact_rows_vals = true;  // "compact_vals": "rows" (a quarter wave per row) or "flat" (runs of rows)
+  bool compact_rows_vals = false;  // "compact_vals": "flat" (runs of rows) or "rows" (a quarter wave per row)
   bool timing_detail = false;  // "timing_detail": decode / grid event pairs (tsdbhip_timing)
   bool check_clean = false;    // "check_clean": verify the zero-on-entry invariants (stderr)
   int events = 0;              // "events": timing events on kernel launches (0), marker packets (1), none (2)

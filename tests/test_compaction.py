@@ -3,7 +3,6 @@ the reference's TestCompactionQueue vectors (test_oracle.py) and an
 independent Python restatement on edge cases and random C5-style batches
 (CPU), then the GPU path (tsdbhip_compact_rows) against the oracle,
 byte-exact (-m gpu)."""
-import os
 import struct
 
 import numpy as np
@@ -192,14 +191,14 @@ def test_pack_rejects_long_kv():
 
 
 # ------------------------------------------------------------------ GPU ----
-# (TSDBHIP_TEST_FLAT=1: also the value copy over runs of rows, option
-# compact_vals=flat, while it is opt-in)
-@pytest.fixture(autouse=True, params=["plain", "tiles"] + (["plain_flat"] if os.environ.get("TSDBHIP_TEST_FLAT") else []))
+@pytest.fixture(autouse=True, params=["plain", "plain_rowvals", "tiles"])
 def compact_path(request):
-    """every GPU test twice: the plain-row path (classify / shifted copy /
-    LDS row kernel, the default) and all rows through the LDS tiles"""
-    if request.param == "plain_flat":
-        yield from with_option(request, "compact_vals", "flat", "rows")
+    """every GPU test three times: the plain-row path (classify / shifted copy
+    / LDS row kernel, the default, its value copy flat over runs of rows),
+    the same with the value copy a quarter wave per row, and all rows through
+    the LDS tiles"""
+    if request.param == "plain_rowvals":
+        yield from with_option(request, "compact_vals", "rows", "flat")
     else:
         yield from with_option(request, "compact", "tiles" if request.param == "tiles" else "auto", "auto")
 
