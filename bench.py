@@ -389,8 +389,8 @@ def bench_c5(args):
     hot_ms = float(np.mean(hot))
     achieved = alg_all / (max(call_ms, 1e-9) * 1e-3) / 1e9
     kname = "tsdbhip_compact_rows (whole call)"
-    call_kernels = ("k_compact_quals+k_compact_classify+k_compact_vals+k_compact_rows+k_compact_complex"
-                    "+k_compact_dups")
+    call_kernels = ("k_compact_quals+k_compact_classify+k_compact_vals+k_compact_vals_flat+k_compact_rows"
+                    "+k_compact_complex+k_compact_dups")
     traffic, traffic_src = pmc_traffic("c5", call_kernels, 1)
     res = {
         "metric": "raw cells/sec compacted (CompactionQueue.compact) + % HBM roofline, 1 MI355X",
