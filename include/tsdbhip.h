@@ -165,7 +165,9 @@ typedef struct tsdbhip_timing {
   uint64_t n_grid;          /* |G|                                           */
   uint64_t n_emitted;       /* Σ|E_s| (points after downsampling)           */
   uint32_t paths;           /* TSDBHIP_PATH_* bits: which variants ran (ABI v5) */
-  uint32_t reserved;
+  uint32_t late_stamp;      /* 1: the call-end stamp (the host's proof that the
+                               snapshot and results are this call's) arrived
+                               only after the stream sync; summed in totals */
   uint64_t x_bytes;         /* sharded calls: bytes this rank received in the
                                call's collectives (ABI v6)                  */
 } tsdbhip_timing;

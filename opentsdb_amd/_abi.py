@@ -110,7 +110,7 @@ class Timing(C.Structure):
         ("n_grid", C.c_uint64),
         ("n_emitted", C.c_uint64),
         ("paths", C.c_uint32),
-        ("reserved", C.c_uint32),
+        ("late_stamp", C.c_uint32),
         ("x_bytes", C.c_uint64),
     ]
 

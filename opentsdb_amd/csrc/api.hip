@@ -22,6 +22,7 @@
 #include <map>
 #include <memory>
 #include <mutex>
+#include <chrono>
 #include <string>
 #include <thread>
 #include <vector>
@@ -76,6 +77,10 @@ struct Options {
 // each on its own stream with its own scratch (the reference's Netty workers
 // and gnuplot pool call SpanGroup concurrently, GraphHandler.java:182,285).
 struct Xchg;
+// The mapped output block's header: the call-state snapshot (Small), the
+// call's end stamp in its last word (small_snap / check_stamp)
+constexpr size_t OUT_HDR = 1024;
+
 struct Slot {
   int device = 0;
   hipStream_t stream = nullptr;
@@ -87,6 +92,7 @@ struct Slot {
   uint64_t* map_state = nullptr;  // [0, 511]: state words, [512]: flag
   uint64_t* map_state_dev = nullptr;
   uint64_t pub_seq = 0;
+  uint32_t timing_late = 0;  // this call's end stamp arrived after the stream sync (check_stamp)
   uint8_t* map_out = nullptr;
   uint8_t* map_out_dev = nullptr;
   size_t map_out_n = 0;
@@ -307,6 +313,7 @@ static void timing_add(tsdbhip_ctx* c, const tsdbhip_timing& t) {  // (c->mu hel
   c->sum.n_emitted += t.n_emitted;
   c->sum.paths |= t.paths;
   c->sum.x_bytes += t.x_bytes;
+  c->sum.late_stamp += t.late_stamp;
   c->n_sum++;
 }
 
@@ -332,6 +339,10 @@ struct Lease {
     }
     s->x = nullptr;
     s->want_output = true;
+    // (no start event pending from an earlier call on this thread that threw
+    // between EV_START and its LAUNCH: ADVICE r4)
+    g_ev_pend = nullptr;
+    g_ev_pend_i = -1;
     {
       std::lock_guard<std::mutex> lk(c->mu);
       s->opt = c->opt;
@@ -581,6 +592,12 @@ extern "C" int tsdbhip_ranks(tsdbhip_ctx* ctx) {
   return ctx->multi ? ctx->multi->n : 1;
 }
 
+// The registered host ranges [p, p + n): the in-kernel finalize writes a long
+// result through a mapped pointer only into a range that holds all of it
+// (mapped_dev_ptr).
+static std::mutex g_reg_mu;
+static std::map<uintptr_t, size_t> g_reg;
+
 extern "C" int tsdbhip_host_register(tsdbhip_ctx* ctx, void* p, size_t n) {
   if (!ctx || !p || !n) return TSDBHIP_E_INVALID_ARG;
   try {
@@ -591,6 +608,8 @@ extern "C" int tsdbhip_host_register(tsdbhip_ctx* ctx, void* p, size_t n) {
   } catch (Fail& f) {
     return f.code;
   }
+  std::lock_guard<std::mutex> lk(g_reg_mu);
+  g_reg[(uintptr_t)p] = n;
   return TSDBHIP_OK;
 }
 
@@ -602,6 +621,8 @@ extern "C" int tsdbhip_host_unregister(tsdbhip_ctx* ctx, void* p) {
   } catch (Fail& f) {
     return f.code;
   }
+  std::lock_guard<std::mutex> lk(g_reg_mu);
+  g_reg.erase((uintptr_t)p);
   return TSDBHIP_OK;
 }
 
@@ -728,6 +749,27 @@ static void wait_pub(Slot* ctx, const HostPub& p, void* host, size_t bytes) {
   std::memcpy(host, ctx->map_state, bytes);
 }
 
+// The call-end stamp (small_snap) after the stream sync: the snapshot, and
+// every result the call wrote into host memory, are this call's iff it reads
+// `seq`. A stamp that is late (the stream has drained, so the writes are on
+// their way) is waited for briefly; one that never comes is an error, never a
+// stale result (the red test_nan_in_a_long_grid run).
+static void check_stamp(Slot* ctx, uint64_t seq) {
+  const uint64_t* stamp = (const uint64_t*)(ctx->map_out + OUT_HDR - 8);
+  uint64_t v = __atomic_load_n(stamp, __ATOMIC_ACQUIRE);
+  if (v == seq) return;
+  const auto t0 = std::chrono::steady_clock::now();
+  for (uint32_t i = 1; v != seq; i++) {
+    __builtin_ia32_pause();
+    v = __atomic_load_n(stamp, __ATOMIC_ACQUIRE);
+    if ((i & 1023) == 0 && v != seq && std::chrono::steady_clock::now() - t0 > std::chrono::milliseconds(200)) {
+      set_error(ctx, "stale snapshot: seq %llu, expected %llu", (unsigned long long)v, (unsigned long long)seq);
+      throw Fail{TSDBHIP_E_HIP};
+    }
+  }
+  ctx->timing_late = 1;
+}
+
 // grow-only mapped pinned result area (device pointer in map_out_dev)
 static void map_out_reserve(Slot* ctx, size_t bytes) {
   if (ctx->map_out_n >= bytes) return;
@@ -738,6 +780,7 @@ static void map_out_reserve(Slot* ctx, size_t bytes) {
   HIPCHK(hipHostMalloc((void**)&ctx->map_out, n, hipHostMallocMapped | hipHostMallocCoherent));
   HIPCHK(hipHostGetDevicePointer((void**)&ctx->map_out_dev, ctx->map_out, 0));
   ctx->map_out_n = n;
+  *(volatile uint64_t*)(ctx->map_out + OUT_HDR - 8) = 0;  // (no call's stamp)
 }
 
 // runtime aggregator id -> F::template run<AGG>(args...)
@@ -1122,11 +1165,10 @@ constexpr uint32_t XM_MAX = 14;
 struct XExtra { void* p; uint64_t count; XType t; XOp op; };
 static void xchg_minmax(Slot* ctx, Xchg* X, const XField* f, uint32_t n, uint64_t* sum_u64 = nullptr,
                         uint64_t* buf = nullptr, const XExtra* extra = nullptr, uint32_t n_extra = 0);
-constexpr size_t OUT_HDR = 1024;  // the Small snapshot ahead of the outputs
 // sharded double partials exchange rank-owned slices of G from this |G| on
 // (below it, one allgather of every rank's partials is the cheaper collective)
 constexpr uint64_t XSLICE_MIN_T = 65536;
-static_assert(sizeof(Small) <= OUT_HDR, "Small must fit the output header");
+static_assert(sizeof(Small) <= OUT_HDR - 8, "Small and the call's stamp must fit the output header");
 
 // End of a call, after the finalize: the call state is snapshot ahead of the
 // outputs (one D2H copy brings both back) and reset for the next call; the
@@ -1239,21 +1281,31 @@ __global__ void __launch_bounds__(1024) k_assemble_small(AssembleArgs a, KeptArg
 // calling (one thread copying the ~1 KB across PCIe took most of a 10-12 us
 // single-block launch)
 static_assert(sizeof(Small) % 8 == 0, "Small is copied in 8-byte words");
-DEVI void small_snap(Small* sm, Small* snap, const Small* init) {
+// The call's stamp (the word after the snapshot, OUT_HDR - 8): the call's
+// sequence number, stored last by thread 0 with a system-scope release once
+// every thread's snapshot words are fenced. Every host-visible result of the
+// call was written before it: the finalize's small results into the same
+// mapped block and the reduce's long results into registered caller buffers
+// by kernels that completed earlier in the stream, the aligned-group finish's
+// results by this block before the fence. The host checks the stamp before it
+// reads any of them (check_stamp).
+DEVI void small_snap(Small* sm, Small* snap, const Small* init, uint64_t seq) {
   constexpr uint32_t NW = sizeof(Small) / 8;
   const volatile uint64_t* s = (const volatile uint64_t*)sm;
   uint64_t* d = (uint64_t*)snap;
   for (uint32_t i = threadIdx.x; i < NW; i += blockDim.x) d[i] = s[i];
   __threadfence_system();  // (the snapshot's host writes complete before this kernel does)
+  __syncthreads();  // (every word read and fenced before any is reset, and before the stamp)
+  if (threadIdx.x == 0)
+    __hip_atomic_store((uint64_t*)((uint8_t*)snap + OUT_HDR - 8), seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
   if (!init) return;
-  __syncthreads();  // (every word read before any is reset)
   const uint64_t* in = (const uint64_t*)init;
   uint64_t* w = (uint64_t*)sm;
   for (uint32_t i = threadIdx.x; i < NW; i += blockDim.x) w[i] = in[i];
 }
 __global__ void __launch_bounds__(256) k_call_end(Small* sm, Small* snap, Small init, uint32_t* bitmap,
                                                   const uint32_t* grid, uint64_t T, int64_t lo, BadArgs bad,
-                                                  const uint32_t* done = nullptr) {
+                                                  uint64_t seq, const uint32_t* done = nullptr) {
   __shared__ unsigned long long s_min[4];
   if (done) {
     __shared__ uint64_t s_t;
@@ -1264,7 +1316,7 @@ __global__ void __launch_bounds__(256) k_call_end(Small* sm, Small* snap, Small 
     }
     __syncthreads();
     if (!s_over) {
-      if (blockIdx.x == 0) small_snap(sm, snap, nullptr);
+      if (blockIdx.x == 0) small_snap(sm, snap, nullptr, seq);
       return;
     }
     T = s_t;
@@ -1283,7 +1335,7 @@ __global__ void __launch_bounds__(256) k_call_end(Small* sm, Small* snap, Small 
       }
     }
     __syncthreads();  // (bad_at final)
-    small_snap(sm, snap, &init);
+    small_snap(sm, snap, &init, seq);
     __syncthreads();  // (the ranks above read the bitmap cleared below)
   }
   if (bitmap)
@@ -1332,7 +1384,8 @@ __global__ void k_fap_neutral64(int64_t* p_i, uint32_t* p_cnt, int op, Small* sm
 template <int AGG>
 __global__ void __launch_bounds__(256) k_fap_finish_end(Small* sm, const int64_t* p_i, const uint32_t* p_cnt,
                                                         FinalArgs f, int32_t sharded, XMove unpack, Small* snap,
-                                                        Small init, uint32_t* bitmap, const uint32_t* grid, int64_t lo) {
+                                                        Small init, uint32_t* bitmap, const uint32_t* grid, int64_t lo,
+                                                        uint64_t seq) {
   __shared__ uint32_t s_ok, s_T;
   const uint32_t t = threadIdx.x;
   if (t == 0) {
@@ -1346,7 +1399,7 @@ __global__ void __launch_bounds__(256) k_fap_finish_end(Small* sm, const int64_t
   }
   __syncthreads();
   if (!s_ok) {  // the group did not stand: the state stays for the usual path
-    small_snap(sm, snap, nullptr);
+    small_snap(sm, snap, nullptr, seq);
     return;
   }
   if (t < s_T) {
@@ -1359,7 +1412,7 @@ __global__ void __launch_bounds__(256) k_fap_finish_end(Small* sm, const int64_t
   __syncthreads();
   if (t == 0) sm->fap_done = 1;
   __syncthreads();
-  small_snap(sm, snap, &init);
+  small_snap(sm, snap, &init, seq);
   __syncthreads();  // (the grid read below is this block's own)
   if (bitmap && t < s_T) bitmap[(uint64_t)((int64_t)grid[t] - lo) >> 5] = 0u;
 }
@@ -1371,11 +1424,20 @@ __global__ void k_count_nonzero(const uint32_t* p, uint64_t n, unsigned long lon
     if (p[i]) atomicAdd(out, 1ull);
 }
 
-// The device address of a host buffer registered mapped (tsdbhip_host_register),
-// or null for unregistered memory.
-static void* mapped_dev_ptr(void* h) {
+// The device address of a host buffer registered mapped (tsdbhip_host_register)
+// whose registration covers all `bytes` from h, or null (unregistered, or a
+// registration shorter than the result: the caller copies D2H instead).
+static void* mapped_dev_ptr(void* h, size_t bytes) {
+  if (!h) return nullptr;
+  {
+    std::lock_guard<std::mutex> lk(g_reg_mu);
+    auto it = g_reg.upper_bound((uintptr_t)h);
+    if (it == g_reg.begin()) return nullptr;
+    --it;
+    if ((uintptr_t)h + bytes > it->first + it->second) return nullptr;
+  }
   void* d = nullptr;
-  if (!h || hipHostGetDevicePointer(&d, h, 0) != hipSuccess) {
+  if (hipHostGetDevicePointer(&d, h, 0) != hipSuccess) {
     (void)hipGetLastError();
     return nullptr;
   }
@@ -1419,6 +1481,7 @@ static int spangroup_run_once(Slot* ctx, const tsdbhip_sg_desc* d, tsdbhip_sg_ou
   const int32_t interval = d->ds_interval > 0 ? d->ds_interval : 0;
   hipStream_t st = ctx->stream;
   tsdbhip_timing tm = {};
+  ctx->timing_late = 0;
   ctx->hot_kernel = TSDBHIP_HOT_NONE;
   ctx->time_reduce = false;
   out->n_out = 0;
@@ -1846,6 +1909,7 @@ static int spangroup_run_once(Slot* ctx, const tsdbhip_sg_desc* d, tsdbhip_sg_ou
       xchg_group(ctx, X, pack, (uint64_t*)&sm->n_input, ex, 2);
     }
     map_out_reserve(ctx, OUT_HDR + 17 * WAVE);
+    const uint64_t end_seq = ++ctx->pub_seq;
     FinalArgs fo;
     std::memset(&fo, 0, sizeof fo);
     fo.T = WAVE;
@@ -1860,17 +1924,20 @@ static int spangroup_run_once(Slot* ctx, const tsdbhip_sg_desc* d, tsdbhip_sg_ou
       const XMove um = sharded ? unpack : XMove{};
       Small* snap = (Small*)ctx->map_out_dev;
       const Small ini = small_init();
+      const uint64_t seq = end_seq;
       if (agg == TSDBHIP_AGG_MIN)
-        LAUNCH(k_fap_finish_end<1>, dim3(1), dim3(256), 0, st, sm, (const int64_t*)o_pi, (const uint32_t*)o_pc, fo, (int32_t)sharded, um, snap, ini, bitmap, (const uint32_t*)gridv_o, lo);
+        LAUNCH(k_fap_finish_end<1>, dim3(1), dim3(256), 0, st, sm, (const int64_t*)o_pi, (const uint32_t*)o_pc, fo, (int32_t)sharded, um, snap, ini, bitmap, (const uint32_t*)gridv_o, lo, seq);
       else if (agg == TSDBHIP_AGG_MAX)
-        LAUNCH(k_fap_finish_end<2>, dim3(1), dim3(256), 0, st, sm, (const int64_t*)o_pi, (const uint32_t*)o_pc, fo, (int32_t)sharded, um, snap, ini, bitmap, (const uint32_t*)gridv_o, lo);
+        LAUNCH(k_fap_finish_end<2>, dim3(1), dim3(256), 0, st, sm, (const int64_t*)o_pi, (const uint32_t*)o_pc, fo, (int32_t)sharded, um, snap, ini, bitmap, (const uint32_t*)gridv_o, lo, seq);
       else if (agg == TSDBHIP_AGG_AVG)
-        LAUNCH(k_fap_finish_end<3>, dim3(1), dim3(256), 0, st, sm, (const int64_t*)o_pi, (const uint32_t*)o_pc, fo, (int32_t)sharded, um, snap, ini, bitmap, (const uint32_t*)gridv_o, lo);
+        LAUNCH(k_fap_finish_end<3>, dim3(1), dim3(256), 0, st, sm, (const int64_t*)o_pi, (const uint32_t*)o_pc, fo, (int32_t)sharded, um, snap, ini, bitmap, (const uint32_t*)gridv_o, lo, seq);
       else
-        LAUNCH(k_fap_finish_end<0>, dim3(1), dim3(256), 0, st, sm, (const int64_t*)o_pi, (const uint32_t*)o_pc, fo, (int32_t)sharded, um, snap, ini, bitmap, (const uint32_t*)gridv_o, lo);
+        LAUNCH(k_fap_finish_end<0>, dim3(1), dim3(256), 0, st, sm, (const int64_t*)o_pi, (const uint32_t*)o_pc, fo, (int32_t)sharded, um, snap, ini, bitmap, (const uint32_t*)gridv_o, lo, seq);
     }
     EV_FINAL(ctx, 5);
     HIPCHK(hipStreamSynchronize(st));
+    check_stamp(ctx, end_seq);
+    tm.late_stamp = ctx->timing_late;
     std::memcpy(&h, ctx->map_out, sizeof h);
     if (h.fap_done) {  // the call is over (state reset, bitmap clear)
       ctx->sm_ready = true;
@@ -1970,11 +2037,19 @@ static int spangroup_run_once(Slot* ctx, const tsdbhip_sg_desc* d, tsdbhip_sg_ou
   // its pattern (sharded: no other rank put a point elsewhere). A rank whose
   // proposal stood but whose grid is wider cannot use it: the call is marked
   // broken and runs again on the proven path (every rank, after the exchange)
+  // The reduce mode is the agreed one (sharded: every rank's flags); a rank
+  // whose lockstep proposal would reduce in another mode (an int shard next
+  // to a float shard on one cadence: MODE_INT where the group is MODE_DUAL,
+  // so the double partials would go unwritten) cannot use it either
+  const bool anyf = h.gflags[0] != 0, anyi = h.gflags[1] != 0;
+  const int mode = rate ? MODE_DBL : (!anyf ? MODE_INT : (!anyi ? MODE_DBL : MODE_DUAL));
   bool ls_use = false;
   LsPlan lsp = {};
   if (ls_try && h.cnt[5] == 0 && h.ls_key[0] != ~0ull && h.ls_key[0] == h.ls_key[1] && h.ls_key[2] == h.ls_key[3]) {
     const uint32_t ln = (uint32_t)h.ls_key[0];
-    if (h.T == (uint64_t)(rate ? ln - 1 : ln)) {
+    const bool ls_flt = (h.ls_key[2] & 8u) != 0;
+    const int ls_mode = (rate || ls_flt) ? MODE_DBL : MODE_INT;
+    if (h.T == (uint64_t)(rate ? ln - 1 : ln) && ls_mode == mode) {
       ls_use = true;
       lsp.a.d_voff = dg.voff;
       lsp.a.d_qoff = d_qoff;
@@ -2016,7 +2091,6 @@ static int spangroup_run_once(Slot* ctx, const tsdbhip_sg_desc* d, tsdbhip_sg_ou
                          0, st, fa, row_ncells, row_val_len);
     }
   }
-  const bool anyf = h.gflags[0] != 0, anyi = h.gflags[1] != 0;
   const uint64_t fstar = h.fstar;
   // the aligned-group partials stand for the reduce iff every kept span was in
   // the one class (no span outside it, one key) and G is the class's bucket
@@ -2047,7 +2121,6 @@ static int spangroup_run_once(Slot* ctx, const tsdbhip_sg_desc* d, tsdbhip_sg_ou
   // (long) truncation, Aggregators.java:196-217, or EXACT_ORDER), exact
   // integer partials, or order-dependent doubles; sharded doubles over a long
   // grid exchange rank-owned slices of G (below) ----
-  const int mode = rate ? MODE_DBL : (!anyf ? MODE_INT : (!anyi ? MODE_DBL : MODE_DUAL));
   const bool seq = exact || (agg == TSDBHIP_AGG_DEV && mode != MODE_DBL);
   const bool int_parts = mode == MODE_INT && agg != TSDBHIP_AGG_DEV;
   // (per rank (N-1)/N (esz + 17) B a point against (N-1) esz: a gain from 3
@@ -2072,9 +2145,9 @@ static int spangroup_run_once(Slot* ctx, const tsdbhip_sg_desc* d, tsdbhip_sg_ou
   FinalArgs fin_map;
   std::memset(&fin_map, 0, sizeof fin_map);
   if (!sharded && !small_out && ctx->want_output && T >= 65536 && out->capacity >= T) {
-    fin_map.out_ts = (int64_t*)mapped_dev_ptr(out->ts);
-    fin_map.out_bits = (int64_t*)mapped_dev_ptr(out->bits);
-    fin_map.out_isint = (uint8_t*)mapped_dev_ptr(out->is_int);
+    fin_map.out_ts = (int64_t*)mapped_dev_ptr(out->ts, T * 8);
+    fin_map.out_bits = (int64_t*)mapped_dev_ptr(out->bits, T * 8);
+    fin_map.out_isint = (uint8_t*)mapped_dev_ptr(out->is_int, T);
     if (!fin_map.out_ts || !fin_map.out_bits || !fin_map.out_isint) fin_map.out_ts = nullptr;
   }
   bool out_direct = false;  // the results are already in the caller's buffers
@@ -2369,18 +2442,25 @@ static int spangroup_run_once(Slot* ctx, const tsdbhip_sg_desc* d, tsdbhip_sg_ou
     X->group_end(ctx);
   }
   // ---- end of call: snapshot + reset of the call state, bitmap cleared ----
+  const uint64_t end_seq = ++ctx->pub_seq;
   LAUNCH(k_call_end, dim3(bad_at_end ? 1u : grid_for(T, 256, 1024)), dim3(256), 0, st, sm,
               (Small*)ctx->map_out_dev, small_init(), bitmap, (const uint32_t*)gridv, T, lo, bad_at_end ? bad : BadArgs{},
-              (const uint32_t*)nullptr);
+              end_seq, (const uint32_t*)nullptr);
   EV_FINAL(ctx, 5);
   HIPCHK(hipStreamSynchronize(st));  // (the header and small results are already in host memory)
+  check_stamp(ctx, end_seq);
+  tm.late_stamp = ctx->timing_late;
   const uint8_t* hb = ctx->map_out;
   std::memcpy(&h, hb, sizeof h);
   ctx->sm_ready = true;
   ctx->bitmap_clean = true;
   if (used_bitmap_x) ctx->bitmapx_clean = true;
   if (tgd_used) ctx->tgdone_clean = true;  // (every counter reset by its group's last wave)
-  if (ls_try && h.ls_broken) {  // (agreed over the ranks) the proposal did not hold: discard, run again
+  // the proposal did not hold: discard, run again. Sharded, from the agreed
+  // flag alone (MAX over the ranks): whether a rank tried depends on its own
+  // shard (empty, short rows), and every rank must issue the rerun's
+  // collectives. Unsharded the flag is only ever set by a try.
+  if (h.ls_broken) {
     ctx->timing = tm;
     return RC_REDO;
   }

@@ -221,6 +221,58 @@ def test_lockstep_sharded_ranks_disagree(mctx):
 
 
 @pytest.mark.gpu
+@pytest.mark.timeout(120)
+@pytest.mark.parametrize("rate", [False, True])
+def test_lockstep_broken_next_to_an_empty_rank(mctx, rate):
+    """fewer spans than ranks, one qualifier off the cadence.
+    The ranks holding spans try the lockstep proposal and break it; the empty
+    rank never tries. The rerun is decided from the agreed flag alone, so the
+    empty rank reruns too (a per-rank decision left its peers waiting in the
+    rerun's collectives)."""
+    n = mctx.ranks - 1
+    ss = synth.regular(n, 900, _abi.SYN_INT64_COUNTER, seed=4, step=2)
+    ss = corrupt_qual(ss, n - 1, 400, lambda q: q + 16)
+    for agg in (0, 2):
+        g, o = both(mctx, ss, agg=agg, rate=rate)
+        assert_same(g, o)
+        assert mctx.timing().paths & _abi.PATH_DIRECT_REDO
+
+
+@pytest.mark.gpu
+@pytest.mark.timeout(120)
+def test_lockstep_broken_next_to_a_short_row_rank(mctx):
+    """the last rank's shard is a series of short rows (the
+    general decode: no lockstep try there) while the other ranks' proposal is
+    broken by a corrupted qualifier: every rank reruns"""
+    n = mctx.ranks - 1
+    spans = [I([(T0 + 2 * i, 1000 * s + 3 * i) for i in range(900)], minimal=False) for s in range(n)]
+    # 20 points on the same grid in one row: < 64 cells a row, the general decode
+    sparse = I([(T0 + 2 * i, i) for i in range(0, 900, 45)], minimal=False)
+    ss = corrupt_qual(packing.pack_spans(spans + [sparse]), 0, 300, lambda q: q + 16)
+    for agg, rate in ((0, False), (2, True)):
+        g, o = both(mctx, ss, agg=agg, rate=rate)
+        assert_same(g, o)
+
+
+@pytest.mark.gpu
+@pytest.mark.timeout(120)
+@pytest.mark.parametrize("agg", [0, 1, 3])
+def test_lockstep_int_shard_next_to_float_shard(mctx, agg):
+    """int shards and float shards on one cadence. Each rank
+    proposes lockstep in its own cell type, but the group's reduce mode is the
+    agreed dual one: an int rank's MODE_INT partials would leave the double
+    fields unwritten. Such a rank cannot use its proposal: every rank reruns
+    on the proven path."""
+    n = 2 * mctx.ranks
+    spans = [I([(T0 + 2 * i, 100 * s + i) for i in range(700)], minimal=False) for s in range(n // 2)]
+    spans += [F([(T0 + 2 * i, 0.5 * s + i) for i in range(700)], double=True) for s in range(n // 2)]
+    ss = packing.pack_spans(spans)
+    g, o = both(mctx, ss, agg=agg)
+    assert_same(g, o)
+    assert mctx.timing().paths & _abi.PATH_DIRECT_REDO
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("agg", AGGS)
 @pytest.mark.parametrize("rate", [False, True])
 def test_long_grid_sliced_exchange(mctx, agg, rate):

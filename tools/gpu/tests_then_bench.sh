@@ -3,7 +3,7 @@
 set -o pipefail
 mkdir -p gpurun_out
 ARGS=${@:-tests}
-timeout -k 10 900 python -u -m pytest $ARGS -q -x --timeout 600 --timeout-method thread -m gpu \
+timeout -k 10 900 python -u -m pytest $ARGS -q -x --tb=short -rf --timeout 600 --timeout-method thread -m gpu \
   > gpurun_out/pytest_gpu.log 2>&1
 rc=$?
 tail -5 gpurun_out/pytest_gpu.log
