@@ -181,6 +181,11 @@ typedef struct tsdbhip_timing {
 #define TSDBHIP_PATH_DIRECT_REDO   8u  /* k_lockstep found a qualifier off the
                                           proposal: the call ran again on the
                                           proven (scan + reduce) path         */
+#define TSDBHIP_PATH_UNIFORM      16u  /* every kept span proposed one class key
+                                          at assembly: G from the key, no grid
+                                          kernels, one host round trip        */
+#define TSDBHIP_PATH_UNIFORM_FALLBACK 32u  /* the uniform aligned group did not
+                                          stand: the general path ran the call */
 
 /* ---- row compaction (CompactionQueue.compact) -------------------------- */
 /*

@@ -11,6 +11,8 @@ PATH_ALIGNED_GROUP = 1  # tsdbhip_timing.paths (include/tsdbhip.h)
 PATH_ALIGNED_RERUN = 2
 PATH_LOCKSTEP = 4  # k_lockstep: one pass over the qualifiers and values of a lockstep group
 PATH_DIRECT_REDO = 8  # its proposal did not hold: the call ran again on the proven path
+PATH_UNIFORM = 16  # every kept span proposed one class key at assembly: G from the key, one round trip
+PATH_UNIFORM_FALLBACK = 32  # the uniform aligned group did not stand: the general path ran the call
 
 OK = 0
 E_ILLEGAL_DATA = -1

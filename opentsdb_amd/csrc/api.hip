@@ -942,6 +942,9 @@ struct LsPlan {
   LockstepArgs a;
   bool w8, flt;
 };
+#ifndef LS_MIN_SPC
+#define LS_MIN_SPC 128  // fewest spans a lockstep chunk (the n_chunks x T partials the combine reads; 64: the C3 rate-sum 8-way shard 1.07 ms, 128: 0.98-1.00, 256: 0.99-1.00; 1M spans unchanged)
+#endif
 template <int AGG, bool RATE, uint32_t W, bool FLT>
 static void launch_lockstep_wf(Slot* ctx, unsigned blocks, const ReduceArgs& r, const LockstepArgs& a,
                                const FinalArgs& f, bool finalize) {
@@ -1125,6 +1128,10 @@ struct Small {
   unsigned long long ls_key[4];
   uint32_t ls_broken, ls_pad;
   unsigned long long xh[14];  // (XH_N, + the aligned-group validity in an optimistic call)
+  // the uniform-group proposal (assembly): the kept spans' class keys
+  // (x0 << 32 | n, step << 32 | q0) as [min, max, min, max]; a span that
+  // proposes none holds ~0 in the first word
+  unsigned long long ukey[4];
 };
 // Small.xh slots of the grid-agreement header. Every rank decides from these
 // agreed words alone (never from its own lo / hi against them), so the ranks
@@ -1152,6 +1159,7 @@ static Small small_init() {
   init.bound[3] = ~0ull;
   init.fap_key[0] = init.fap_key[2] = ~0ull;
   init.ls_key[0] = init.ls_key[2] = ~0ull;
+  init.ukey[0] = init.ukey[2] = ~0ull;
   return init;
 }
 // Several MIN / MAX agreements on call-state fields as one MIN allreduce of a
@@ -1185,22 +1193,27 @@ struct XMove {
   uint64_t imm[XM_MAX];   // kinds 3 / 4
   int32_t out;            // 0: fields -> buf, 1: buf -> fields
 };
-DEVI void xmove_run(const XMove& m) {
-  for (uint32_t i = 0; i < m.n; i++) {
-    const uint8_t k = m.kind[i];
-    const bool cpl = k == 1 || k == 2 || k == 4 || k == 6;  // MAX kinds travel complemented
-    if (!m.out) {
-      const uint64_t v = k == 2 ? (uint64_t)*(const uint32_t*)m.field[i]
-                         : (k == 3 || k == 4) ? m.imm[i] : *(const uint64_t*)m.field[i];
-      m.buf[i] = cpl ? ~v : v;
-    } else if (k <= 2) {
-      const uint64_t v = cpl ? ~m.buf[i] : m.buf[i];
-      if (k == 2) *(uint32_t*)m.field[i] = (uint32_t)v;
-      else *(uint64_t*)m.field[i] = v;
-    }
+DEVI void xmove_one(const XMove& m, uint32_t i) {
+  const uint8_t k = m.kind[i];
+  const bool cpl = k == 1 || k == 2 || k == 4 || k == 6;  // MAX kinds travel complemented
+  if (!m.out) {
+    const uint64_t v = k == 2 ? (uint64_t)*(const uint32_t*)m.field[i]
+                       : (k == 3 || k == 4) ? m.imm[i] : *(const uint64_t*)m.field[i];
+    m.buf[i] = cpl ? ~v : v;
+  } else if (k <= 2) {
+    const uint64_t v = cpl ? ~m.buf[i] : m.buf[i];
+    if (k == 2) *(uint32_t*)m.field[i] = (uint32_t)v;
+    else *(uint64_t*)m.field[i] = v;
   }
 }
-__global__ void k_xmove(XMove m) { xmove_run(m); }
+DEVI void xmove_run(const XMove& m) {
+  for (uint32_t i = 0; i < m.n; i++) xmove_one(m, i);
+}
+// a thread a field (one thread walking them paid a dependent round trip each:
+// 6.7 us for the 12-field header)
+__global__ void __launch_bounds__(64) k_xmove(XMove m) {
+  if (threadIdx.x < m.n) xmove_one(m, threadIdx.x);
+}
 
 // (sum_u64: one more field, a u64 SUM, in the same collective group. The
 // pack / unpack kernels stay outside the group: RCCL issues a group's
@@ -1227,14 +1240,14 @@ static void xchg_minmax(Slot* ctx, Xchg* X, const XField* f, uint32_t n, uint64_
   m.n = n;
   m.buf = buf ? buf : scratch<uint64_t>(ctx, "x_pack", XM_MAX);
   for (uint32_t i = 0; i < n; i++) { m.kind[i] = f[i].kind; m.field[i] = f[i].p; m.imm[i] = f[i].imm; }
-  LAUNCH(k_xmove, dim3(1), dim3(1), 0, ctx->stream, m);
+  LAUNCH(k_xmove, dim3(1), dim3(64), 0, ctx->stream, m);
   X->group_start(ctx);
   X->allreduce(ctx, m.buf, n, X_U64, X_MIN);
   if (sum_u64) X->allreduce(ctx, sum_u64, 1, X_U64, X_SUM);
   for (uint32_t i = 0; i < n_extra; i++) X->allreduce(ctx, extra[i].p, extra[i].count, extra[i].t, extra[i].op);
   X->group_end(ctx);
   m.out = 1;
-  LAUNCH(k_xmove, dim3(1), dim3(1), 0, ctx->stream, m);
+  LAUNCH(k_xmove, dim3(1), dim3(64), 0, ctx->stream, m);
 }
 
 // dst (global geometry [dst_lo, ...]) = src (a rank's bitmap over [src_lo,
@@ -1270,6 +1283,72 @@ __global__ void __launch_bounds__(1024) k_assemble_small(AssembleArgs a, KeptArg
   for (uint32_t w = t / WAVE; w < nd; w += 1024 / WAVE) assemble_span_wave(a, s_list[w]);
   __syncthreads();  // (the block's global writes visible to the whole block)
   kept_compact_block(K);
+}
+
+// Groups of (nearly) single-row spans beyond one block (rows <= 2 x spans:
+// C3's 1M series): a tile of 256 spans assembled (a thread a span, the
+// block's waves walking the deferred ones, as k_assemble_small) and its kept
+// sums in one launch, instead of k_assemble_fast, k_assemble and
+// k_kept_tiles. The sums of the tile travel as one wave-reduced row per wave
+// through LDS (one barrier).
+__global__ void __launch_bounds__(256) k_assemble_tiles(AssembleArgs a, KeptTile* tile_sum, ulonglong2* tile_ke) {
+  __shared__ uint32_t s_list[256];
+  __shared__ uint32_t s_n;
+  __shared__ uint64_t s_r[4][11];
+  const uint32_t t = threadIdx.x, lane = lane_id(), w = t / WAVE;
+  const uint32_t s = blockIdx.x * 256 + t;
+  if (t == 0) s_n = 0;
+  __syncthreads();
+  if (s < a.n_spans && assemble_fast_one(a, s)) s_list[atomicAdd(&s_n, 1u)] = s;
+  __syncthreads();
+  const uint32_t nd = s_n;
+  for (uint32_t i = w; i < nd; i += 256 / WAVE) assemble_span_wave(a, s_list[i]);
+  if (nd) __syncthreads();  // (the block's global writes visible to the whole block)
+  uint64_t sk = 0, se = 0, cnt = 0;
+  int64_t f = INT64_MAX, l = INT64_MIN, fx = INT64_MIN, ln = INT64_MAX;
+  UKeyAcc u;
+  u.init();
+  if (s < a.n_spans) {
+    se = a.sp_cap[s];
+    if (a.sp_kept[s]) {
+      sk = 1;
+      cnt = a.sp_ncells[s];
+      f = fx = a.sp_first[s];
+      l = ln = a.sp_last[s];
+      if (a.u_key1) u.add(a.u_key1[s], a.u_key2[s]);
+    }
+  }
+#pragma unroll
+  for (int m = 1; m < WAVE; m <<= 1) {
+    sk += shfl_xor_u64(sk, m);
+    se += shfl_xor_u64(se, m);
+    cnt += shfl_xor_u64(cnt, m);
+    f = min(f, (int64_t)shfl_xor_u64((uint64_t)f, m));
+    l = max(l, (int64_t)shfl_xor_u64((uint64_t)l, m));
+    fx = max(fx, (int64_t)shfl_xor_u64((uint64_t)fx, m));
+    ln = min(ln, (int64_t)shfl_xor_u64((uint64_t)ln, m));
+  }
+  if (a.u_key1) u.wave_reduce();
+  if (lane == 0) {
+    uint64_t* r = s_r[w];
+    r[0] = sk; r[1] = se; r[2] = cnt; r[3] = (uint64_t)f; r[4] = (uint64_t)l; r[5] = (uint64_t)fx; r[6] = (uint64_t)ln;
+    r[7] = u.a0; r[8] = u.a1; r[9] = u.b0; r[10] = u.b1;
+  }
+  __syncthreads();
+  if (t == 0) {
+    for (int i = 1; i < 4; i++) {
+      const uint64_t* r = s_r[i];
+      sk += r[0]; se += r[1]; cnt += r[2];
+      f = min(f, (int64_t)r[3]); l = max(l, (int64_t)r[4]); fx = max(fx, (int64_t)r[5]); ln = min(ln, (int64_t)r[6]);
+      u.a0 = min(u.a0, r[7]); u.a1 = max(u.a1, r[8]); u.b0 = min(u.b0, r[9]); u.b1 = max(u.b1, r[10]);
+    }
+    KeptTile o;
+    o.k = sk; o.e = se; o.cnt = cnt; o.pad = 0;
+    o.f = cnt ? f : INT64_MAX; o.l = cnt ? l : INT64_MIN; o.fx = cnt ? fx : INT64_MIN; o.ln = cnt ? ln : INT64_MAX;
+    o.u = u;
+    tile_sum[blockIdx.x] = o;
+    tile_ke[blockIdx.x] = make_ulonglong2(sk, se);
+  }
 }
 
 // Small unsharded calls also compute the lazy error index here (block 0,
@@ -1348,11 +1427,17 @@ __global__ void __launch_bounds__(256) k_call_end(Small* sm, Small* snap, Small 
 // this rank's partials stand: every kept span in the one class, G its bucket
 // sequence of at most 64 points, no float, no error
 // (one thread; then, sharded, the agreement header packed for the group)
-DEVI void fap_valid_pack(Small* sm, uint32_t fap_ran, const XMove& pack) {
+// (a whole wave: lane i packs field i; the validity is this wave's own value,
+// not re-read from the call state)
+DEVI void fap_valid_pack(Small* sm, uint32_t fap_ran, const XMove& pack, uint64_t T) {
   const bool v = fap_ran && sm->err == ERR_NONE && !sm->fap_broken && sm->fap_key[0] == sm->fap_key[1] &&
-                 sm->fap_key[2] == sm->fap_key[3] && sm->T > 0 && sm->T <= WAVE && sm->gflags[0] == 0;
-  sm->fap_valid = v ? 1ull : 0ull;
-  if (pack.n) xmove_run(pack);
+                 sm->fap_key[2] == sm->fap_key[3] && T > 0 && T <= WAVE && sm->gflags[0] == 0;
+  const uint32_t lane = lane_id();
+  if (lane == 0) sm->fap_valid = v ? 1ull : 0ull;
+  if (lane < pack.n) {
+    if (pack.field[lane] == (void*)&sm->fap_valid) pack.buf[lane] = v ? 1ull : 0ull;  // (kind 0: MIN, as is)
+    else xmove_one(pack, lane);
+  }
 }
 // this rank's 64-slot partials (k_fap_final64's reduce), its validity, the pack
 template <int OP>
@@ -1364,17 +1449,44 @@ __global__ void __launch_bounds__(1024) k_fap_final64v(const int64_t* tmp, uint3
   int64_t acc = fap_rows_wave<OP>(tmp, w, 16, n);
   acc = fap_block_comb<OP>(acc, s);
   if (w == 0) {
-    const bool in = (uint64_t)lane < *(volatile const uint64_t*)&sm->T;
+    const uint64_t T = *(volatile const uint64_t*)&sm->T;
+    const bool in = (uint64_t)lane < T;
     p_i[lane] = in ? acc : fap_neutral(OP);
     p_cnt[lane] = in ? n_kept : 0u;
-    if (lane == 0) fap_valid_pack(sm, 1u, pack);
+    fap_valid_pack(sm, 1u, pack, T);
+  }
+}
+// The uniform path's aligned group: k_fap_final64v, plus G from the class key
+// (bucket b of every span: t0 + b kk step + floor(step (m_b - 1) / 2), its
+// m_b cells, Span.java:377-422) and |G| = nb into the call state (every
+// bucket ts <= the spans' last point <= end, SpanGroup.java:510-608)
+template <int OP>
+__global__ void __launch_bounds__(1024) k_ug_fap_final64v(const int64_t* tmp, uint32_t n, uint32_t n_kept, int64_t* p_i,
+                                                          uint32_t* p_cnt, Small* sm, XMove pack, uint32_t* grid,
+                                                          uint32_t t0, uint32_t step, uint32_t kk, uint32_t ncell,
+                                                          uint32_t nb) {
+  __shared__ int64_t s[16][WAVE];
+  const int lane = lane_id();
+  const uint32_t w = threadIdx.x / WAVE;
+  int64_t acc = fap_rows_wave<OP>(tmp, w, 16, n);
+  acc = fap_block_comb<OP>(acc, s);
+  if (w == 0) {
+    const bool in = (uint32_t)lane < nb;
+    if (in) {
+      const uint32_t sb = (uint32_t)lane * kk, m = min(sb + kk, ncell) - sb;
+      grid[lane] = t0 + sb * step + (uint32_t)((uint64_t)step * (m - 1) / 2);
+    }
+    p_i[lane] = in ? acc : fap_neutral(OP);
+    p_cnt[lane] = in ? n_kept : 0u;
+    if (lane == 0) sm->T = nb;
+    fap_valid_pack(sm, 1u, pack, nb);
   }
 }
 // a rank without an aligned-group attempt: neutral partials for the exchange
 __global__ void k_fap_neutral64(int64_t* p_i, uint32_t* p_cnt, int op, Small* sm, XMove pack) {
   p_i[threadIdx.x] = fap_neutral(op);
   p_cnt[threadIdx.x] = 0;
-  if (threadIdx.x == 0) fap_valid_pack(sm, 0u, pack);
+  fap_valid_pack(sm, 0u, pack, 0);
 }
 // The finalize of the (exchanged) 64-slot partials when the group stands
 // everywhere (sharded: and every rank's grid is the global one; outputs at a
@@ -1388,8 +1500,9 @@ __global__ void __launch_bounds__(256) k_fap_finish_end(Small* sm, const int64_t
                                                         uint64_t seq) {
   __shared__ uint32_t s_ok, s_T;
   const uint32_t t = threadIdx.x;
+  if (t < unpack.n) xmove_one(unpack, t);  // the agreed header back into the call state (sharded), a field a thread
+  __syncthreads();
   if (t == 0) {
-    if (unpack.n) xmove_run(unpack);  // the agreed header back into the call state (sharded)
     bool ok = sm->fap_valid != 0 && sm->err == ERR_NONE && sm->gflags[0] == 0 && sm->T > 0 && sm->T <= WAVE;
     // (sharded: rank-independent: an empty grid anywhere makes lo's MIN / MAX
     // differ, ~0 vs a real lo; all empty fails T > 0 on every rank)
@@ -1459,11 +1572,389 @@ static T* scratch_zero_kept(Slot* ctx, const char* name, size_t count, bool clea
   return p;
 }
 
+// per-t partial fields ([n][T] layout) under scratch names prefix + field
+static void alloc_partials(Slot* ctx, ReduceArgs& r, const char* pre, uint64_t np, int agg) {
+  auto nm = [&](const char* f) { return std::string(pre) + f; };
+  r.p_cnt = scratch<uint32_t>(ctx, nm("cnt").c_str(), np);
+  r.p_flag = scratch<uint8_t>(ctx, nm("flag").c_str(), np);
+  r.p_i = scratch<int64_t>(ctx, nm("i").c_str(), np);
+  r.p_d = scratch<double>(ctx, nm("d").c_str(), np);
+  r.p_dhas = scratch<uint32_t>(ctx, nm("dhas").c_str(), np);
+  r.p_wim = r.p_wiv = r.p_wdm = r.p_wdv = nullptr;
+  if (agg == TSDBHIP_AGG_DEV) {
+    r.p_wim = scratch<double>(ctx, nm("wim").c_str(), np);
+    r.p_wiv = scratch<double>(ctx, nm("wiv").c_str(), np);
+    r.p_wdm = scratch<double>(ctx, nm("wdm").c_str(), np);
+    r.p_wdv = scratch<double>(ctx, nm("wdv").c_str(), np);
+  }
+}
+// the fields acc_store writes for (agg, mode), at slot offset `off`, with the
+// element type and the reduction an exchange applies to them
+struct Fld { void* p; size_t esz; XType t; XOp op; };
+static std::vector<Fld> partial_fields(const ReduceArgs& r, uint64_t off, int agg, int mode) {
+  std::vector<Fld> v;
+  v.push_back({r.p_cnt + off, 4, X_U32, X_SUM});
+  if (mode == MODE_DUAL || agg == 1 || agg == 2) v.push_back({r.p_flag + off, 1, X_U8, X_MAX});
+  if (mode != MODE_DBL && agg != 4)
+    v.push_back({r.p_i + off, 8, agg == 1 ? X_I64 : agg == 2 ? X_I64 : X_U64,
+                 agg == 1 ? X_MIN : agg == 2 ? X_MAX : X_SUM});
+  if (mode != MODE_INT && agg != 4) v.push_back({r.p_d + off, 8, X_F64, X_SUM});
+  if (mode != MODE_INT && (agg == 1 || agg == 2)) v.push_back({r.p_dhas + off, 4, X_U32, X_MAX});
+  if (agg == 4) {
+    if (mode != MODE_DBL) { v.push_back({r.p_wim + off, 8, X_F64, X_SUM}); v.push_back({r.p_wiv + off, 8, X_F64, X_SUM}); }
+    if (mode != MODE_INT) { v.push_back({r.p_wdm + off, 8, X_F64, X_SUM}); v.push_back({r.p_wdv + off, 8, X_F64, X_SUM}); }
+  }
+  return v;
+}
+
+// ------------------------------------------------ the uniform path ----
+// Every kept span one row on one cadence with one class key (x0, n, step,
+// flags) proposed at assembly (ug_probe) — C3's and C3*'s series written in
+// lockstep. The union grid is then that cadence (SpanGroup.java:510-608):
+// no bitmap, no grid kernels, no second host round trip. Two variants:
+//
+//  * lockstep (no downsampling): k_lockstep streams every span's qualifiers
+//    and values once, proving the cadence as it reduces; G is written by its
+//    chunk-0 waves. Sharded, the ranks agreed on the key before the host's
+//    round trip (one MIN allreduce of the packed key words, issued by every
+//    rank for such a query), so every rank sizes G alike; the partials then
+//    travel in one collective group with the broken flag and the input count.
+//    Collectives: 2. A qualifier off the proposal: RC_REDO (the proven path).
+//  * aligned group (downsampled integer sum / min / max / avg): k_ds_reg's
+//    block partials, G from the key, and the optimistic finish of the
+//    general path (k_fap_finish_end), the key agreed in the partials' group.
+//    Collectives: 1. A group that does not stand anywhere: RC_UG_FALLBACK
+//    (the call state reset; the general path runs the call).
+constexpr int RC_REDO = 1000;  // a lockstep proposal did not hold: the proven path runs the call
+constexpr int RC_UG_FALLBACK = 1001;
+struct UgIn {
+  const tsdbhip_sg_desc* d;
+  Xchg* X;
+  Small* sm;
+  DecodeArgs da;  // (the aligned group: k_ds_reg's inputs, E of the call)
+  const uint32_t* row_ncells;
+  const uint32_t* row_val_len;
+  const uint64_t* uk_vo;  // [n_kept] row offsets of the kept spans (k_lockstep)
+  const uint64_t* uk_qo;
+  uint32_t n_kept;
+  uint64_t k1, k2;  // the class key (agreed, sharded lockstep)
+  bool lockstep;     // else the aligned group
+  bool mine;         // (aligned group) this rank's spans make the attempt
+};
+
+static int uniform_run(Slot* ctx, const UgIn& u, tsdbhip_sg_out* out, tsdbhip_timing& tm) {
+  const tsdbhip_sg_desc* d = u.d;
+  Xchg* X = u.X;
+  const bool sharded = X != nullptr;
+  Small* sm = u.sm;
+  hipStream_t st = ctx->stream;
+  const bool rate = d->rate != 0;
+  const int agg = d->agg;
+  const uint32_t n = (uint32_t)u.k1, x0 = (uint32_t)(u.k1 >> 32);
+  const uint32_t q0 = (uint32_t)(u.k2 & 0xFFFFu), step = (uint32_t)(u.k2 >> 32);
+  const uint32_t n_kept = u.n_kept;
+  Small h;
+  tm.paths |= TSDBHIP_PATH_UNIFORM;
+  if (!u.lockstep) {
+    // ---- aligned group ----
+    const int32_t I = d->ds_interval;
+    // (a rank making no attempt may hold no key: step 0)
+    const uint32_t kk = u.mine ? (uint32_t)(((int64_t)I + step - 1) / step) : 1u;
+    const uint32_t nb = u.mine ? (n + kk - 1) / kk : 0u;
+    const int fop = agg == TSDBHIP_AGG_MIN ? 1 : (agg == TSDBHIP_AGG_MAX ? 2 : 0);
+    uint32_t* gridv = scratch<uint32_t>(ctx, "grid", WAVE);
+    int64_t* o_pi = scratch<int64_t>(ctx, "fo_i", WAVE);
+    uint32_t* o_pc = scratch<uint32_t>(ctx, "fo_cnt", WAVE);
+    // the agreement header of the general path's optimistic finish, with the
+    // class key in the grid-geometry words: xh_grids_agree() holds iff every
+    // rank made the attempt on the same key
+    const uint64_t a1 = u.mine ? u.k1 : ~0ull, a2 = u.mine ? u.k2 : 0ull;
+    const XField fx[XH_N + 1] = {{&sm->err, 0, 0},  {&sm->gflags[0], 2, 0}, {&sm->gflags[1], 2, 0},
+                                 {&sm->fstar, 1, 0}, {nullptr, 3, a1},       {nullptr, 4, a2},
+                                 {nullptr, 3, 0},    {nullptr, 4, 0},        {nullptr, 3, 0},
+                                 {nullptr, 4, 0},    {nullptr, 4, a1},       {nullptr, 3, a2},
+                                 {&sm->fap_valid, 0, 0}};
+    XMove pack = {};
+    if (sharded) pack = xchg_desc(ctx, fx, XH_N + 1, (uint64_t*)sm->xh);
+    XMove unpack = pack;
+    unpack.out = 1;
+    auto go = [&](auto opc) {
+      constexpr int OP = decltype(opc)::value;
+      if (!u.mine) {
+        LAUNCH(k_fap_neutral64, dim3(1), dim3(WAVE), 0, st, o_pi, o_pc, OP, sm, pack);
+        return;
+      }
+      // k_ds_reg, a wave a span, in the aligned group's mode: each block's
+      // buckets combined in LDS into one partial row (LaunchChunks' k_ds_reg)
+      const uint32_t rblocks = (n_kept + 3) / 4;
+      SpanDsArgs gr = {};
+      gr.nseg = CK_NSEG;
+      gr.seg_cap = 4u * ((rblocks + CK_NSEG - 1) / CK_NSEG);
+      gr.list = scratch<uint32_t>(ctx, "cr_list", (uint64_t)gr.seg_cap * CK_NSEG);
+      gr.list_count = sm->seg2;
+      gr.rate = 0;
+      FapArgs fa = {};
+      fa.op = OP;
+      fa.key = sm->fap_key;
+      fa.broken = &sm->fap_broken;
+      fa.nrows = rblocks;
+      fa.part = scratch<int64_t>(ctx, "fap_part", (uint64_t)rblocks * WAVE);
+      const unsigned g1 = std::max(1u, std::min(256u, rblocks / 128));
+      int64_t* tmp = scratch<int64_t>(ctx, "fap_tmp", (uint64_t)g1 * WAVE);
+      auto reg = [&](auto aggc) {
+        constexpr int A = decltype(aggc)::value;
+        static const unsigned stat_lds = [] {
+          hipFuncAttributes at = {};
+          return hipFuncGetAttributes(&at, (const void*)k_ds_reg<A>) == hipSuccess ? (unsigned)at.sharedSizeBytes
+                                                                                    : 18960u;
+        }();
+        const unsigned pad = stat_lds < 40960u ? 40960u - stat_lds : 0u;
+        EV_START(ctx, 8);
+        LAUNCH_STOP(EV_STOP_K(ctx, 9), (k_ds_reg<A>), dim3(rblocks), dim3(256), pad, st, u.da, gr, u.row_ncells,
+                    u.row_val_len, 0u, fa);
+        EV_STOP_M(ctx, 9);
+      };
+      switch (d->ds_agg) {
+        case 0: reg(std::integral_constant<int, 0>()); break;
+        case 1: reg(std::integral_constant<int, 1>()); break;
+        case 2: reg(std::integral_constant<int, 2>()); break;
+        default: reg(std::integral_constant<int, 3>()); break;
+      }
+      ctx->hot_kernel = TSDBHIP_HOT_DS_CHUNKS;
+      LAUNCH((k_fap_rows<OP>), dim3(g1), dim3(1024), 0, st, (const int64_t*)fa.part, rblocks, tmp);
+      LAUNCH((k_ug_fap_final64v<OP>), dim3(1), dim3(1024), 0, st, (const int64_t*)tmp, g1, n_kept, o_pi, o_pc, sm,
+             pack, gridv, x0, step, kk, n, nb);
+    };
+    if (fop == 1) go(std::integral_constant<int, 1>());
+    else if (fop == 2) go(std::integral_constant<int, 2>());
+    else go(std::integral_constant<int, 0>());
+    if (sharded) {  // the agreement, the validity (MIN) and the 64-slot partials: one collective group
+      const XExtra ex[2] = {{o_pi, WAVE, fop ? X_I64 : X_U64, fop == 1 ? X_MIN : (fop == 2 ? X_MAX : X_SUM)},
+                            {o_pc, WAVE, X_U32, X_SUM}};
+      xchg_group(ctx, X, pack, (uint64_t*)&sm->n_input, ex, 2);
+    }
+    map_out_reserve(ctx, OUT_HDR + 17 * WAVE);
+    const uint64_t end_seq = ++ctx->pub_seq;
+    FinalArgs fo;
+    std::memset(&fo, 0, sizeof fo);
+    fo.T = WAVE;
+    fo.n_chunks = 1;
+    fo.grid = gridv;
+    fo.out_ts = (int64_t*)(ctx->map_out_dev + OUT_HDR);
+    fo.out_bits = fo.out_ts + WAVE;
+    fo.out_isint = (uint8_t*)(fo.out_bits + WAVE);
+    fo.nan_t = &sm->nan_t;
+    const XMove um = sharded ? unpack : XMove{};
+    Small* snap = (Small*)ctx->map_out_dev;
+    const Small ini = small_init();
+    auto fin = [&](auto aggc) {
+      constexpr int A = decltype(aggc)::value;
+      LAUNCH(k_fap_finish_end<A>, dim3(1), dim3(256), 0, st, sm, (const int64_t*)o_pi, (const uint32_t*)o_pc, fo,
+             (int32_t)sharded, um, snap, ini, (uint32_t*)nullptr, (const uint32_t*)gridv, (int64_t)0, end_seq);
+    };
+    if (agg == TSDBHIP_AGG_MIN) fin(std::integral_constant<int, 1>());
+    else if (agg == TSDBHIP_AGG_MAX) fin(std::integral_constant<int, 2>());
+    else if (agg == TSDBHIP_AGG_AVG) fin(std::integral_constant<int, 3>());
+    else fin(std::integral_constant<int, 0>());
+    EV_FINAL(ctx, 5);
+    HIPCHK(hipStreamSynchronize(st));
+    check_stamp(ctx, end_seq);
+    tm.late_stamp = ctx->timing_late;
+    std::memcpy(&h, ctx->map_out, sizeof h);
+    if (!h.fap_done) {
+      // the group did not stand (somewhere): the call state back to its
+      // initial values, the general path runs the call
+      const uint64_t seq2 = ++ctx->pub_seq;
+      LAUNCH(k_call_end, dim3(1), dim3(256), 0, st, sm, (Small*)ctx->map_out_dev, small_init(), (uint32_t*)nullptr,
+             (const uint32_t*)nullptr, (uint64_t)0, (int64_t)0, BadArgs{}, seq2, (const uint32_t*)nullptr);
+      HIPCHK(hipStreamSynchronize(st));
+      check_stamp(ctx, seq2);
+      ctx->sm_ready = true;
+      return RC_UG_FALLBACK;
+    }
+    ctx->sm_ready = true;
+    const uint64_t T = h.T;
+    out->n_input_points = h.n_input;
+    tm.n_grid = T;
+    tm.paths |= TSDBHIP_PATH_ALIGNED_GROUP;
+    if (sharded) {
+      tm.n_collectives = X->n_coll;
+      tm.x_bytes = X->x_bytes;
+    }
+    if (ctx->hot_kernel) tm.hot_ms = ev_ms(ctx, 8, 9);
+    tm.hot_kernel = ctx->hot_kernel;
+    tm.total_ms = ev_ms(ctx, 0, 5);
+    tm.n_emitted = (uint64_t)nb * n_kept;
+    ctx->timing = tm;
+    if (T > out->capacity && ctx->want_output) {
+      out->err_code = TSDBHIP_E_CAPACITY;
+      return TSDBHIP_E_CAPACITY;
+    }
+    if (ctx->want_output) {
+      const uint8_t* hb = ctx->map_out;
+      std::memcpy(out->ts, hb + OUT_HDR, T * 8);
+      std::memcpy(out->bits, hb + OUT_HDR + 8 * WAVE, T * 8);
+      std::memcpy(out->is_int, hb + OUT_HDR + 16 * WAVE, T);
+    }
+    out->n_out = T;
+    out->err_code = TSDBHIP_OK;
+    out->err_index = -1;
+    return TSDBHIP_OK;
+  }
+
+  // ---- lockstep ----
+  const uint64_t T = rate ? n - 1 : n;
+  const bool flt = (q0 & 8u) != 0;
+  const int mode = (rate || flt) ? MODE_DBL : MODE_INT;
+  uint32_t* gridv = scratch<uint32_t>(ctx, "grid", T);
+  const bool small_out = T * 17 <= (256u << 10) && ctx->want_output;
+  map_out_reserve(ctx, OUT_HDR + (small_out ? 17 * T : 0));
+  uint8_t* outblk = small_out ? ctx->map_out_dev : scratch<uint8_t>(ctx, "outblk", OUT_HDR + 17 * T);
+  FinalArgs fin;
+  std::memset(&fin, 0, sizeof fin);
+  fin.T = T;
+  fin.n_chunks = 1;
+  fin.grid = gridv;
+  fin.rate = rate;
+  fin.out_ts = (int64_t*)(outblk + OUT_HDR);
+  fin.out_bits = fin.out_ts + T;
+  fin.out_isint = (uint8_t*)(fin.out_bits + T);
+  fin.nan_t = &sm->nan_t;
+  // tiles of LS_TILE grid points x chunks of spans (as the general path's ls_reduce)
+  const uint32_t n_tiles = (uint32_t)((T + LS_TILE - 1) / LS_TILE);
+  uint64_t want = std::max<uint64_t>(1, 16384 / n_tiles);
+  want = std::min<uint64_t>(want, std::max<uint32_t>(1, n_kept / LS_MIN_SPC));
+  const uint32_t spc = (uint32_t)((n_kept + want - 1) / want);
+  const uint32_t n_chunks_s = (n_kept + spc - 1) / spc;
+  const uint32_t n_chunks = (n_chunks_s + LS_GROUP - 1) / LS_GROUP;  // (a block's chunks merged in LDS)
+  ReduceArgs r;
+  std::memset(&r, 0, sizeof r);
+  r.T = T;
+  r.n_chunks = n_chunks;
+  r.n_kept = n_kept;
+  alloc_partials(ctx, r, "p_", (uint64_t)n_chunks * T, agg);
+  LsPlan lsp = {};
+  lsp.a.d_voff = u.uk_vo;
+  lsp.a.d_qoff = u.uk_qo;
+  lsp.a.val = u.da.val;
+  lsp.a.qual = u.da.qual;
+  lsp.a.n = n;
+  lsp.a.q0 = q0;
+  lsp.a.step = step;
+  lsp.a.broken = &sm->ls_broken;
+  lsp.a.spc = spc;
+  lsp.a.n_tiles = n_tiles;
+  lsp.a.n_chunks = n_chunks_s;
+  lsp.a.grid_out = gridv;
+  lsp.a.x0 = x0;
+  lsp.a.g_off = rate ? 1u : 0u;
+  lsp.w8 = (q0 & 7u) == 7u;
+  lsp.flt = flt;
+  tm.paths |= TSDBHIP_PATH_LOCKSTEP;
+  ctx->hot_kernel = TSDBHIP_HOT_LOCKSTEP;
+  const unsigned blocks = n_tiles * n_chunks;
+  FinalArgs f = fin;
+  f.n_chunks = n_chunks;
+  if (!sharded) {
+    dispatch_lockstep(ctx, agg, rate, blocks, r, lsp, f, true);
+  } else {
+    const int nr = X->nranks, rk = X->rank;
+    dispatch_lockstep(ctx, agg, rate, blocks, r, lsp, f, false);
+    ReduceArgs src;
+    uint32_t n_src = 1;
+    if (mode == MODE_INT) {  // exact integer partials: one allreduce a field
+      ReduceArgs mine = r;
+      alloc_partials(ctx, mine, "m_", T, agg);
+      dispatch_combine(ctx, agg, mode, r, mine, T, n_chunks);
+      X->group_start(ctx);
+      for (const Fld& fl : partial_fields(mine, 0, agg, mode)) X->allreduce(ctx, fl.p, T, fl.t, fl.op);
+      X->allreduce(ctx, &sm->ls_broken, 1, X_U32, X_MAX);
+      X->allreduce(ctx, &sm->n_input, 1, X_U64, X_SUM);
+      X->group_end(ctx);
+      src = mine;
+    } else {  // doubles: every rank's slot gathered, merged in rank order
+      ReduceArgs all = r;
+      alloc_partials(ctx, all, "x_", (uint64_t)nr * T, agg);
+      ReduceArgs mine = all;
+      const uint64_t off = (uint64_t)rk * T;
+      mine.p_cnt += off; mine.p_flag += off; mine.p_i += off; mine.p_d += off; mine.p_dhas += off;
+      if (agg == TSDBHIP_AGG_DEV) { mine.p_wim += off; mine.p_wiv += off; mine.p_wdm += off; mine.p_wdv += off; }
+      dispatch_combine(ctx, agg, mode, r, mine, T, n_chunks);
+      const std::vector<Fld> fm = partial_fields(mine, 0, agg, mode), fa = partial_fields(all, 0, agg, mode);
+      X->group_start(ctx);
+      for (size_t i = 0; i < fm.size(); i++) X->allgather(ctx, fm[i].p, fa[i].p, T * fm[i].esz);
+      X->allreduce(ctx, &sm->ls_broken, 1, X_U32, X_MAX);
+      X->allreduce(ctx, &sm->n_input, 1, X_U64, X_SUM);
+      X->group_end(ctx);
+      src = all;
+      n_src = (uint32_t)nr;
+    }
+    FinalArgs ff = fin;
+    ff.n_chunks = n_src;
+    src.n_chunks = n_src;
+    dispatch_final(ctx, agg, mode, rate, src, ff);
+  }
+  const uint64_t end_seq = ++ctx->pub_seq;
+  LAUNCH(k_call_end, dim3(1), dim3(256), 0, st, sm, (Small*)ctx->map_out_dev, small_init(), (uint32_t*)nullptr,
+         (const uint32_t*)nullptr, (uint64_t)0, (int64_t)0, BadArgs{}, end_seq, (const uint32_t*)nullptr);
+  EV_FINAL(ctx, 5);
+  HIPCHK(hipStreamSynchronize(st));
+  check_stamp(ctx, end_seq);
+  tm.late_stamp = ctx->timing_late;
+  const uint8_t* hb = ctx->map_out;
+  std::memcpy(&h, hb, sizeof h);
+  ctx->sm_ready = true;
+  if (h.ls_broken) {  // (agreed over the ranks) the proposal did not hold: the proven path runs the call
+    ctx->timing = tm;
+    return RC_REDO;
+  }
+  out->n_input_points = h.n_input;
+  if (sharded) {
+    tm.n_collectives = X->n_coll;
+    tm.x_bytes = X->x_bytes;
+  }
+  tm.n_grid = T;
+  if (ctx->hot_kernel) tm.hot_ms = ev_ms(ctx, 8, 9);
+  tm.hot_kernel = ctx->hot_kernel;
+  tm.total_ms = ev_ms(ctx, 0, 5);
+  tm.n_emitted = 0;
+  ctx->timing = tm;
+  uint64_t n_ok = T;
+  int code = TSDBHIP_OK;
+  int64_t err_at = -1;
+  if (h.nan_t != ~0ull) {
+    err_at = (int64_t)h.nan_t;
+    code = TSDBHIP_E_NAN_INF;
+    n_ok = (uint64_t)err_at;
+  }
+  if (n_ok > out->capacity && ctx->want_output) {
+    out->err_code = TSDBHIP_E_CAPACITY;
+    return TSDBHIP_E_CAPACITY;
+  }
+  if (!ctx->want_output) {
+  } else if (n_ok && small_out) {
+    std::memcpy(out->ts, hb + OUT_HDR, n_ok * 8);
+    std::memcpy(out->bits, hb + OUT_HDR + 8 * T, n_ok * 8);
+    std::memcpy(out->is_int, hb + OUT_HDR + 16 * T, n_ok);
+  } else if (n_ok) {
+    HIPCHK(hipMemcpyAsync(out->ts, fin.out_ts, n_ok * 8, hipMemcpyDeviceToHost, st));
+    HIPCHK(hipMemcpyAsync(out->is_int, fin.out_isint, n_ok, hipMemcpyDeviceToHost, st));
+    HIPCHK(hipMemcpyAsync(out->bits, fin.out_bits, n_ok * 8, hipMemcpyDeviceToHost, st));
+    HIPCHK(hipStreamSynchronize(st));
+  }
+  out->n_out = n_ok;
+  out->err_code = code;
+  out->err_index = err_at;
+  return code;
+}
+
 // ------------------------------------------------------- the hot path ----
 // ls_allow: the lockstep proposal may be tried (k_direct_opt / k_lockstep);
 // false for the rerun after k_lockstep found a qualifier off the proposal
-constexpr int RC_REDO = 1000;
-static int spangroup_run_once(Slot* ctx, const tsdbhip_sg_desc* d, tsdbhip_sg_out* out, bool ls_allow) {
+// ug_allow: the uniform path (uniform_run) may be taken; false for the rerun
+// after it found the group not uniform
+static int spangroup_run_once(Slot* ctx, const tsdbhip_sg_desc* d, tsdbhip_sg_out* out, bool ls_allow,
+                              bool ug_allow) {
   const bool dev = (d->flags & TSDBHIP_DESC_DEVICE) != 0;
   const bool exact = (d->flags & TSDBHIP_EXACT_ORDER) != 0;
   // (a 1-rank communicator runs the same exchange code: tests use it)
@@ -1544,6 +2035,24 @@ static int spangroup_run_once(Slot* ctx, const tsdbhip_sg_desc* d, tsdbhip_sg_ou
   uint64_t* eoff = nullptr;
   bool pub1 = false;
   HostPub p1 = {};
+  // the uniform path's queries (uniform_run): lockstep (no downsampling, the
+  // conditions of the general path's lockstep try) or the aligned group
+  // (downsampled exact integer aggregation); the spans' class keys are
+  // proposed at assembly for them
+  const bool auto_dec = ctx->opt.decode == DEC_AUTO;
+  const bool ug_ls_q = ug_allow && auto_dec && interval == 0 && ls_allow && ctx->opt.lockstep && !exact &&
+                       (agg != TSDBHIP_AGG_DEV || rate);
+  const bool ug_fap_q = ug_allow && auto_dec && interval > 0 && !rate && ds_agg <= 3 && agg <= 3 && !exact &&
+                        ctx->opt.aligned_group && !ctx->opt.timing_detail;
+  const bool ug_q = ug_ls_q || ug_fap_q;
+  // sharded lockstep: the ranks agree on the key before the host's round trip
+  const bool ug_agree = ug_ls_q && sharded;
+  uint64_t* u_key1 = ug_q ? scratch<uint64_t>(ctx, "u_key1", S) : nullptr;
+  uint64_t* u_key2 = ug_q ? scratch<uint64_t>(ctx, "u_key2", S) : nullptr;
+  uint64_t* u_vo = ug_q ? scratch<uint64_t>(ctx, "u_vo", S) : nullptr;
+  uint64_t* u_qo = ug_q ? scratch<uint64_t>(ctx, "u_qo", S) : nullptr;
+  uint64_t* uk_vo = ug_q ? scratch<uint64_t>(ctx, "uk_vo", S) : nullptr;
+  uint64_t* uk_qo = ug_q ? scratch<uint64_t>(ctx, "uk_qo", S) : nullptr;
   {
     AssembleArgs a;
     a.span_row_start = span_row_start; a.row_base = row_base; a.row_ncells = row_ncells;
@@ -1553,21 +2062,37 @@ static int spangroup_run_once(Slot* ctx, const tsdbhip_sg_desc* d, tsdbhip_sg_ou
     a.sp_last = sp_last; a.sp_kept = sp_kept; a.sp_cap = sp_cap; a.sp_q1 = sp_q1;
     a.sp_q1_shift = sp_q1s; a.sp_q1_rs = sp_q1rs; a.sp_ovf_cell = sp_ovf; a.err = &sm->err;
     a.span0 = sharded ? d->span0 : 0;
+    a.row_val_off = row_val_off;
+    a.u_key1 = u_key1; a.u_key2 = u_key2; a.u_vo = u_vo; a.u_qo = u_qo;
     // kept list, E offsets, counts and bounds (unsharded groups of up to
     // KC_MAX spans: the kernel hands the call state to the host itself)
     kept = scratch<uint32_t>(ctx, "kept", S);
     eoff = scratch<uint64_t>(ctx, "eoff", S);
-    pub1 = S && S <= KC_MAX;
+    pub1 = S && S <= KC_MAX && !ug_agree;
     p1 = pub1 ? next_pub(ctx, sizeof(Small)) : HostPub{};
     KeptArgs K;
     K.kept = sp_kept; K.cap = sp_cap; K.ncells = sp_ncells; K.n = S; K.kept_list = kept; K.eoff_k = eoff;
     K.n_input = &sm->n_input; K.sp_first = sp_first; K.sp_last = sp_last; K.bound = sm->bound;
     K.n_kept_out = &sm->n_kept; K.e_total_out = &sm->e_total; K.pub = p1; K.pub_src = (const uint64_t*)sm;
+    K.u_key1 = u_key1; K.u_key2 = u_key2; K.u_vo = u_vo; K.u_qo = u_qo; K.uk_vo = uk_vo; K.uk_qo = uk_qo;
+    K.ukey = sm->ukey;
     // one block: assembly + kept list in one launch, for groups with few rows
     // (the block's 16 waves walk the deferred spans: a group of long spans of
     // many rows, C4's, needs the wave-per-span kernel's whole grid)
     if (S && S <= 1024 && R <= 8192) {
       LAUNCH(k_assemble_small, dim3(1), dim3(1024), 0, st, a, K);
+    } else if (S > KC_MAX && R <= 2ull * S) {
+      // (nearly) single-row spans: assembly + tile sums in one launch, then
+      // the scatter (its last block publishes the call state)
+      const uint32_t na = (S + 255) / 256, nt = (S + 1023) / 1024;  // (assembly tiles of 256, scatter tiles of 1024)
+      KeptTile* ts = scratch<KeptTile>(ctx, "kept_tiles", na);
+      ulonglong2* tke = scratch<ulonglong2>(ctx, "kept_tiles_ke", na);
+      LAUNCH(k_assemble_tiles, dim3(na), dim3(256), 0, st, a, ts, tke);
+      pub1 = !ug_agree;
+      p1 = pub1 ? next_pub(ctx, sizeof(Small)) : HostPub{};
+      LAUNCH(k_kept_scatter_tiles, dim3(nt), dim3(256), 0, st, sp_kept, sp_cap, S, (const KeptTile*)ts,
+             (const ulonglong2*)tke, 4u, na, kept, eoff, &sm->n_input, sm->bound, &sm->n_kept, &sm->e_total, p1,
+             (const uint64_t*)sm, K);
     } else if (S) {  // thread per span, then a wave per span for the ones it queued
       uint32_t* alist = scratch<uint32_t>(ctx, "asm_list", S);
       uint32_t* acount = &sm->cnt[0];
@@ -1579,12 +2104,15 @@ static int spangroup_run_once(Slot* ctx, const tsdbhip_sg_desc* d, tsdbhip_sg_ou
       } else {  // bigger groups: tile sums, then per-tile offsets + scatter
         const uint32_t nt = (S + 1023) / 1024;
         KeptTile* ts = scratch<KeptTile>(ctx, "kept_tiles", nt);
-        LAUNCH(k_kept_tiles, dim3(nt), dim3(256), 0, st, sp_kept, sp_cap, sp_ncells, sp_first, sp_last, S, ts);
+        ulonglong2* tke = scratch<ulonglong2>(ctx, "kept_tiles_ke", nt);
+        LAUNCH(k_kept_tiles, dim3(nt), dim3(256), 0, st, sp_kept, sp_cap, sp_ncells, sp_first, sp_last, S, ts, tke,
+               (const uint64_t*)u_key1, (const uint64_t*)u_key2);
         // (its last block publishes the call state)
-        pub1 = true;
-        p1 = next_pub(ctx, sizeof(Small));
-        LAUNCH(k_kept_scatter_tiles, dim3(nt), dim3(256), 0, st, sp_kept, sp_cap, S, (const KeptTile*)ts, kept,
-               eoff, &sm->n_input, sm->bound, &sm->n_kept, &sm->e_total, p1, (const uint64_t*)sm);
+        pub1 = !ug_agree;
+        p1 = pub1 ? next_pub(ctx, sizeof(Small)) : HostPub{};
+        LAUNCH(k_kept_scatter_tiles, dim3(nt), dim3(256), 0, st, sp_kept, sp_cap, S, (const KeptTile*)ts,
+               (const ulonglong2*)tke, 1u, nt, kept, eoff, &sm->n_input, sm->bound, &sm->n_kept, &sm->e_total, p1,
+               (const uint64_t*)sm, K);
       }
     }
   }
@@ -1592,6 +2120,18 @@ static int spangroup_run_once(Slot* ctx, const tsdbhip_sg_desc* d, tsdbhip_sg_ou
   // bounds; one collective after the local grids tells whether they agree,
   // and only when they do not are the bitmaps remapped and exchanged.)
   Small h;
+  if (ug_agree) {
+    // the uniform path's key agreement (sharded lockstep queries, every rank):
+    // the first error, the fewest kept spans and the keys' [min, max] over
+    // the ranks, one MIN allreduce into Small.xh[0..5]
+    const XField ag[6] = {{&sm->err, 5, 0},     {&sm->n_kept, 5, 0},  {&sm->ukey[0], 5, 0},
+                          {&sm->ukey[1], 6, 0}, {&sm->ukey[2], 5, 0}, {&sm->ukey[3], 6, 0}};
+    const XMove m = xchg_desc(ctx, ag, 6, (uint64_t*)sm->xh);
+    LAUNCH(k_xmove, dim3(1), dim3(64), 0, st, m);
+    X->group_start(ctx);
+    X->allreduce(ctx, m.buf, 6, X_U64, X_MIN);
+    X->group_end(ctx);
+  }
   if (!pub1) {  // (the state's last writer cannot publish it: a one-wave kernel does)
     p1 = next_pub(ctx, sizeof(Small));
     LAUNCH(k_publish, dim3(1), dim3(64), 0, st, p1, (const uint64_t*)sm);
@@ -1658,6 +2198,48 @@ static int spangroup_run_once(Slot* ctx, const tsdbhip_sg_desc* d, tsdbhip_sg_ou
   da.e_flt = e_flt; da.e_len = e_len; da.e_bad = e_bad; da.start = d->start_time; da.end = d->end_time;
   da.interval = interval; da.ds_agg = ds_agg; da.rate = rate; da.err = &sm->err; da.gflags = sm->gflags;
   da.range = sm->range; da.fstar = &sm->fstar; da.span0 = sharded ? d->span0 : 0; da.sp_first = sp_first;
+  // ---- the uniform path (uniform_run): every kept span proposed one class key
+  if (ug_q) {
+    UgIn u = {};
+    u.d = d; u.X = X; u.sm = sm; u.da = da; u.row_ncells = row_ncells; u.row_val_len = row_val_len;
+    u.uk_vo = uk_vo; u.uk_qo = uk_qo; u.n_kept = n_kept;
+    bool take = false;
+    const bool local_ok = !poisoned && n_kept > 0 && h.ukey[0] != ~0ull && h.ukey[0] == h.ukey[1] &&
+                          h.ukey[2] == h.ukey[3] && (uint32_t)h.ukey[0] >= 64;
+    if (ug_ls_q) {
+      u.lockstep = true;
+      if (sharded) {  // (from the agreed words alone: every rank takes the same branch)
+        const unsigned long long* x = h.xh;
+        take = x[0] == ERR_NONE && x[1] > 0 && x[2] != ~0ull && x[2] == ~x[3] && x[4] == ~x[5] &&
+               (uint32_t)x[2] >= 64;
+        u.k1 = x[2];
+        u.k2 = x[4];
+      } else {
+        const uint32_t n = (uint32_t)h.ukey[0];
+        const uint64_t ls_waves = (n + LS_TILE - 1) / LS_TILE * std::max<uint64_t>(1, n_kept / 64);
+        take = local_ok && (ctx->opt.lockstep == 2 || ls_waves >= 2048);
+        u.k1 = h.ukey[0];
+        u.k2 = h.ukey[2];
+      }
+    } else {
+      u.lockstep = false;
+      u.k1 = h.ukey[0];
+      u.k2 = h.ukey[2];
+      const uint32_t step = (uint32_t)(u.k2 >> 32), n = (uint32_t)u.k1;
+      const uint64_t kk = step ? ((uint64_t)interval + step - 1) / step : 0;
+      u.mine = local_ok && !(u.k2 & 8u) && kk && (n + kk - 1) / kk <= WAVE;
+      // (sharded: every rank makes the attempt, the key and the validity
+      // agreed in its one collective group; unsharded: only a group that is one)
+      take = sharded || u.mine;
+    }
+    if (take) {
+      const int rc = uniform_run(ctx, u, out, tm);
+      // (no bitmap was touched: it is as clean as scratch_zero_kept left it)
+      ctx->bitmap_clean = bm_clean || bitmap != nullptr;
+      ctx->tgdone_clean = tgd_clean;
+      return rc;
+    }
+  }
   if (detail) HIPCHK(hipEventRecord(ctx->ev[1], st));
   bool chunk_marked = false;     // k_ds_spans marked G for the spans it took
   bool direct = false;           // k_direct_scan took the no-downsampling path
@@ -2166,39 +2748,8 @@ static int spangroup_run_once(Slot* ctx, const tsdbhip_sg_desc* d, tsdbhip_sg_ou
     fin.out_isint = o_isint;
     fin.out_bits = o_bits;
     fin.nan_t = &sm->nan_t;
-    // per-t partial fields ([n][T] layout) under scratch names prefix + field
-    auto partials = [&](ReduceArgs& r, const char* pre, uint64_t np) {
-      auto nm = [&](const char* f) { return std::string(pre) + f; };
-      r.p_cnt = scratch<uint32_t>(ctx, nm("cnt").c_str(), np);
-      r.p_flag = scratch<uint8_t>(ctx, nm("flag").c_str(), np);
-      r.p_i = scratch<int64_t>(ctx, nm("i").c_str(), np);
-      r.p_d = scratch<double>(ctx, nm("d").c_str(), np);
-      r.p_dhas = scratch<uint32_t>(ctx, nm("dhas").c_str(), np);
-      r.p_wim = r.p_wiv = r.p_wdm = r.p_wdv = nullptr;
-      if (agg == TSDBHIP_AGG_DEV) {
-        r.p_wim = scratch<double>(ctx, nm("wim").c_str(), np);
-        r.p_wiv = scratch<double>(ctx, nm("wiv").c_str(), np);
-        r.p_wdm = scratch<double>(ctx, nm("wdm").c_str(), np);
-        r.p_wdv = scratch<double>(ctx, nm("wdv").c_str(), np);
-      }
-    };
-    // the fields acc_store writes for (agg, mode), at slot offset `off`
-    struct Fld { void* p; size_t esz; XType t; XOp op; };
-    auto fields = [&](const ReduceArgs& r, uint64_t off) {
-      std::vector<Fld> v;
-      v.push_back({r.p_cnt + off, 4, X_U32, X_SUM});
-      if (mode == MODE_DUAL || agg == 1 || agg == 2) v.push_back({r.p_flag + off, 1, X_U8, X_MAX});
-      if (mode != MODE_DBL && agg != 4)
-        v.push_back({r.p_i + off, 8, agg == 1 ? X_I64 : agg == 2 ? X_I64 : X_U64,
-                     agg == 1 ? X_MIN : agg == 2 ? X_MAX : X_SUM});
-      if (mode != MODE_INT && agg != 4) v.push_back({r.p_d + off, 8, X_F64, X_SUM});
-      if (mode != MODE_INT && (agg == 1 || agg == 2)) v.push_back({r.p_dhas + off, 4, X_U32, X_MAX});
-      if (agg == 4) {
-        if (mode != MODE_DBL) { v.push_back({r.p_wim + off, 8, X_F64, X_SUM}); v.push_back({r.p_wiv + off, 8, X_F64, X_SUM}); }
-        if (mode != MODE_INT) { v.push_back({r.p_wdm + off, 8, X_F64, X_SUM}); v.push_back({r.p_wdv + off, 8, X_F64, X_SUM}); }
-      }
-      return v;
-    };
+    auto partials = [&](ReduceArgs& r, const char* pre, uint64_t np) { alloc_partials(ctx, r, pre, np, agg); };
+    auto fields = [&](const ReduceArgs& r, uint64_t off) { return partial_fields(r, off, agg, mode); };
     // one reduce launch over this rank's kept spans; `init`: the per-t state
     // to continue from (one chunk)
     auto run_reduce = [&](bool one_chunk, bool finalize, const ReduceArgs* init) {
@@ -2259,29 +2810,27 @@ static int spangroup_run_once(Slot* ctx, const tsdbhip_sg_desc* d, tsdbhip_sg_ou
       return r;
     };
     // the lockstep group: tiles of LS_TILE grid points x chunks of spans
-#ifndef LS_MIN_SPC
-#define LS_MIN_SPC 128  // fewest spans a lockstep chunk (the n_chunks x T partials the combine reads; 64: the C3 rate-sum 8-way shard 1.07 ms, 128: 0.98-1.00, 256: 0.99-1.00; 1M spans unchanged)
-#endif
     auto ls_reduce = [&](bool finalize) {
       const uint32_t n_tiles = (uint32_t)((T + LS_TILE - 1) / LS_TILE);
       uint64_t want = std::max<uint64_t>(1, 16384 / n_tiles);
       want = std::min<uint64_t>(want, std::max<uint32_t>(1, n_kept / LS_MIN_SPC));
       const uint32_t spc = (uint32_t)((n_kept + want - 1) / want);
       const uint32_t n_chunks = (n_kept + spc - 1) / spc;
+      const uint32_t n_cg = (n_chunks + LS_GROUP - 1) / LS_GROUP;  // (a block's chunks merged in LDS)
       ReduceArgs r;
       std::memset(&r, 0, sizeof r);
       r.T = T;
-      r.n_chunks = n_chunks;
+      r.n_chunks = n_cg;
       r.n_kept = n_kept;
-      partials(r, "p_", (uint64_t)n_chunks * T);
+      partials(r, "p_", (uint64_t)n_cg * T);
       LsPlan p = lsp;
       p.a.spc = spc;
       p.a.n_tiles = n_tiles;
+      p.a.n_chunks = n_chunks;
       FinalArgs f = fin;
-      f.n_chunks = n_chunks;
+      f.n_chunks = n_cg;
       ctx->hot_kernel = TSDBHIP_HOT_LOCKSTEP;
-      const uint64_t n_waves = (uint64_t)n_tiles * n_chunks;
-      dispatch_lockstep(ctx, agg, rate, (unsigned)((n_waves + 3) / 4), r, p, f, finalize);
+      dispatch_lockstep(ctx, agg, rate, n_tiles * n_cg, r, p, f, finalize);
       return r;
     };
     // the aligned group: its block partials reduced into the 1-chunk layout
@@ -2523,11 +3072,18 @@ static int spangroup_run_once(Slot* ctx, const tsdbhip_sg_desc* d, tsdbhip_sg_ou
 // qualifier off the lockstep proposal (every rank of a sharded call agrees
 // on that, so all of them rerun)
 static int spangroup_run(Slot* ctx, const tsdbhip_sg_desc* d, tsdbhip_sg_out* out) {
-  const int rc = spangroup_run_once(ctx, d, out, true);
-  if (rc != RC_REDO) return rc;
-  const int rc2 = spangroup_run_once(ctx, d, out, false);
-  ctx->timing.paths |= TSDBHIP_PATH_DIRECT_REDO;
-  return rc2;
+  int rc = spangroup_run_once(ctx, d, out, true, true);
+  uint32_t paths = 0;
+  if (rc == RC_UG_FALLBACK) {  // (the uniform path's aligned group did not stand)
+    paths |= TSDBHIP_PATH_UNIFORM_FALLBACK;
+    rc = spangroup_run_once(ctx, d, out, true, false);
+  }
+  if (rc == RC_REDO) {
+    paths |= TSDBHIP_PATH_DIRECT_REDO;
+    rc = spangroup_run_once(ctx, d, out, false, false);
+  }
+  ctx->timing.paths |= paths;
+  return rc;
 }
 
 // One call on a plain context: a slot of its pool; x = the exchange of a

@@ -163,6 +163,8 @@ static int spangroup_run_batch(Slot* ctx, const tsdbhip_sg_desc* d, uint32_t G, 
     a.sp_last = sp_last; a.sp_kept = sp_kept; a.sp_cap = sp_cap; a.sp_q1 = sp_q1;
     a.sp_q1_shift = sp_q1s; a.sp_q1_rs = sp_q1rs; a.sp_ovf_cell = sp_ovf; a.err = &sm->err;
     a.span0 = 0;
+    a.row_val_off = nullptr;
+    a.u_key1 = a.u_key2 = a.u_vo = a.u_qo = nullptr;
     uint32_t* alist = scratch<uint32_t>(ctx, "asm_list", S);
     uint32_t* acount = scratch<uint32_t>(ctx, "asm_count", 1, true);
     LAUNCH(k_assemble_fast, dim3(grid_for(S, 256)), dim3(256), 0, st, a, alist, acount);

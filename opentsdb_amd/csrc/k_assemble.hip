@@ -41,6 +41,14 @@ struct AssembleArgs {
   unsigned long long* err;  // [1] first error (err_raise key)
   uint64_t span0;           // global index of span 0 (a shard's offset): the
                             // error order across ranks is the global span order
+  // the uniform-group proposal (spangroup_run's uniform path; null: not
+  // made): per span its class key (x0 << 32 | n, step << 32 | q0), ~0 in the
+  // first word when the span proposes none, and its row's byte offsets
+  const uint64_t* row_val_off;
+  uint64_t* u_key1;
+  uint64_t* u_key2;
+  uint64_t* u_vo;
+  uint64_t* u_qo;
 };
 
 DEVI int64_t row_first_ts(const AssembleArgs& a, uint64_t r) {
@@ -198,6 +206,35 @@ DEVI void assemble_finish(const AssembleArgs& a, uint32_t s, bool has_rows) {
 // chain after the other: spans of many rows — a day of hourly rows — go to
 // the wave kernel, which loads 64 rows at once.)
 constexpr uint32_t ASM_ROWS = 4;
+// The uniform-group proposal of a one-row span of n >= 2 cells (every row
+// check of the fast case passed): one value width W (8 or 4 B), the
+// qualifiers of cells 0, 1 and n-1 on ts = x0 + c*step with one flags nibble,
+// every point inside [start, end]. Spans proposing one key are one RowSeq on
+// one cadence each (RowSeq.java:360-497), so their union grid is that cadence
+// (SpanGroup.java:510-608); the kernels that take the group prove every other
+// qualifier as they stream (k_lockstep, k_ds_reg).
+DEVI bool ug_probe(const AssembleArgs& a, uint64_t r0, uint32_t n, uint64_t& k1, uint64_t& k2, uint64_t& vo,
+                   uint64_t& qo) {
+  const uint32_t vb = a.row_val_len[r0] - 1;  // (n >= 2: a compacted row ends with its meta byte)
+  const uint32_t W = vb / n;
+  qo = a.row_qual_off[r0];
+  vo = a.row_val_off[r0];
+  if (!((W == 8 || W == 4) && vb == W * n && (qo & 1) == 0 && (vo & (W - 1)) == 0)) return false;
+  const uint32_t q0 = load_qual(a.qual, qo), q1 = load_qual(a.qual, qo + 2), ql = load_qual(a.qual, qo + 2ull * (n - 1));
+  const uint32_t fl = q0 & 15u;
+  const uint32_t d0 = q0 >> 4, d1 = q1 >> 4, dl = ql >> 4;
+  if (!((fl & 7u) == W - 1 && (q1 & 15u) == fl && (ql & 15u) == fl && d1 > d0 &&
+        (uint64_t)d0 + (uint64_t)(n - 1) * (d1 - d0) == dl))
+    return false;
+  const uint32_t step = d1 - d0;
+  const int64_t first = (int64_t)a.row_base[r0] + d0;
+  const int64_t last = first + (int64_t)(n - 1) * step;
+  if (!(first >= a.start && last <= a.end && last < (1ll << 32))) return false;
+  k1 = ((uint64_t)first << 32) | n;
+  k2 = ((uint64_t)step << 32) | q0;
+  return true;
+}
+
 // The thread-per-span case for span s (< n_spans); true: deferred to the
 // wave walk.
 DEVI bool assemble_fast_one(const AssembleArgs& a, uint32_t s) {
@@ -236,6 +273,14 @@ DEVI bool assemble_fast_one(const AssembleArgs& a, uint32_t s) {
       assemble_finish(a, s, true);
     } else {
       defer = true;
+    }
+    if (a.u_key1) {  // (a deferred span proposes nothing)
+      uint64_t k1 = ~0ull, k2 = 0, vo = 0, qo = 0;
+      if (ok && r1 - r0 == 1 && cell >= 2 && !ug_probe(a, r0, cell, k1, k2, vo, qo)) k1 = ~0ull;
+      a.u_key1[s] = k1;
+      a.u_key2[s] = k2;
+      a.u_vo[s] = vo;
+      a.u_qo[s] = qo;
     }
   }
   return defer;

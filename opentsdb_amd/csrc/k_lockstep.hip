@@ -21,8 +21,12 @@
 // Work unit: one wave = a tile of 512 grid points (8 consecutive points a
 // lane: one 16-B qualifier load and 2 / 4 16-B value loads a span) x a chunk
 // of spans, the spans streamed in order with the next span's loads in flight
-// while the current one is accumulated; per-t partials [n_chunks][T] in the
-// layout of k_reduce, combined in chunk order by the same finalize / exchange.
+// while the current one is accumulated. A block's four waves take four
+// consecutive chunks of one tile and merge their states in chunk order
+// through LDS, so the per-t partials [n_chunks / 4][T] (the layout of
+// k_reduce, combined in chunk order by the same finalize / exchange) are a
+// quarter of one a wave: C3's 2048 chunks x 3600 points x 21 B made the
+// combine read 155 MB.
 #pragma once
 #include "dev_common.h"
 #include "k_reduce.hip"
@@ -30,6 +34,14 @@
 namespace tsdb {
 
 constexpr uint32_t LS_TILE = 512;  // grid points a wave (8 a lane)
+constexpr uint32_t LS_GROUP = 4;   // chunks a block (its waves), merged into one partial
+
+// one lane's slot state as it crosses LDS for the block's merge
+struct LsSlot {
+  uint32_t cnt, flag, dhas, pad;
+  int64_t ia;
+  double da, wim, wiv, wdm, wdv;
+};
 
 struct LockstepArgs {
   const uint64_t* d_voff;  // [n_kept] value byte offset of the span's cell 0
@@ -41,7 +53,12 @@ struct LockstepArgs {
   uint32_t step;
   uint32_t spc;            // spans a chunk
   uint32_t n_tiles;
+  uint32_t n_chunks;       // chunks of spc spans; a block's 4 waves take 4 consecutive ones
+                           // of one tile and combine them in order (LS_GROUP partials a block)
   uint32_t* broken;        // [1] set when a qualifier differs from the proposal
+  // (the uniform path: G written by chunk 0's waves, G[g] = x0 + (g + g_off) step)
+  uint32_t* grid_out;
+  uint32_t x0, g_off;
 };
 
 template <uint32_t W, bool FLT>
@@ -87,13 +104,14 @@ DEVI void ls_load(const LockstepArgs& L, uint32_t k, uint32_t c0, uint32_t tile_
 
 template <int AGG, int MODE, bool RATE, uint32_t W, bool FLT>
 __global__ void __launch_bounds__(256) k_lockstep(ReduceArgs r, LockstepArgs L) {
+  __shared__ LsSlot s_x[LS_GROUP - 1][WAVE];
   const int lane = lane_id();
   // (uniform: the span loop's offsets and buffer descriptors stay scalar)
-  const uint32_t wave = __builtin_amdgcn_readfirstlane((blockIdx.x * blockDim.x + threadIdx.x) / WAVE);
-  if (wave >= L.n_tiles * r.n_chunks) return;
-  const uint32_t tile = wave % L.n_tiles, chunk = wave / L.n_tiles;
+  const uint32_t w = __builtin_amdgcn_readfirstlane(threadIdx.x / WAVE);
+  const uint32_t tile = blockIdx.x % L.n_tiles, cg = blockIdx.x / L.n_tiles;
+  const uint32_t chunk = cg * LS_GROUP + w;
   const uint32_t k0 = chunk * L.spc, k1 = min(r.n_kept, k0 + L.spc);
-  if (k0 >= k1) return;
+  const bool act = chunk < L.n_chunks && k0 < k1;  // (every wave reaches the block's merge)
   const uint32_t c0 = tile * LS_TILE + 8u * (uint32_t)lane;  // this lane's first grid point (and cell)
   const uint32_t tile_end = tile * LS_TILE + LS_TILE;
   const uint32_t n = L.n;
@@ -189,20 +207,49 @@ __global__ void __launch_bounds__(256) k_lockstep(ReduceArgs r, LockstepArgs L) 
   };
   // two register sets: the next span's loads are in flight while one is
   // accumulated (the last span reloads itself, so the loads stay straight-line)
-  LsRaw<W> ra, rb;
-  ls_load<W, RATE>(L, k0, c0, tile_end, ra);
-  for (uint32_t k = k0;;) {
-    ls_load<W, RATE>(L, min(k + 1, k1 - 1), c0, tile_end, rb);
-    process(ra, k);
-    if (++k >= k1) break;
-    ls_load<W, RATE>(L, min(k + 1, k1 - 1), c0, tile_end, ra);
-    process(rb, k);
-    if (++k >= k1) break;
-  }
-  if (ballot(bad != 0) && lane == 0) atomicOr(L.broken, 1u);
+  if (act) {
+    LsRaw<W> ra, rb;
+    ls_load<W, RATE>(L, k0, c0, tile_end, ra);
+    for (uint32_t k = k0;;) {
+      ls_load<W, RATE>(L, min(k + 1, k1 - 1), c0, tile_end, rb);
+      process(ra, k);
+      if (++k >= k1) break;
+      ls_load<W, RATE>(L, min(k + 1, k1 - 1), c0, tile_end, ra);
+      process(rb, k);
+      if (++k >= k1) break;
+    }
+    if (ballot(bad != 0) && lane == 0) atomicOr(L.broken, 1u);
+    if (L.grid_out && chunk == 0) {
 #pragma unroll
-  for (int i = 0; i < 8; i++)
-    if (valid[i]) acc_store<AGG, MODE>(r, (uint64_t)chunk * T + c0 + i, acc[i]);
+      for (int i = 0; i < 8; i++)
+        if (valid[i]) L.grid_out[c0 + i] = L.x0 + (c0 + (uint32_t)i + L.g_off) * L.step;
+    }
+  }
+  // the block's chunks merged in chunk order (span order), one slot at a time
+#pragma unroll
+  for (int i = 0; i < 8; i++) {
+    if (w > 0) {
+      LsSlot& x = s_x[w - 1][lane];
+      x.cnt = acc[i].cnt; x.flag = acc[i].flag; x.dhas = acc[i].dhas;
+      x.ia = acc[i].ia; x.da = acc[i].da;
+      x.wim = acc[i].wi.mean; x.wiv = acc[i].wi.var; x.wdm = acc[i].wd.mean; x.wdv = acc[i].wd.var;
+    }
+    __syncthreads();
+    if (w == 0) {
+#pragma unroll
+      for (uint32_t j = 0; j < LS_GROUP - 1; j++) {
+        const LsSlot& x = s_x[j][lane];
+        Acc b;
+        acc_init(b);
+        b.cnt = x.cnt; b.flag = x.flag; b.dhas = x.dhas; b.ia = x.ia; b.da = x.da;
+        b.wi.n = x.cnt; b.wi.mean = x.wim; b.wi.var = x.wiv;
+        b.wd.n = x.cnt; b.wd.mean = x.wdm; b.wd.var = x.wdv;
+        acc_merge<AGG, MODE>(acc[i], b);
+      }
+      if (valid[i]) acc_store<AGG, MODE>(r, (uint64_t)cg * T + c0 + i, acc[i]);
+    }
+    __syncthreads();
+  }
 }
 
 }  // namespace tsdb

@@ -123,6 +123,34 @@ struct KeptArgs {
   uint64_t* e_total_out;
   HostPub pub;
   const uint64_t* pub_src;
+  // the uniform-group proposal (null: not made): the spans' keys and row
+  // offsets (AssembleArgs.u_*), the kept spans' offsets by kept index, and
+  // the keys' [min, max, min, max] over the kept spans (Small.ukey)
+  const uint64_t* u_key1;
+  const uint64_t* u_key2;
+  const uint64_t* u_vo;
+  const uint64_t* u_qo;
+  uint64_t* uk_vo;
+  uint64_t* uk_qo;
+  unsigned long long* ukey;
+};
+// [min, max] of the kept spans' keys (uniform-group proposal), per thread
+struct UKeyAcc {
+  uint64_t a0, a1, b0, b1;
+  DEVI void init() { a0 = b0 = ~0ull; a1 = b1 = 0; }
+  DEVI void add(uint64_t k1, uint64_t k2) {
+    a0 = min(a0, k1); a1 = max(a1, k1); b0 = min(b0, k2); b1 = max(b1, k2);
+  }
+  DEVI void add(const UKeyAcc& o) {
+    a0 = min(a0, o.a0); a1 = max(a1, o.a1); b0 = min(b0, o.b0); b1 = max(b1, o.b1);
+  }
+  DEVI void wave_reduce() {
+#pragma unroll
+    for (int m = 1; m < WAVE; m <<= 1) {
+      a0 = min(a0, shfl_xor_u64(a0, m)); a1 = max(a1, shfl_xor_u64(a1, m));
+      b0 = min(b0, shfl_xor_u64(b0, m)); b1 = max(b1, shfl_xor_u64(b1, m));
+    }
+  }
 };
 // (a 1024-thread block)
 DEVI void kept_compact_block(const KeptArgs& A) {
@@ -134,6 +162,9 @@ DEVI void kept_compact_block(const KeptArgs& A) {
   __shared__ uint64_t s_wk[16], s_we[16];
   __shared__ uint64_t s_c[16];
   __shared__ int64_t s_f[16], s_l[16], s_fx[16], s_ln[16];
+  __shared__ UKeyAcc s_u[16];
+  UKeyAcc u;
+  u.init();
   const int t = threadIdx.x, lane = lane_id(), w = t / WAVE;
   const int wu = __builtin_amdgcn_readfirstlane(w);
   uint64_t ck = 0, ce = 0;  // carries: kept spans / E capacity before this round
@@ -178,6 +209,11 @@ DEVI void kept_compact_block(const KeptArgs& A) {
       if (fk[i]) {
         kept_list[rk] = (uint32_t)s;
         eoff_k[rk] = re;
+        if (A.u_key1) {
+          u.add(A.u_key1[s], A.u_key2[s]);
+          A.uk_vo[rk] = A.u_vo[s];
+          A.uk_qo[rk] = A.u_qo[s];
+        }
         cnt += fn[i];
         f = min(f, ff[i]);
         l = max(l, fl[i]);
@@ -199,12 +235,14 @@ DEVI void kept_compact_block(const KeptArgs& A) {
     fx = max(fx, (int64_t)shfl_xor_u64((uint64_t)fx, m));
     ln = min(ln, (int64_t)shfl_xor_u64((uint64_t)ln, m));
   }
+  if (A.u_key1) u.wave_reduce();
   if (lane == 0) {
     s_c[w] = cnt;
     s_f[w] = f;
     s_l[w] = l;
     s_fx[w] = fx;
     s_ln[w] = ln;
+    s_u[w] = u;
   }
   __syncthreads();
   if (t == 0) {
@@ -214,6 +252,11 @@ DEVI void kept_compact_block(const KeptArgs& A) {
       l = max(l, s_l[i]);
       fx = max(fx, s_fx[i]);
       ln = min(ln, s_ln[i]);
+      u.add(s_u[i]);
+    }
+    if (A.u_key1) {  // (the call state's initial keys are neutral: [~0, 0, ~0, 0])
+      A.ukey[0] = min((uint64_t)A.ukey[0], u.a0); A.ukey[1] = max((uint64_t)A.ukey[1], u.a1);
+      A.ukey[2] = min((uint64_t)A.ukey[2], u.b0); A.ukey[3] = max((uint64_t)A.ukey[3], u.b1);
     }
     *n_kept_out = ck;
     *e_total_out = ce;
@@ -243,15 +286,33 @@ struct KeptTile {
   uint64_t k, e, cnt;
   int64_t f, l, fx, ln;  // over the tile's kept spans with cells (neutral otherwise)
   uint64_t pad;
+  UKeyAcc u;             // the uniform-group keys over the tile's kept spans
 };
+// the block's UKeyAcc (256 threads) into thread 0's
+DEVI UKeyAcc ukey_block_256(UKeyAcc u, UKeyAcc* sh /* [4] */) {
+  u.wave_reduce();
+  __syncthreads();
+  if (lane_id() == 0) sh[threadIdx.x / WAVE] = u;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    u.add(sh[1]);
+    u.add(sh[2]);
+    u.add(sh[3]);
+  }
+  return u;
+}
 __global__ void __launch_bounds__(256) k_kept_tiles(const uint8_t* kept, const uint64_t* cap, const uint32_t* ncells,
                                                     const int64_t* sp_first, const int64_t* sp_last, uint32_t n,
-                                                    KeptTile* tile_sum) {
+                                                    KeptTile* tile_sum, ulonglong2* tile_ke, const uint64_t* u_key1,
+                                                    const uint64_t* u_key2) {
   __shared__ uint64_t sh_k[4], sh_e[4], sh_c[4];
   __shared__ int64_t sh_f[4], sh_l[4];
+  __shared__ UKeyAcc sh_u[4];
   const uint64_t base = (uint64_t)blockIdx.x * 1024 + 4 * threadIdx.x;
   uint64_t sk = 0, se = 0, cnt = 0;
   int64_t f = INT64_MAX, l = INT64_MIN, fx = INT64_MIN, ln = INT64_MAX;
+  UKeyAcc u;
+  u.init();
 #pragma unroll
   for (int i = 0; i < 4; i++) {
     const uint64_t s = base + i;
@@ -259,6 +320,7 @@ __global__ void __launch_bounds__(256) k_kept_tiles(const uint8_t* kept, const u
       se += cap[s];
       if (kept[s]) {
         sk++;
+        if (u_key1) u.add(u_key1[s], u_key2[s]);
         cnt += ncells[s];
         f = min(f, sp_first[s]);
         l = max(l, sp_last[s]);
@@ -275,26 +337,36 @@ __global__ void __launch_bounds__(256) k_kept_tiles(const uint8_t* kept, const u
   __syncthreads();
   fx = block_reduce_256(fx, [](int64_t x, int64_t y) { return max(x, y); }, sh_f);
   ln = block_reduce_256(ln, [](int64_t x, int64_t y) { return min(x, y); }, sh_l);
+  if (u_key1) u = ukey_block_256(u, sh_u);
   if (threadIdx.x == 0) {
     KeptTile o;
     o.k = sk; o.e = se; o.cnt = cnt; o.pad = 0;
+    o.u = u;
     // (a tile whose kept spans hold no cell leaves the bounds alone, as the
     // per-block atomics of the single-block path do)
     o.f = cnt ? f : INT64_MAX; o.l = cnt ? l : INT64_MIN; o.fx = cnt ? fx : INT64_MIN; o.ln = cnt ? ln : INT64_MAX;
     tile_sum[blockIdx.x] = o;
+    tile_ke[blockIdx.x] = make_ulonglong2(sk, se);
   }
 }
 
+// (tile_ke: the kept / capacity sums of the producer's tiles, `sub` of them
+// per 1024 spans of this kernel's tile, nt_sub in all: the prefix reads 16 B
+// a producer tile, the last block every tile's whole sums)
 __global__ void __launch_bounds__(256) k_kept_scatter_tiles(const uint8_t* kept, const uint64_t* cap, uint32_t n,
-                                                            const KeptTile* tile_sum, uint32_t* kept_list,
+                                                            const KeptTile* tile_sum, const ulonglong2* tile_ke,
+                                                            uint32_t sub, uint32_t nt_sub, uint32_t* kept_list,
                                                             uint64_t* eoff_k, unsigned long long* n_input,
                                                             unsigned long long* bound, uint64_t* n_kept_out,
                                                             uint64_t* e_total_out, HostPub pub,
-                                                            const uint64_t* pub_src) {
+                                                            const uint64_t* pub_src, KeptArgs U) {
   __shared__ uint64_t s_wk[4], s_we[4];
   __shared__ uint64_t sh_c[4];
   __shared__ int64_t sh_f[4], sh_l[4];
+  __shared__ UKeyAcc sh_u[4];
   __shared__ uint64_t s_pk, s_pe;
+  UKeyAcc u;
+  u.init();
   const int t = threadIdx.x, lane = lane_id(), w = t / WAVE;
   const uint32_t tile = blockIdx.x;
   const bool last = tile == gridDim.x - 1;
@@ -302,18 +374,21 @@ __global__ void __launch_bounds__(256) k_kept_scatter_tiles(const uint8_t* kept,
   // the totals of every tile)
   uint64_t pk = 0, pe = 0, cnt = 0;
   int64_t f = INT64_MAX, l = INT64_MIN, fx = INT64_MIN, ln = INT64_MAX;
-  for (uint32_t q = t; q < (last ? gridDim.x : tile); q += 256) {
-    const KeptTile v = tile_sum[q];
-    if (q < tile) {
-      pk += v.k;
-      pe += v.e;
-    }
-    cnt += v.cnt;
-    f = min(f, v.f);
-    l = max(l, v.l);
-    fx = max(fx, v.fx);
-    ln = min(ln, v.ln);
+  for (uint32_t q = t; q < tile * sub; q += 256) {
+    const ulonglong2 v = tile_ke[q];
+    pk += v.x;
+    pe += v.y;
   }
+  if (last)
+    for (uint32_t q = t; q < nt_sub; q += 256) {
+      const KeptTile v = tile_sum[q];
+      cnt += v.cnt;
+      f = min(f, v.f);
+      l = max(l, v.l);
+      fx = max(fx, v.fx);
+      ln = min(ln, v.ln);
+      u.add(v.u);
+    }
   pk = block_reduce_256(pk, [](uint64_t x, uint64_t y) { return x + y; }, sh_c);
   __syncthreads();
   pe = block_reduce_256(pe, [](uint64_t x, uint64_t y) { return x + y; }, sh_c);
@@ -353,6 +428,10 @@ __global__ void __launch_bounds__(256) k_kept_scatter_tiles(const uint8_t* kept,
     if (fk[i]) {
       kept_list[rk] = (uint32_t)s;
       eoff_k[rk] = re;
+      if (U.u_key1) {
+        U.uk_vo[rk] = U.u_vo[s];
+        U.uk_qo[rk] = U.u_qo[s];
+      }
     }
     rk += fk[i];
     re += fe[i];
@@ -366,6 +445,11 @@ __global__ void __launch_bounds__(256) k_kept_scatter_tiles(const uint8_t* kept,
   fx = block_reduce_256(fx, [](int64_t x, int64_t y) { return max(x, y); }, sh_f);
   __syncthreads();
   ln = block_reduce_256(ln, [](int64_t x, int64_t y) { return min(x, y); }, sh_l);
+  if (U.u_key1) u = ukey_block_256(u, sh_u);
+  if (t == 0 && U.u_key1) {
+    U.ukey[0] = min((uint64_t)U.ukey[0], u.a0); U.ukey[1] = max((uint64_t)U.ukey[1], u.a1);
+    U.ukey[2] = min((uint64_t)U.ukey[2], u.b0); U.ukey[3] = max((uint64_t)U.ukey[3], u.b1);
+  }
   if (t == 0 && cnt) {
     *n_input += cnt;
     bound[0] = min(bound[0], (unsigned long long)f);

@@ -146,8 +146,10 @@ def test_aligned_grids_skip_the_grid_exchange(mctx, dsi):
     rank's local grid is the global one, which the agreement header proves,
     so a call issues two collective launches, the header and the partials
      -- one when downsampled: the aligned group's partials
-    travel in the header's collective group; shards whose grids differ also
-    exchange bitmaps."""
+    travel in the header's collective group. Without downsampling these
+    shards take the uniform lockstep path: the key agreement, then the
+    partials. Shards whose grids differ also exchange bitmaps (after the
+    uniform path's key agreement, which every rank issues for such a query)."""
     ss = synth.regular(64, 600, _abi.SYN_INT64_COUNTER, seed=2, step=1)
     for agg in (0, 2):
         g, o = both(mctx, ss, agg=agg, dsi=dsi, dsa=3)
@@ -156,7 +158,7 @@ def test_aligned_grids_skip_the_grid_exchange(mctx, dsi):
     ss = synth.jittered(13, 70, seed=1, span_range=400_000, max_gap=700)
     g, o = both(mctx, ss, agg=0)
     assert_same(g, o)
-    assert mctx.timing().n_collectives == 3
+    assert mctx.timing().n_collectives == 4
 
 
 @pytest.mark.gpu

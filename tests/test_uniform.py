@@ -1,0 +1,154 @@
+"""The uniform path (uniform_run in api.hip): every kept span one row on one
+cadence with one class key (x0, n, step, flags), proposed at assembly from
+the qualifiers of cells 0, 1 and n-1 (ug_probe). The union grid is then that
+cadence (SpanGroup.java:510-608) and the call skips the grid kernels and the
+second host round trip: the lockstep reduction without downsampling, the
+aligned-group reduction with it (k_ds_reg). Every case is compared with the
+oracle (integers bit-exact, doubles at 1e-9 relative); the proposal's
+failures — a middle qualifier off the cadence that only the streaming kernel
+sees — fall back to the proven path and must give the same results and
+errors (timing.paths: PATH_UNIFORM, PATH_UNIFORM_FALLBACK, PATH_DIRECT_REDO)."""
+import pytest
+
+from helpers import I, T0, U32MAX, assert_same, corrupt_qual, run_both, with_option
+from opentsdb_amd import _abi, core, packing, synth
+
+pytestmark = pytest.mark.gpu
+I64, F32, F64 = _abi.SYN_INT64_COUNTER, _abi.SYN_FLOAT32, _abi.SYN_FLOAT64
+
+
+@pytest.fixture(autouse=True)
+def always(request):
+    """small groups: "always" takes the lockstep reduction whatever the size"""
+    yield from with_option(request, "lockstep", "always", "on")
+
+
+def paths(c):
+    return c.timing().paths
+
+
+@pytest.mark.parametrize("kind", [I64, F32, F64])
+@pytest.mark.parametrize("agg", [0, 1, 2, 3, 4])
+@pytest.mark.parametrize("rate", [False, True])
+def test_uniform_lockstep(ctx, kind, agg, rate):
+    ss = synth.regular(150, 1300, kind, seed=6, step=2)
+    g, o = run_both(ctx, ss, agg=agg, rate=rate)
+    assert_same(g, o)
+    if agg != 4 or rate:  # (integer dev: the span-ordered pass, never lockstep)
+        assert paths(ctx) & _abi.PATH_UNIFORM and paths(ctx) & _abi.PATH_LOCKSTEP
+    if (agg, rate, kind) == (4, False, I64):
+        assert not paths(ctx) & _abi.PATH_UNIFORM
+
+
+@pytest.mark.parametrize("agg", [0, 1, 2, 3])
+@pytest.mark.parametrize("dsa", [0, 1, 2, 3])
+def test_uniform_aligned_group(ctx, agg, dsa):
+    ss = synth.regular(200, 3600, I64, seed=12, step=1)
+    g, o = run_both(ctx, ss, 0, U32MAX, agg, False, 60, dsa)
+    assert_same(g, o)
+    p = paths(ctx)
+    assert p & _abi.PATH_UNIFORM and p & _abi.PATH_ALIGNED_GROUP and not p & _abi.PATH_UNIFORM_FALLBACK
+
+
+@pytest.mark.parametrize("what", ["delta+1", "float-flag", "width-4"])
+def test_uniform_aligned_group_broken_falls_back(ctx, what):
+    """a middle qualifier the proposal never read: k_ds_reg finds the span off
+    the cadence, the group does not stand, the general path runs the call"""
+    fn = {"delta+1": lambda q: q + 16, "float-flag": lambda q: q | 0x8, "width-4": lambda q: (q & ~0x7) | 0x3}[what]
+    # (step 2: the shifted delta stays increasing; a duplicate timestamp in a
+    # row is input the reference never produces, E_UNSORTED here)
+    ss = corrupt_qual(synth.regular(120, 1800, I64, seed=2, step=2), 77, 900, fn)
+    for agg in (0, 2):
+        g, o = run_both(ctx, ss, 0, U32MAX, agg, False, 60, 3)
+        assert_same(g, o)
+        assert paths(ctx) & _abi.PATH_UNIFORM_FALLBACK
+
+
+def test_uniform_not_proposed(ctx):
+    """spans that propose no key or different keys: the general path alone
+    (a window cutting the spans, minimal-width cells, a second row, phases)"""
+    ss = synth.regular(60, 1000, I64, seed=2, step=1)
+    for start, end in ((T0 + 10, U32MAX), (0, T0 + 500)):
+        g, o = run_both(ctx, ss, start=start, end=end, agg=0)
+        assert_same(g, o)
+        assert not paths(ctx) & _abi.PATH_UNIFORM
+    minimal = packing.pack_spans([I([(T0 + i, 7 * i + s) for i in range(300)]) for s in range(40)])
+    two_rows = packing.pack_spans([I([(T0 + 3000 + i, i) for i in range(1200)], minimal=False) for _ in range(40)])
+    phases = packing.pack_spans([I([(T0 + (s % 3) + 3 * i, i) for i in range(400)], minimal=False) for s in range(40)])
+    for ss in (minimal, two_rows, phases):
+        for dsi in (0, 60):
+            g, o = run_both(ctx, ss, agg=0, ds_interval=dsi, ds_agg=3 if dsi else 0)
+            assert_same(g, o)
+            assert not paths(ctx) & _abi.PATH_UNIFORM
+
+
+@pytest.fixture(scope="module", params=[2, 4, 8])
+def mctx(request):
+    from opentsdb_amd._lib import Context
+    c = Context(devices=[0] * request.param)
+    yield c
+    c.close()
+
+
+def both(c, ss, **kw):
+    import oracle
+    a = dict(start=0, end=U32MAX, agg=0, rate=False, dsi=0, dsa=0)
+    a.update(kw)
+    g = core.run_spanset(c, ss, a["start"], a["end"], a["agg"], a["rate"], a["dsi"], a["dsa"])
+    o = oracle.spangroup(ss, a["start"], a["end"], a["agg"], a["rate"], a["dsi"], a["dsa"])
+    return g, o
+
+
+@pytest.mark.timeout(120)
+@pytest.mark.parametrize("agg", [0, 2, 3, 4])
+@pytest.mark.parametrize("rate", [False, True])
+def test_uniform_sharded_lockstep(mctx, agg, rate):
+    """the ranks agree on the key before the round trip (one collective), the
+    partials travel in a second one"""
+    ss = synth.regular(8 * mctx.ranks, 900, I64, seed=4, step=1)
+    g, o = both(mctx, ss, agg=agg, rate=rate)
+    assert_same(g, o)
+    if agg != 4 or rate:
+        assert paths(mctx) & _abi.PATH_UNIFORM
+        assert mctx.timing().n_collectives == 2
+
+
+@pytest.mark.timeout(120)
+@pytest.mark.parametrize("agg", [0, 1, 2, 3])
+def test_uniform_sharded_aligned_group(mctx, agg):
+    """the key agreement, the validity and the 64-slot partials in one collective"""
+    ss = synth.regular(8 * mctx.ranks, 3600, I64, seed=9, step=1)
+    g, o = both(mctx, ss, agg=agg, dsi=60, dsa=3)
+    assert_same(g, o)
+    assert paths(mctx) & _abi.PATH_UNIFORM and paths(mctx) & _abi.PATH_ALIGNED_GROUP
+    assert mctx.timing().n_collectives == 1
+
+
+@pytest.mark.timeout(120)
+def test_uniform_sharded_ranks_on_other_keys(mctx):
+    """each rank uniform on its own key (phases differ by rank): the agreement
+    refuses the uniform path everywhere (lockstep) / the aligned group does
+    not stand anywhere (downsampled), and the general path gives the results"""
+    n = 4 * mctx.ranks
+    spans = [I([(T0 + (s >= n // 2) + 2 * i, s * 7 + i) for i in range(900)], minimal=False) for s in range(n)]
+    ss = packing.pack_spans(spans)
+    g, o = both(mctx, ss, agg=0)
+    assert_same(g, o)
+    assert not paths(mctx) & _abi.PATH_UNIFORM
+    g, o = both(mctx, ss, agg=2, dsi=60, dsa=3)
+    assert_same(g, o)
+    assert paths(mctx) & _abi.PATH_UNIFORM_FALLBACK
+
+
+@pytest.mark.timeout(120)
+def test_uniform_sharded_broken_in_one_rank(mctx):
+    """a middle qualifier off the cadence in the last rank: lockstep reruns on
+    the proven path, the aligned group falls back, every rank alike"""
+    ss = corrupt_qual(synth.regular(8 * mctx.ranks, 1800, I64, seed=4, step=2), 8 * mctx.ranks - 1, 1000,
+                      lambda q: q + 16)
+    g, o = both(mctx, ss, agg=0)
+    assert_same(g, o)
+    assert paths(mctx) & _abi.PATH_DIRECT_REDO
+    g, o = both(mctx, ss, agg=0, dsi=60, dsa=3)
+    assert_same(g, o)
+    assert paths(mctx) & _abi.PATH_UNIFORM_FALLBACK
