@@ -225,7 +225,14 @@ static void EV_START(Slot* ctx, int i) {
 // makes the call-end kernels' writes into mapped host memory (the state
 // snapshot, small results) visible to the host after the stream sync.
 #define EV_FINAL(ctx, i) HIPCHK(hipEventRecord((ctx)->ev[i], (ctx)->stream))
-#define LAUNCH(k, g, b, sh, st, ...) hipExtLaunchKernelGGL(k, g, b, sh, st, ev_take(), nullptr, 0, ##__VA_ARGS__)
+// (a launch without an event goes the plain way: hipExtLaunchKernel costs
+// more host time a call)
+#define LAUNCH(k, g, b, sh, st, ...)                                          \
+  do {                                                                        \
+    hipEvent_t e_ = ev_take();                                                \
+    if (e_) hipExtLaunchKernelGGL(k, g, b, sh, st, e_, nullptr, 0, ##__VA_ARGS__); \
+    else hipLaunchKernelGGL(k, g, b, sh, st, ##__VA_ARGS__);                  \
+  } while (0)
 #define LAUNCH_STOP(ev, k, g, b, sh, st, ...) hipExtLaunchKernelGGL(k, g, b, sh, st, ev_take(), ev, 0, ##__VA_ARGS__)
 static float ev_ms(Slot* ctx, int a, int b) {
   float ms = 0;
@@ -1162,6 +1169,18 @@ static Small small_init() {
   init.ukey[0] = init.ukey[2] = ~0ull;
   return init;
 }
+// the initial call state in device memory (a kernel argument by pointer: by
+// value it made every call-end launch copy ~1 KB of kernel arguments)
+static const Small* small_init_dev(Slot* ctx) {
+  Buf& b = ctx->bufs["small_init"];
+  if (!b.p) {
+    const Small init = small_init();
+    HIPCHK(hipMalloc(&b.p, sizeof init));
+    b.n = sizeof init;
+    HIPCHK(hipMemcpy(b.p, &init, sizeof init, hipMemcpyHostToDevice));
+  }
+  return (const Small*)b.p;
+}
 // Several MIN / MAX agreements on call-state fields as one MIN allreduce of a
 // packed buffer (across GPUs each collective costs a latency of its own;
 // one rank: the plain per-field calls)
@@ -1382,7 +1401,7 @@ DEVI void small_snap(Small* sm, Small* snap, const Small* init, uint64_t seq) {
   uint64_t* w = (uint64_t*)sm;
   for (uint32_t i = threadIdx.x; i < NW; i += blockDim.x) w[i] = in[i];
 }
-__global__ void __launch_bounds__(256) k_call_end(Small* sm, Small* snap, Small init, uint32_t* bitmap,
+__global__ void __launch_bounds__(256) k_call_end(Small* sm, Small* snap, const Small* init, uint32_t* bitmap,
                                                   const uint32_t* grid, uint64_t T, int64_t lo, BadArgs bad,
                                                   uint64_t seq, const uint32_t* done = nullptr) {
   __shared__ unsigned long long s_min[4];
@@ -1414,7 +1433,7 @@ __global__ void __launch_bounds__(256) k_call_end(Small* sm, Small* snap, Small 
       }
     }
     __syncthreads();  // (bad_at final)
-    small_snap(sm, snap, &init, seq);
+    small_snap(sm, snap, init, seq);
     __syncthreads();  // (the ranks above read the bitmap cleared below)
   }
   if (bitmap)
@@ -1496,7 +1515,7 @@ __global__ void k_fap_neutral64(int64_t* p_i, uint32_t* p_cnt, int op, Small* sm
 template <int AGG>
 __global__ void __launch_bounds__(256) k_fap_finish_end(Small* sm, const int64_t* p_i, const uint32_t* p_cnt,
                                                         FinalArgs f, int32_t sharded, XMove unpack, Small* snap,
-                                                        Small init, uint32_t* bitmap, const uint32_t* grid, int64_t lo,
+                                                        const Small* init, uint32_t* bitmap, const uint32_t* grid, int64_t lo,
                                                         uint64_t seq) {
   __shared__ uint32_t s_ok, s_T;
   const uint32_t t = threadIdx.x;
@@ -1525,7 +1544,7 @@ __global__ void __launch_bounds__(256) k_fap_finish_end(Small* sm, const int64_t
   __syncthreads();
   if (t == 0) sm->fap_done = 1;
   __syncthreads();
-  small_snap(sm, snap, &init, seq);
+  small_snap(sm, snap, init, seq);
   __syncthreads();  // (the grid read below is this block's own)
   if (bitmap && t < s_T) bitmap[(uint64_t)((int64_t)grid[t] - lo) >> 5] = 0u;
 }
@@ -1746,7 +1765,7 @@ static int uniform_run(Slot* ctx, const UgIn& u, tsdbhip_sg_out* out, tsdbhip_ti
     fo.nan_t = &sm->nan_t;
     const XMove um = sharded ? unpack : XMove{};
     Small* snap = (Small*)ctx->map_out_dev;
-    const Small ini = small_init();
+    const Small* ini = small_init_dev(ctx);
     auto fin = [&](auto aggc) {
       constexpr int A = decltype(aggc)::value;
       LAUNCH(k_fap_finish_end<A>, dim3(1), dim3(256), 0, st, sm, (const int64_t*)o_pi, (const uint32_t*)o_pc, fo,
@@ -1765,7 +1784,7 @@ static int uniform_run(Slot* ctx, const UgIn& u, tsdbhip_sg_out* out, tsdbhip_ti
       // the group did not stand (somewhere): the call state back to its
       // initial values, the general path runs the call
       const uint64_t seq2 = ++ctx->pub_seq;
-      LAUNCH(k_call_end, dim3(1), dim3(256), 0, st, sm, (Small*)ctx->map_out_dev, small_init(), (uint32_t*)nullptr,
+      LAUNCH(k_call_end, dim3(1), dim3(256), 0, st, sm, (Small*)ctx->map_out_dev, small_init_dev(ctx), (uint32_t*)nullptr,
              (const uint32_t*)nullptr, (uint64_t)0, (int64_t)0, BadArgs{}, seq2, (const uint32_t*)nullptr);
       HIPCHK(hipStreamSynchronize(st));
       check_stamp(ctx, seq2);
@@ -1895,7 +1914,7 @@ static int uniform_run(Slot* ctx, const UgIn& u, tsdbhip_sg_out* out, tsdbhip_ti
     dispatch_final(ctx, agg, mode, rate, src, ff);
   }
   const uint64_t end_seq = ++ctx->pub_seq;
-  LAUNCH(k_call_end, dim3(1), dim3(256), 0, st, sm, (Small*)ctx->map_out_dev, small_init(), (uint32_t*)nullptr,
+  LAUNCH(k_call_end, dim3(1), dim3(256), 0, st, sm, (Small*)ctx->map_out_dev, small_init_dev(ctx), (uint32_t*)nullptr,
          (const uint32_t*)nullptr, (uint64_t)0, (int64_t)0, BadArgs{}, end_seq, (const uint32_t*)nullptr);
   EV_FINAL(ctx, 5);
   HIPCHK(hipStreamSynchronize(st));
@@ -2505,7 +2524,7 @@ static int spangroup_run_once(Slot* ctx, const tsdbhip_sg_desc* d, tsdbhip_sg_ou
       // the finish and the end of the call in one single-block launch
       const XMove um = sharded ? unpack : XMove{};
       Small* snap = (Small*)ctx->map_out_dev;
-      const Small ini = small_init();
+      const Small* ini = small_init_dev(ctx);
       const uint64_t seq = end_seq;
       if (agg == TSDBHIP_AGG_MIN)
         LAUNCH(k_fap_finish_end<1>, dim3(1), dim3(256), 0, st, sm, (const int64_t*)o_pi, (const uint32_t*)o_pc, fo, (int32_t)sharded, um, snap, ini, bitmap, (const uint32_t*)gridv_o, lo, seq);
@@ -2993,7 +3012,7 @@ static int spangroup_run_once(Slot* ctx, const tsdbhip_sg_desc* d, tsdbhip_sg_ou
   // ---- end of call: snapshot + reset of the call state, bitmap cleared ----
   const uint64_t end_seq = ++ctx->pub_seq;
   LAUNCH(k_call_end, dim3(bad_at_end ? 1u : grid_for(T, 256, 1024)), dim3(256), 0, st, sm,
-              (Small*)ctx->map_out_dev, small_init(), bitmap, (const uint32_t*)gridv, T, lo, bad_at_end ? bad : BadArgs{},
+              (Small*)ctx->map_out_dev, small_init_dev(ctx), bitmap, (const uint32_t*)gridv, T, lo, bad_at_end ? bad : BadArgs{},
               end_seq, (const uint32_t*)nullptr);
   EV_FINAL(ctx, 5);
   HIPCHK(hipStreamSynchronize(st));  // (the header and small results are already in host memory)
