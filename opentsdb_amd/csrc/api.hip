@@ -1139,6 +1139,7 @@ struct Small {
   // (x0 << 32 | n, step << 32 | q0) as [min, max, min, max]; a span that
   // proposes none holds ~0 in the first word
   unsigned long long ukey[4];
+  uint32_t ug_done, ug_pad;  // k_ug_ds_reg's blocks done (its last block runs the tail)
 };
 // Small.xh slots of the grid-agreement header. Every rank decides from these
 // agreed words alone (never from its own lo / hi against them), so the ranks
@@ -1475,32 +1476,6 @@ __global__ void __launch_bounds__(1024) k_fap_final64v(const int64_t* tmp, uint3
     fap_valid_pack(sm, 1u, pack, T);
   }
 }
-// The uniform path's aligned group: k_fap_final64v, plus G from the class key
-// (bucket b of every span: t0 + b kk step + floor(step (m_b - 1) / 2), its
-// m_b cells, Span.java:377-422) and |G| = nb into the call state (every
-// bucket ts <= the spans' last point <= end, SpanGroup.java:510-608)
-template <int OP>
-__global__ void __launch_bounds__(1024) k_ug_fap_final64v(const int64_t* tmp, uint32_t n, uint32_t n_kept, int64_t* p_i,
-                                                          uint32_t* p_cnt, Small* sm, XMove pack, uint32_t* grid,
-                                                          uint32_t t0, uint32_t step, uint32_t kk, uint32_t ncell,
-                                                          uint32_t nb) {
-  __shared__ int64_t s[16][WAVE];
-  const int lane = lane_id();
-  const uint32_t w = threadIdx.x / WAVE;
-  int64_t acc = fap_rows_wave<OP>(tmp, w, 16, n);
-  acc = fap_block_comb<OP>(acc, s);
-  if (w == 0) {
-    const bool in = (uint32_t)lane < nb;
-    if (in) {
-      const uint32_t sb = (uint32_t)lane * kk, m = min(sb + kk, ncell) - sb;
-      grid[lane] = t0 + sb * step + (uint32_t)((uint64_t)step * (m - 1) / 2);
-    }
-    p_i[lane] = in ? acc : fap_neutral(OP);
-    p_cnt[lane] = in ? n_kept : 0u;
-    if (lane == 0) sm->T = nb;
-    fap_valid_pack(sm, 1u, pack, nb);
-  }
-}
 // a rank without an aligned-group attempt: neutral partials for the exchange
 __global__ void k_fap_neutral64(int64_t* p_i, uint32_t* p_cnt, int op, Small* sm, XMove pack) {
   p_i[threadIdx.x] = fap_neutral(op);
@@ -1547,6 +1522,122 @@ __global__ void __launch_bounds__(256) k_fap_finish_end(Small* sm, const int64_t
   small_snap(sm, snap, init, seq);
   __syncthreads();  // (the grid read below is this block's own)
   if (bitmap && t < s_T) bitmap[(uint64_t)((int64_t)grid[t] - lo) >> 5] = 0u;
+}
+
+// ---- the uniform path's aligned group in one launch (uniform_run) ----
+// k_ds_reg's body with each block's 64 bucket partials combined by device
+// atomics into one of `ncopy` copies (neutral on entry), then the tail in the
+// launch's last block (the blocks count themselves done on Small.ug_done
+// after their atomics are acknowledged): the copies combined (and reset), G
+// from the class key (bucket b of every span: t0 + b kk step +
+// floor(step (m_b - 1) / 2) over its m_b cells, Span.java:377-422), the
+// group's validity; unsharded, also k_fap_finish_end's finish (the results
+// into mapped host memory, the state snapshot + reset + stamp); sharded, the
+// 64-slot partials and the agreement header for the exchange, the finish
+// after it. One launch for k_ds_reg + k_fap_rows + k_fap_final64v
+// (+ k_fap_finish_end).
+constexpr uint32_t UG_NCOPY = 16;  // (4 a thread of the tail, loaded together)
+__global__ void k_fill_u64(unsigned long long* p, uint32_t n, unsigned long long v) {
+  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) p[i] = v;
+}
+struct UgTail {
+  Small* sm;
+  int op;        // the block combine (0 wrapping add, 1 min, 2 max)
+  int agg;       // the cross-series aggregator (finalize)
+  int32_t sharded;
+  uint32_t n_kept, t0, step, kk, ncell, nb;
+  uint32_t* grid;    // G (<= 64 points)
+  int64_t* p_i;      // (sharded) the 64-slot partials for the exchange
+  uint32_t* p_cnt;
+  XMove pack;        // (sharded) the agreement header
+  FinalArgs fo;      // (unsharded) the results into mapped host memory
+  Small* snap;
+  const Small* init;
+  uint64_t seq;
+};
+template <typename T>
+DEVI T coherent_load(const T* p) {  // (past any stale L2 line: the other blocks wrote by atomics)
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+DEVI void ug_fap_tail(const FapArgs& fap, const UgTail& t) {
+  __shared__ int64_t s_acc[4][WAVE];
+  const uint32_t tid = threadIdx.x, lane = tid % WAVE, w = tid / WAVE;
+  const int op = t.op;
+  const int64_t neutral = fap_neutral(op);
+  auto comb = [&](int64_t x, int64_t y) { return op == 0 ? ladd(x, y) : (op == 1 ? min(x, y) : max(x, y)); };
+  int64_t acc = neutral;
+  {  // (coherent loads, all in flight together; the copies reset to neutral after)
+    int64_t v[UG_NCOPY / 4];
+#pragma unroll
+    for (uint32_t i = 0; i < UG_NCOPY / 4; i++)
+      v[i] = (int64_t)coherent_load(fap.copies + (uint64_t)(w + 4 * i) * WAVE + lane);
+#pragma unroll
+    for (uint32_t i = 0; i < UG_NCOPY / 4; i++) {
+      acc = comb(acc, v[i]);
+      fap.copies[(uint64_t)(w + 4 * i) * WAVE + lane] = (unsigned long long)neutral;
+    }
+  }
+  s_acc[w][lane] = acc;
+  __syncthreads();
+  Small* sm = t.sm;
+  __shared__ uint32_t s_ok;
+  if (w == 0) {
+    acc = comb(comb(s_acc[0][lane], s_acc[1][lane]), comb(s_acc[2][lane], s_acc[3][lane]));
+    const bool in = lane < t.nb;
+    if (in) {
+      const uint32_t sb = lane * t.kk, m = min(sb + t.kk, t.ncell) - sb;
+      t.grid[lane] = t.t0 + sb * t.step + (uint32_t)((uint64_t)t.step * (m - 1) / 2);
+    }
+    const bool v = coherent_load(&sm->err) == ERR_NONE && !coherent_load(&sm->fap_broken) &&
+                   coherent_load(&sm->fap_key[0]) == coherent_load(&sm->fap_key[1]) &&
+                   coherent_load(&sm->fap_key[2]) == coherent_load(&sm->fap_key[3]) && t.nb > 0 && t.nb <= WAVE &&
+                   coherent_load(&sm->gflags[0]) == 0;
+    if (lane == 0) {
+      sm->T = t.nb;
+      sm->fap_valid = v ? 1ull : 0ull;
+      s_ok = v ? 1u : 0u;
+    }
+    if (t.sharded) {
+      t.p_i[lane] = in ? acc : neutral;
+      t.p_cnt[lane] = in ? t.n_kept : 0u;
+      if (lane < t.pack.n) {
+        if (t.pack.field[lane] == (void*)&sm->fap_valid) t.pack.buf[lane] = v ? 1ull : 0ull;
+        else xmove_one(t.pack, lane);
+      }
+    } else if (v && in) {
+      Acc a;
+      acc_init(a);
+      a.cnt = t.n_kept;
+      a.ia = acc;
+      switch (t.agg) {
+        case 1: finalize_one<1, MODE_INT, false>(t.fo, lane, a); break;
+        case 2: finalize_one<2, MODE_INT, false>(t.fo, lane, a); break;
+        case 3: finalize_one<3, MODE_INT, false>(t.fo, lane, a); break;
+        default: finalize_one<0, MODE_INT, false>(t.fo, lane, a); break;
+      }
+    }
+  }
+  __syncthreads();
+  if (t.sharded) return;
+  // the finish: the results written, the state snapshot and, when the group
+  // stood, reset (the host reads fap_done; else the general path runs)
+  if (s_ok && tid == 0) sm->fap_done = 1;
+  __syncthreads();
+  small_snap(sm, t.snap, s_ok ? t.init : nullptr, t.seq);
+}
+template <int AGG>
+__global__ void __launch_bounds__(256) k_ug_ds_reg(DecodeArgs a, SpanDsArgs g, const uint32_t* ncells,
+                                                   const uint32_t* vlen, FapArgs fap, UgTail t) {
+  extern __shared__ uint8_t s_pad[];
+  if (threadIdx.x == 0 && a.n_kept == 0xFFFFFFFFu) s_pad[0] = 1;
+  ds_reg_body<AGG>(a, g, ncells, vlen, 0u, fap);
+  __shared__ uint32_t s_last;
+  __builtin_amdgcn_s_waitcnt(0);  // (this wave's atomics acknowledged)
+  __syncthreads();
+  if (threadIdx.x == 0) s_last = atomicAdd(&t.sm->ug_done, 1u) == gridDim.x - 1 ? 1u : 0u;
+  __syncthreads();
+  if (!s_last) return;
+  ug_fap_tail(fap, t);
 }
 
 // TSDBHIP_CHECK_CLEAN: counts non-zero words of a buffer (debug of the
@@ -1697,61 +1788,6 @@ static int uniform_run(Slot* ctx, const UgIn& u, tsdbhip_sg_out* out, tsdbhip_ti
     if (sharded) pack = xchg_desc(ctx, fx, XH_N + 1, (uint64_t*)sm->xh);
     XMove unpack = pack;
     unpack.out = 1;
-    auto go = [&](auto opc) {
-      constexpr int OP = decltype(opc)::value;
-      if (!u.mine) {
-        LAUNCH(k_fap_neutral64, dim3(1), dim3(WAVE), 0, st, o_pi, o_pc, OP, sm, pack);
-        return;
-      }
-      // k_ds_reg, a wave a span, in the aligned group's mode: each block's
-      // buckets combined in LDS into one partial row (LaunchChunks' k_ds_reg)
-      const uint32_t rblocks = (n_kept + 3) / 4;
-      SpanDsArgs gr = {};
-      gr.nseg = CK_NSEG;
-      gr.seg_cap = 4u * ((rblocks + CK_NSEG - 1) / CK_NSEG);
-      gr.list = scratch<uint32_t>(ctx, "cr_list", (uint64_t)gr.seg_cap * CK_NSEG);
-      gr.list_count = sm->seg2;
-      gr.rate = 0;
-      FapArgs fa = {};
-      fa.op = OP;
-      fa.key = sm->fap_key;
-      fa.broken = &sm->fap_broken;
-      fa.nrows = rblocks;
-      fa.part = scratch<int64_t>(ctx, "fap_part", (uint64_t)rblocks * WAVE);
-      const unsigned g1 = std::max(1u, std::min(256u, rblocks / 128));
-      int64_t* tmp = scratch<int64_t>(ctx, "fap_tmp", (uint64_t)g1 * WAVE);
-      auto reg = [&](auto aggc) {
-        constexpr int A = decltype(aggc)::value;
-        static const unsigned stat_lds = [] {
-          hipFuncAttributes at = {};
-          return hipFuncGetAttributes(&at, (const void*)k_ds_reg<A>) == hipSuccess ? (unsigned)at.sharedSizeBytes
-                                                                                    : 18960u;
-        }();
-        const unsigned pad = stat_lds < 40960u ? 40960u - stat_lds : 0u;
-        EV_START(ctx, 8);
-        LAUNCH_STOP(EV_STOP_K(ctx, 9), (k_ds_reg<A>), dim3(rblocks), dim3(256), pad, st, u.da, gr, u.row_ncells,
-                    u.row_val_len, 0u, fa);
-        EV_STOP_M(ctx, 9);
-      };
-      switch (d->ds_agg) {
-        case 0: reg(std::integral_constant<int, 0>()); break;
-        case 1: reg(std::integral_constant<int, 1>()); break;
-        case 2: reg(std::integral_constant<int, 2>()); break;
-        default: reg(std::integral_constant<int, 3>()); break;
-      }
-      ctx->hot_kernel = TSDBHIP_HOT_DS_CHUNKS;
-      LAUNCH((k_fap_rows<OP>), dim3(g1), dim3(1024), 0, st, (const int64_t*)fa.part, rblocks, tmp);
-      LAUNCH((k_ug_fap_final64v<OP>), dim3(1), dim3(1024), 0, st, (const int64_t*)tmp, g1, n_kept, o_pi, o_pc, sm,
-             pack, gridv, x0, step, kk, n, nb);
-    };
-    if (fop == 1) go(std::integral_constant<int, 1>());
-    else if (fop == 2) go(std::integral_constant<int, 2>());
-    else go(std::integral_constant<int, 0>());
-    if (sharded) {  // the agreement, the validity (MIN) and the 64-slot partials: one collective group
-      const XExtra ex[2] = {{o_pi, WAVE, fop ? X_I64 : X_U64, fop == 1 ? X_MIN : (fop == 2 ? X_MAX : X_SUM)},
-                            {o_pc, WAVE, X_U32, X_SUM}};
-      xchg_group(ctx, X, pack, (uint64_t*)&sm->n_input, ex, 2);
-    }
     map_out_reserve(ctx, OUT_HDR + 17 * WAVE);
     const uint64_t end_seq = ++ctx->pub_seq;
     FinalArgs fo;
@@ -1763,18 +1799,79 @@ static int uniform_run(Slot* ctx, const UgIn& u, tsdbhip_sg_out* out, tsdbhip_ti
     fo.out_bits = fo.out_ts + WAVE;
     fo.out_isint = (uint8_t*)(fo.out_bits + WAVE);
     fo.nan_t = &sm->nan_t;
-    const XMove um = sharded ? unpack : XMove{};
     Small* snap = (Small*)ctx->map_out_dev;
     const Small* ini = small_init_dev(ctx);
-    auto fin = [&](auto aggc) {
-      constexpr int A = decltype(aggc)::value;
-      LAUNCH(k_fap_finish_end<A>, dim3(1), dim3(256), 0, st, sm, (const int64_t*)o_pi, (const uint32_t*)o_pc, fo,
-             (int32_t)sharded, um, snap, ini, (uint32_t*)nullptr, (const uint32_t*)gridv, (int64_t)0, end_seq);
-    };
-    if (agg == TSDBHIP_AGG_MIN) fin(std::integral_constant<int, 1>());
-    else if (agg == TSDBHIP_AGG_MAX) fin(std::integral_constant<int, 2>());
-    else if (agg == TSDBHIP_AGG_AVG) fin(std::integral_constant<int, 3>());
-    else fin(std::integral_constant<int, 0>());
+    if (!u.mine) {
+      LAUNCH(k_fap_neutral64, dim3(1), dim3(WAVE), 0, st, o_pi, o_pc, fop, sm, pack);
+    } else {
+      // k_ds_reg, a wave a span, in the aligned group's mode, with the tail
+      // in its last block (k_ug_ds_reg)
+      const uint32_t rblocks = (n_kept + 3) / 4;
+      SpanDsArgs gr = {};
+      gr.nseg = CK_NSEG;
+      gr.seg_cap = 4u * ((rblocks + CK_NSEG - 1) / CK_NSEG);
+      gr.list = scratch<uint32_t>(ctx, "cr_list", (uint64_t)gr.seg_cap * CK_NSEG);
+      gr.list_count = sm->seg2;
+      gr.rate = 0;
+      FapArgs fa = {};
+      fa.op = fop;
+      fa.key = sm->fap_key;
+      fa.broken = &sm->fap_broken;
+      fa.nrows = rblocks;
+      fa.ncopy = UG_NCOPY;
+      {  // the copies, neutral on entry (left neutral by every tail; a new allocation filled once)
+        static const char* names[3] = {"ug_copies0", "ug_copies1", "ug_copies2"};
+        fa.copies = scratch<unsigned long long>(ctx, names[fop], (uint64_t)UG_NCOPY * WAVE);
+        Buf& b = ctx->bufs[names[fop]];
+        Buf& seen = ctx->zeroed[names[fop]];
+        if (b.p != seen.p || b.n != seen.n) {
+          LAUNCH(k_fill_u64, dim3(UG_NCOPY), dim3(WAVE), 0, st, fa.copies, UG_NCOPY * WAVE,
+                 (unsigned long long)(fop == 1 ? INT64_MAX : (fop == 2 ? INT64_MIN : 0)));
+          seen = b;
+        }
+      }
+      UgTail t = {};
+      t.sm = sm; t.op = fop; t.agg = agg; t.sharded = sharded ? 1 : 0;
+      t.n_kept = n_kept; t.t0 = x0; t.step = step; t.kk = kk; t.ncell = n; t.nb = nb;
+      t.grid = gridv; t.p_i = o_pi; t.p_cnt = o_pc; t.pack = pack; t.fo = fo; t.snap = snap; t.init = ini;
+      t.seq = end_seq;
+      auto reg = [&](auto aggc) {
+        constexpr int A = decltype(aggc)::value;
+        static const unsigned stat_lds = [] {
+          hipFuncAttributes at = {};
+          return hipFuncGetAttributes(&at, (const void*)k_ug_ds_reg<A>) == hipSuccess ? (unsigned)at.sharedSizeBytes
+                                                                                       : 21000u;
+        }();
+        const unsigned pad = stat_lds < 40960u ? 40960u - stat_lds : 0u;
+        EV_START(ctx, 8);
+        LAUNCH_STOP(EV_STOP_K(ctx, 9), (k_ug_ds_reg<A>), dim3(rblocks), dim3(256), pad, st, u.da, gr,
+                    u.row_ncells, u.row_val_len, fa, t);
+        EV_STOP_M(ctx, 9);
+      };
+      switch (d->ds_agg) {
+        case 0: reg(std::integral_constant<int, 0>()); break;
+        case 1: reg(std::integral_constant<int, 1>()); break;
+        case 2: reg(std::integral_constant<int, 2>()); break;
+        default: reg(std::integral_constant<int, 3>()); break;
+      }
+      ctx->hot_kernel = TSDBHIP_HOT_DS_CHUNKS;
+    }
+    if (sharded) {
+      // the agreement, the validity (MIN) and the 64-slot partials: one
+      // collective group; then the finish
+      const XExtra ex[2] = {{o_pi, WAVE, fop ? X_I64 : X_U64, fop == 1 ? X_MIN : (fop == 2 ? X_MAX : X_SUM)},
+                            {o_pc, WAVE, X_U32, X_SUM}};
+      xchg_group(ctx, X, pack, (uint64_t*)&sm->n_input, ex, 2);
+      auto fin = [&](auto aggc) {
+        constexpr int A = decltype(aggc)::value;
+        LAUNCH(k_fap_finish_end<A>, dim3(1), dim3(256), 0, st, sm, (const int64_t*)o_pi, (const uint32_t*)o_pc, fo,
+               (int32_t)1, unpack, snap, ini, (uint32_t*)nullptr, (const uint32_t*)gridv, (int64_t)0, end_seq);
+      };
+      if (agg == TSDBHIP_AGG_MIN) fin(std::integral_constant<int, 1>());
+      else if (agg == TSDBHIP_AGG_MAX) fin(std::integral_constant<int, 2>());
+      else if (agg == TSDBHIP_AGG_AVG) fin(std::integral_constant<int, 3>());
+      else fin(std::integral_constant<int, 0>());
+    }
     EV_FINAL(ctx, 5);
     HIPCHK(hipStreamSynchronize(st));
     check_stamp(ctx, end_seq);
@@ -1784,7 +1881,7 @@ static int uniform_run(Slot* ctx, const UgIn& u, tsdbhip_sg_out* out, tsdbhip_ti
       // the group did not stand (somewhere): the call state back to its
       // initial values, the general path runs the call
       const uint64_t seq2 = ++ctx->pub_seq;
-      LAUNCH(k_call_end, dim3(1), dim3(256), 0, st, sm, (Small*)ctx->map_out_dev, small_init_dev(ctx), (uint32_t*)nullptr,
+      LAUNCH(k_call_end, dim3(1), dim3(256), 0, st, sm, (Small*)ctx->map_out_dev, ini, (uint32_t*)nullptr,
              (const uint32_t*)nullptr, (uint64_t)0, (int64_t)0, BadArgs{}, seq2, (const uint32_t*)nullptr);
       HIPCHK(hipStreamSynchronize(st));
       check_stamp(ctx, seq2);

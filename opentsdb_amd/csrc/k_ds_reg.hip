@@ -305,23 +305,24 @@ struct FapArgs {
   unsigned long long* key;  // [4] Small.fap_key
   uint32_t* broken;         // Small.fap_broken
   uint32_t nrows;           // (host) partial rows written: the launch's blocks
+  // (the uniform path) instead of a row a block: the block's partial combined
+  // by device atomics into copy (block % ncopy) of 64 slots, neutral on entry
+  unsigned long long* copies;
+  uint32_t ncopy;
 };
 
 DEVI int64_t fap_neutral(int op) { return op == 1 ? INT64_MAX : (op == 2 ? INT64_MIN : 0); }
 
 // Blocks of 4 waves; 1 << wps_log2 waves per span (a span's rows split into
 // that many contiguous pieces), 4 >> wps_log2 spans per block. (FAP: one wave
-// per span.)
+// per span.) The body of k_ds_reg and of the uniform path's k_ug_ds_reg.
 template <int AGG>
-__global__ void __launch_bounds__(256) k_ds_reg(DecodeArgs a, SpanDsArgs g, const uint32_t* ncells,
-                                                const uint32_t* vlen, uint32_t wps_log2, FapArgs fap) {
+DEVI void ds_reg_body(const DecodeArgs& a, const SpanDsArgs& g, const uint32_t* ncells, const uint32_t* vlen,
+                      uint32_t wps_log2, const FapArgs& fap) {
   __shared__ uint64_t s_v[4][DCH];
   __shared__ int64_t s_bk[4][WAVE];
   __shared__ int64_t s_part[WAVE];
   __shared__ uint32_t s_bad[4];
-  // (dynamic LDS: padding that caps the resident blocks per CU, see LaunchChunks)
-  extern __shared__ uint8_t s_pad[];
-  if (threadIdx.x == 0 && a.n_kept == 0xFFFFFFFFu) s_pad[0] = 1;
   const int lane = lane_id();
   const uint32_t wib = ufl(threadIdx.x / WAVE);  // (uniform: the span prologue and the row walk use scalar loads)
   const uint32_t wps = 1u << wps_log2;
@@ -445,8 +446,27 @@ __global__ void __launch_bounds__(256) k_ds_reg(DecodeArgs a, SpanDsArgs g, cons
   }
   if (fop >= 0) {  // the block's partial row
     __syncthreads();
-    if (threadIdx.x < WAVE) fap.part[(uint64_t)blockIdx.x * WAVE + threadIdx.x] = s_part[threadIdx.x];
+    if (threadIdx.x < WAVE) {
+      const int64_t v = s_part[threadIdx.x];
+      if (!fap.copies) {
+        fap.part[(uint64_t)blockIdx.x * WAVE + threadIdx.x] = v;
+      } else if (v != fap_neutral(fop)) {
+        unsigned long long* c = fap.copies + (uint64_t)(blockIdx.x % fap.ncopy) * WAVE + threadIdx.x;
+        if (fop == 0) atomicAdd(c, (unsigned long long)v);
+        else if (fop == 1) atomicMin((long long*)c, (long long)v);
+        else atomicMax((long long*)c, (long long)v);
+      }
+    }
   }
+}
+
+template <int AGG>
+__global__ void __launch_bounds__(256) k_ds_reg(DecodeArgs a, SpanDsArgs g, const uint32_t* ncells,
+                                                const uint32_t* vlen, uint32_t wps_log2, FapArgs fap) {
+  // (dynamic LDS: padding that caps the resident blocks per CU, see LaunchChunks)
+  extern __shared__ uint8_t s_pad[];
+  if (threadIdx.x == 0 && a.n_kept == 0xFFFFFFFFu) s_pad[0] = 1;
+  ds_reg_body<AGG>(a, g, ncells, vlen, wps_log2, fap);
 }
 
 // FAP rows -> one 1-chunk partial per t: block b (16 waves) combines rows
