@@ -409,10 +409,60 @@ def bench_c5(args):
                      "complex_kernel_ms": float(np.mean(cx)), "classify_kernel_ms": float(np.mean(cls)),
                      "rows_kernel_ms": float(np.mean(rows_k))},
     }
+    if args.h2d:
+        try:
+            res["h2d"] = h2d_leg_c5(ctx, L, b)
+        except Exception as e:  # diagnostics only; never costs the line
+            res["h2d"] = {"error": repr(e)}
     if not args.no_cpu:
         res["cpu_baseline"] = cpu_baseline_c5(b, args.cpu_seconds)
     emit(res)
     ctx.close()
+
+
+def h2d_leg_c5(ctx, L, b, steps=3):
+    """PCIe-inclusive C5 leg — beside the line, never its value: the same
+    1M-row batch with the desc and output arrays in registered pinned host
+    memory (as CompactionQueue's JNI bridge would hand them over), so every
+    call stages the rows H2D and brings the compacted rows back D2H."""
+    R = b.n_rows
+    qcap, vcap = b.qual_extent + 64, b.val_extent + R + 64
+    outs = {k: np.zeros(n, dt) for k, n, dt in
+            [("st", R, np.uint8), ("qo", R, np.uint64), ("ql", R, np.uint32), ("vo", R, np.uint64),
+             ("vl", R, np.uint32), ("q", qcap, np.uint8), ("v", vcap, np.uint8), ("w", R, np.uint8),
+             ("k", R, np.int32)]}
+    ins = [b.row_kv_start, b.row_qual_off, b.row_val_off, b.kv_qual_len, b.kv_val_len, b.qual_bytes, b.val_bytes]
+    reg = [a for a in ins + list(outs.values()) if a.nbytes]
+    for a in reg:
+        ctx.check(L.tsdbhip_host_register(ctx.handle, a.ctypes.data_as(C.c_void_p), a.nbytes))
+    try:
+        d = _abi.RowsDesc(flags=0, n_rows=R, n_kvs=b.n_kvs, row_kv_start=_abi.ptr(b.row_kv_start, C.c_uint64),
+                          row_qual_off=_abi.ptr(b.row_qual_off, C.c_uint64),
+                          row_val_off=_abi.ptr(b.row_val_off, C.c_uint64),
+                          kv_qual_len=_abi.ptr(b.kv_qual_len, C.c_uint16), kv_val_len=_abi.ptr(b.kv_val_len, C.c_uint16),
+                          qual_bytes=_abi.ptr(b.qual_bytes, C.c_uint8), qual_nbytes=len(b.qual_bytes),
+                          val_bytes=_abi.ptr(b.val_bytes, C.c_uint8), val_nbytes=len(b.val_bytes))
+        o = outs
+        out = _abi.RowsOut(qual_capacity=qcap, val_capacity=vcap, row_status=_abi.ptr(o["st"], C.c_uint8),
+                           row_qual_off=_abi.ptr(o["qo"], C.c_uint64), row_qual_len=_abi.ptr(o["ql"], C.c_uint32),
+                           row_val_off=_abi.ptr(o["vo"], C.c_uint64), row_val_len=_abi.ptr(o["vl"], C.c_uint32),
+                           qual_bytes=_abi.ptr(o["q"], C.c_uint8), val_bytes=_abi.ptr(o["v"], C.c_uint8),
+                           row_write=_abi.ptr(o["w"], C.c_uint8), row_keep_kv=_abi.ptr(o["k"], C.c_int32))
+        ctx.check(L.tsdbhip_compact_rows(ctx.handle, C.byref(d), C.byref(out)))  # warm-up
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            ctx.check(L.tsdbhip_compact_rows(ctx.handle, C.byref(d), C.byref(out)))
+        dt = (time.perf_counter() - t0) / steps
+    finally:
+        for a in reg:
+            L.tsdbhip_host_unregister(ctx.handle, a.ctypes.data_as(C.c_void_p))
+    h2d = sum(a.nbytes for a in ins)
+    d2h = sum(a.nbytes for a in outs.values())
+    cells = int(b.kv_qual_len.astype(np.int64).sum() // 2)
+    return {"value": cells / dt, "unit": "raw cells/s", "ms_per_step": dt * 1e3, "h2d_bytes_per_step": h2d,
+            "d2h_bytes_per_step": d2h, "effective_GBs": (h2d + d2h) / dt / 1e9, "steps": steps,
+            "pinned_h2d_GBs": pinned_h2d_rate(h2d),
+            "sample": "the whole C5 batch, desc and output arrays in registered pinned host memory"}
 
 
 def shard_ranges(n_series, world):

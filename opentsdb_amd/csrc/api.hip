@@ -1750,6 +1750,7 @@ struct UgIn {
   uint64_t k1, k2;  // the class key (agreed, sharded lockstep)
   bool lockstep;     // else the aligned group
   bool mine;         // (aligned group) this rank's spans make the attempt
+  bool dev;          // (lockstep, unsharded) integer dev: the chains of k_ug_dev
 };
 
 static int uniform_run(Slot* ctx, const UgIn& u, tsdbhip_sg_out* out, tsdbhip_timing& tm) {
@@ -1966,12 +1967,22 @@ static int uniform_run(Slot* ctx, const UgIn& u, tsdbhip_sg_out* out, tsdbhip_ti
   lsp.a.g_off = rate ? 1u : 0u;
   lsp.w8 = (q0 & 7u) == 7u;
   lsp.flt = flt;
-  tm.paths |= TSDBHIP_PATH_LOCKSTEP;
+  if (!u.dev) tm.paths |= TSDBHIP_PATH_LOCKSTEP;
   ctx->hot_kernel = TSDBHIP_HOT_LOCKSTEP;
   const unsigned blocks = n_tiles * n_chunks;
   FinalArgs f = fin;
   f.n_chunks = n_chunks;
-  if (!sharded) {
+  if (u.dev) {  // integer dev: one sequential chain a grid point (k_ug_dev)
+    ctx->hot_kernel = TSDBHIP_HOT_REDUCE_DIRECT;
+    EV_START(ctx, 8);
+    if (lsp.w8)
+      LAUNCH_STOP(EV_STOP_K(ctx, 9), k_ug_dev<8>, dim3((unsigned)((T + WAVE - 1) / WAVE)), dim3(256), 0, st,
+                  u.da.val, u.uk_vo, u.da.qual, u.uk_qo, q0, &sm->ls_broken, n_kept, T, gridv, x0, step, fin);
+    else
+      LAUNCH_STOP(EV_STOP_K(ctx, 9), k_ug_dev<4>, dim3((unsigned)((T + WAVE - 1) / WAVE)), dim3(256), 0, st,
+                  u.da.val, u.uk_vo, u.da.qual, u.uk_qo, q0, &sm->ls_broken, n_kept, T, gridv, x0, step, fin);
+    EV_STOP_M(ctx, 9);
+  } else if (!sharded) {
     dispatch_lockstep(ctx, agg, rate, blocks, r, lsp, f, true);
   } else {
     const int nr = X->nranks, rk = X->rank;
@@ -2160,7 +2171,10 @@ static int spangroup_run_once(Slot* ctx, const tsdbhip_sg_desc* d, tsdbhip_sg_ou
                        (agg != TSDBHIP_AGG_DEV || rate);
   const bool ug_fap_q = ug_allow && auto_dec && interval > 0 && !rate && ds_agg <= 3 && agg <= 3 && !exact &&
                         ctx->opt.aligned_group && !ctx->opt.timing_detail;
-  const bool ug_q = ug_ls_q || ug_fap_q;
+  // (integer dev without rate, unsharded: the sequential chains of k_ug_dev)
+  const bool ug_dev_q = ug_allow && auto_dec && interval == 0 && !exact && agg == TSDBHIP_AGG_DEV && !rate &&
+                        !sharded;
+  const bool ug_q = ug_ls_q || ug_fap_q || ug_dev_q;
   // sharded lockstep: the ranks agree on the key before the host's round trip
   const bool ug_agree = ug_ls_q && sharded;
   uint64_t* u_key1 = ug_q ? scratch<uint64_t>(ctx, "u_key1", S) : nullptr;
@@ -2322,7 +2336,13 @@ static int spangroup_run_once(Slot* ctx, const tsdbhip_sg_desc* d, tsdbhip_sg_ou
     bool take = false;
     const bool local_ok = !poisoned && n_kept > 0 && h.ukey[0] != ~0ull && h.ukey[0] == h.ukey[1] &&
                           h.ukey[2] == h.ukey[3] && (uint32_t)h.ukey[0] >= 64;
-    if (ug_ls_q) {
+    if (ug_dev_q) {
+      u.lockstep = true;
+      u.dev = true;
+      u.k1 = h.ukey[0];
+      u.k2 = h.ukey[2];
+      take = local_ok && !(u.k2 & 8u);  // (integer cells)
+    } else if (ug_ls_q) {
       u.lockstep = true;
       if (sharded) {  // (from the agreed words alone: every rank takes the same branch)
         const unsigned long long* x = h.xh;

@@ -34,10 +34,37 @@ def test_uniform_lockstep(ctx, kind, agg, rate):
     ss = synth.regular(150, 1300, kind, seed=6, step=2)
     g, o = run_both(ctx, ss, agg=agg, rate=rate)
     assert_same(g, o)
-    if agg != 4 or rate:  # (integer dev: the span-ordered pass, never lockstep)
+    if agg != 4 or rate:
         assert paths(ctx) & _abi.PATH_UNIFORM and paths(ctx) & _abi.PATH_LOCKSTEP
-    if (agg, rate, kind) == (4, False, I64):
-        assert not paths(ctx) & _abi.PATH_UNIFORM
+    elif kind == I64:  # integer dev: the sequential chains of k_ug_dev (bit-exact)
+        assert paths(ctx) & _abi.PATH_UNIFORM and not paths(ctx) & _abi.PATH_LOCKSTEP
+        assert_same(g, o, exact_double=True)
+
+
+@pytest.mark.parametrize("n_spans", [1, 95, 96, 97, 1000])
+@pytest.mark.parametrize("width", [8, 4])
+def test_uniform_integer_dev_chains(ctx, n_spans, width):
+    """k_ug_dev: one sequential Welford chain a grid point over the spans in
+    span order (Aggregators.java:196-237), phases of 96 spans; bit-exact
+    against the oracle, counters near 2^40 (8-byte) or past 2^16 (4-byte)"""
+    if width == 8:
+        ss = synth.regular(n_spans, 700, I64, seed=13, step=1)
+    else:
+        # (values past 2^16 and inside int32: every cell 4 bytes wide)
+        ss = packing.pack_spans([I([(T0 + 2 * i, 1_000_000 + 13 * i * (s + 1) - 70_000 * (s % 3)) for i in range(300)])
+                                 for s in range(n_spans)])
+    g, o = run_both(ctx, ss, agg=4)
+    assert_same(g, o, exact_double=True)
+    assert paths(ctx) & _abi.PATH_UNIFORM
+
+
+def test_uniform_integer_dev_broken_reruns(ctx):
+    """a middle qualifier off the cadence: k_ug_dev's producers see it, the
+    call runs again on the proven path"""
+    ss = corrupt_qual(synth.regular(300, 1300, I64, seed=3, step=2), 201, 700, lambda q: q + 16)
+    g, o = run_both(ctx, ss, agg=4)
+    assert_same(g, o, exact_double=True)
+    assert paths(ctx) & _abi.PATH_DIRECT_REDO
 
 
 @pytest.mark.parametrize("agg", [0, 1, 2, 3])
