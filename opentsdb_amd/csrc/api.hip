@@ -3656,19 +3656,30 @@ static int compact_rows(Slot* ctx, const tsdbhip_rows_desc* d, tsdbhip_rows_out*
       // around the holes; the other rows through the LDS row kernel
       a.tile_bad = scratch<uint8_t>(ctx, "c_tbad", R / CC_ROWS + 1);
       a.row_holes = scratch<uint2>(ctx, "c_holes", R);
-      // (each boundary event the stop of the kernel before it)
+      // (each boundary event the stop of the kernel before it, under
+      // "timing_detail"; else only the call's first and last events: an
+      // event carried by a launch holds the next kernel back ~4.6 us, four
+      // boundaries 2 % of the call — the breakdown then reads 0 and hot_ms
+      // the whole call)
+      const bool det = ctx->opt.timing_detail;
+      if (!det) ctx->ev_alias[4] = ctx->ev_alias[2] = ctx->ev_alias[9] = ctx->ev_alias[3] = 1;
       EV_START(ctx, 8);
-      LAUNCH_STOP(EV_STOP_K(ctx, 4), k_compact_quals, dim3(grid_for(R, CC_ROWS, 1u << 16)), dim3(256), 0, st, a);
-      EV_STOP_M(ctx, 4);
-      LAUNCH_STOP(EV_STOP_K(ctx, 2), k_compact_classify, dim3(grid_for(R, 16, 1u << 16)), dim3(256), 0, st, a);
-      EV_STOP_M(ctx, 2);
+      LAUNCH_STOP(det ? EV_STOP_K(ctx, 4) : nullptr, k_compact_quals, dim3(grid_for(R, CC_ROWS, 1u << 16)),
+                  dim3(256), 0, st, a);
+      if (det) EV_STOP_M(ctx, 4);
+      LAUNCH_STOP(det ? EV_STOP_K(ctx, 2) : nullptr, k_compact_classify, dim3(grid_for(R, 16, 1u << 16)),
+                  dim3(256), 0, st, a);
+      if (det) EV_STOP_M(ctx, 2);
       if (ctx->opt.compact_rows_vals)
-        LAUNCH_STOP(EV_STOP_K(ctx, 9), k_compact_vals, dim3(grid_for(R, 16, 1u << 16)), dim3(256), 0, st, a);
+        LAUNCH_STOP(det ? EV_STOP_K(ctx, 9) : nullptr, k_compact_vals, dim3(grid_for(R, 16, 1u << 16)), dim3(256), 0,
+                    st, a);
       else
-        LAUNCH_STOP(EV_STOP_K(ctx, 9), k_compact_vals_flat, dim3(grid_for(R, CV_ROWS, 1u << 16)), dim3(256), 0, st, a);
-      EV_STOP_M(ctx, 9);
-      LAUNCH_STOP(EV_STOP_K(ctx, 3), k_compact_rows, dim3(grid_for(R, CR_RANGE, 1u << 14)), dim3(256), 0, st, a);
-      EV_STOP_M(ctx, 3);
+        LAUNCH_STOP(det ? EV_STOP_K(ctx, 9) : nullptr, k_compact_vals_flat, dim3(grid_for(R, CV_ROWS, 1u << 16)),
+                    dim3(256), 0, st, a);
+      if (det) EV_STOP_M(ctx, 9);
+      LAUNCH_STOP(det ? EV_STOP_K(ctx, 3) : nullptr, k_compact_rows, dim3(grid_for(R, CR_RANGE, 1u << 14)),
+                  dim3(256), 0, st, a);
+      if (det) EV_STOP_M(ctx, 3);
     }
     HIPCHK(hipGetLastError());
     LAUNCH(k_compact_complex<true>, dim3(1024), dim3(256), 0, ctx->stream, a);
