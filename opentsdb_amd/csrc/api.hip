@@ -993,6 +993,34 @@ static void dispatch_lockstep(Slot* ctx, int agg, bool rate, unsigned blocks, co
   }
 }
 
+// the uniform path's E variant: k_ug_reduce, then launch_reduce's finalize
+template <int AGG, int MODE>
+static void launch_ug_reduce(Slot* ctx, const ReduceArgs& r, const FinalArgs& f) {
+  const uint64_t n_waves = (r.T + WAVE - 1) / WAVE * r.n_chunks;
+  LAUNCH((k_ug_reduce<AGG, MODE>), dim3((unsigned)((n_waves + 3) / 4)), dim3(256), 0, ctx->stream, r);
+  if (f.n_chunks >= 64 && f.T >= 1024)
+    LAUNCH((k_chunks_cols<AGG, MODE, false, true>), dim3((unsigned)((f.T + 63) / 64)), dim3(64 * COLW), 0,
+           ctx->stream, r, r, f, f.T, f.n_chunks);
+  else if (f.n_chunks >= 64)
+    LAUNCH((k_finalize_par<AGG, MODE, false>), dim3((unsigned)f.T), dim3(256), 0, ctx->stream, r, f);
+  else
+    LAUNCH((k_finalize_seq<AGG, MODE, false>), dim3(grid_for(f.T, 256)), dim3(256), 0, ctx->stream, r, f);
+}
+template <int AGG>
+static void ug_reduce_mode(Slot* ctx, int mode, const ReduceArgs& r, const FinalArgs& f) {
+  if (mode == MODE_INT) launch_ug_reduce<AGG, MODE_INT>(ctx, r, f);
+  else launch_ug_reduce<AGG, MODE_DBL>(ctx, r, f);
+}
+static void dispatch_ug_reduce(Slot* ctx, int agg, int mode, const ReduceArgs& r, const FinalArgs& f) {
+  switch (agg) {
+    case 0: return ug_reduce_mode<0>(ctx, mode, r, f);
+    case 1: return ug_reduce_mode<1>(ctx, mode, r, f);
+    case 2: return ug_reduce_mode<2>(ctx, mode, r, f);
+    case 3: return ug_reduce_mode<3>(ctx, mode, r, f);
+    default: return ug_reduce_mode<4>(ctx, mode, r, f);
+  }
+}
+
 template <int AGG>
 static void dispatch_mode(Slot* ctx, int mode, bool rate, unsigned blocks, const ReduceArgs& r,
                           const FinalArgs& f, bool par, bool fin) {
@@ -1735,6 +1763,10 @@ static std::vector<Fld> partial_fields(const ReduceArgs& r, uint64_t off, int ag
 //    general path (k_fap_finish_end), the key agreed in the partials' group.
 //    Collectives: 1. A group that does not stand anywhere: RC_UG_FALLBACK
 //    (the call state reset; the general path runs the call).
+//  * E (unsharded, other downsampled queries: doubles, dev, > 64 buckets,
+//    spans of many rows — C2): k_ds_reg writes each span's bucket values on
+//    the key's buckets and G; k_ug_reduce reads span k at g as E_k[g]. A span
+//    off the cadence: RC_UG_FALLBACK after the call (results dropped).
 constexpr int RC_REDO = 1000;  // a lockstep proposal did not hold: the proven path runs the call
 constexpr int RC_UG_FALLBACK = 1001;
 struct UgIn {
@@ -1751,6 +1783,7 @@ struct UgIn {
   bool lockstep;     // else the aligned group
   bool mine;         // (aligned group) this rank's spans make the attempt
   bool dev;          // (lockstep, unsharded) integer dev: the chains of k_ug_dev
+  bool e;            // (unsharded, downsampled) k_ds_reg's E + k_reduce's aligned spans
 };
 
 static int uniform_run(Slot* ctx, const UgIn& u, tsdbhip_sg_out* out, tsdbhip_timing& tm) {
@@ -1766,7 +1799,7 @@ static int uniform_run(Slot* ctx, const UgIn& u, tsdbhip_sg_out* out, tsdbhip_ti
   const uint32_t n_kept = u.n_kept;
   Small h;
   tm.paths |= TSDBHIP_PATH_UNIFORM;
-  if (!u.lockstep) {
+  if (!u.lockstep && !u.e) {
     // ---- aligned group ----
     const int32_t I = d->ds_interval;
     // (a rank making no attempt may hold no key: step 0)
@@ -1919,8 +1952,9 @@ static int uniform_run(Slot* ctx, const UgIn& u, tsdbhip_sg_out* out, tsdbhip_ti
     return TSDBHIP_OK;
   }
 
-  // ---- lockstep ----
-  const uint64_t T = rate ? n - 1 : n;
+  // ---- lockstep, E ----
+  const uint32_t e_kk = u.e ? (uint32_t)(((int64_t)d->ds_interval + step - 1) / step) : 0u;
+  const uint64_t T = u.e ? (n + e_kk - 1) / e_kk : (rate ? n - 1 : n);
   const bool flt = (q0 & 8u) != 0;
   const int mode = (rate || flt) ? MODE_DBL : MODE_INT;
   uint32_t* gridv = scratch<uint32_t>(ctx, "grid", T);
@@ -1949,7 +1983,7 @@ static int uniform_run(Slot* ctx, const UgIn& u, tsdbhip_sg_out* out, tsdbhip_ti
   r.T = T;
   r.n_chunks = n_chunks;
   r.n_kept = n_kept;
-  alloc_partials(ctx, r, "p_", (uint64_t)n_chunks * T, agg);
+  if (!u.e) alloc_partials(ctx, r, "p_", (uint64_t)n_chunks * T, agg);
   LsPlan lsp = {};
   lsp.a.d_voff = u.uk_vo;
   lsp.a.d_qoff = u.uk_qo;
@@ -1972,7 +2006,54 @@ static int uniform_run(Slot* ctx, const UgIn& u, tsdbhip_sg_out* out, tsdbhip_ti
   const unsigned blocks = n_tiles * n_chunks;
   FinalArgs f = fin;
   f.n_chunks = n_chunks;
-  if (u.dev) {  // integer dev: one sequential chain a grid point (k_ug_dev)
+  if (u.e) {
+    // k_ds_reg in E mode (its block 0 writes G from the key, the spans their
+    // bucket values; an outsider sets the broken flag), then k_ug_reduce:
+    // every span's E is G itself (no bitmap, no grid ranks, no cursors)
+    ctx->hot_kernel = TSDBHIP_HOT_DS_CHUNKS;
+    const uint64_t rps = d->n_rows / std::max<uint32_t>(n_kept, 1);
+    const uint32_t wps_log2 = rps >= 12 ? 2 : (rps >= 6 ? 1 : 0);
+    const uint32_t rblocks = (uint32_t)(((uint64_t)n_kept * (1u << wps_log2) + 3) / 4);
+    SpanDsArgs gr = {};
+    gr.nseg = CK_NSEG;
+    FapArgs fa = {};
+    fa.op = -1;
+    fa.broken = &sm->ls_broken;
+    fa.ug_grid = gridv;
+    fa.ug_t0 = x0; fa.ug_step = step; fa.ug_kk = e_kk; fa.ug_n = n;
+    auto reg = [&](auto aggc) {
+      constexpr int A = decltype(aggc)::value;
+      static const unsigned stat_lds = [] {
+        hipFuncAttributes at = {};
+        return hipFuncGetAttributes(&at, (const void*)k_ds_reg<A>) == hipSuccess ? (unsigned)at.sharedSizeBytes
+                                                                                 : 18960u;
+      }();
+      const unsigned pad = wps_log2 == 0 ? (stat_lds < 40960u ? 40960u - stat_lds : 0u) : 0u;
+      EV_START(ctx, 8);
+      LAUNCH_STOP(EV_STOP_K(ctx, 9), (k_ds_reg<A>), dim3(rblocks), dim3(256), pad, st, u.da, gr, u.row_ncells,
+                  u.row_val_len, wps_log2, fa);
+      EV_STOP_M(ctx, 9);
+    };
+    switch (d->ds_agg) {
+      case 0: reg(std::integral_constant<int, 0>()); break;
+      case 1: reg(std::integral_constant<int, 1>()); break;
+      case 2: reg(std::integral_constant<int, 2>()); break;
+      default: reg(std::integral_constant<int, 3>()); break;
+    }
+    // (integer dev: one span-ordered chunk, Aggregators.java:196-217; else
+    // chunks of 64 spans, merged in chunk order by the finalize)
+    const bool seq = agg == TSDBHIP_AGG_DEV && mode != MODE_DBL;
+    const uint32_t spc = seq ? std::max<uint32_t>(n_kept, 1) : 64u;
+    ReduceArgs re;
+    std::memset(&re, 0, sizeof re);
+    re.e_off = u.da.e_off; re.e_val = u.da.e_val; re.n_kept = n_kept; re.grid = gridv; re.T = T;
+    re.spans_per_chunk = spc;
+    re.n_chunks = (n_kept + spc - 1) / spc;
+    alloc_partials(ctx, re, "p_", (uint64_t)re.n_chunks * T, agg);
+    FinalArgs fe = fin;
+    fe.n_chunks = re.n_chunks;
+    dispatch_ug_reduce(ctx, agg, mode, re, fe);
+  } else if (u.dev) {  // integer dev: one sequential chain a grid point (k_ug_dev)
     ctx->hot_kernel = TSDBHIP_HOT_REDUCE_DIRECT;
     EV_START(ctx, 8);
     if (lsp.w8)
@@ -2033,7 +2114,7 @@ static int uniform_run(Slot* ctx, const UgIn& u, tsdbhip_sg_out* out, tsdbhip_ti
   ctx->sm_ready = true;
   if (h.ls_broken) {  // (agreed over the ranks) the proposal did not hold: the proven path runs the call
     ctx->timing = tm;
-    return RC_REDO;
+    return u.e ? RC_UG_FALLBACK : RC_REDO;
   }
   out->n_input_points = h.n_input;
   if (sharded) {
@@ -2044,7 +2125,7 @@ static int uniform_run(Slot* ctx, const UgIn& u, tsdbhip_sg_out* out, tsdbhip_ti
   if (ctx->hot_kernel) tm.hot_ms = ev_ms(ctx, 8, 9);
   tm.hot_kernel = ctx->hot_kernel;
   tm.total_ms = ev_ms(ctx, 0, 5);
-  tm.n_emitted = 0;
+  tm.n_emitted = u.e ? T * n_kept : 0;
   ctx->timing = tm;
   uint64_t n_ok = T;
   int code = TSDBHIP_OK;
@@ -2174,7 +2255,10 @@ static int spangroup_run_once(Slot* ctx, const tsdbhip_sg_desc* d, tsdbhip_sg_ou
   // (integer dev without rate, unsharded: the sequential chains of k_ug_dev)
   const bool ug_dev_q = ug_allow && auto_dec && interval == 0 && !exact && agg == TSDBHIP_AGG_DEV && !rate &&
                         !sharded;
-  const bool ug_q = ug_ls_q || ug_fap_q || ug_dev_q;
+  // (other downsampled queries, unsharded: k_ds_reg's E on the key's buckets)
+  const bool ug_e_q = ug_allow && auto_dec && interval > 0 && !rate && ds_agg <= 3 && !exact && !sharded &&
+                      !ctx->opt.timing_detail;
+  const bool ug_q = ug_ls_q || ug_fap_q || ug_dev_q || ug_e_q;
   // sharded lockstep: the ranks agree on the key before the host's round trip
   const bool ug_agree = ug_ls_q && sharded;
   uint64_t* u_key1 = ug_q ? scratch<uint64_t>(ctx, "u_key1", S) : nullptr;
@@ -2336,24 +2420,26 @@ static int spangroup_run_once(Slot* ctx, const tsdbhip_sg_desc* d, tsdbhip_sg_ou
     bool take = false;
     const bool local_ok = !poisoned && n_kept > 0 && h.ukey[0] != ~0ull && h.ukey[0] == h.ukey[1] &&
                           h.ukey[2] == h.ukey[3] && (uint32_t)h.ukey[0] >= 64;
+    // (k_lockstep and k_ug_dev read one row a span: k2 bit 16 clear)
+    const bool one_row = !(h.ukey[2] & 0x10000u);
     if (ug_dev_q) {
       u.lockstep = true;
       u.dev = true;
       u.k1 = h.ukey[0];
       u.k2 = h.ukey[2];
-      take = local_ok && !(u.k2 & 8u);  // (integer cells)
+      take = local_ok && one_row && !(u.k2 & 8u);  // (integer cells)
     } else if (ug_ls_q) {
       u.lockstep = true;
       if (sharded) {  // (from the agreed words alone: every rank takes the same branch)
         const unsigned long long* x = h.xh;
         take = x[0] == ERR_NONE && x[1] > 0 && x[2] != ~0ull && x[2] == ~x[3] && x[4] == ~x[5] &&
-               (uint32_t)x[2] >= 64;
+               (uint32_t)x[2] >= 64 && !(x[4] & 0x10000u);
         u.k1 = x[2];
         u.k2 = x[4];
       } else {
         const uint32_t n = (uint32_t)h.ukey[0];
         const uint64_t ls_waves = (n + LS_TILE - 1) / LS_TILE * std::max<uint64_t>(1, n_kept / 64);
-        take = local_ok && (ctx->opt.lockstep == 2 || ls_waves >= 2048);
+        take = local_ok && one_row && (ctx->opt.lockstep == 2 || ls_waves >= 2048);
         u.k1 = h.ukey[0];
         u.k2 = h.ukey[2];
       }
@@ -2363,10 +2449,16 @@ static int spangroup_run_once(Slot* ctx, const tsdbhip_sg_desc* d, tsdbhip_sg_ou
       u.k2 = h.ukey[2];
       const uint32_t step = (uint32_t)(u.k2 >> 32), n = (uint32_t)u.k1;
       const uint64_t kk = step ? ((uint64_t)interval + step - 1) / step : 0;
-      u.mine = local_ok && !(u.k2 & 8u) && kk && (n + kk - 1) / kk <= WAVE;
-      // (sharded: every rank makes the attempt, the key and the validity
-      // agreed in its one collective group; unsharded: only a group that is one)
-      take = sharded || u.mine;
+      const bool fits = local_ok && !(u.k2 & 8u) && kk && (n + kk - 1) / kk <= WAVE;
+      if (ug_fap_q && (sharded || fits)) {
+        // (sharded: every rank makes the attempt, the key and the validity
+        // agreed in its one collective group; unsharded: only a group that is one)
+        u.mine = fits;
+        take = true;
+      } else if (ug_e_q && local_ok && kk) {
+        u.e = true;
+        take = true;
+      }
     }
     if (take) {
       const int rc = uniform_run(ctx, u, out, tm);

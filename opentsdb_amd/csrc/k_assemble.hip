@@ -206,32 +206,40 @@ DEVI void assemble_finish(const AssembleArgs& a, uint32_t s, bool has_rows) {
 // chain after the other: spans of many rows — a day of hourly rows — go to
 // the wave kernel, which loads 64 rows at once.)
 constexpr uint32_t ASM_ROWS = 4;
-// The uniform-group proposal of a one-row span of n >= 2 cells (every row
-// check of the fast case passed): one value width W (8 or 4 B), the
-// qualifiers of cells 0, 1 and n-1 on ts = x0 + c*step with one flags nibble,
-// every point inside [start, end]. Spans proposing one key are one RowSeq on
-// one cadence each (RowSeq.java:360-497), so their union grid is that cadence
-// (SpanGroup.java:510-608); the kernels that take the group prove every other
-// qualifier as they stream (k_lockstep, k_ds_reg).
-DEVI bool ug_probe(const AssembleArgs& a, uint64_t r0, uint32_t n, uint64_t& k1, uint64_t& k2, uint64_t& vo,
-                   uint64_t& qo) {
-  const uint32_t vb = a.row_val_len[r0] - 1;  // (n >= 2: a compacted row ends with its meta byte)
-  const uint32_t W = vb / n;
+// The uniform-group proposal of a span of n >= 2 cells whose rows all passed
+// the assembly checks (one RowSeq a row, no Q1 / overflow): one value width
+// W (8 or 4 B) in its first row, the qualifiers of the first row's cells 0
+// and 1 and of the last row's last cell on ts = x0 + c*step with one flags
+// nibble, every point inside [start, end]. Spans proposing one key are one
+// cadence each (RowSeq.java:360-497), so their union grid is that cadence
+// (SpanGroup.java:510-608), downsampled: one bucket sequence; the kernels
+// that take the group prove every other qualifier as they stream (k_lockstep,
+// k_ds_reg). Bit 16 of k2: a span of several rows (k_lockstep and k_ug_dev
+// read one row a span; k_ds_reg any).
+DEVI bool ug_probe(const AssembleArgs& a, uint64_t r0, uint64_t r1, uint32_t n, uint64_t& k1, uint64_t& k2,
+                   uint64_t& vo, uint64_t& qo) {
+  const bool one = r1 - r0 == 1;
+  const uint32_t n0 = one ? n : a.row_ncells[r0];
+  if (n0 < 2) return false;
+  const uint32_t vb = a.row_val_len[r0] - 1;  // (n0 >= 2: a compacted row ends with its meta byte)
+  const uint32_t W = vb / n0;
   qo = a.row_qual_off[r0];
   vo = a.row_val_off[r0];
-  if (!((W == 8 || W == 4) && vb == W * n && (qo & 1) == 0 && (vo & (W - 1)) == 0)) return false;
-  const uint32_t q0 = load_qual(a.qual, qo), q1 = load_qual(a.qual, qo + 2), ql = load_qual(a.qual, qo + 2ull * (n - 1));
+  if (!((W == 8 || W == 4) && vb == W * n0 && (qo & 1) == 0 && (vo & (W - 1)) == 0)) return false;
+  const uint64_t rl = r1 - 1;
+  const uint32_t nl = one ? n : a.row_ncells[rl];
+  const uint64_t qol = one ? qo : a.row_qual_off[rl];
+  const uint32_t q0 = load_qual(a.qual, qo), q1 = load_qual(a.qual, qo + 2), ql = load_qual(a.qual, qol + 2ull * (nl - 1));
   const uint32_t fl = q0 & 15u;
   const uint32_t d0 = q0 >> 4, d1 = q1 >> 4, dl = ql >> 4;
-  if (!((fl & 7u) == W - 1 && (q1 & 15u) == fl && (ql & 15u) == fl && d1 > d0 &&
-        (uint64_t)d0 + (uint64_t)(n - 1) * (d1 - d0) == dl))
-    return false;
+  if (!((fl & 7u) == W - 1 && (q1 & 15u) == fl && (ql & 15u) == fl && d1 > d0)) return false;
   const uint32_t step = d1 - d0;
   const int64_t first = (int64_t)a.row_base[r0] + d0;
   const int64_t last = first + (int64_t)(n - 1) * step;
+  if ((int64_t)a.row_base[rl] + dl != last) return false;
   if (!(first >= a.start && last <= a.end && last < (1ll << 32))) return false;
   k1 = ((uint64_t)first << 32) | n;
-  k2 = ((uint64_t)step << 32) | q0;
+  k2 = ((uint64_t)step << 32) | (one ? 0u : 0x10000u) | q0;
   return true;
 }
 
@@ -276,7 +284,7 @@ DEVI bool assemble_fast_one(const AssembleArgs& a, uint32_t s) {
     }
     if (a.u_key1) {  // (a deferred span proposes nothing)
       uint64_t k1 = ~0ull, k2 = 0, vo = 0, qo = 0;
-      if (ok && r1 - r0 == 1 && cell >= 2 && !ug_probe(a, r0, cell, k1, k2, vo, qo)) k1 = ~0ull;
+      if (ok && cell >= 2 && !ug_probe(a, r0, r1, cell, k1, k2, vo, qo)) k1 = ~0ull;
       a.u_key1[s] = k1;
       a.u_key2[s] = k2;
       a.u_vo[s] = vo;
@@ -510,6 +518,14 @@ DEVI void assemble_span_wave(const AssembleArgs& a, uint32_t s) {
         a.sp_ovf_cell[s] = -1;
         a.sp_q1[s] = -1;
         a.sp_q1_shift[s] = 0;
+        if (a.u_key1) {  // (a span of many rows: the proposal here, not in k_assemble_fast)
+          uint64_t k1 = ~0ull, k2 = 0, vo = 0, qo = 0;
+          if (cell >= 2 && !ug_probe(a, r0, r1, cell, k1, k2, vo, qo)) k1 = ~0ull;
+          a.u_key1[s] = k1;
+          a.u_key2[s] = k2;
+          a.u_vo[s] = vo;
+          a.u_qo[s] = qo;
+        }
       }
     } else if (r1 == r0) {
       if (lane == 0) {

@@ -85,12 +85,14 @@ DEVI void reg_flush(const DecodeArgs& a, const RegSpan& sp, const int64_t* BK, u
     const uint32_t sb = b * sp.kk, m = min(sb + sp.kk, sp.n) - sb;
     const int64_t v = BK[i];
     const uint64_t o = sp.eo + b;
-    a.e_ts[o] = sp.t0 + sb * sp.step + (uint32_t)((uint64_t)sp.step * (m - 1) / 2);
+    // (fop -2, the uniform path's E variant: values only, the timestamps
+    // being G and the type the key's)
+    if (fop != -2) a.e_ts[o] = sp.t0 + sb * sp.step + (uint32_t)((uint64_t)sp.step * (m - 1) / 2);
     if (FLT)  // Aggregators.Avg.runDouble: sum / n
       a.e_val[o] = AGG == 3 ? dbits(bitsd(v) / (double)(int32_t)m) : v;
     else
       a.e_val[o] = AGG == 3 ? ldiv64_32(v, m) : v;
-    a.e_flt[o] = FLT ? 1 : 0;
+    if (fop != -2) a.e_flt[o] = FLT ? 1 : 0;
   }
   wave_lds_sync();
 }
@@ -309,7 +311,19 @@ struct FapArgs {
   // by device atomics into copy (block % ncopy) of 64 slots, neutral on entry
   unsigned long long* copies;
   uint32_t ncopy;
+  // (the uniform path's E variant, op -1) every kept span proposed one key:
+  // block 0 writes G, the key's bucket timestamps; the spans' E values only
+  // (k_ug_reduce); a span the kernel does not take sets `broken` (the call
+  // then runs again on the general path, these results dropped)
+  uint32_t* ug_grid;
+  uint32_t ug_t0, ug_step, ug_kk, ug_n;
 };
+
+// bucket b's timestamp of the key's span (Span.java:399: the mean of its cells' ts)
+DEVI uint32_t ug_bucket_ts(const FapArgs& f, uint32_t b) {
+  const uint32_t sb = b * f.ug_kk, m = min(sb + f.ug_kk, f.ug_n) - sb;
+  return f.ug_t0 + sb * f.ug_step + (uint32_t)((uint64_t)f.ug_step * (m - 1) / 2);
+}
 
 DEVI int64_t fap_neutral(int op) { return op == 1 ? INT64_MAX : (op == 2 ? INT64_MIN : 0); }
 
@@ -332,6 +346,10 @@ DEVI void ds_reg_body(const DecodeArgs& a, const SpanDsArgs& g, const uint32_t* 
   if (fop >= 0) {
     if (threadIdx.x < WAVE) s_part[threadIdx.x] = fap_neutral(fop);
     __syncthreads();
+  }
+  if (fap.ug_grid && blockIdx.x == 0) {
+    const uint32_t nbk = (fap.ug_n + fap.ug_kk - 1) / fap.ug_kk;
+    for (uint32_t b = threadIdx.x; b < nbk; b += blockDim.x) fap.ug_grid[b] = ug_bucket_ts(fap, b);
   }
   const int64_t I = a.interval;
   bool ok = k < a.n_kept && I > 0;
@@ -379,14 +397,15 @@ DEVI void ds_reg_body(const DecodeArgs& a, const SpanDsArgs& g, const uint32_t* 
   }
   // an aligned-group member: its buckets go to the block partial, not to E
   const bool fused = fop >= 0 && ok && !flt && nb <= WAVE;
-  const int sfop = fused ? fop : -1;
+  const int efop = fap.ug_grid ? -2 : -1;
+  const int sfop = fused ? fop : efop;
   if (ok && ra < rb) {
     bool fail;
     if (W == 8)
-      fail = flt ? reg_piece<AGG, 8, true>(a, sp, ra, rb, ncells, s_v[wib], s_bk[wib], -1, s_part)
+      fail = flt ? reg_piece<AGG, 8, true>(a, sp, ra, rb, ncells, s_v[wib], s_bk[wib], efop, s_part)
                  : reg_piece<AGG, 8, false>(a, sp, ra, rb, ncells, s_v[wib], s_bk[wib], sfop, s_part);
     else
-      fail = flt ? reg_piece<AGG, 4, true>(a, sp, ra, rb, ncells, s_v[wib], s_bk[wib], -1, s_part)
+      fail = flt ? reg_piece<AGG, 4, true>(a, sp, ra, rb, ncells, s_v[wib], s_bk[wib], efop, s_part)
                  : reg_piece<AGG, 4, false>(a, sp, ra, rb, ncells, s_v[wib], s_bk[wib], sfop, s_part);
     ok = !fail;
   }
@@ -410,7 +429,9 @@ DEVI void ds_reg_body(const DecodeArgs& a, const SpanDsArgs& g, const uint32_t* 
     }
   }
   if (k < a.n_kept) {
-    if (!ok) {
+    if (!ok && fap.ug_grid) {  // (a uniform group's outsider: see FapArgs.ug_grid)
+      if (piece == 0 && lane == 0 && !*(volatile uint32_t*)fap.broken) atomicOr(fap.broken, 1u);
+    } else if (!ok) {
       if (piece == 0 && lane == 0 && !fap.rewrite) {  // the whole span to k_ds_spans
         const uint32_t sg = blockIdx.x % g.nseg;
         g.list[(uint64_t)sg * g.seg_cap + atomicAdd(&g.list_count[sg], 1u)] = k;

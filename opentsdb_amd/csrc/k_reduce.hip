@@ -1199,6 +1199,44 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) k
   reduce_wave<AGG, MODE, RATE, DONLY>(r, (blockIdx.x * blockDim.x + threadIdx.x) / WAVE, w);
 }
 
+// The uniform path's E variant (uniform_run): every kept span's E is G
+// itself (the key's bucket sequence, k_ds_reg), so span k's value at grid
+// point g is e_val[e_off[k] + g] — no cursor, bracket or grid rank
+// (SpanGroup.java:702-784 with x_cur == t at every t). A wave per (tile of
+// 64 grid points, chunk of spans) pushes its chunk's spans in span order,
+// 8 spans' values in flight; the partials are k_reduce's ([n_chunks][T]).
+template <int AGG, int MODE>
+__global__ void __launch_bounds__(256) k_ug_reduce(ReduceArgs r) {
+  const int lane = lane_id();
+  const uint32_t wave = __builtin_amdgcn_readfirstlane((blockIdx.x * blockDim.x + threadIdx.x) / WAVE);
+  const uint64_t n_tiles = (r.T + WAVE - 1) / WAVE;
+  if (wave >= n_tiles * r.n_chunks) return;
+  const uint32_t chunk = wave % r.n_chunks;
+  const uint64_t g = (uint64_t)(wave / r.n_chunks) * WAVE + lane;
+  const bool gv = g < r.T;
+  const uint32_t k0 = chunk * r.spans_per_chunk, k1 = min(r.n_kept, k0 + r.spans_per_chunk);
+  Acc acc;
+  acc_init(acc);
+  acc.fastdiv = AGG == 4 && MODE != MODE_INT;
+  constexpr uint32_t U = 8;
+  for (uint32_t kb = k0; kb < k1; kb += WAVE) {
+    const uint32_t nk = min((uint32_t)WAVE, k1 - kb);
+    const uint64_t eo_l = (uint32_t)lane < nk ? r.e_off[kb + lane] : 0;
+    for (uint32_t i = 0; i < nk; i += U) {
+      int64_t v[U];
+#pragma unroll
+      for (uint32_t u = 0; u < U; u++) {
+        const uint64_t eo = readlane_u64(eo_l, (int)min(i + u, (uint32_t)WAVE - 1));
+        v[u] = (i + u < nk && gv) ? r.e_val[eo + g] : 0;
+      }
+#pragma unroll
+      for (uint32_t u = 0; u < U; u++)
+        if (i + u < nk && gv) acc_push<AGG, MODE>(acc, v[u], MODE == MODE_INT ? 0.0 : to_double(v[u], true));
+    }
+  }
+  if (gv) acc_store<AGG, MODE>(r, (uint64_t)chunk * r.T + g, acc);
+}
+
 __global__ void k_chunk_flags(const uint32_t* d_info, uint32_t n_kept, uint32_t spc, uint32_t* chunk_e) {
   const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
   if (k < n_kept && !(d_info[k] & 1u)) chunk_e[k / spc] = 1u;

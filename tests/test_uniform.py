@@ -106,7 +106,56 @@ def test_uniform_not_proposed(ctx):
         for dsi in (0, 60):
             g, o = run_both(ctx, ss, agg=0, ds_interval=dsi, ds_agg=3 if dsi else 0)
             assert_same(g, o)
-            assert not paths(ctx) & _abi.PATH_UNIFORM
+            # (spans of two rows: the downsampled kernels take them, k_lockstep not)
+            assert bool(paths(ctx) & _abi.PATH_UNIFORM) == (ss is two_rows and dsi > 0)
+
+
+@pytest.mark.parametrize("kind", [F32, F64, I64])
+@pytest.mark.parametrize("agg", [0, 1, 2, 3, 4])
+@pytest.mark.parametrize("dsa", [0, 1, 3])
+@pytest.mark.parametrize("dsi", [60, 10])
+def test_uniform_e(ctx, kind, agg, dsa, dsi):
+    """downsampled groups outside the aligned group (floats, dev, more than 64
+    buckets a span): k_ds_reg writes each span's E on the key's buckets and
+    G from the key, k_reduce finds every span aligned on every tile"""
+    ss = synth.regular(150, 1300, kind, seed=6, step=2)
+    g, o = run_both(ctx, ss, 0, U32MAX, agg, False, dsi, dsa)
+    assert_same(g, o)
+    p = paths(ctx)
+    assert p & _abi.PATH_UNIFORM and not p & _abi.PATH_UNIFORM_FALLBACK
+    fap = kind == I64 and agg <= 3 and (1300 + dsi // 2 - 1) // (dsi // 2) <= 64
+    assert bool(p & _abi.PATH_ALIGNED_GROUP) == fap
+
+
+@pytest.mark.parametrize("kind", [F64, I64])
+@pytest.mark.parametrize("agg", [0, 3, 4])
+def test_uniform_e_many_rows(ctx, kind, agg):
+    """C2's shape: a day of hourly rows a span (k_ds_reg's 4 waves a span),
+    1-minute buckets"""
+    ss = synth.regular(40, 8640, kind, seed=7, step=10)
+    g, o = run_both(ctx, ss, 0, U32MAX, agg, False, 60, 3)
+    assert_same(g, o)
+    assert paths(ctx) & _abi.PATH_UNIFORM
+
+
+@pytest.mark.parametrize("row", [0, 5, 23])
+def test_uniform_e_broken_falls_back(ctx, row):
+    """a qualifier off the cadence in some row of one span: k_ds_reg leaves
+    the span out, the call runs again on the general path"""
+    ss = corrupt_qual(synth.regular(40, 8640, F64, seed=8, step=10), 17, 100, lambda q: q + 16, row=row)
+    for agg in (0, 4):
+        g, o = run_both(ctx, ss, 0, U32MAX, agg, False, 60, 3)
+        assert_same(g, o)
+        assert paths(ctx) & _abi.PATH_UNIFORM_FALLBACK
+
+
+def test_uniform_e_window(ctx):
+    """a window cutting the spans proposes nothing; one holding them whole does"""
+    ss = synth.regular(40, 8640, F64, seed=9, step=10)
+    for start, end, uni in ((0, U32MAX, True), (0, T0 + 86390, True), (0, T0 + 86389, False), (T0 + 5, U32MAX, False)):
+        g, o = run_both(ctx, ss, start, end, 0, False, 60, 3)
+        assert_same(g, o)
+        assert bool(paths(ctx) & _abi.PATH_UNIFORM) == uni
 
 
 @pytest.fixture(scope="module", params=[2, 4, 8])
