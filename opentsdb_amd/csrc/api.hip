@@ -2001,7 +2001,7 @@ static int uniform_run(Slot* ctx, const UgIn& u, tsdbhip_sg_out* out, tsdbhip_ti
   lsp.a.g_off = rate ? 1u : 0u;
   lsp.w8 = (q0 & 7u) == 7u;
   lsp.flt = flt;
-  if (!u.dev) tm.paths |= TSDBHIP_PATH_LOCKSTEP;
+  if (!u.dev && !u.e) tm.paths |= TSDBHIP_PATH_LOCKSTEP;
   ctx->hot_kernel = TSDBHIP_HOT_LOCKSTEP;
   const unsigned blocks = n_tiles * n_chunks;
   FinalArgs f = fin;
@@ -2013,14 +2013,19 @@ static int uniform_run(Slot* ctx, const UgIn& u, tsdbhip_sg_out* out, tsdbhip_ti
     ctx->hot_kernel = TSDBHIP_HOT_DS_CHUNKS;
     const uint64_t rps = d->n_rows / std::max<uint32_t>(n_kept, 1);
     const uint32_t wps_log2 = rps >= 12 ? 2 : (rps >= 6 ? 1 : 0);
-    const uint32_t rblocks = (uint32_t)(((uint64_t)n_kept * (1u << wps_log2) + 3) / 4);
+    // (waves a span, its rows in contiguous pieces: C2's 24 rows a span, 0.266
+    // ms a step with 3 pieces, 0.269 with 2, 0.281 with 4, 0.290 with 1,
+    // 0.310 with 8, 0.489 with 24 — same box)
+    uint32_t pieces = (uint32_t)std::max<uint64_t>(1, rps / 8);
+    if (const char* e = getenv("TSDBHIP_UG_P")) pieces = (uint32_t)std::max(1, atoi(e));  // (A/B runs)
+    const uint32_t rblocks = (uint32_t)(((uint64_t)n_kept * pieces + 3) / 4);
     SpanDsArgs gr = {};
     gr.nseg = CK_NSEG;
     FapArgs fa = {};
     fa.op = -1;
     fa.broken = &sm->ls_broken;
     fa.ug_grid = gridv;
-    fa.ug_t0 = x0; fa.ug_step = step; fa.ug_kk = e_kk; fa.ug_n = n;
+    fa.ug_t0 = x0; fa.ug_step = step; fa.ug_kk = e_kk; fa.ug_n = n; fa.ug_pieces = pieces;
     auto reg = [&](auto aggc) {
       constexpr int A = decltype(aggc)::value;
       static const unsigned stat_lds = [] {
@@ -2028,7 +2033,7 @@ static int uniform_run(Slot* ctx, const UgIn& u, tsdbhip_sg_out* out, tsdbhip_ti
         return hipFuncGetAttributes(&at, (const void*)k_ds_reg<A>) == hipSuccess ? (unsigned)at.sharedSizeBytes
                                                                                  : 18960u;
       }();
-      const unsigned pad = wps_log2 == 0 ? (stat_lds < 40960u ? 40960u - stat_lds : 0u) : 0u;
+      const unsigned pad = pieces == 1 ? (stat_lds < 40960u ? 40960u - stat_lds : 0u) : 0u;
       EV_START(ctx, 8);
       LAUNCH_STOP(EV_STOP_K(ctx, 9), (k_ds_reg<A>), dim3(rblocks), dim3(256), pad, st, u.da, gr, u.row_ncells,
                   u.row_val_len, wps_log2, fa);

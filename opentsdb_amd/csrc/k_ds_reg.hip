@@ -317,6 +317,7 @@ struct FapArgs {
   // then runs again on the general path, these results dropped)
   uint32_t* ug_grid;
   uint32_t ug_t0, ug_step, ug_kk, ug_n;
+  uint32_t ug_pieces;  // waves a span (0: wps_log2's blocks)
 };
 
 // bucket b's timestamp of the key's span (Span.java:399: the mean of its cells' ts)
@@ -339,9 +340,12 @@ DEVI void ds_reg_body(const DecodeArgs& a, const SpanDsArgs& g, const uint32_t* 
   __shared__ uint32_t s_bad[4];
   const int lane = lane_id();
   const uint32_t wib = ufl(threadIdx.x / WAVE);  // (uniform: the span prologue and the row walk use scalar loads)
-  const uint32_t wps = 1u << wps_log2;
-  const uint32_t piece = wib & (wps - 1);
-  const uint32_t k = blockIdx.x * (4u >> wps_log2) + (wib >> wps_log2);
+  // (the uniform path's E variant: ug_pieces waves a span, anywhere in the
+  // grid — its pieces need no agreement, an outsider breaks the whole call)
+  const uint32_t gw = blockIdx.x * 4u + wib;
+  const uint32_t wps = fap.ug_pieces ? fap.ug_pieces : 1u << wps_log2;
+  const uint32_t piece = fap.ug_pieces ? gw % wps : wib & (wps - 1);
+  const uint32_t k = fap.ug_pieces ? gw / wps : blockIdx.x * (4u >> wps_log2) + (wib >> wps_log2);
   const int fop = fap.op;
   if (fop >= 0) {
     if (threadIdx.x < WAVE) s_part[threadIdx.x] = fap_neutral(fop);
@@ -389,7 +393,7 @@ DEVI void ds_reg_body(const DecodeArgs& a, const SpanDsArgs& g, const uint32_t* 
     }
   }
   if (ok) {  // this wave's rows: a contiguous piece that starts at a bucket head
-    const uint64_t rp = (r1 - r0 + wps - 1) >> wps_log2;
+    const uint64_t rp = (r1 - r0 + wps - 1) / wps;
     ra = min(r0 + piece * rp, r1);
     rb = min(ra + rp, r1);
     if (ra < rb && piece > 0) ok = sld(&a.row_cell0[ra]) % sp.kk == 0;
@@ -409,7 +413,7 @@ DEVI void ds_reg_body(const DecodeArgs& a, const SpanDsArgs& g, const uint32_t* 
                  : reg_piece<AGG, 4, false>(a, sp, ra, rb, ncells, s_v[wib], s_bk[wib], sfop, s_part);
     ok = !fail;
   }
-  if (wps > 1) {  // the span's pieces agree (every wave of the block reaches this)
+  if (wps > 1 && !fap.ug_pieces) {  // the span's pieces agree (every wave of the block reaches this)
     if (lane == 0) s_bad[wib] = ok ? 0u : 1u;
     __syncthreads();
     uint32_t any = 0;
@@ -430,7 +434,7 @@ DEVI void ds_reg_body(const DecodeArgs& a, const SpanDsArgs& g, const uint32_t* 
   }
   if (k < a.n_kept) {
     if (!ok && fap.ug_grid) {  // (a uniform group's outsider: see FapArgs.ug_grid)
-      if (piece == 0 && lane == 0 && !*(volatile uint32_t*)fap.broken) atomicOr(fap.broken, 1u);
+      if (lane == 0 && !*(volatile uint32_t*)fap.broken) atomicOr(fap.broken, 1u);  // (any piece)
     } else if (!ok) {
       if (piece == 0 && lane == 0 && !fap.rewrite) {  // the whole span to k_ds_spans
         const uint32_t sg = blockIdx.x % g.nseg;

@@ -122,7 +122,7 @@ def test_uniform_e(ctx, kind, agg, dsa, dsi):
     g, o = run_both(ctx, ss, 0, U32MAX, agg, False, dsi, dsa)
     assert_same(g, o)
     p = paths(ctx)
-    assert p & _abi.PATH_UNIFORM and not p & _abi.PATH_UNIFORM_FALLBACK
+    assert p & _abi.PATH_UNIFORM and not p & (_abi.PATH_UNIFORM_FALLBACK | _abi.PATH_LOCKSTEP)
     fap = kind == I64 and agg <= 3 and (1300 + dsi // 2 - 1) // (dsi // 2) <= 64
     assert bool(p & _abi.PATH_ALIGNED_GROUP) == fap
 
