@@ -92,6 +92,7 @@ struct Slot {
   uint64_t* map_state = nullptr;  // [0, 511]: state words, [512]: flag
   uint64_t* map_state_dev = nullptr;
   uint64_t pub_seq = 0;
+  uint64_t ug_spec_seq = 0;  // the stamp of the speculative aligned group's launch (uniform_run)
   uint32_t timing_late = 0;  // this call's end stamp arrived after the stream sync (check_stamp)
   uint8_t* map_out = nullptr;
   uint8_t* map_out_dev = nullptr;
@@ -1167,7 +1168,8 @@ struct Small {
   // (x0 << 32 | n, step << 32 | q0) as [min, max, min, max]; a span that
   // proposes none holds ~0 in the first word
   unsigned long long ukey[4];
-  uint32_t ug_done, ug_pad;  // k_ug_ds_reg's blocks done (its last block runs the tail)
+  uint32_t ug_done;   // k_ug_ds_reg's blocks done (its last block runs the tail)
+  uint32_t ug_tried;  // (speculative k_ug_ds_reg) the group was attempted
 };
 // Small.xh slots of the grid-agreement header. Every rank decides from these
 // agreed words alone (never from its own lo / hi against them), so the ranks
@@ -1582,6 +1584,10 @@ struct UgTail {
   Small* snap;
   const Small* init;
   uint64_t seq;
+  // (speculative, unsharded: the key, n_kept, kk and nb come from the call
+  // state; a group that is not one leaves the state as the host would find it)
+  uint32_t spec;
+  int64_t interval;
 };
 template <typename T>
 DEVI T coherent_load(const T* p) {  // (past any stale L2 line: the other blocks wrote by atomics)
@@ -1590,6 +1596,32 @@ DEVI T coherent_load(const T* p) {  // (past any stale L2 line: the other blocks
 DEVI void ug_fap_tail(const FapArgs& fap, const UgTail& t) {
   __shared__ int64_t s_acc[4][WAVE];
   const uint32_t tid = threadIdx.x, lane = tid % WAVE, w = tid / WAVE;
+  // (the key's fields as locals: a copy of the UgTail, whose pack arrays are
+  // indexed by lane, put the whole struct in scratch — 928 B a lane, the
+  // launch 3x slower)
+  uint32_t n_kept = t.n_kept, t0 = t.t0, step = t.step, kk0 = t.kk, ncell = t.ncell, nbk = t.nb;
+  bool fits = true;
+  if (t.spec) {
+    Small* sm = t.sm;
+    uint32_t nb = 0, kk = 0;
+    fits = ug_spec_fits(sm->ukey[0], sm->ukey[1], sm->ukey[2], sm->ukey[3], sm->n_kept, sm->err, t.interval, &nb, &kk);
+    if (!fits && !t.sharded) {
+      // not attempted (the host, deciding alike, goes on without waiting for
+      // this launch): no block touched the state but for ug_done, and nothing
+      // is written to host memory
+      if (tid == 0) sm->ug_done = 0;
+      return;
+    }
+    // (sharded and not one: this rank's partials neutral, its validity 0, as
+    // k_fap_neutral64's; the exchange is every rank's)
+    n_kept = fits ? (uint32_t)sm->n_kept : 0u;
+    t0 = (uint32_t)(sm->ukey[0] >> 32);
+    ncell = (uint32_t)sm->ukey[0];
+    step = (uint32_t)(sm->ukey[2] >> 32);
+    kk0 = fits ? kk : 1u;
+    nbk = fits ? nb : 0u;
+    if (tid == 0) sm->ug_tried = 1;
+  }
   const int op = t.op;
   const int64_t neutral = fap_neutral(op);
   auto comb = [&](int64_t x, int64_t y) { return op == 0 ? ladd(x, y) : (op == 1 ? min(x, y) : max(x, y)); };
@@ -1611,31 +1643,40 @@ DEVI void ug_fap_tail(const FapArgs& fap, const UgTail& t) {
   __shared__ uint32_t s_ok;
   if (w == 0) {
     acc = comb(comb(s_acc[0][lane], s_acc[1][lane]), comb(s_acc[2][lane], s_acc[3][lane]));
-    const bool in = lane < t.nb;
+    const bool in = lane < nbk;
     if (in) {
-      const uint32_t sb = lane * t.kk, m = min(sb + t.kk, t.ncell) - sb;
-      t.grid[lane] = t.t0 + sb * t.step + (uint32_t)((uint64_t)t.step * (m - 1) / 2);
+      const uint32_t sb = lane * kk0, m = min(sb + kk0, ncell) - sb;
+      t.grid[lane] = t0 + sb * step + (uint32_t)((uint64_t)step * (m - 1) / 2);
     }
     const bool v = coherent_load(&sm->err) == ERR_NONE && !coherent_load(&sm->fap_broken) &&
                    coherent_load(&sm->fap_key[0]) == coherent_load(&sm->fap_key[1]) &&
-                   coherent_load(&sm->fap_key[2]) == coherent_load(&sm->fap_key[3]) && t.nb > 0 && t.nb <= WAVE &&
+                   coherent_load(&sm->fap_key[2]) == coherent_load(&sm->fap_key[3]) && nbk > 0 && nbk <= WAVE &&
                    coherent_load(&sm->gflags[0]) == 0;
     if (lane == 0) {
-      sm->T = t.nb;
+      sm->T = nbk;
       sm->fap_valid = v ? 1ull : 0ull;
       s_ok = v ? 1u : 0u;
     }
     if (t.sharded) {
       t.p_i[lane] = in ? acc : neutral;
-      t.p_cnt[lane] = in ? t.n_kept : 0u;
+      t.p_cnt[lane] = in ? n_kept : 0u;
       if (lane < t.pack.n) {
-        if (t.pack.field[lane] == (void*)&sm->fap_valid) t.pack.buf[lane] = v ? 1ull : 0ull;
-        else xmove_one(t.pack, lane);
+        if (t.pack.field[lane] == (void*)&sm->fap_valid) {
+          t.pack.buf[lane] = v ? 1ull : 0ull;
+        } else if (t.spec && (lane == 4 || lane == 5 || lane == 10 || lane == 11)) {
+          // (speculative: the class key's header words, uniform_run's fx[4, 5,
+          // 10, 11], from the device key — ~0 / 0 for a rank without a group)
+          const uint64_t a1 = fits ? sm->ukey[0] : ~0ull, a2 = fits ? sm->ukey[2] : 0ull;
+          const uint64_t val = (lane == 4 || lane == 10) ? a1 : a2;
+          t.pack.buf[lane] = t.pack.kind[lane] == 4 ? ~val : val;
+        } else {
+          xmove_one(t.pack, lane);
+        }
       }
     } else if (v && in) {
       Acc a;
       acc_init(a);
-      a.cnt = t.n_kept;
+      a.cnt = n_kept;
       a.ia = acc;
       switch (t.agg) {
         case 1: finalize_one<1, MODE_INT, false>(t.fo, lane, a); break;
@@ -1784,7 +1825,11 @@ struct UgIn {
   bool mine;         // (aligned group) this rank's spans make the attempt
   bool dev;          // (lockstep, unsharded) integer dev: the chains of k_ug_dev
   bool e;            // (unsharded, downsampled) k_ds_reg's E + k_reduce's aligned spans
+  bool spec;         // (aligned group, unsharded) launched before the host read the call state:
+                     // n_kept is the span count, the key comes from the device
+  int phase;         // (spec) 1: the launch only (RC_CONTINUE); 2: the finish of that launch
 };
+constexpr int RC_CONTINUE = 1002;  // the speculative aligned group found no group: the call goes on
 
 static int uniform_run(Slot* ctx, const UgIn& u, tsdbhip_sg_out* out, tsdbhip_timing& tm) {
   const tsdbhip_sg_desc* d = u.d;
@@ -1802,9 +1847,10 @@ static int uniform_run(Slot* ctx, const UgIn& u, tsdbhip_sg_out* out, tsdbhip_ti
   if (!u.lockstep && !u.e) {
     // ---- aligned group ----
     const int32_t I = d->ds_interval;
-    // (a rank making no attempt may hold no key: step 0)
-    const uint32_t kk = u.mine ? (uint32_t)(((int64_t)I + step - 1) / step) : 1u;
-    const uint32_t nb = u.mine ? (n + kk - 1) / kk : 0u;
+    // (a rank making no attempt may hold no key: step 0; speculative: the
+    // device's key)
+    const uint32_t kk = u.mine && !u.spec ? (uint32_t)(((int64_t)I + step - 1) / step) : 1u;
+    const uint32_t nb = u.mine && !u.spec ? (n + kk - 1) / kk : 0u;
     const int fop = agg == TSDBHIP_AGG_MIN ? 1 : (agg == TSDBHIP_AGG_MAX ? 2 : 0);
     uint32_t* gridv = scratch<uint32_t>(ctx, "grid", WAVE);
     int64_t* o_pi = scratch<int64_t>(ctx, "fo_i", WAVE);
@@ -1822,8 +1868,9 @@ static int uniform_run(Slot* ctx, const UgIn& u, tsdbhip_sg_out* out, tsdbhip_ti
     if (sharded) pack = xchg_desc(ctx, fx, XH_N + 1, (uint64_t*)sm->xh);
     XMove unpack = pack;
     unpack.out = 1;
-    map_out_reserve(ctx, OUT_HDR + 17 * WAVE);
-    const uint64_t end_seq = ++ctx->pub_seq;
+    // (phase 2: the stamp the launch's tail writes is phase 1's)
+    if (u.phase != 2) map_out_reserve(ctx, OUT_HDR + 17 * WAVE);
+    const uint64_t end_seq = u.phase == 2 ? ctx->ug_spec_seq : ++ctx->pub_seq;
     FinalArgs fo;
     std::memset(&fo, 0, sizeof fo);
     fo.T = WAVE;
@@ -1835,7 +1882,9 @@ static int uniform_run(Slot* ctx, const UgIn& u, tsdbhip_sg_out* out, tsdbhip_ti
     fo.nan_t = &sm->nan_t;
     Small* snap = (Small*)ctx->map_out_dev;
     const Small* ini = small_init_dev(ctx);
-    if (!u.mine) {
+    if (u.phase == 2) {
+      ctx->hot_kernel = TSDBHIP_HOT_DS_CHUNKS;  // (the launch of phase 1)
+    } else if (!u.mine) {
       LAUNCH(k_fap_neutral64, dim3(1), dim3(WAVE), 0, st, o_pi, o_pc, fop, sm, pack);
     } else {
       // k_ds_reg, a wave a span, in the aligned group's mode, with the tail
@@ -1853,6 +1902,10 @@ static int uniform_run(Slot* ctx, const UgIn& u, tsdbhip_sg_out* out, tsdbhip_ti
       fa.broken = &sm->fap_broken;
       fa.nrows = rblocks;
       fa.ncopy = UG_NCOPY;
+      if (u.spec) {
+        fa.spec_n_kept = &sm->n_kept;
+        fa.spec_ukey = sm->ukey;
+      }
       {  // the copies, neutral on entry (left neutral by every tail; a new allocation filled once)
         static const char* names[3] = {"ug_copies0", "ug_copies1", "ug_copies2"};
         fa.copies = scratch<unsigned long long>(ctx, names[fop], (uint64_t)UG_NCOPY * WAVE);
@@ -1869,6 +1922,8 @@ static int uniform_run(Slot* ctx, const UgIn& u, tsdbhip_sg_out* out, tsdbhip_ti
       t.n_kept = n_kept; t.t0 = x0; t.step = step; t.kk = kk; t.ncell = n; t.nb = nb;
       t.grid = gridv; t.p_i = o_pi; t.p_cnt = o_pc; t.pack = pack; t.fo = fo; t.snap = snap; t.init = ini;
       t.seq = end_seq;
+      t.spec = u.spec ? 1u : 0u;
+      t.interval = I;
       auto reg = [&](auto aggc) {
         constexpr int A = decltype(aggc)::value;
         static const unsigned stat_lds = [] {
@@ -1889,6 +1944,11 @@ static int uniform_run(Slot* ctx, const UgIn& u, tsdbhip_sg_out* out, tsdbhip_ti
         default: reg(std::integral_constant<int, 3>()); break;
       }
       ctx->hot_kernel = TSDBHIP_HOT_DS_CHUNKS;
+    }
+    if (u.phase == 1) {  // (the host reads the call state back, then decides)
+      ctx->ug_spec_seq = end_seq;
+      tm.paths &= ~TSDBHIP_PATH_UNIFORM;
+      return RC_CONTINUE;
     }
     if (sharded) {
       // the agreement, the validity (MIN) and the 64-slot partials: one
@@ -1934,7 +1994,7 @@ static int uniform_run(Slot* ctx, const UgIn& u, tsdbhip_sg_out* out, tsdbhip_ti
     if (ctx->hot_kernel) tm.hot_ms = ev_ms(ctx, 8, 9);
     tm.hot_kernel = ctx->hot_kernel;
     tm.total_ms = ev_ms(ctx, 0, 5);
-    tm.n_emitted = (uint64_t)nb * n_kept;
+    tm.n_emitted = T * h.n_kept;
     ctx->timing = tm;
     if (T > out->capacity && ctx->want_output) {
       out->err_code = TSDBHIP_E_CAPACITY;
@@ -2351,11 +2411,59 @@ static int spangroup_run_once(Slot* ctx, const tsdbhip_sg_desc* d, tsdbhip_sg_ou
     X->allreduce(ctx, m.buf, 6, X_U64, X_MIN);
     X->group_end(ctx);
   }
+  // the speculative aligned group (unsharded downsampled integer sum / min /
+  // max / avg): k_ug_ds_reg launched now, over every span slot, deciding on
+  // the device from the call state whether the kept spans are one group —
+  // no host round trip before the hot kernel (C3*: ~20 us of host latency).
+  // The host decides alike from the published state below (ug_spec_fits);
+  // not one: that launch touched nothing (but ug_done, reset by itself) and
+  // the call goes on behind it in the stream.
+  UgIn spec_u = {};
+  bool spec_launched = false;
+  // (sharded: every rank, whatever its shard — the collectives are everyone's)
+  if (ug_fap_q && (sharded || S > 0)) {
+    DecodeArgs sa;
+    std::memset(&sa, 0, sizeof sa);
+    sa.span_row_start = span_row_start; sa.row_base = row_base; sa.row_qual_off = row_qual_off;
+    sa.row_val_off = row_val_off; sa.qual = qual; sa.val = val; sa.row_ok = row_ok; sa.row_cell0 = row_cell0;
+    sa.kept = kept; sa.n_kept = 0; sa.sp_ncells = sp_ncells; sa.sp_q1 = sp_q1; sa.sp_q1_shift = sp_q1s;
+    sa.sp_q1_rs = sp_q1rs; sa.row_ncells = row_ncells; sa.row_val_len = row_val_len; sa.sp_ovf_cell = sp_ovf;
+    sa.sp_cap = sp_cap; sa.e_off = eoff; sa.start = d->start_time; sa.end = d->end_time; sa.interval = interval;
+    sa.ds_agg = ds_agg; sa.rate = rate; sa.err = &sm->err; sa.gflags = sm->gflags; sa.range = sm->range;
+    sa.fstar = &sm->fstar; sa.span0 = 0; sa.sp_first = sp_first;
+    spec_u.d = d; spec_u.X = nullptr; spec_u.sm = sm; spec_u.da = sa; spec_u.row_ncells = row_ncells;
+    spec_u.row_val_len = row_val_len; spec_u.n_kept = S; spec_u.lockstep = false; spec_u.mine = true;
+    spec_u.spec = true;
+    if (sharded) {
+      // the one collective group and the finish follow the launch: no host
+      // round trip at all before the call's end
+      spec_u.X = X;
+      spec_u.mine = S > 0;
+      spec_u.phase = 0;
+      const int rc = uniform_run(ctx, spec_u, out, tm);
+      ctx->bitmap_clean = bm_clean;  // (no bitmap touched)
+      ctx->tgdone_clean = tgd_clean;
+      return rc;
+    }
+    spec_u.phase = 1;
+    uniform_run(ctx, spec_u, out, tm);  // (RC_CONTINUE)
+    spec_launched = true;
+    ctx->hot_kernel = TSDBHIP_HOT_NONE;
+  }
   if (!pub1) {  // (the state's last writer cannot publish it: a one-wave kernel does)
     p1 = next_pub(ctx, sizeof(Small));
     LAUNCH(k_publish, dim3(1), dim3(64), 0, st, p1, (const uint64_t*)sm);
   }
   wait_pub(ctx, p1, &h, sizeof h);  // sync 1
+  if (spec_launched && ug_spec_fits(h.ukey[0], h.ukey[1], h.ukey[2], h.ukey[3], h.n_kept, h.err, interval)) {
+    // the speculative aligned group was attempted (its tail decided alike):
+    // its results, or the fallback
+    spec_u.phase = 2;
+    const int rc = uniform_run(ctx, spec_u, out, tm);
+    ctx->bitmap_clean = bm_clean;  // (no bitmap touched)
+    ctx->tgdone_clean = tgd_clean;
+    return rc;
+  }
   // a rank whose own scan failed still takes part in the agreement below (its
   // peers wait there for it), with nothing kept; every rank throws after it
   const bool poisoned = h.err != ERR_NONE;

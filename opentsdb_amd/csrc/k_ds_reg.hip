@@ -318,7 +318,31 @@ struct FapArgs {
   uint32_t* ug_grid;
   uint32_t ug_t0, ug_step, ug_kk, ug_n;
   uint32_t ug_pieces;  // waves a span (0: wps_log2's blocks)
+  // (the uniform path's speculative aligned group, launched before the host
+  // has read the call state back) the kept-span count and the class keys from
+  // the device; the group is attempted iff ug_spec_fits(); non-members write
+  // nothing (there is no E yet)
+  const uint64_t* spec_n_kept;
+  const unsigned long long* spec_ukey;
 };
+
+// The speculative aligned group's condition, read from the call state as the
+// host would read it (uniform_run's "fits"): no error, every kept span
+// proposed one integer key of >= 64 cells, at most 64 buckets a span.
+// (the host decides with the same function from the published state)
+__host__ __device__ inline bool ug_spec_fits(unsigned long long k0, unsigned long long k1, unsigned long long k2,
+                                             unsigned long long k3, uint64_t n_kept, unsigned long long err,
+                                             int64_t interval, uint32_t* nb_out = nullptr, uint32_t* kk_out = nullptr) {
+  if (!(err == ERR_NONE && n_kept > 0 && k0 != ~0ull && k0 == k1 && k2 == k3 && (uint32_t)k0 >= 64 && !(k2 & 8u) &&
+        interval > 0))
+    return false;
+  const uint64_t step = k2 >> 32, n = (uint32_t)k0;
+  if (step == 0) return false;
+  const uint64_t kk = ((uint64_t)interval + step - 1) / step, nb = (n + kk - 1) / kk;
+  if (nb_out) *nb_out = (uint32_t)nb;
+  if (kk_out) *kk_out = (uint32_t)kk;
+  return nb <= WAVE;
+}
 
 // bucket b's timestamp of the key's span (Span.java:399: the mean of its cells' ts)
 DEVI uint32_t ug_bucket_ts(const FapArgs& f, uint32_t b) {
@@ -356,7 +380,16 @@ DEVI void ds_reg_body(const DecodeArgs& a, const SpanDsArgs& g, const uint32_t* 
     for (uint32_t b = threadIdx.x; b < nbk; b += blockDim.x) fap.ug_grid[b] = ug_bucket_ts(fap, b);
   }
   const int64_t I = a.interval;
-  bool ok = k < a.n_kept && I > 0;
+  // (speculative: the kept count from the call state, the whole launch idle
+  // unless the group is one)
+  const bool spec = fap.spec_n_kept != nullptr;
+  const uint32_t nk = spec ? (uint32_t)sld(fap.spec_n_kept) : a.n_kept;
+  // (scalar loads and a wave-uniform verdict: a per-lane `ok` would turn the
+  // span prologue's scalar loads and branches into vector ones)
+  const bool go = !spec || __builtin_amdgcn_readfirstlane(
+                               ug_spec_fits(sld(&fap.spec_ukey[0]), sld(&fap.spec_ukey[1]), sld(&fap.spec_ukey[2]),
+                                            sld(&fap.spec_ukey[3]), nk, sld(a.err), I) ? 1 : 0) != 0;
+  bool ok = go && k < nk && I > 0;
   uint32_t s = 0, W = 0, nb = 0;
   bool flt = false;
   RegSpan sp = {};
@@ -401,6 +434,7 @@ DEVI void ds_reg_body(const DecodeArgs& a, const SpanDsArgs& g, const uint32_t* 
   }
   // an aligned-group member: its buckets go to the block partial, not to E
   const bool fused = fop >= 0 && ok && !flt && nb <= WAVE;
+  if (spec && !fused) ok = false;
   const int efop = fap.ug_grid ? -2 : -1;
   const int sfop = fused ? fop : efop;
   if (ok && ra < rb) {
@@ -420,7 +454,7 @@ DEVI void ds_reg_body(const DecodeArgs& a, const SpanDsArgs& g, const uint32_t* 
     for (uint32_t i = 0; i < wps; i++) any |= s_bad[(wib & ~(wps - 1)) + i];
     ok = any == 0;
   }
-  if (fop >= 0 && k < a.n_kept && lane == 0) {  // the group's class: one key, no span outside it
+  if (fop >= 0 && go && k < nk && lane == 0) {  // the group's class: one key, no span outside it
     if (!(ok && fused)) {
       if (!*(volatile uint32_t*)fap.broken) atomicOr(fap.broken, 1u);
     } else {
@@ -432,7 +466,9 @@ DEVI void ds_reg_body(const DecodeArgs& a, const SpanDsArgs& g, const uint32_t* 
       if (k2 > kv[3]) atomicMax(&fap.key[3], k2);
     }
   }
-  if (k < a.n_kept) {
+  if (spec) {
+    // (nothing past the class bookkeeping above: no list, no E)
+  } else if (k < nk) {
     if (!ok && fap.ug_grid) {  // (a uniform group's outsider: see FapArgs.ug_grid)
       if (lane == 0 && !*(volatile uint32_t*)fap.broken) atomicOr(fap.broken, 1u);  // (any piece)
     } else if (!ok) {
