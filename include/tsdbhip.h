@@ -84,6 +84,8 @@ extern "C" {
 #define TSDBHIP_HOT_DECODE_GEN  3 /* general per-span decode(+downsample)   */
 #define TSDBHIP_HOT_REDUCE_DIRECT 5 /* k_reduce over direct spans (no-downsampling path) */
 #define TSDBHIP_HOT_LOCKSTEP    6 /* k_lockstep: one pass over qualifiers + values of a lockstep group */
+#define TSDBHIP_HOT_UG_DS_REG   7 /* k_ug_ds_reg: the uniform aligned group in one launch */
+#define TSDBHIP_HOT_UG_DEV      8 /* k_ug_dev: integer dev chains of a uniform group */
 #define TSDBHIP_HOT_COMPACT     4 /* k_compact_tiles: classification + single/trivial/short complex
                                      compaction (tsdbhip_compact_rows)      */
 

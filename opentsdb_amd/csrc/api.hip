@@ -1883,7 +1883,7 @@ static int uniform_run(Slot* ctx, const UgIn& u, tsdbhip_sg_out* out, tsdbhip_ti
     Small* snap = (Small*)ctx->map_out_dev;
     const Small* ini = small_init_dev(ctx);
     if (u.phase == 2) {
-      ctx->hot_kernel = TSDBHIP_HOT_DS_CHUNKS;  // (the launch of phase 1)
+      ctx->hot_kernel = TSDBHIP_HOT_UG_DS_REG;  // (the launch of phase 1)
     } else if (!u.mine) {
       LAUNCH(k_fap_neutral64, dim3(1), dim3(WAVE), 0, st, o_pi, o_pc, fop, sm, pack);
     } else {
@@ -1943,7 +1943,7 @@ static int uniform_run(Slot* ctx, const UgIn& u, tsdbhip_sg_out* out, tsdbhip_ti
         case 2: reg(std::integral_constant<int, 2>()); break;
         default: reg(std::integral_constant<int, 3>()); break;
       }
-      ctx->hot_kernel = TSDBHIP_HOT_DS_CHUNKS;
+      ctx->hot_kernel = TSDBHIP_HOT_UG_DS_REG;
     }
     if (u.phase == 1) {  // (the host reads the call state back, then decides)
       ctx->ug_spec_seq = end_seq;
@@ -2119,7 +2119,7 @@ static int uniform_run(Slot* ctx, const UgIn& u, tsdbhip_sg_out* out, tsdbhip_ti
     fe.n_chunks = re.n_chunks;
     dispatch_ug_reduce(ctx, agg, mode, re, fe);
   } else if (u.dev) {  // integer dev: one sequential chain a grid point (k_ug_dev)
-    ctx->hot_kernel = TSDBHIP_HOT_REDUCE_DIRECT;
+    ctx->hot_kernel = TSDBHIP_HOT_UG_DEV;
     EV_START(ctx, 8);
     if (lsp.w8)
       LAUNCH_STOP(EV_STOP_K(ctx, 9), k_ug_dev<8>, dim3((unsigned)((T + WAVE - 1) / WAVE)), dim3(256), 0, st,

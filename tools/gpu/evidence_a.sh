@@ -1,10 +1,12 @@
 #!/bin/bash
-# GPU box, round-4 evidence (part a): the -m gpu suite, smoke, the default
-# bench line and the rocprofv3 kernel stats of that same command, the 2/4/8-way
-# shard rehearsals (C3*, and C3 rate sum 8-way). Output under gpurun_out/r04/.
+# GPU box, a round's evidence (part a): the -m gpu suite (short tracebacks
+# kept), smoke, the default bench line and the rocprofv3 kernel stats of that
+# same command, the 2/4/8-way shard rehearsals (C3*, and C3 rate sum 8-way)
+# with the 8-way C3* step trace. Output under gpurun_out/$R/ (R: round tag).
 set -o pipefail
-O=gpurun_out/r04; mkdir -p $O
-timeout -k 10 900 python -u -m pytest tests -q -x --timeout 600 --timeout-method thread -m gpu --durations=15 \
+R=${R:-r05}
+O=gpurun_out/$R; mkdir -p $O
+timeout -k 10 900 python -u -m pytest tests -q -x --tb=short -rf --timeout 600 --timeout-method thread -m gpu --durations=15 \
   > $O/pytest_gpu.log 2>&1; rc=$?; tail -3 $O/pytest_gpu.log; [ $rc -eq 0 ] || exit $rc
 timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1 || exit 1
 cat $O/smoke.log
@@ -19,4 +21,5 @@ for n in 2 4 8; do
 done
 timeout -k 10 300 python -u bench.py --config c3r_sum --no-cpu --steps 20 --warmup 3 --rehearse-shards 8 > $O/rehearse_c3r_sum_8.json 2>$O/rehearse_c3r_sum_8.err || exit 1
 cut -c1-160 $O/rehearse_c3r_sum_8.json
-echo final_a_done
+bash tools/gpu/trace.sh c3s8 k_assemble_tiles --config c3s --rehearse-shards 8 || exit 1
+echo evidence_a_done
