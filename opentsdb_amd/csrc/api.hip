@@ -92,7 +92,6 @@ struct Slot {
   uint64_t* map_state = nullptr;  // [0, 511]: state words, [512]: flag
   uint64_t* map_state_dev = nullptr;
   uint64_t pub_seq = 0;
-  uint64_t ug_spec_seq = 0;  // the stamp of the speculative aligned group's launch (uniform_run)
   uint32_t timing_late = 0;  // this call's end stamp arrived after the stream sync (check_stamp)
   uint8_t* map_out = nullptr;
   uint8_t* map_out_dev = nullptr;
@@ -1170,6 +1169,8 @@ struct Small {
   unsigned long long ukey[4];
   uint32_t ug_done;   // k_ug_ds_reg's blocks done (its last block runs the tail)
   uint32_t ug_tried;  // (speculative k_ug_ds_reg) the group was attempted
+  uint32_t ug_go;     // (speculative) ug_spec_fits() of the kept spans, by the kept-list kernel
+  uint32_t ug_pad2;
 };
 // Small.xh slots of the grid-agreement header. Every rank decides from these
 // agreed words alone (never from its own lo / hi against them), so the ranks
@@ -1604,15 +1605,9 @@ DEVI void ug_fap_tail(const FapArgs& fap, const UgTail& t) {
   if (t.spec) {
     Small* sm = t.sm;
     uint32_t nb = 0, kk = 0;
-    fits = ug_spec_fits(sm->ukey[0], sm->ukey[1], sm->ukey[2], sm->ukey[3], sm->n_kept, sm->err, t.interval, &nb, &kk);
-    if (!fits && !t.sharded) {
-      // not attempted (the host, deciding alike, goes on without waiting for
-      // this launch): no block touched the state but for ug_done, and nothing
-      // is written to host memory
-      if (tid == 0) sm->ug_done = 0;
-      return;
-    }
-    // (sharded and not one: this rank's partials neutral, its validity 0, as
+    fits = sm->ug_go != 0;
+    ug_spec_fits(sm->ukey[0], sm->ukey[1], sm->ukey[2], sm->ukey[3], sm->n_kept, sm->err, t.interval, &nb, &kk);
+    // (not one: this rank's partials neutral, its validity 0, as
     // k_fap_neutral64's; the exchange is every rank's)
     n_kept = fits ? (uint32_t)sm->n_kept : 0u;
     t0 = (uint32_t)(sm->ukey[0] >> 32);
@@ -1694,12 +1689,18 @@ DEVI void ug_fap_tail(const FapArgs& fap, const UgTail& t) {
   __syncthreads();
   small_snap(sm, t.snap, s_ok ? t.init : nullptr, t.seq);
 }
-template <int AGG>
+template <int AGG, bool SPEC>
 __global__ void __launch_bounds__(256) k_ug_ds_reg(DecodeArgs a, SpanDsArgs g, const uint32_t* ncells,
                                                    const uint32_t* vlen, FapArgs fap, UgTail t) {
   extern __shared__ uint8_t s_pad[];
   if (threadIdx.x == 0 && a.n_kept == 0xFFFFFFFFu) s_pad[0] = 1;
-  ds_reg_body<AGG>(a, g, ncells, vlen, 0u, fap);
+  if (SPEC && !sld(&t.sm->ug_go)) {
+    // (speculative, no group: every block leaves at once — no counter; the
+    // sharded tail, which packs this rank's neutral share, runs in block 0)
+    if (t.sharded && blockIdx.x == 0) ug_fap_tail(fap, t);
+    return;
+  }
+  ds_reg_body<AGG, SPEC>(a, g, ncells, vlen, 0u, fap);
   __shared__ uint32_t s_last;
   __builtin_amdgcn_s_waitcnt(0);  // (this wave's atomics acknowledged)
   __syncthreads();
@@ -1825,11 +1826,9 @@ struct UgIn {
   bool mine;         // (aligned group) this rank's spans make the attempt
   bool dev;          // (lockstep, unsharded) integer dev: the chains of k_ug_dev
   bool e;            // (unsharded, downsampled) k_ds_reg's E + k_reduce's aligned spans
-  bool spec;         // (aligned group, unsharded) launched before the host read the call state:
-                     // n_kept is the span count, the key comes from the device
-  int phase;         // (spec) 1: the launch only (RC_CONTINUE); 2: the finish of that launch
+  bool spec;         // (aligned group, sharded) launched before the host read the call state:
+                     // n_kept is the span count, the group's verdict and key come from the device
 };
-constexpr int RC_CONTINUE = 1002;  // the speculative aligned group found no group: the call goes on
 
 static int uniform_run(Slot* ctx, const UgIn& u, tsdbhip_sg_out* out, tsdbhip_timing& tm) {
   const tsdbhip_sg_desc* d = u.d;
@@ -1868,9 +1867,8 @@ static int uniform_run(Slot* ctx, const UgIn& u, tsdbhip_sg_out* out, tsdbhip_ti
     if (sharded) pack = xchg_desc(ctx, fx, XH_N + 1, (uint64_t*)sm->xh);
     XMove unpack = pack;
     unpack.out = 1;
-    // (phase 2: the stamp the launch's tail writes is phase 1's)
-    if (u.phase != 2) map_out_reserve(ctx, OUT_HDR + 17 * WAVE);
-    const uint64_t end_seq = u.phase == 2 ? ctx->ug_spec_seq : ++ctx->pub_seq;
+    map_out_reserve(ctx, OUT_HDR + 17 * WAVE);
+    const uint64_t end_seq = ++ctx->pub_seq;
     FinalArgs fo;
     std::memset(&fo, 0, sizeof fo);
     fo.T = WAVE;
@@ -1882,9 +1880,7 @@ static int uniform_run(Slot* ctx, const UgIn& u, tsdbhip_sg_out* out, tsdbhip_ti
     fo.nan_t = &sm->nan_t;
     Small* snap = (Small*)ctx->map_out_dev;
     const Small* ini = small_init_dev(ctx);
-    if (u.phase == 2) {
-      ctx->hot_kernel = TSDBHIP_HOT_UG_DS_REG;  // (the launch of phase 1)
-    } else if (!u.mine) {
+    if (!u.mine) {
       LAUNCH(k_fap_neutral64, dim3(1), dim3(WAVE), 0, st, o_pi, o_pc, fop, sm, pack);
     } else {
       // k_ds_reg, a wave a span, in the aligned group's mode, with the tail
@@ -1904,7 +1900,7 @@ static int uniform_run(Slot* ctx, const UgIn& u, tsdbhip_sg_out* out, tsdbhip_ti
       fa.ncopy = UG_NCOPY;
       if (u.spec) {
         fa.spec_n_kept = &sm->n_kept;
-        fa.spec_ukey = sm->ukey;
+        fa.spec_go = &sm->ug_go;
       }
       {  // the copies, neutral on entry (left neutral by every tail; a new allocation filled once)
         static const char* names[3] = {"ug_copies0", "ug_copies1", "ug_copies2"};
@@ -1928,13 +1924,18 @@ static int uniform_run(Slot* ctx, const UgIn& u, tsdbhip_sg_out* out, tsdbhip_ti
         constexpr int A = decltype(aggc)::value;
         static const unsigned stat_lds = [] {
           hipFuncAttributes at = {};
-          return hipFuncGetAttributes(&at, (const void*)k_ug_ds_reg<A>) == hipSuccess ? (unsigned)at.sharedSizeBytes
-                                                                                       : 21000u;
+          return hipFuncGetAttributes(&at, (const void*)k_ug_ds_reg<A, false>) == hipSuccess
+                     ? (unsigned)at.sharedSizeBytes
+                     : 21000u;
         }();
         const unsigned pad = stat_lds < 40960u ? 40960u - stat_lds : 0u;
         EV_START(ctx, 8);
-        LAUNCH_STOP(EV_STOP_K(ctx, 9), (k_ug_ds_reg<A>), dim3(rblocks), dim3(256), pad, st, u.da, gr,
-                    u.row_ncells, u.row_val_len, fa, t);
+        if (u.spec)
+          LAUNCH_STOP(EV_STOP_K(ctx, 9), (k_ug_ds_reg<A, true>), dim3(rblocks), dim3(256), pad, st, u.da, gr,
+                      u.row_ncells, u.row_val_len, fa, t);
+        else
+          LAUNCH_STOP(EV_STOP_K(ctx, 9), (k_ug_ds_reg<A, false>), dim3(rblocks), dim3(256), pad, st, u.da, gr,
+                      u.row_ncells, u.row_val_len, fa, t);
         EV_STOP_M(ctx, 9);
       };
       switch (d->ds_agg) {
@@ -1944,11 +1945,6 @@ static int uniform_run(Slot* ctx, const UgIn& u, tsdbhip_sg_out* out, tsdbhip_ti
         default: reg(std::integral_constant<int, 3>()); break;
       }
       ctx->hot_kernel = TSDBHIP_HOT_UG_DS_REG;
-    }
-    if (u.phase == 1) {  // (the host reads the call state back, then decides)
-      ctx->ug_spec_seq = end_seq;
-      tm.paths &= ~TSDBHIP_PATH_UNIFORM;
-      return RC_CONTINUE;
     }
     if (sharded) {
       // the agreement, the validity (MIN) and the 64-slot partials: one
@@ -2355,6 +2351,10 @@ static int spangroup_run_once(Slot* ctx, const tsdbhip_sg_desc* d, tsdbhip_sg_ou
     K.n_kept_out = &sm->n_kept; K.e_total_out = &sm->e_total; K.pub = p1; K.pub_src = (const uint64_t*)sm;
     K.u_key1 = u_key1; K.u_key2 = u_key2; K.u_vo = u_vo; K.u_qo = u_qo; K.uk_vo = uk_vo; K.uk_qo = uk_qo;
     K.ukey = sm->ukey;
+    // (the speculative aligned group's verdict: every fap query, see below)
+    K.ug_go = ug_fap_q && sharded ? &sm->ug_go : nullptr;
+    K.err = &sm->err;
+    K.ug_interval = interval;
     // one block: assembly + kept list in one launch, for groups with few rows
     // (the block's 16 waves walk the deferred spans: a group of long spans of
     // many rows, C4's, needs the wave-per-span kernel's whole grid)
@@ -2411,17 +2411,16 @@ static int spangroup_run_once(Slot* ctx, const tsdbhip_sg_desc* d, tsdbhip_sg_ou
     X->allreduce(ctx, m.buf, 6, X_U64, X_MIN);
     X->group_end(ctx);
   }
-  // the speculative aligned group (unsharded downsampled integer sum / min /
-  // max / avg): k_ug_ds_reg launched now, over every span slot, deciding on
-  // the device from the call state whether the kept spans are one group —
-  // no host round trip before the hot kernel (C3*: ~20 us of host latency).
-  // The host decides alike from the published state below (ug_spec_fits);
-  // not one: that launch touched nothing (but ug_done, reset by itself) and
-  // the call goes on behind it in the stream.
-  UgIn spec_u = {};
-  bool spec_launched = false;
-  // (sharded: every rank, whatever its shard — the collectives are everyone's)
-  if (ug_fap_q && (sharded || S > 0)) {
+  // the speculative aligned group (sharded downsampled integer sum / min /
+  // max / avg): k_ug_ds_reg launched now, over every span slot, its blocks
+  // reading the kept-list kernel's verdict (Small.ug_go) and the key from the
+  // call state; the one collective group and the finish follow — no host
+  // round trip before the call's end. Every rank, whatever its shard (the
+  // collectives are everyone's). It saves ~35 us of a 0.94 ms C3* 8-way
+  // shard step; unsharded, a launch that finds no group cost C2 ~10 us and
+  // C3*'s own gained nothing measurable (same-box A/Bs, round 5), so the
+  // unsharded aligned group waits for the round trip below.
+  if (ug_fap_q && sharded) {
     DecodeArgs sa;
     std::memset(&sa, 0, sizeof sa);
     sa.span_row_start = span_row_start; sa.row_base = row_base; sa.row_qual_off = row_qual_off;
@@ -2430,40 +2429,20 @@ static int spangroup_run_once(Slot* ctx, const tsdbhip_sg_desc* d, tsdbhip_sg_ou
     sa.sp_q1_rs = sp_q1rs; sa.row_ncells = row_ncells; sa.row_val_len = row_val_len; sa.sp_ovf_cell = sp_ovf;
     sa.sp_cap = sp_cap; sa.e_off = eoff; sa.start = d->start_time; sa.end = d->end_time; sa.interval = interval;
     sa.ds_agg = ds_agg; sa.rate = rate; sa.err = &sm->err; sa.gflags = sm->gflags; sa.range = sm->range;
-    sa.fstar = &sm->fstar; sa.span0 = 0; sa.sp_first = sp_first;
-    spec_u.d = d; spec_u.X = nullptr; spec_u.sm = sm; spec_u.da = sa; spec_u.row_ncells = row_ncells;
-    spec_u.row_val_len = row_val_len; spec_u.n_kept = S; spec_u.lockstep = false; spec_u.mine = true;
-    spec_u.spec = true;
-    if (sharded) {
-      // the one collective group and the finish follow the launch: no host
-      // round trip at all before the call's end
-      spec_u.X = X;
-      spec_u.mine = S > 0;
-      spec_u.phase = 0;
-      const int rc = uniform_run(ctx, spec_u, out, tm);
-      ctx->bitmap_clean = bm_clean;  // (no bitmap touched)
-      ctx->tgdone_clean = tgd_clean;
-      return rc;
-    }
-    spec_u.phase = 1;
-    uniform_run(ctx, spec_u, out, tm);  // (RC_CONTINUE)
-    spec_launched = true;
-    ctx->hot_kernel = TSDBHIP_HOT_NONE;
+    sa.fstar = &sm->fstar; sa.span0 = d->span0; sa.sp_first = sp_first;
+    UgIn u = {};
+    u.d = d; u.X = X; u.sm = sm; u.da = sa; u.row_ncells = row_ncells; u.row_val_len = row_val_len;
+    u.n_kept = S; u.lockstep = false; u.mine = S > 0; u.spec = true;
+    const int rc = uniform_run(ctx, u, out, tm);
+    ctx->bitmap_clean = bm_clean;  // (no bitmap touched)
+    ctx->tgdone_clean = tgd_clean;
+    return rc;
   }
   if (!pub1) {  // (the state's last writer cannot publish it: a one-wave kernel does)
     p1 = next_pub(ctx, sizeof(Small));
     LAUNCH(k_publish, dim3(1), dim3(64), 0, st, p1, (const uint64_t*)sm);
   }
   wait_pub(ctx, p1, &h, sizeof h);  // sync 1
-  if (spec_launched && ug_spec_fits(h.ukey[0], h.ukey[1], h.ukey[2], h.ukey[3], h.n_kept, h.err, interval)) {
-    // the speculative aligned group was attempted (its tail decided alike):
-    // its results, or the fallback
-    spec_u.phase = 2;
-    const int rc = uniform_run(ctx, spec_u, out, tm);
-    ctx->bitmap_clean = bm_clean;  // (no bitmap touched)
-    ctx->tgdone_clean = tgd_clean;
-    return rc;
-  }
   // a rank whose own scan failed still takes part in the agreement below (its
   // peers wait there for it), with nothing kept; every rank throws after it
   const bool poisoned = h.err != ERR_NONE;

@@ -33,6 +33,24 @@ DEVI int64_t dbits(double d) { return __double_as_longlong(d); }
 // scans rows (row-key order: base time, then span), 1 SpanGroup.add in span
 // order (TsdbQuery.java:301-307), 2 iteration.
 #define ERR_NONE (~0ull)
+
+// The speculative aligned group's condition, read from the call state as the
+// host would read it (uniform_run's "fits"): no error, every kept span
+// proposed one integer key of >= 64 cells, at most 64 buckets a span.
+// (the host decides with the same function from the published state)
+__host__ __device__ inline bool ug_spec_fits(unsigned long long k0, unsigned long long k1, unsigned long long k2,
+                                             unsigned long long k3, uint64_t n_kept, unsigned long long err,
+                                             int64_t interval, uint32_t* nb_out = nullptr, uint32_t* kk_out = nullptr) {
+  if (!(err == ERR_NONE && n_kept > 0 && k0 != ~0ull && k0 == k1 && k2 == k3 && (uint32_t)k0 >= 64 && !(k2 & 8u) &&
+        interval > 0))
+    return false;
+  const uint64_t step = k2 >> 32, n = (uint32_t)k0;
+  if (step == 0) return false;
+  const uint64_t kk = ((uint64_t)interval + step - 1) / step, nb = (n + kk - 1) / kk;
+  if (nb_out) *nb_out = (uint32_t)nb;
+  if (kk_out) *kk_out = (uint32_t)kk;
+  return nb <= WAVE;
+}
 DEVI void err_raise(unsigned long long* e, uint32_t stage, uint64_t order, int code) {
   atomicMin(e, ((unsigned long long)stage << 62) | ((order & ((1ull << 54) - 1)) << 8) |
                    (unsigned long long)(uint8_t)(-code));

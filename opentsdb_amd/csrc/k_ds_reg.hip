@@ -323,26 +323,9 @@ struct FapArgs {
   // the device; the group is attempted iff ug_spec_fits(); non-members write
   // nothing (there is no E yet)
   const uint64_t* spec_n_kept;
-  const unsigned long long* spec_ukey;
+  const uint32_t* spec_go;  // Small.ug_go: ug_spec_fits() of the call state, set by the kept-list kernel
 };
 
-// The speculative aligned group's condition, read from the call state as the
-// host would read it (uniform_run's "fits"): no error, every kept span
-// proposed one integer key of >= 64 cells, at most 64 buckets a span.
-// (the host decides with the same function from the published state)
-__host__ __device__ inline bool ug_spec_fits(unsigned long long k0, unsigned long long k1, unsigned long long k2,
-                                             unsigned long long k3, uint64_t n_kept, unsigned long long err,
-                                             int64_t interval, uint32_t* nb_out = nullptr, uint32_t* kk_out = nullptr) {
-  if (!(err == ERR_NONE && n_kept > 0 && k0 != ~0ull && k0 == k1 && k2 == k3 && (uint32_t)k0 >= 64 && !(k2 & 8u) &&
-        interval > 0))
-    return false;
-  const uint64_t step = k2 >> 32, n = (uint32_t)k0;
-  if (step == 0) return false;
-  const uint64_t kk = ((uint64_t)interval + step - 1) / step, nb = (n + kk - 1) / kk;
-  if (nb_out) *nb_out = (uint32_t)nb;
-  if (kk_out) *kk_out = (uint32_t)kk;
-  return nb <= WAVE;
-}
 
 // bucket b's timestamp of the key's span (Span.java:399: the mean of its cells' ts)
 DEVI uint32_t ug_bucket_ts(const FapArgs& f, uint32_t b) {
@@ -355,7 +338,9 @@ DEVI int64_t fap_neutral(int op) { return op == 1 ? INT64_MAX : (op == 2 ? INT64
 // Blocks of 4 waves; 1 << wps_log2 waves per span (a span's rows split into
 // that many contiguous pieces), 4 >> wps_log2 spans per block. (FAP: one wave
 // per span.) The body of k_ds_reg and of the uniform path's k_ug_ds_reg.
-template <int AGG>
+// (SPEC: the speculative aligned group, FapArgs.spec_*; a template argument,
+// so the other launches carry none of its code)
+template <int AGG, bool SPEC = false>
 DEVI void ds_reg_body(const DecodeArgs& a, const SpanDsArgs& g, const uint32_t* ncells, const uint32_t* vlen,
                       uint32_t wps_log2, const FapArgs& fap) {
   __shared__ uint64_t s_v[4][DCH];
@@ -382,13 +367,11 @@ DEVI void ds_reg_body(const DecodeArgs& a, const SpanDsArgs& g, const uint32_t* 
   const int64_t I = a.interval;
   // (speculative: the kept count from the call state, the whole launch idle
   // unless the group is one)
-  const bool spec = fap.spec_n_kept != nullptr;
+  constexpr bool spec = SPEC;
   const uint32_t nk = spec ? (uint32_t)sld(fap.spec_n_kept) : a.n_kept;
   // (scalar loads and a wave-uniform verdict: a per-lane `ok` would turn the
   // span prologue's scalar loads and branches into vector ones)
-  const bool go = !spec || __builtin_amdgcn_readfirstlane(
-                               ug_spec_fits(sld(&fap.spec_ukey[0]), sld(&fap.spec_ukey[1]), sld(&fap.spec_ukey[2]),
-                                            sld(&fap.spec_ukey[3]), nk, sld(a.err), I) ? 1 : 0) != 0;
+  const bool go = !spec || sld(fap.spec_go) != 0;
   bool ok = go && k < nk && I > 0;
   uint32_t s = 0, W = 0, nb = 0;
   bool flt = false;

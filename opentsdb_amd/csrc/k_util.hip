@@ -133,6 +133,11 @@ struct KeptArgs {
   uint64_t* uk_vo;
   uint64_t* uk_qo;
   unsigned long long* ukey;
+  // (null: not wanted) the speculative aligned group's verdict, written with
+  // the keys: ug_spec_fits(keys, n_kept, *err, ug_interval)
+  uint32_t* ug_go;
+  const unsigned long long* err;
+  int64_t ug_interval;
 };
 // [min, max] of the kept spans' keys (uniform-group proposal), per thread
 struct UKeyAcc {
@@ -260,6 +265,8 @@ DEVI void kept_compact_block(const KeptArgs& A) {
     }
     *n_kept_out = ck;
     *e_total_out = ce;
+    if (A.ug_go)
+      *A.ug_go = ug_spec_fits(A.ukey[0], A.ukey[1], A.ukey[2], A.ukey[3], ck, *A.err, A.ug_interval) ? 1u : 0u;
     if (cnt) {
       atomicAdd(n_input, (unsigned long long)cnt);
       atomicMin(&bound[0], (unsigned long long)f);
@@ -449,6 +456,9 @@ __global__ void __launch_bounds__(256) k_kept_scatter_tiles(const uint8_t* kept,
   if (t == 0 && U.u_key1) {
     U.ukey[0] = min((uint64_t)U.ukey[0], u.a0); U.ukey[1] = max((uint64_t)U.ukey[1], u.a1);
     U.ukey[2] = min((uint64_t)U.ukey[2], u.b0); U.ukey[3] = max((uint64_t)U.ukey[3], u.b1);
+    if (U.ug_go)  // (n_kept_out: thread 255 of this block, before the reductions' barriers)
+      *U.ug_go = ug_spec_fits(U.ukey[0], U.ukey[1], U.ukey[2], U.ukey[3], *n_kept_out, *U.err, U.ug_interval)
+                     ? 1u : 0u;
   }
   if (t == 0 && cnt) {
     *n_input += cnt;
