@@ -65,8 +65,9 @@ struct Options {
   int decode = DEC_AUTO;       // "decode": the decode / downsample path forced
   bool aligned_group = true;   // "aligned_group": k_ds_reg's aligned-group reduction may be tried
   int lockstep = 1;            // "lockstep": "off" (0), "on" (1: groups big enough), "always" (2)
-  bool compact_tiles = false;  // "compact": "tiles" sends every row through k_compact_tiles
-  bool compact_rows_vals = false;  // "compact_vals": "flat" (runs of rows) or "rows" (a quarter wave per row)
+  int compact = 0;             // "compact": "auto" (0: k_compact_plain), "split" (1: quals / classify / values
+                               // kernels), "tiles" (2: every row through k_compact_tiles)
+  bool compact_rows_vals = false;  // "compact_vals" (split path): "flat" (runs of rows) or "rows" (a quarter wave per row)
   bool timing_detail = false;  // "timing_detail": decode / grid event pairs (tsdbhip_timing)
   bool check_clean = false;    // "check_clean": verify the zero-on-entry invariants (stderr)
   int events = 0;              // "events": timing events on kernel launches (0), marker packets (1), none (2)
@@ -564,8 +565,8 @@ extern "C" int tsdbhip_set_option(tsdbhip_ctx* ctx, const char* name, const char
     o.lockstep = v == "off" ? 0 : (v == "on" ? 1 : 2);
   }
   else if (n == "compact") {
-    ok = v == "auto" || v == "tiles";
-    o.compact_tiles = v == "tiles";
+    ok = v == "auto" || v == "split" || v == "tiles";
+    o.compact = v == "split" ? 1 : v == "tiles" ? 2 : 0;
   } else if (n == "timing_detail") ok = on_off(o.timing_detail);
   else if (n == "check_clean") ok = on_off(o.check_clean);
   else if (n == "compact_vals") {
@@ -3900,13 +3901,27 @@ static int compact_rows(Slot* ctx, const tsdbhip_rows_desc* d, tsdbhip_rows_out*
     g_ev_pend = nullptr;
     g_ev_pend_i = -1;
     std::memset(ctx->ev_alias, 0xff, sizeof ctx->ev_alias);
-    if (ctx->opt.compact_tiles) {  // (every row through the LDS tiles: the A/B reference)
+    const bool det = ctx->opt.timing_detail;
+    if (ctx->opt.compact == 2) {  // (every row through the LDS tiles: the A/B reference)
       HIPCHK(hipEventRecord(ctx->ev[8], st));
       HIPCHK(hipEventRecord(ctx->ev[4], st));
       HIPCHK(hipEventRecord(ctx->ev[2], st));
       hipLaunchKernelGGL(k_compact_tiles, dim3(grid_for(R, CT_ROWS, 1u << 16)), dim3(256), 0, st, a);
       HIPCHK(hipEventRecord(ctx->ev[9], st));
       HIPCHK(hipEventRecord(ctx->ev[3], st));
+    } else if (ctx->opt.compact == 0) {
+      // plain rows in one pass over runs of rows (k_compact_plain), the others
+      // through the LDS row kernel; k_compact_plain's time reads as the copy
+      // kernels' (hot_ms), the classification's as 0
+      if (!det) ctx->ev_alias[4] = ctx->ev_alias[2] = ctx->ev_alias[9] = ctx->ev_alias[3] = 1;
+      else ctx->ev_alias[4] = ctx->ev_alias[2] = 8;
+      EV_START(ctx, 8);
+      LAUNCH_STOP(det ? EV_STOP_K(ctx, 9) : nullptr, k_compact_plain, dim3(grid_for(R, CP_ROWS, CP_GRID)),
+                  dim3(CP_THREADS), 0, st, a);
+      if (det) EV_STOP_M(ctx, 9);
+      LAUNCH_STOP(det ? EV_STOP_K(ctx, 3) : nullptr, k_compact_rows, dim3(grid_for(R, CR_RANGE, 1u << 14)),
+                  dim3(256), 0, st, a);
+      if (det) EV_STOP_M(ctx, 3);
     } else {
       // plain rows: qualifiers copied, classified (a row per quarter wave,
       // flag fix-ups in place, legacy-float holes recorded), values copied
@@ -3918,7 +3933,6 @@ static int compact_rows(Slot* ctx, const tsdbhip_rows_desc* d, tsdbhip_rows_out*
       // event carried by a launch holds the next kernel back ~4.6 us, four
       // boundaries 2 % of the call — the breakdown then reads 0 and hot_ms
       // the whole call)
-      const bool det = ctx->opt.timing_detail;
       if (!det) ctx->ev_alias[4] = ctx->ev_alias[2] = ctx->ev_alias[9] = ctx->ev_alias[3] = 1;
       EV_START(ctx, 8);
       LAUNCH_STOP(det ? EV_STOP_K(ctx, 4) : nullptr, k_compact_quals, dim3(grid_for(R, CC_ROWS, 1u << 16)),

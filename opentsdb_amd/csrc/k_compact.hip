@@ -1294,8 +1294,18 @@ DEVI uint64_t cv_meta(const CvRow& w) { return w.e - 1 - 4ull * ((w.h0 != ~0u) +
 // One aligned 16-B output chunk c (absolute address) whose first byte lies in
 // row r (w; n = row r + 1, when there is one): one source, one hole or the
 // row end inside (two sources selected by byte), or byte by byte.
-DEVI void cv_chunk(const CompactArgs& a, uint64_t r, const CvRow& w, const CvRow& n, uintptr_t c,
-                   uintptr_t ov_abs, uint64_t V0, bool act) {
+struct CvGlobal {
+  const uint8_t* v;
+  DEVI uint4 v16(uint64_t x) const { return ld16_any(v, x); }
+  DEVI uint8_t b(uint64_t x) const { return v[x]; }
+};
+// (row_at(ru, u): row ru's CvRow into u, false past the rows the caller may
+// write: the batch's, or a piece's in k_compact_plain)
+// (src.v16(x) / src.b(x): 16 bytes / the byte at input value offset x, from
+// global memory or a block's LDS copy)
+template <class RowAt, class Src>
+DEVI void cv_chunk_t(const CompactArgs& a, uint64_t r, const CvRow& w, const CvRow& n, uintptr_t c,
+                     uintptr_t ov_abs, bool act, RowAt row_at, const Src& src) {
   const uint64_t m = cv_meta(w);
   const uint64_t o = c - ov_abs, y0 = o - w.s, x = w.in + y0;
   const uint64_t xa = x + 4 * ((w.h0 <= y0) + (w.h1 <= y0));
@@ -1316,23 +1326,33 @@ DEVI void cv_chunk(const CompactArgs& a, uint64_t r, const CvRow& w, const CvRow
   if (act && (c1 || c2)) {
     const uint64_t xB = c1 ? xa + 4 : xb;
     const int pos = c1 ? (in0 ? (int)(w.h0 - y0) : in1 ? (int)(w.h1 - y0) : 16) : (int)(m - o);
-    *(uint4*)c = cq_funnel(ld16_any(a.val, xa), ld16_any(a.val, xB), pos, !c1);
+    *(uint4*)c = cq_funnel(src.v16(xa), src.v16(xB), pos, !c1);
   } else if (act) {  // byte by byte, walking the rows (two boundaries in the chunk)
     CvRow u = w;
     uint64_t ru = r;
     for (int b = 0; b < 16; b++) {
       const uint64_t ob = o + b;
-      while (ob >= u.e && u.ok) {
-        if (++ru >= a.n_rows) u.ok = false;
-        else u = cv_row(a, ru, V0);
-      }
+      while (ob >= u.e && u.ok)
+        if (!row_at(++ru, u)) u.ok = false;
       if (!u.ok) break;
       const uint64_t mu = cv_meta(u);
       if (ob > mu) continue;  // (unused)
       const uint64_t y = ob - u.s;
-      *(uint8_t*)(c + b) = ob == mu ? (uint8_t)0 : a.val[u.in + y + 4 * ((u.h0 <= y) + (u.h1 <= y))];
+      *(uint8_t*)(c + b) = ob == mu ? (uint8_t)0 : src.b(u.in + y + 4 * ((u.h0 <= y) + (u.h1 <= y)));
     }
   }
+}
+
+DEVI void cv_chunk(const CompactArgs& a, uint64_t r, const CvRow& w, const CvRow& n, uintptr_t c,
+                   uintptr_t ov_abs, uint64_t V0, bool act) {
+  cv_chunk_t(
+      a, r, w, n, c, ov_abs, act,
+      [&](uint64_t ru, CvRow& u) {
+        if (ru >= a.n_rows) return false;
+        u = cv_row(a, ru, V0);
+        return true;
+      },
+      CvGlobal{a.val});
 }
 
 __global__ void __launch_bounds__(256) k_compact_vals(CompactArgs a) {
@@ -1419,6 +1439,404 @@ __global__ void __launch_bounds__(256) k_compact_vals_flat(CompactArgs a) {
       CvRow n = {};
       if (r0 + lo + 1 < a.n_rows) n = s_w[lo + 1];
       cv_chunk(a, r0 + lo, s_w[lo], n, c, ov_abs, V0, true);
+    }
+  }
+}
+
+// ===========================================================================
+// k_compact_plain: the plain-row path in one launch (round 5; the three
+// kernels above stay as the "split" option). A block takes a run of CP_ROWS
+// rows, in pieces whose KV lengths and row bytes fit its LDS (normally
+// the whole run):
+//   1. the piece's KV lengths, qualifier and value bytes staged with 16-B
+//      loads (one round trip);
+//   2. the plain test flat over the piece's KVs, a thread per <= 8
+//      consecutive KVs: value offsets and legacy-float counts inside each row
+//      from one block scan (the prefix at each row's first KV rebuilt from the
+//      owning thread's exclusive prefix), the delta order, the value lengths,
+//      the legacy floats' zero prefixes; the flag fix-ups patched in LDS;
+//   3. per row: status / lengths / write decision (plain) or CQ_PENDING;
+//   4. the qualifiers written from LDS and the values copied around the holes
+//      (cv_chunk), 16-B stores; byte stores only at the piece's two edges, so
+//      no two blocks write one byte.
+// Every row byte is read from HBM once (the KV lengths, the qualifiers, the
+// values), and the output is built from LDS. A run holding
+// a row with offsets out of bounds, and a row whose bytes alone overflow the
+// LDS budget, are left CQ_PENDING for k_compact_rows.
+// ===========================================================================
+#ifndef CP_ROWS
+#define CP_ROWS 32u    // rows per run (a block iteration)
+#endif
+#ifndef CP_KCAP
+#define CP_KCAP 2048u  // KVs per piece
+#endif
+#ifndef CP_QCAP
+#define CP_QCAP 6144u  // qualifier bytes per piece
+#endif
+#ifndef CP_GRID
+#define CP_GRID 65536u  // blocks (each loops over runs, the next run's offsets in flight)
+#endif
+#ifndef CP_THREADS
+#define CP_THREADS 256u  // threads a block
+#endif
+constexpr uint32_t CP_KPT = CP_KCAP / CP_THREADS;  // KVs a thread
+static_assert(CP_KPT == 4 || CP_KPT == 8, "k_compact_plain: 4 or 8 KVs a thread");
+#ifndef CP_VCAP
+#define CP_VCAP 12288u  // value bytes per piece
+#endif
+
+// the staged piece: four segments back to back in 16-B chunk order (the KV
+// qualifier lengths, the KV value lengths, the qualifier bytes, the value
+// bytes; each from its source's aligned 16-B chunk holding the piece's first
+// byte), so that chunk c lands at buf + 16 c and one global_load_lds of a wave
+// writes 64 consecutive chunks
+constexpr uint32_t CP_CHUNKS = 2 * ((14 + 2 * CP_KCAP + 15) / 16) + (15 + CP_QCAP + 15) / 16 + (15 + CP_VCAP + 15) / 16;
+struct __attribute__((aligned(16))) CpLds {
+  uint8_t pad0[16];  // (cv_chunk's second source may start one byte before the piece's values)
+  uint8_t buf[16 * CP_CHUNKS + 64];
+  uint64_t kv[CP_ROWS + 1], qo[CP_ROWS + 1], vo[CP_ROWS + 1];  // the run's row offsets
+  CvRow w[CP_ROWS];
+  // the piece's rows (index i = row - j0): first KV (relative) | plain
+  // candidate (>= 2 KVs, 2 qualifier bytes each) << 31, LDS index of the
+  // first qualifier byte, value bytes, first value byte (relative)
+  uint4 rec[CP_ROWS];
+  uint32_t pstart[CP_ROWS], pend[CP_ROWS];  // scan prefix (value bytes | legacy floats << 16) around the row's KVs
+  uint32_t bad[CP_ROWS], h0[CP_ROWS], h1[CP_ROWS];
+  uint8_t krow[CP_KCAP + 16];  // each KV's row
+  uint32_t scan[CP_THREADS / 64];
+  uint32_t insane;
+};
+static_assert(sizeof(CpLds) <= 80 * 1024, "k_compact_plain: 2 blocks a CU");
+static_assert(CP_QCAP % 16 == 0 && CP_KCAP % 8 == 0, "16-B aligned LDS buffers");
+
+
+// 16 bytes from LDS at any byte index (dword loads + alignbyte).
+DEVI uint4 lds_ld16_any(const uint8_t* L, uint32_t i) {
+  const uint32_t* d = (const uint32_t*)(L + (i & ~3u));
+  const uint32_t sb = i & 3u;
+  uint32_t v[5];
+#pragma unroll
+  for (int k = 0; k < 5; k++) v[k] = d[k];
+  return make_uint4(__builtin_amdgcn_alignbyte(v[1], v[0], sb), __builtin_amdgcn_alignbyte(v[2], v[1], sb),
+                    __builtin_amdgcn_alignbyte(v[3], v[2], sb), __builtin_amdgcn_alignbyte(v[4], v[3], sb));
+}
+
+struct CpBufs {  // the piece's segments in CpLds::buf
+  const uint16_t* ql;
+  const uint16_t* vl;
+  uint8_t* q;  // (index: qualifier offset - the piece's first + hq)
+  const uint8_t* x;  // (index: value offset - the piece's first)
+};
+
+struct CvLds {  // cv_chunk's source: the piece's value bytes in LDS
+  const uint8_t* v;
+  uint64_t base;  // input offset of LDS byte 0
+  DEVI uint4 v16(uint64_t x) const { return lds_ld16_any(v, (uint32_t)(x - base)); }
+  DEVI uint8_t b(uint64_t x) const { return v[x - base]; }
+};
+
+// The block barrier of k_compact_plain: LDS writes complete, no wait for the
+// global stores issued before it (__syncthreads waits vmcnt(0), which
+// includes every outstanding store: ~2 us a barrier under load). No
+// thread of the block reads global memory another one wrote.
+DEVI void cp_sync() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
+
+// Block exclusive scan of x over cp_sync; *total the sum.
+DEVI uint32_t cp_scan(uint32_t x, uint32_t& total, uint32_t* sh /* [CP_THREADS / WAVE] */) {
+  const int lane = lane_id(), w = threadIdx.x / WAVE;
+  const uint32_t ix = wave_incl_scan_u32_dpp(x);
+  if (lane == 63) sh[w] = ix;
+  cp_sync();
+  uint32_t p = 0;
+  total = 0;
+#pragma unroll
+  for (int k = 0; k < (int)(CP_THREADS / WAVE); k++) {
+    if (k < w) p += sh[k];
+    total += sh[k];
+  }
+  return p + ix - x;
+}
+
+// One piece [j0, j1) of the run starting at row r0.
+DEVI void cp_piece(const CompactArgs& a, CpLds& L, uint64_t r0, uint32_t j0, uint32_t j1, uint64_t Q0, uint64_t V0) {
+  const uint32_t t = threadIdx.x, np = j1 - j0;
+  const uint64_t KA = L.kv[j0], QA = L.qo[j0], QB = L.qo[j1], VA = L.vo[j0], VB = L.vo[j1];
+  const uint32_t NK = (uint32_t)(L.kv[j1] - KA);
+  cp_sync();  // (the previous piece's LDS consumed)
+  // ---- 1. staging: KV lengths, qualifier bytes (16-B loads, several in flight) ----
+  const uintptr_t sk = (uintptr_t)(a.kv_qual_len + KA), sv = (uintptr_t)(a.kv_val_len + KA), sq = (uintptr_t)(a.qual + QA);
+  const uintptr_t sx = (uintptr_t)(a.val + VA);
+  const uint32_t hkb = (uint32_t)(sk & 15u), hvb = (uint32_t)(sv & 15u), hq = (uint32_t)(sq & 15u);
+  const uint32_t hx = (uint32_t)(sx & 15u);
+  const uint32_t nk1 = NK ? (hkb + 2 * NK + 15) / 16 : 0u, nv1 = NK ? (hvb + 2 * NK + 15) / 16 : 0u;
+  const uint32_t nq1 = QB > QA ? (uint32_t)((hq + (QB - QA) + 15) / 16) : 0u;
+  const uint32_t nx1 = VB > VA ? (uint32_t)((hx + (VB - VA) + 15) / 16) : 0u;
+  const uint32_t e1 = nk1 + nv1, e2 = e1 + nq1, tot = e2 + nx1;
+  // (four loads in flight a thread, then their LDS writes: the barriers of
+  // this kernel wait for LDS only, never for the global stores before them;
+  // global_load_lds would need a vmcnt(0) wait at the barrier, which also
+  // waits for those stores)
+  auto src = [&](uint32_t c) {
+    return c < nk1  ? (const uint4*)(sk - hkb) + c
+           : c < e1 ? (const uint4*)(sv - hvb) + (c - nk1)
+           : c < e2 ? (const uint4*)(sq - hq) + (c - e1)
+                    : (const uint4*)(sx - hx) + (c - e2);
+  };
+  uint4* const dst = (uint4*)L.buf;
+  constexpr uint32_t T = CP_THREADS;
+  for (uint32_t c = t; c < tot; c += 4 * T) {  // (four named register sets: an array lands in scratch)
+    const bool b1 = c + T < tot, b2 = c + 2 * T < tot, b3 = c + 3 * T < tot;
+    const uint4 v0 = *src(c);
+    uint4 v1 = {}, v2 = {}, v3 = {};
+    if (b1) v1 = *src(c + T);
+    if (b2) v2 = *src(c + 2 * T);
+    if (b3) v3 = *src(c + 3 * T);
+    dst[c] = v0;
+    if (b1) dst[c + T] = v1;
+    if (b2) dst[c + 2 * T] = v2;
+    if (b3) dst[c + 3 * T] = v3;
+  }
+  const CpBufs B{(const uint16_t*)(L.buf + hkb), (const uint16_t*)(L.buf + 16 * nk1 + hvb), L.buf + 16 * e1,
+                 L.buf + 16 * e2 + hx};
+  if (t < np) {  // the piece's rows: record, scan prefixes, flags; each KV's row index in krow
+    const uint32_t j = j0 + t;
+    const uint64_t nk = L.kv[j + 1] - L.kv[j];
+    const uint32_t k0 = (uint32_t)(L.kv[j] - KA), k1 = (uint32_t)(L.kv[j + 1] - KA);
+    const bool cand = nk >= 2 && L.qo[j + 1] - L.qo[j] == 2 * nk;
+    L.rec[t] = make_uint4(k0 | (cand ? 1u << 31 : 0u), (uint32_t)(L.qo[j] - QA) + hq, (uint32_t)(L.vo[j + 1] - L.vo[j]),
+                          (uint32_t)(L.vo[j] - VA));
+    L.pstart[t] = L.pend[t] = 0;
+    L.bad[t] = 0;
+    L.h0[t] = L.h1[t] = ~0u;
+    uint32_t k = k0;
+    for (; k < k1 && (k & 3u); k++) L.krow[k] = (uint8_t)t;
+    for (; k + 4 <= k1; k += 4) *(uint32_t*)(L.krow + k) = t * 0x01010101u;
+    for (; k < k1; k++) L.krow[k] = (uint8_t)t;
+  }
+  cp_sync();
+#ifndef CP_ABL
+#define CP_ABL 0  // (ablation builds only: 1 no value copy, 2 no qualifier copy, 4 no plain test)
+#endif
+  // ---- 2. the plain test, flat over the KVs: a thread per 8 consecutive
+  // KVs, every LDS load of the 8 issued together (no dependent walk) ----
+  const uint32_t kb = CP_KPT * t;
+  const bool any = kb < NK && !(CP_ABL & 4);
+  uint32_t ir[CP_KPT], q_[CP_KPT], ql_[CP_KPT], vl_[CP_KPT], c_[CP_KPT], pre_[CP_KPT];
+  uint32_t sum = 0;
+  {
+    uint32_t kr[CP_KPT / 4] = {};
+    uint4 ql4[(CP_KPT + 7) / 8] = {}, vl4[(CP_KPT + 7) / 8] = {};
+    if (any) {
+#pragma unroll
+      for (int w = 0; w < (int)(CP_KPT / 4); w++) kr[w] = *(const uint32_t*)(L.krow + kb + 4 * w);
+#pragma unroll
+      for (int w = 0; w < (int)((CP_KPT + 7) / 8); w++) {
+        ql4[w] = lds_ld16_any((const uint8_t*)B.ql, 2 * kb + 16 * w);
+        vl4[w] = lds_ld16_any((const uint8_t*)B.vl, 2 * kb + 16 * w);
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < (int)CP_KPT; u++) {
+      const uint32_t k = kb + u;
+      const bool act = k < NK;
+      const uint32_t qw = u % 8 < 2 ? ql4[u / 8].x : u % 8 < 4 ? ql4[u / 8].y : u % 8 < 6 ? ql4[u / 8].z : ql4[u / 8].w;
+      const uint32_t vw = u % 8 < 2 ? vl4[u / 8].x : u % 8 < 4 ? vl4[u / 8].y : u % 8 < 6 ? vl4[u / 8].z : vl4[u / 8].w;
+      ir[u] = (kr[u / 4] >> (8 * (u % 4))) & 0xFFu;
+      ql_[u] = act ? (qw >> (16 * (u % 2))) & 0xFFFFu : 0u;
+      vl_[u] = act ? (vw >> (16 * (u % 2))) & 0xFFFFu : 0u;
+      q_[u] = 0;
+      c_[u] = 0;
+      if (act) {
+        const uint4 R = L.rec[ir[u]];
+        if ((R.x >> 31) && ql_[u] == 2) q_[u] = lds_q16(B.q, R.y + 2 * (k - (R.x & 0x7FFFFFFFu)));
+        const bool leg = (R.x >> 31) && ql_[u] == 2 && cq_legacy(q_[u] & 0xFFu, vl_[u]);  // :510-515
+        c_[u] = min(vl_[u], 9u) | (leg ? 1u << 16 : 0u);
+      }
+      pre_[u] = sum;  // (exclusive, inside the thread)
+      sum += c_[u];
+    }
+  }
+  uint32_t tx;
+  const uint32_t ex = cp_scan(sum, tx, L.scan);
+  // each row's scan prefix before its first KV and after its last, by the
+  // threads owning those KVs (a row without KVs is not plain: never read)
+  if (any) {
+    const uint32_t nxt = kb + CP_KPT < NK ? L.krow[kb + CP_KPT] : 0xFFu;
+#pragma unroll
+    for (int u = 0; u < (int)CP_KPT; u++) {
+      const uint32_t k = kb + u;
+      if (k < NK) {
+        const uint32_t i = ir[u];
+        if (u == 0 ? (k == 0 || L.krow[k - 1] != i) : ir[u - 1] != i) L.pstart[i] = ex + pre_[u];
+        if (u + 1 < (int)CP_KPT ? (k + 1 >= NK || ir[u + 1] != i) : (k + 1 >= NK || nxt != i))
+          L.pend[i] = ex + pre_[u] + c_[u];
+      }
+    }
+  }
+  cp_sync();
+  if (any) {
+#pragma unroll
+    for (int u = 0; u < (int)CP_KPT; u++) {
+      const uint32_t k = kb + u;
+      if (k >= NK) continue;
+      const uint32_t i = ir[u];
+      const uint4 R = L.rec[i];
+      if (!(R.x >> 31)) continue;
+      const uint32_t kv_i = R.x & 0x7FFFFFFFu;
+      const uint32_t rel = ex + pre_[u] - L.pstart[i], vin = rel & 0xFFFFu, nl = rel >> 16;
+      const uint32_t ql = ql_[u], vl = vl_[u], q = q_[u];
+      const bool leg = (c_[u] >> 16) != 0;
+      const uint32_t qpos = R.y + 2 * (k - kv_i);
+      bool kbad = ql != 2 || vl == 0 || vl > 8;
+      if (!kbad && k > kv_i) {  // deltas strictly increasing (the KV before is in the row)
+        const uint32_t qp = u > 0 ? q_[u > 0 ? u - 1 : 0] : lds_q16(B.q, qpos - 2);
+        kbad = (q >> 4) <= (qp >> 4);
+      }
+      if (!kbad) kbad = vin + vl > R.z;
+      if (leg && !kbad) {  // the 4-byte zero prefix (fixFloatingPointValue :530-544)
+        const uint8_t* vp = B.x + R.w + vin;
+        kbad = (vp[0] | vp[1] | vp[2] | vp[3]) != 0;
+      }
+      if (!kbad) {  // fixQualifierFlags :490-499 (delta bits unchanged: a neighbour's order check
+                    // reads the same delta before or after the patch)
+        const uint8_t f = (uint8_t)cq_fixq(q & 0xFFu, leg ? 4u : vl);
+        if (f != (uint8_t)q) B.q[qpos + 1] = f;
+      } else {
+        L.bad[i] = 1;
+      }
+      if (leg) {  // the holes: output positions of the row's first two legacy floats
+        if (nl == 0) L.h0[i] = vin;
+        else if (nl == 1) L.h1[i] = vin - 4;
+      }
+    }
+  }
+  cp_sync();
+  // ---- 3. the rows' results ----
+  if (t < np) {
+    const uint32_t j = j0 + t;
+    const uint64_t r = r0 + j;
+    const uint4 R = L.rec[t];
+    const uint32_t d = L.pend[t] - L.pstart[t], vsum = d & 0xFFFFu, legs = d >> 16;
+    const bool plain = (R.x >> 31) && !L.bad[t] && legs <= 2 && vsum == R.z;
+    CvRow w;
+    w.s = L.vo[j] - V0 + r;
+    w.e = L.vo[j + 1] - V0 + r + 1;
+    w.in = L.vo[j];
+    w.h0 = plain ? L.h0[t] : ~0u;
+    w.h1 = plain ? L.h1[t] : ~0u;
+    w.ok = true;
+    L.w[t] = w;
+    if (plain) {
+      a.out_qoff[r] = L.qo[j] - Q0;
+      a.out_voff[r] = w.s;
+      cq_finish(a, r, CQ_TRIVIAL, (uint32_t)(L.qo[j + 1] - L.qo[j]), vsum - 4 * legs + 1);
+    } else {
+      a.status[r] = CQ_PENDING;  // (to the LDS row kernel)
+    }
+  }
+  cp_sync();
+  // ---- 4. qualifiers from LDS, values around the holes ----
+  {
+    const uintptr_t d0 = (uintptr_t)a.oq + (QA - Q0), d1 = (uintptr_t)a.oq + (QB - Q0);
+    const uintptr_t c0 = (d0 + 15) & ~(uintptr_t)15, c1 = d1 & ~(uintptr_t)15;
+    for (uintptr_t c = c0 + 16ull * t; c < c1 && !(CP_ABL & 2); c += 16ull * CP_THREADS)
+      *(uint4*)c = lds_ld16_any(B.q, (uint32_t)(c - d0) + hq);
+    const uintptr_t he = c0 < d1 ? c0 : d1, ts = c1 > he ? c1 : he;  // edge bytes [d0, he), [ts, d1)
+    const uintptr_t x = t < 16 ? d0 + t : ts + (t - 16);
+    if ((t < 16 && x < he) || (t >= 16 && t < 32 && x < d1)) *(uint8_t*)x = B.q[(uint32_t)(x - d0) + hq];
+  }
+  {
+    const uintptr_t ov_abs = (uintptr_t)a.ov;
+    const uintptr_t d0 = ov_abs + L.w[0].s, d1 = ov_abs + L.w[np - 1].e;
+    const uintptr_t c0 = (d0 + 15) & ~(uintptr_t)15, c1 = d1 & ~(uintptr_t)15;
+    auto row_at = [&](uint64_t ru, CvRow& u) {
+      if (ru >= r0 + j1) return false;
+      u = L.w[ru - r0 - j0];
+      return true;
+    };
+    auto find = [&](uint64_t o) {  // the piece's last row whose output starts at or before o
+      uint32_t lo = 0, hi = np - 1;
+      while (lo < hi) {
+        const uint32_t mid = (lo + hi + 1) >> 1;
+        if (L.w[mid].s <= o) lo = mid; else hi = mid - 1;
+      }
+      return lo;
+    };
+    const CvLds xs{L.pad0, VA - 16 - 16 * e2 - hx};
+    for (uintptr_t c = c0 + 16ull * t; c < c1 && !(CP_ABL & 1); c += 16ull * CP_THREADS) {
+      const uint32_t i = find(c - ov_abs);
+      CvRow n = {};
+      if (i + 1 < np) n = L.w[i + 1];
+      cv_chunk_t(a, r0 + j0 + i, L.w[i], n, c, ov_abs, true, row_at, xs);
+    }
+    const uintptr_t he = c0 < d1 ? c0 : d1, ts = c1 > he ? c1 : he;
+    const uintptr_t x = t < 16 ? d0 + t : ts + (t - 16);
+    if ((t < 16 && x < he) || (t >= 16 && t < 32 && x < d1)) {
+      const uint64_t o = x - ov_abs;
+      const CvRow& u = L.w[find(o)];
+      const uint64_t m = cv_meta(u), y = o - u.s;
+      if (o <= m) *(uint8_t*)x = o == m ? (uint8_t)0 : xs.b(u.in + y + 4 * ((u.h0 <= y) + (u.h1 <= y)));
+    }
+  }
+}
+
+__global__ void __launch_bounds__(CP_THREADS) k_compact_plain(CompactArgs a) {
+  __shared__ CpLds L;
+  const uint32_t t = threadIdx.x;
+  const uint64_t Q0 = a.row_qual_off[0], V0 = a.row_val_off[0];
+  const uint64_t nrun = (a.n_rows + CP_ROWS - 1) / CP_ROWS;
+  // the next run's row offsets are loaded while this run is compacted
+  uint64_t hk = 0, hq = 0, hv = 0;
+  auto fetch = [&](uint64_t rn) {
+    if (rn < nrun && t <= min((uint64_t)CP_ROWS, a.n_rows - rn * CP_ROWS)) {
+      hk = a.row_kv_start[rn * CP_ROWS + t];
+      hq = a.row_qual_off[rn * CP_ROWS + t];
+      hv = a.row_val_off[rn * CP_ROWS + t];
+    }
+  };
+  fetch(blockIdx.x);
+  for (uint64_t run = blockIdx.x; run < nrun; run += gridDim.x) {
+    const uint64_t r0 = run * CP_ROWS;
+    const uint32_t nr = (uint32_t)min((uint64_t)CP_ROWS, a.n_rows - r0);
+    cp_sync();  // (the previous run's LDS consumed)
+    if (t <= nr) {
+      L.kv[t] = hk;
+      L.qo[t] = hq;
+      L.vo[t] = hv;
+    }
+    fetch(run + gridDim.x);
+    if (t == 0) L.insane = 0;
+    cp_sync();
+    if (t < nr) {  // the row's offsets in bounds (then its ranges are disjoint from every other row's)
+      const uint64_t r = r0 + t;
+      const uint64_t kv = L.kv[t], kv_n = L.kv[t + 1], qo = L.qo[t], qo_n = L.qo[t + 1], vo = L.vo[t], vo_n = L.vo[t + 1];
+      const bool sane = kv_n >= kv && kv_n <= a.n_kvs && qo_n >= qo && vo_n >= vo && qo >= Q0 && vo >= V0 &&
+                        qo_n <= a.qual_nbytes && vo_n <= a.val_nbytes && qo_n - Q0 <= a.qcap &&
+                        vo_n - V0 + r + 1 <= a.vcap && vo_n - vo < (1ull << 32);
+      if (!sane) L.insane = 1;
+    }
+    cp_sync();
+    if (L.insane) {  // the whole run to the row kernel (which finds the bad offsets)
+      if (t < nr) a.status[r0 + t] = CQ_PENDING;
+      continue;
+    }
+    uint32_t j0 = 0;
+    while (j0 < nr) {  // (uniform)
+      uint32_t lo = j0, hi = nr;  // the most rows from j0 whose KVs and qualifier bytes fit
+      while (lo < hi) {
+        const uint32_t mid = (lo + hi + 1) >> 1;
+        if (L.kv[mid] - L.kv[j0] <= CP_KCAP && L.qo[mid] - L.qo[j0] <= CP_QCAP && L.vo[mid] - L.vo[j0] <= CP_VCAP)
+          lo = mid;
+        else
+          hi = mid - 1;
+      }
+      if (lo == j0) {  // one row over the budget alone
+        if (t == 0) a.status[r0 + j0] = CQ_PENDING;
+        j0++;
+        continue;
+      }
+      cp_piece(a, L, r0, j0, lo, Q0, V0);
+      j0 = lo;
     }
   }
 }

@@ -191,16 +191,22 @@ def test_pack_rejects_long_kv():
 
 
 # ------------------------------------------------------------------ GPU ----
-@pytest.fixture(autouse=True, params=["plain", "plain_rowvals", "tiles"])
+@pytest.fixture(autouse=True, params=["plain", "split", "split_rowvals", "tiles"])
 def compact_path(request):
-    """every GPU test three times: the plain-row path (classify / shifted copy
-    / LDS row kernel, the default, its value copy flat over runs of rows),
-    the same with the value copy a quarter wave per row, and all rows through
-    the LDS tiles"""
-    if request.param == "plain_rowvals":
-        yield from with_option(request, "compact_vals", "rows", "flat")
+    """every GPU test four times: the plain rows in one pass over runs of rows
+    (k_compact_plain, the default) and the others through the LDS row kernel;
+    the round-4 split path (qualifier copy / classify / value copy flat over
+    runs of rows); the same with the value copy a quarter wave per row; all
+    rows through the LDS tiles"""
+    if request.param == "split_rowvals":
+        request.getfixturevalue("ctx").set_option("compact", "split") if request.node.get_closest_marker("gpu") else None
+        try:
+            yield from with_option(request, "compact_vals", "rows", "flat")
+        finally:
+            if request.node.get_closest_marker("gpu"):
+                request.getfixturevalue("ctx").set_option("compact", "auto")
     else:
-        yield from with_option(request, "compact", "tiles" if request.param == "tiles" else "auto", "auto")
+        yield from with_option(request, "compact", {"plain": "auto"}.get(request.param, request.param), "auto")
 
 
 def assert_same(g, o):
@@ -261,6 +267,35 @@ def test_gpu_compaction_long_rows(ctx):
     """Rows of up to 900 KVs (several waves of KVs per row)."""
     b = compaction.synth_rows(3000, seed=9, min_cells=300, max_cells=900, p_complex=0.5, p_conflict=0.01)
     assert_same(compaction.compact_rows(ctx, b), oracle.compact_rows(b))
+
+
+@pytest.mark.gpu
+def test_gpu_compaction_rows_over_budget(ctx):
+    """Rows of 2100-3000 KVs: each alone over k_compact_plain's LDS budget
+    (2048 KVs a piece), next to short rows (pieces of one row, rows skipped)."""
+    b = compaction.synth_rows(60, seed=11, min_cells=2100, max_cells=3000, p_complex=0.2, p_conflict=0.0)
+    assert_same(compaction.compact_rows(ctx, b), oracle.compact_rows(b))
+    rows = [[(Q(d, 7), L(d)) for d in range(n)] for n in (2, 2200, 3, 40, 2500, 2, 1)]
+    b = compaction.pack_rows(rows)
+    assert_same(compaction.compact_rows(ctx, b), oracle.compact_rows(b))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("seed", [1, 2])
+def test_gpu_compaction_tiny_rows(ctx, seed):
+    """Rows of 1-3 cells: many rows a 16-B chunk, piece edges inside rows' heads."""
+    b = compaction.synth_rows(50000, seed=seed, min_cells=1, max_cells=3, p_complex=0.1, p_conflict=0.01)
+    assert_same(compaction.compact_rows(ctx, b), oracle.compact_rows(b))
+
+
+@pytest.mark.gpu
+def test_gpu_compaction_legacy_heavy(ctx):
+    """Half the cells legacy 8-byte floats: rows with 0, 1, 2 and more holes
+    (more than two go to the row kernel)."""
+    kp = np.array([0.1, 0.1, 0.1, 0.1, 0.05, 0.05, 0.5, 0.0])
+    for lo, hi in ((2, 4), (2, 40)):
+        b = compaction.synth_rows(20000, seed=13, min_cells=lo, max_cells=hi, p_complex=0.05, kind_p=kp / kp.sum())
+        assert_same(compaction.compact_rows(ctx, b), oracle.compact_rows(b))
 
 
 @pytest.mark.gpu

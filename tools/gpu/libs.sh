@@ -18,5 +18,5 @@ for f in sorted(os.listdir(d)):
     if f.endswith(".json"):
         j = json.load(open(os.path.join(d, f)))
         r = j["roofline"]
-        print(f, round(j["ms_per_step"], 4), {k: round(v, 3) for k, v in r.items() if k.endswith("_ms")})
+        print(f, round(j["ms_per_step"], 4), {k: round(v, 3) for k, v in r.items() if k.endswith("_ms") and v is not None})
 PY

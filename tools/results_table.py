@@ -25,6 +25,12 @@ for key, name in ORDER:
         pct = f"{100 * r['frac']:.0f} % of VALU issue"
     elif r.get("bound") == "valu":
         ach, pct = f"{r['kernel']} {r['kernel_ms']:.1f} ms, VALU-bound", "-"
+    elif key != "c5" and r.get("kernel_ms") and r["kernel_ms"] < 0.25 * x["ms_per_step"]:
+        # (the dominant kernel is a small share of the step: a roofline of it
+        # would describe a fraction of the time)
+        ach = (f"launch / latency-bound: {r['kernel']} {r['kernel_ms']:.3f} ms of the "
+               f"{x['ms_per_step']:.3f} ms step")
+        pct = "-"
     else:
         hbm = r.get("hbm", r)
         ach = f"{hbm['achieved']:.0f} GB/s ({r['kernel']} {r['kernel_ms']:.3f} ms)"
