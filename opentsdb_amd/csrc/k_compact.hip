@@ -1535,11 +1535,10 @@ struct CvLds {  // cv_chunk's source: the piece's value bytes in LDS
   DEVI uint8_t b(uint64_t x) const { return v[x - base]; }
 };
 
-// The block barrier of k_compact_plain: LDS writes complete, no wait for the
-// global stores issued before it (__syncthreads waits vmcnt(0), which
-// includes every outstanding store: ~2 us a barrier under load). No
-// thread of the block reads global memory another one wrote.
-DEVI void cp_sync() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
+// The block barrier of k_compact_plain. (A barrier waiting for LDS only —
+// s_waitcnt lgkmcnt(0) + s_barrier, not for the global stores before it —
+// measured 1 % slower on C5 than __syncthreads, profiles/r05/c5/.)
+DEVI void cp_sync() { __syncthreads(); }
 
 // Block exclusive scan of x over cp_sync; *total the sum.
 DEVI uint32_t cp_scan(uint32_t x, uint32_t& total, uint32_t* sh /* [CP_THREADS / WAVE] */) {
@@ -1572,10 +1571,8 @@ DEVI void cp_piece(const CompactArgs& a, CpLds& L, uint64_t r0, uint32_t j0, uin
   const uint32_t nq1 = QB > QA ? (uint32_t)((hq + (QB - QA) + 15) / 16) : 0u;
   const uint32_t nx1 = VB > VA ? (uint32_t)((hx + (VB - VA) + 15) / 16) : 0u;
   const uint32_t e1 = nk1 + nv1, e2 = e1 + nq1, tot = e2 + nx1;
-  // (four loads in flight a thread, then their LDS writes: the barriers of
-  // this kernel wait for LDS only, never for the global stores before them;
-  // global_load_lds would need a vmcnt(0) wait at the barrier, which also
-  // waits for those stores)
+  // (four loads in flight a thread, then their LDS writes; global_load_lds
+  // staging measured slower: profiles/r05/c5/)
   auto src = [&](uint32_t c) {
     return c < nk1  ? (const uint4*)(sk - hkb) + c
            : c < e1 ? (const uint4*)(sv - hvb) + (c - nk1)
