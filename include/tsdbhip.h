@@ -324,9 +324,12 @@ int         tsdbhip_open_devices(const int32_t* devices, uint32_t n, tsdbhip_ctx
  *   "lockstep"      "on" | "off" | "always"   the lockstep proposal (k_lockstep):
  *                   "on" for groups of >= 2048 lockstep waves (and sharded
  *                   groups), "always" for any group
- *   "compact"       "auto" | "tiles"  (tiles: every row through k_compact_tiles)
- *   "compact_vals"  "flat" | "rows"  plain rows' value copy: a block per run
- *                   of rows with a thread per 16-B chunk (default), or a
+ *   "compact"       "auto" | "split" | "tiles"  plain rows in one pass over
+ *                   runs of rows (k_compact_plain, auto), or through the
+ *                   qualifier copy / classification / value copy kernels
+ *                   (split), or every row through k_compact_tiles (tiles)
+ *   "compact_vals"  "flat" | "rows"  the split path's value copy: a block per
+ *                   run of rows with a thread per 16-B chunk (default), or a
  *                   quarter wave per row
  *   "timing_detail" "on" | "off"   decode / grid event pairs in tsdbhip_timing
  *   "check_clean"   "on" | "off"   check the zero-on-entry invariants (stderr)
