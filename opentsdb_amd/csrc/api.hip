@@ -2383,8 +2383,16 @@ static int spangroup_run_once(Slot* ctx, const tsdbhip_sg_desc* d, tsdbhip_sg_ou
   // (downsampled exact integer aggregation); the spans' class keys are
   // proposed at assembly for them
   const bool auto_dec = ctx->opt.decode == DEC_AUTO;
+  // (unsharded, lockstep "on": the group needs >= 2048 lockstep waves, and
+  // with C <= qual_nbytes / 2 cells in all and n in each of n_kept <= S
+  // spans, ceil(n / LS_TILE) * max(1, n_kept / 64) <= max(ceil(C / LS_TILE),
+  // C / (64 LS_TILE) + S / 64 + 1): a group under that bound cannot take it,
+  // and its assembly skips the key probe — C1's 100 spans: 7 us)
+  const uint64_t c_max = d->qual_nbytes / 2;
+  const bool ls_size_ok = sharded || ctx->opt.lockstep == 2 ||
+                          std::max<uint64_t>((c_max + LS_TILE - 1) / LS_TILE, c_max / (64 * LS_TILE) + S / 64 + 1) >= 2048;
   const bool ug_ls_q = ug_allow && auto_dec && interval == 0 && ls_allow && ctx->opt.lockstep && !exact &&
-                       (agg != TSDBHIP_AGG_DEV || rate);
+                       (agg != TSDBHIP_AGG_DEV || rate) && ls_size_ok;
   const bool ug_fap_q = ug_allow && auto_dec && interval > 0 && !rate && ds_agg <= 3 && agg <= 3 && !exact &&
                         ctx->opt.aligned_group && !ctx->opt.timing_detail;
   // (integer dev without rate, unsharded: the sequential chains of k_ug_dev)
