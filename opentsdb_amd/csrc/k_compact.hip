@@ -1883,11 +1883,13 @@ __global__ void __launch_bounds__(256) k_compact_rows(CompactArgs a) {
   for (uint64_t rb = (uint64_t)blockIdx.x * CR_RANGE; rb < a.n_rows; rb += (uint64_t)gridDim.x * CR_RANGE) {
     // ---- the range's CQ_PENDING rows, in row order, into s_list ----
     __syncthreads();  // (the previous range's list consumed)
-    uint32_t pend[CR_RANGE / 256], wpos = 0;
+    constexpr int CR_U = CR_RANGE >= 256 ? (int)(CR_RANGE / 256) : 1;  // (ranges of 64 / 128 rows: lanes idle)
+    uint32_t pend[CR_U], wpos = 0;
 #pragma unroll
-    for (int u = 0; u < (int)(CR_RANGE / 256); u++) {
-      const uint64_t r = rb + (uint64_t)w * (CR_RANGE / 4) + u * WAVE + lane;  // (wave w: a quarter of the range)
-      const bool pd = r < a.n_rows && a.status[r] == CQ_PENDING;
+    for (int u = 0; u < CR_U; u++) {
+      const uint32_t q = u * WAVE + lane;  // (wave w: a quarter of the range)
+      const uint64_t r = rb + (uint64_t)w * (CR_RANGE / 4) + q;
+      const bool pd = q < CR_RANGE / 4 && r < a.n_rows && a.status[r] == CQ_PENDING;
       const uint64_t m = ballot(pd);
       pend[u] = pd ? wpos + (uint32_t)__popcll(m & lanemask_lt(lane)) : ~0u;
       wpos += (uint32_t)__popcll(m);
@@ -1898,7 +1900,7 @@ __global__ void __launch_bounds__(256) k_compact_rows(CompactArgs a) {
     for (int v = 0; v < w; v++) woff += s_wn[v];
     const uint32_t n = s_wn[0] + s_wn[1] + s_wn[2] + s_wn[3];
 #pragma unroll
-    for (int u = 0; u < (int)(CR_RANGE / 256); u++)
+    for (int u = 0; u < CR_U; u++)
       if (pend[u] != ~0u) s_list[woff + pend[u]] = (uint32_t)(rb + (uint64_t)w * (CR_RANGE / 4) + u * WAVE + lane);
     const uint32_t* list = s_list;
   for (uint32_t t = 0; t * CT_ROWS < n; t++) {
