@@ -313,6 +313,11 @@ def emit(res):
     print(json.dumps(res), file=out, flush=True)
 
 
+# every kernel tsdbhip_compact_rows launches (the C5 line's traffic is their
+# sum per call, from the committed PMC summary)
+C5_KERNELS = ("k_compact_wave", "k_compact_rows", "k_compact_complex", "k_compact_dups")
+
+
 def bench_c5(args):
     """C5 (configs[4]): tsdbhip_compact_rows over 1M HBM-resident rows."""
     import torch
@@ -395,8 +400,7 @@ def bench_c5(args):
     if not detail:
         hot, cx, cls, rows_k = [float("nan")], [float("nan")], [float("nan")], [float("nan")]
     kname = "tsdbhip_compact_rows (whole call)"
-    call_kernels = ("k_compact_quals+k_compact_classify+k_compact_vals+k_compact_vals_flat+k_compact_rows"
-                    "+k_compact_complex+k_compact_dups")
+    call_kernels = "+".join(C5_KERNELS)
     traffic, traffic_src = pmc_traffic("c5", call_kernels, 1)
     res = {
         "metric": "raw cells/sec compacted (CompactionQueue.compact) + % HBM roofline, 1 MI355X",

@@ -49,7 +49,7 @@
 extern "C" {
 #endif
 
-#define TSDBHIP_ABI_VERSION 6
+#define TSDBHIP_ABI_VERSION 7
 
 /* ---- return codes ---------------------------------------------------- */
 #define TSDBHIP_OK               0
@@ -86,8 +86,8 @@ extern "C" {
 #define TSDBHIP_HOT_LOCKSTEP    6 /* k_lockstep: one pass over qualifiers + values of a lockstep group */
 #define TSDBHIP_HOT_UG_DS_REG   7 /* k_ug_ds_reg: the uniform aligned group in one launch */
 #define TSDBHIP_HOT_UG_DEV      8 /* k_ug_dev: integer dev chains of a uniform group */
-#define TSDBHIP_HOT_COMPACT     4 /* k_compact_tiles: classification + single/trivial/short complex
-                                     compaction (tsdbhip_compact_rows)      */
+#define TSDBHIP_HOT_COMPACT     4 /* k_compact_wave: every row's classification and compaction
+                                     in one pass (tsdbhip_compact_rows)      */
 
 /* ---- desc flags ------------------------------------------------------- */
 #define TSDBHIP_DESC_DEVICE   0x1u /* every array pointer in the desc is a
@@ -150,8 +150,9 @@ typedef struct tsdbhip_sg_out {
 
 /* Per-call device timings of the last tsdbhip_spangroup_run on a ctx,
  * measured with HIP events on the ctx stream (milliseconds). After
- * tsdbhip_compact_rows: total_ms, hot_ms = decode_ms = k_compact_rows,
- * reduce_ms = k_compact_complex, hot_kernel = TSDBHIP_HOT_COMPACT. */
+ * tsdbhip_compact_rows: total_ms (the call), and under "timing_detail"
+ * hot_ms = k_compact_wave, grid_ms = k_compact_rows, reduce_ms =
+ * k_compact_complex + k_compact_dups; hot_kernel = TSDBHIP_HOT_COMPACT. */
 typedef struct tsdbhip_timing {
   float    total_ms;        /* first kernel start .. last kernel end        */
   float    decode_ms;       /* decode(+downsample) kernel — dominant, HBM   */
@@ -172,6 +173,8 @@ typedef struct tsdbhip_timing {
                                only after the stream sync; summed in totals */
   uint64_t x_bytes;         /* sharded calls: bytes this rank received in the
                                call's collectives (ABI v6)                  */
+  uint64_t h2d_bytes;       /* bytes of host-resident inputs the call copied
+                               to HBM (a rerun copies none again; ABI v7)  */
 } tsdbhip_timing;
 /* tsdbhip_timing.paths */
 #define TSDBHIP_PATH_ALIGNED_GROUP 1u  /* k_ds_reg's aligned-group reduction
@@ -324,13 +327,6 @@ int         tsdbhip_open_devices(const int32_t* devices, uint32_t n, tsdbhip_ctx
  *   "lockstep"      "on" | "off" | "always"   the lockstep proposal (k_lockstep):
  *                   "on" for groups of >= 2048 lockstep waves (and sharded
  *                   groups), "always" for any group
- *   "compact"       "auto" | "split" | "tiles"  plain rows in one pass over
- *                   runs of rows (k_compact_plain, auto), or through the
- *                   qualifier copy / classification / value copy kernels
- *                   (split), or every row through k_compact_tiles (tiles)
- *   "compact_vals"  "flat" | "rows"  the split path's value copy: a block per
- *                   run of rows with a thread per 16-B chunk (default), or a
- *                   quarter wave per row
  *   "timing_detail" "on" | "off"   decode / grid event pairs in tsdbhip_timing
  *   "check_clean"   "on" | "off"   check the zero-on-entry invariants (stderr)
  *   "events"        "kernel" | "marker" | "none"   how tsdbhip_timing is measured:

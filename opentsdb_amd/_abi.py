@@ -6,7 +6,7 @@ and the test harness.
 """
 import ctypes as C
 
-ABI_VERSION = 6
+ABI_VERSION = 7
 PATH_ALIGNED_GROUP = 1  # tsdbhip_timing.paths (include/tsdbhip.h)
 PATH_ALIGNED_RERUN = 2
 PATH_LOCKSTEP = 4  # k_lockstep: one pass over the qualifiers and values of a lockstep group
@@ -94,7 +94,7 @@ class SgOut(C.Structure):
 
 
 HOT_NONE, HOT_DS_CHUNKS, HOT_DECODE_FAST, HOT_DECODE_GEN = 0, 1, 2, 3
-HOT_NAMES = {1: "k_ds_reg+k_ds_spans", 2: "k_decode_fast", 3: "k_decode_general", 4: "k_compact_quals+k_compact_vals",
+HOT_NAMES = {1: "k_ds_reg+k_ds_spans", 2: "k_decode_fast", 3: "k_decode_general", 4: "k_compact_wave",
              5: "k_reduce", 6: "k_lockstep", 7: "k_ug_ds_reg", 8: "k_ug_dev"}
 
 
@@ -115,6 +115,7 @@ class Timing(C.Structure):
         ("paths", C.c_uint32),
         ("late_stamp", C.c_uint32),
         ("x_bytes", C.c_uint64),
+        ("h2d_bytes", C.c_uint64),
     ]
 
 

@@ -65,9 +65,6 @@ struct Options {
   int decode = DEC_AUTO;       // "decode": the decode / downsample path forced
   bool aligned_group = true;   // "aligned_group": k_ds_reg's aligned-group reduction may be tried
   int lockstep = 1;            // "lockstep": "off" (0), "on" (1: groups big enough), "always" (2)
-  int compact = 0;             // "compact": "auto" (0: k_compact_plain), "split" (1: quals / classify / values
-                               // kernels), "tiles" (2: every row through k_compact_tiles)
-  bool compact_rows_vals = false;  // "compact_vals" (split path): "flat" (runs of rows) or "rows" (a quarter wave per row)
   bool timing_detail = false;  // "timing_detail": decode / grid event pairs (tsdbhip_timing)
   bool check_clean = false;    // "check_clean": verify the zero-on-entry invariants (stderr)
   int events = 0;              // "events": timing events on kernel launches (0), marker packets (1), none (2)
@@ -107,6 +104,10 @@ struct Slot {
   Xchg* x = nullptr;  // the exchange of a sharded call (its rank / nranks)
   Options opt;        // the context's options, copied at the lease
   bool want_output = true;  // false: a non-zero rank of an in-process sharded call
+  // a rerun of the same call (spangroup_run): the host-resident inputs are
+  // already in HBM (stage() copies nothing); h2d_bytes: this call's copies
+  bool reuse_inputs = false;
+  uint64_t h2d_bytes = 0;
   // left by the previous spangroup_run that completed: its call state reset
   // to the initial values, its grid bitmap all zero (k_call_end)
   bool sm_ready = false, bitmap_clean = false;
@@ -322,6 +323,7 @@ static void timing_add(tsdbhip_ctx* c, const tsdbhip_timing& t) {  // (c->mu hel
   c->sum.paths |= t.paths;
   c->sum.x_bytes += t.x_bytes;
   c->sum.late_stamp += t.late_stamp;
+  c->sum.h2d_bytes += t.h2d_bytes;
   c->n_sum++;
 }
 
@@ -564,15 +566,8 @@ extern "C" int tsdbhip_set_option(tsdbhip_ctx* ctx, const char* name, const char
     ok = v == "on" || v == "off" || v == "always";
     o.lockstep = v == "off" ? 0 : (v == "on" ? 1 : 2);
   }
-  else if (n == "compact") {
-    ok = v == "auto" || v == "split" || v == "tiles";
-    o.compact = v == "split" ? 1 : v == "tiles" ? 2 : 0;
-  } else if (n == "timing_detail") ok = on_off(o.timing_detail);
+  else if (n == "timing_detail") ok = on_off(o.timing_detail);
   else if (n == "check_clean") ok = on_off(o.check_clean);
-  else if (n == "compact_vals") {
-    ok = v == "flat" || v == "rows";
-    o.compact_rows_vals = v == "rows";
-  }
   else if (n == "events") {
     static const char* names[] = {"kernel", "marker", "none"};
     ok = false;
@@ -705,8 +700,10 @@ static const T* stage(Slot* ctx, const char* name, const T* src, size_t count, b
                       size_t pad = 0) {
   if (on_device) return src;
   T* d = scratch<T>(ctx, name, count + pad);
+  if (ctx->reuse_inputs) return d;  // (the same call's earlier attempt staged it)
   if (count) HIPCHK(hipMemcpyAsync(d, src, count * sizeof(T), hipMemcpyHostToDevice, ctx->stream));
   if (pad) HIPCHK(hipMemsetAsync((char*)d + count * sizeof(T), 0, pad * sizeof(T), ctx->stream));
+  ctx->h2d_bytes += count * sizeof(T);
   return d;
 }
 
@@ -1904,6 +1901,37 @@ struct UgIn {
                      // n_kept is the span count, the group's verdict and key come from the device
 };
 
+// The E variant's pieces a span (at most `want`): k_ds_reg's wave p takes
+// rows [p rp, (p + 1) rp), rp = ceil(rows / pieces), and needs its first
+// cell on a bucket head (cell index % kk == 0) — else the span is an
+// outsider and the call falls back. The rows of a span on the key are its
+// hourly rows (Const.MAX_TIMESPAN, RowKey base times: multiples of 3600 s)
+// holding a cell of t0 + c step, c < n; the largest aligned count wins (1
+// always is). A layout other than hourly rows only makes the device check
+// refuse the pieces, as before (45-min or 3-h buckets over hourly
+// 1-s rows).
+static uint32_t ug_e_pieces(uint32_t t0, uint32_t step, uint32_t n, uint32_t kk, uint32_t want) {
+  if (want <= 1 || !step || !kk || n == 0) return 1;
+  const uint64_t last = (uint64_t)t0 + (uint64_t)(n - 1) * step;
+  const uint64_t b0 = t0 - t0 % 3600u, nb = (last - b0) / 3600 + 1;
+  if (nb > (1u << 16)) return 1;
+  std::vector<uint64_t> cell0;  // first cell of each non-empty row
+  cell0.reserve(nb);
+  for (uint64_t i = 0; i < nb; i++) {
+    const uint64_t B = b0 + 3600 * i;
+    const uint64_t c = B <= t0 ? 0 : (B - t0 + step - 1) / step;
+    if (c < n && (cell0.empty() || cell0.back() != c)) cell0.push_back(c);
+  }
+  const uint64_t R = cell0.size();
+  for (uint32_t P = (uint32_t)std::min<uint64_t>(want, R); P > 1; P--) {
+    const uint64_t rp = (R + P - 1) / P;
+    bool ok = true;
+    for (uint64_t p = 1; p < P && p * rp < R && ok; p++) ok = cell0[p * rp] % kk == 0;
+    if (ok) return P;
+  }
+  return 1;
+}
+
 static int uniform_run(Slot* ctx, const UgIn& u, tsdbhip_sg_out* out, tsdbhip_timing& tm) {
   const tsdbhip_sg_desc* d = u.d;
   Xchg* X = u.X;
@@ -2146,7 +2174,7 @@ static int uniform_run(Slot* ctx, const UgIn& u, tsdbhip_sg_out* out, tsdbhip_ti
     // (waves a span, its rows in contiguous pieces: C2's 24 rows a span, 0.266
     // ms a step with 3 pieces, 0.269 with 2, 0.281 with 4, 0.290 with 1,
     // 0.310 with 8, 0.489 with 24 — same box)
-    uint32_t pieces = (uint32_t)std::max<uint64_t>(1, rps / 8);
+    uint32_t pieces = ug_e_pieces(x0, step, n, e_kk, (uint32_t)std::max<uint64_t>(1, rps / 8));
     if (const char* e = getenv("TSDBHIP_UG_P")) pieces = (uint32_t)std::max(1, atoi(e));  // (A/B runs)
     const uint32_t rblocks = (uint32_t)(((uint64_t)n_kept * pieces + 3) / 4);
     SpanDsArgs gr = {};
@@ -3473,18 +3501,29 @@ static int spangroup_run_once(Slot* ctx, const tsdbhip_sg_desc* d, tsdbhip_sg_ou
 // The call, and its rerun on the proven path when k_lockstep found a
 // qualifier off the lockstep proposal (every rank of a sharded call agrees
 // on that, so all of them rerun)
+// (a rerun stages nothing again: the host-resident inputs the first attempt
+// copied are still in HBM — ADVICE r5)
 static int spangroup_run(Slot* ctx, const tsdbhip_sg_desc* d, tsdbhip_sg_out* out) {
+  struct Reuse {  // (reset on every exit, exceptions included)
+    Slot* c;
+    ~Reuse() { c->reuse_inputs = false; }
+  } reuse{ctx};
+  ctx->h2d_bytes = 0;
+  ctx->reuse_inputs = false;
   int rc = spangroup_run_once(ctx, d, out, true, true);
   uint32_t paths = 0;
   if (rc == RC_UG_FALLBACK) {  // (the uniform path's aligned group did not stand)
     paths |= TSDBHIP_PATH_UNIFORM_FALLBACK;
+    ctx->reuse_inputs = true;
     rc = spangroup_run_once(ctx, d, out, true, false);
   }
   if (rc == RC_REDO) {
     paths |= TSDBHIP_PATH_DIRECT_REDO;
+    ctx->reuse_inputs = true;
     rc = spangroup_run_once(ctx, d, out, false, false);
   }
   ctx->timing.paths |= paths;
+  ctx->timing.h2d_bytes = ctx->h2d_bytes;
   return rc;
 }
 
@@ -3809,8 +3848,8 @@ extern "C" int tsdbhip_desc_download(tsdbhip_ctx* c, const tsdbhip_sg_desc* d, u
 
 // ------------------------------------------------------- compaction ------
 // CompactionQueue.compact (CompactionQueue.java:243-743) for a batch of rows:
-// k_compact_tiles (16-row LDS tiles, wave per row) then k_compact_complex for the rows holding a
-// compacted cell (LDS cell table, or global scratch for very long rows).
+// k_compact_wave (a wave per run of rows), k_compact_rows for the rows it leaves, k_compact_complex
+// for the biggest complex rows, k_compact_dups for the pending rows' write/delete decisions.
 static int compact_rows(Slot* ctx, const tsdbhip_rows_desc* d, tsdbhip_rows_out* out);
 extern "C" int tsdbhip_compact_rows(tsdbhip_ctx* c, const tsdbhip_rows_desc* d, tsdbhip_rows_out* out) {
   if (!c || !d || !out) return TSDBHIP_E_INVALID_ARG;
@@ -3835,6 +3874,8 @@ static int compact_rows(Slot* ctx, const tsdbhip_rows_desc* d, tsdbhip_rows_out*
   }
   try {
     const bool dev = (d->flags & TSDBHIP_DESC_DEVICE) != 0;
+    ctx->h2d_bytes = 0;
+    ctx->reuse_inputs = false;
     uint64_t ext[4];  // row_qual_off[0], [R], row_val_off[0], [R]
     if (dev) {
       uint64_t* h = (uint64_t*)ctx->host_small;
@@ -3910,60 +3951,26 @@ static int compact_rows(Slot* ctx, const tsdbhip_rows_desc* d, tsdbhip_rows_out*
     g_ev_pend_i = -1;
     std::memset(ctx->ev_alias, 0xff, sizeof ctx->ev_alias);
     const bool det = ctx->opt.timing_detail;
-    if (ctx->opt.compact == 2) {  // (every row through the LDS tiles: the A/B reference)
-      HIPCHK(hipEventRecord(ctx->ev[8], st));
-      HIPCHK(hipEventRecord(ctx->ev[4], st));
-      HIPCHK(hipEventRecord(ctx->ev[2], st));
-      hipLaunchKernelGGL(k_compact_tiles, dim3(grid_for(R, CT_ROWS, 1u << 16)), dim3(256), 0, st, a);
-      HIPCHK(hipEventRecord(ctx->ev[9], st));
-      HIPCHK(hipEventRecord(ctx->ev[3], st));
-    } else if (ctx->opt.compact == 0) {
-      // plain rows in one pass over runs of rows (k_compact_plain), the others
-      // through the LDS row kernel; k_compact_plain's time reads as the copy
-      // kernels' (hot_ms), the classification's as 0
-      if (!det) ctx->ev_alias[4] = ctx->ev_alias[2] = ctx->ev_alias[9] = ctx->ev_alias[3] = 1;
-      else ctx->ev_alias[4] = ctx->ev_alias[2] = 8;
-      EV_START(ctx, 8);
-      LAUNCH_STOP(det ? EV_STOP_K(ctx, 9) : nullptr, k_compact_plain, dim3(grid_for(R, CP_ROWS, CP_GRID)),
-                  dim3(CP_THREADS), 0, st, a);
-      if (det) EV_STOP_M(ctx, 9);
-      LAUNCH_STOP(det ? EV_STOP_K(ctx, 3) : nullptr, k_compact_rows, dim3(grid_for(R, CR_RANGE, 1u << 14)),
-                  dim3(256), 0, st, a);
-      if (det) EV_STOP_M(ctx, 3);
-    } else {
-      // plain rows: qualifiers copied, classified (a row per quarter wave,
-      // flag fix-ups in place, legacy-float holes recorded), values copied
-      // around the holes; the other rows through the LDS row kernel
-      a.tile_bad = scratch<uint8_t>(ctx, "c_tbad", R / CC_ROWS + 1);
-      a.row_holes = scratch<uint2>(ctx, "c_holes", R);
-      // (each boundary event the stop of the kernel before it, under
-      // "timing_detail"; else only the call's first and last events: an
-      // event carried by a launch holds the next kernel back ~4.6 us, four
-      // boundaries 2 % of the call — the breakdown then reads 0 and hot_ms
-      // the whole call)
-      if (!det) ctx->ev_alias[4] = ctx->ev_alias[2] = ctx->ev_alias[9] = ctx->ev_alias[3] = 1;
-      EV_START(ctx, 8);
-      LAUNCH_STOP(det ? EV_STOP_K(ctx, 4) : nullptr, k_compact_quals, dim3(grid_for(R, CC_ROWS, 1u << 16)),
-                  dim3(256), 0, st, a);
-      if (det) EV_STOP_M(ctx, 4);
-      LAUNCH_STOP(det ? EV_STOP_K(ctx, 2) : nullptr, k_compact_classify, dim3(grid_for(R, 16, 1u << 16)),
-                  dim3(256), 0, st, a);
-      if (det) EV_STOP_M(ctx, 2);
-      if (ctx->opt.compact_rows_vals)
-        LAUNCH_STOP(det ? EV_STOP_K(ctx, 9) : nullptr, k_compact_vals, dim3(grid_for(R, 16, 1u << 16)), dim3(256), 0,
-                    st, a);
-      else
-        LAUNCH_STOP(det ? EV_STOP_K(ctx, 9) : nullptr, k_compact_vals_flat, dim3(grid_for(R, CV_ROWS, 1u << 16)),
-                    dim3(256), 0, st, a);
-      if (det) EV_STOP_M(ctx, 9);
-      LAUNCH_STOP(det ? EV_STOP_K(ctx, 3) : nullptr, k_compact_rows, dim3(grid_for(R, CR_RANGE, 1u << 14)),
-                  dim3(256), 0, st, a);
-      if (det) EV_STOP_M(ctx, 3);
-    }
+    // the plain rows through k_compact_wave (a wave per run of rows,
+    // LDS-staged), the others (CQ_PENDING) through k_compact_rows (a wave per
+    // row), the biggest complex rows through k_compact_complex and their
+    // write/delete decisions. k_compact_wave's time reads as hot_ms,
+    // k_compact_rows' as grid_ms, the rest as reduce_ms (under
+    // "timing_detail": each boundary an event; else only the call's first and
+    // last events, and hot_ms is the whole call)
+    if (!det) ctx->ev_alias[4] = ctx->ev_alias[2] = ctx->ev_alias[9] = ctx->ev_alias[3] = 1;
+    else ctx->ev_alias[4] = ctx->ev_alias[2] = 8;
+    EV_START(ctx, 8);
+    LAUNCH_STOP(det ? EV_STOP_K(ctx, 9) : nullptr, k_compact_wave, dim3(grid_for(R, CW_ROWS * CW_WAVES, 1u << 30)),
+                dim3(WAVE * CW_WAVES), 0, st, a);
+    if (det) EV_STOP_M(ctx, 9);
+    LAUNCH_STOP(det ? EV_STOP_K(ctx, 3) : nullptr, k_compact_rows, dim3(grid_for(R, CR_RANGE, 1u << 14)), dim3(256),
+                0, st, a);
+    if (det) EV_STOP_M(ctx, 3);
     HIPCHK(hipGetLastError());
     LAUNCH(k_compact_complex<true>, dim3(1024), dim3(256), 0, ctx->stream, a);
     LAUNCH(k_compact_complex<false>, dim3(256), dim3(256), 0, ctx->stream, a);
-    if (a.out_write) LAUNCH(k_compact_dups, dim3(grid_for(R, 4 * WAVE, 4096)), dim3(256), 0, ctx->stream, a);
+    if (a.out_write) LAUNCH(k_compact_dups, dim3(256), dim3(256), 0, ctx->stream, a);
     HIPCHK(hipGetLastError());
     EV_FINAL(ctx, 1);
     uint32_t cnt[4];
@@ -3972,6 +3979,7 @@ static int compact_rows(Slot* ctx, const tsdbhip_rows_desc* d, tsdbhip_rows_out*
       set_error(ctx, "tsdbhip_compact_rows: a row's KV lengths do not match its offsets");
       return TSDBHIP_E_INVALID_ARG;
     }
+    const uint64_t n_cx = (uint64_t)cnt[0] + cnt[1] + cnt[3];
     if (!dev) {
       HIPCHK(hipMemcpyAsync(out->row_status, a.status, R, hipMemcpyDeviceToHost, ctx->stream));
       HIPCHK(hipMemcpyAsync(out->row_qual_off, a.out_qoff, 8 * R, hipMemcpyDeviceToHost, ctx->stream));
@@ -3988,15 +3996,16 @@ static int compact_rows(Slot* ctx, const tsdbhip_rows_desc* d, tsdbhip_rows_out*
     }
     tsdbhip_timing t = {};
     t.total_ms = ev_ms(ctx, 8, 1);
-    t.hot_ms = ev_ms(ctx, 8, 4) + ev_ms(ctx, 2, 9);  // k_compact_quals + k_compact_vals (tiles: k_compact_tiles)
+    t.hot_ms = ev_ms(ctx, 8, 4) + ev_ms(ctx, 2, 9);  // k_compact_wave
     t.hot_kernel = TSDBHIP_HOT_COMPACT;
-    t.decode_ms = ev_ms(ctx, 4, 2);  // k_compact_classify
+    t.decode_ms = ev_ms(ctx, 4, 2);  // (0)
     t.grid_ms = ev_ms(ctx, 9, 3);    // k_compact_rows
     t.reduce_ms = ev_ms(ctx, 3, 1);  // k_compact_complex + k_compact_dups
+    t.h2d_bytes = ctx->h2d_bytes;
     ctx->timing = t;
     out->qual_used = qext;
     out->val_used = vext + R;
-    out->n_complex = (uint64_t)cnt[0] + cnt[1] + cnt[3];
+    out->n_complex = n_cx;
   } catch (Fail& f) {
     return f.code;
   }

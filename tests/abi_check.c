@@ -47,7 +47,7 @@ static int layout(void) {
   F(tsdbhip_timing, reduce_ms); F(tsdbhip_timing, exchange_ms); F(tsdbhip_timing, hot_ms);
   F(tsdbhip_timing, hot_kernel); F(tsdbhip_timing, n_collectives); F(tsdbhip_timing, decode_bytes);
   F(tsdbhip_timing, alg_bytes); F(tsdbhip_timing, n_grid); F(tsdbhip_timing, n_emitted);
-  F(tsdbhip_timing, paths); F(tsdbhip_timing, late_stamp); F(tsdbhip_timing, x_bytes);
+  F(tsdbhip_timing, paths); F(tsdbhip_timing, late_stamp); F(tsdbhip_timing, x_bytes); F(tsdbhip_timing, h2d_bytes);
   END();
   BEGIN(tsdbhip_rows_desc);
   F(tsdbhip_rows_desc, flags); F(tsdbhip_rows_desc, reserved0); F(tsdbhip_rows_desc, n_rows);

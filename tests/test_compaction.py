@@ -9,7 +9,6 @@ import numpy as np
 
 import pytest
 
-from helpers import with_option
 
 import closed_form_compaction as cfc
 import oracle
@@ -191,24 +190,6 @@ def test_pack_rejects_long_kv():
 
 
 # ------------------------------------------------------------------ GPU ----
-@pytest.fixture(autouse=True, params=["plain", "split", "split_rowvals", "tiles"])
-def compact_path(request):
-    """every GPU test four times: the plain rows in one pass over runs of rows
-    (k_compact_plain, the default) and the others through the LDS row kernel;
-    the round-4 split path (qualifier copy / classify / value copy flat over
-    runs of rows); the same with the value copy a quarter wave per row; all
-    rows through the LDS tiles"""
-    if request.param == "split_rowvals":
-        request.getfixturevalue("ctx").set_option("compact", "split") if request.node.get_closest_marker("gpu") else None
-        try:
-            yield from with_option(request, "compact_vals", "rows", "flat")
-        finally:
-            if request.node.get_closest_marker("gpu"):
-                request.getfixturevalue("ctx").set_option("compact", "auto")
-    else:
-        yield from with_option(request, "compact", {"plain": "auto"}.get(request.param, request.param), "auto")
-
-
 def assert_same(g, o):
     assert np.array_equal(g.status, o.status)
     assert np.array_equal(g.qual_len, o.qual_len) and np.array_equal(g.val_len, o.val_len)
@@ -271,8 +252,9 @@ def test_gpu_compaction_long_rows(ctx):
 
 @pytest.mark.gpu
 def test_gpu_compaction_rows_over_budget(ctx):
-    """Rows of 2100-3000 KVs: each alone over k_compact_plain's LDS budget
-    (2048 KVs a piece), next to short rows (pieces of one row, rows skipped)."""
+    """Rows of 2100-3000 KVs: each alone over k_compact_wave's and
+    k_compact_rows' LDS budgets, next to short rows (pieces of one row, rows
+    skipped)."""
     b = compaction.synth_rows(60, seed=11, min_cells=2100, max_cells=3000, p_complex=0.2, p_conflict=0.0)
     assert_same(compaction.compact_rows(ctx, b), oracle.compact_rows(b))
     rows = [[(Q(d, 7), L(d)) for d in range(n)] for n in (2, 2200, 3, 40, 2500, 2, 1)]

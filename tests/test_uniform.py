@@ -228,3 +228,56 @@ def test_uniform_sharded_broken_in_one_rank(mctx):
     g, o = both(mctx, ss, agg=0, dsi=60, dsa=3)
     assert_same(g, o)
     assert paths(mctx) & _abi.PATH_UNIFORM_FALLBACK
+
+
+@pytest.mark.timeout(180)
+@pytest.mark.parametrize("dsi", [0, 60])
+def test_uniform_sharded_many_spans_rank_shifted(mctx, dsi):
+    """more than KC_MAX (4096) spans a rank, so the kept list goes through
+    the tiled kernels (k_kept_tiles / k_kept_scatter_tiles, whose last block
+    alone folds the key words: ADVICE r5), and the last rank's spans one row
+    (3600 s) later than everyone else's: the key agreement must see the
+    disagreement — lockstep refuses the uniform path, the aligned group does
+    not stand — and the general path gives the oracle's results"""
+    n = 4200 * mctx.ranks
+    ss = synth.regular(n, 120, I64, seed=21, step=1)
+    last = n - n // mctx.ranks  # (contiguous shards: the last rank's first span)
+    r0 = int(ss.span_row_start[last])
+    ss.row_base[r0:] += 3600
+    g, o = both(mctx, ss, agg=0, dsi=dsi, dsa=3 if dsi else 0)
+    assert_same(g, o)
+    if dsi:
+        assert paths(mctx) & _abi.PATH_UNIFORM_FALLBACK and not paths(mctx) & _abi.PATH_ALIGNED_GROUP
+    else:
+        assert not paths(mctx) & _abi.PATH_UNIFORM
+
+
+@pytest.mark.timeout(120)
+def test_uniform_sharded_fallback_stages_once(mctx):
+    """a downsampled query whose aligned group does not stand reruns on the
+    general path without copying its host-resident inputs again:
+    the rerun's call copies as many bytes as a call that never tried"""
+    n = 4 * mctx.ranks
+    spans = [I([(T0 + (s >= n // 2) + 2 * i, s * 7 + i) for i in range(900)], minimal=False) for s in range(n)]
+    ss = packing.pack_spans(spans)
+    g, o = both(mctx, ss, agg=2, dsi=60, dsa=3)
+    assert_same(g, o)
+    assert paths(mctx) & _abi.PATH_UNIFORM_FALLBACK
+    fell_back = mctx.timing().h2d_bytes
+    g, o = both(mctx, ss, agg=2, dsi=60, dsa=4)  # (dev downsampling: no aligned-group attempt)
+    assert_same(g, o)
+    assert not paths(mctx) & _abi.PATH_UNIFORM_FALLBACK
+    assert fell_back == mctx.timing().h2d_bytes > 0
+
+
+@pytest.mark.parametrize("agg", [0, 4])
+@pytest.mark.parametrize("dsi", [2700, 10800])
+def test_uniform_e_buckets_across_pieces(ctx, agg, dsi):
+    """the E variant's pieces (k_ds_reg waves a span) must each start on a
+    bucket head: 45-minute and 3-hour buckets over 16 hourly rows of 1-s
+    cells do not divide 8 rows, so the host picks fewer pieces and the call
+    takes the uniform path without a fallback"""
+    ss = synth.regular(12, 16 * 3600, F64, seed=23, step=1)
+    g, o = run_both(ctx, ss, 0, U32MAX, agg, False, dsi, 3)
+    assert_same(g, o)
+    assert paths(ctx) & _abi.PATH_UNIFORM and not paths(ctx) & _abi.PATH_UNIFORM_FALLBACK
