@@ -799,6 +799,12 @@ def main():
             n_input = int(t.item())
     ms_step = elapsed / args.steps * 1e3
     value = n_input / (elapsed / args.steps)
+    late_total = int(tsum.late_stamp)
+    if dist is not None:
+        import torch as _t
+        t = _t.tensor([late_total], dtype=_t.int64)
+        dist.all_reduce(t)
+        late_total = int(t.item())
 
     # roofline of the dominant kernel: SURVEY.md §8(d) algorithmic bytes (the
     # row bytes it streams) over its own duration (HIP events on its stream)
@@ -891,6 +897,10 @@ def main():
                         "aligned_rerun": bool(tsum.paths & _abi.PATH_ALIGNED_RERUN)}
         if world > 1 or rehearse:  # collective launches per call on this rank (RCCL groups)
             res["collectives_per_call"] = tsum.n_collectives / ncalls
+        # timed calls whose call-end stamp (the host's proof that the snapshot
+        # and results are this call's) arrived only after the stream sync,
+        # summed over the ranks
+        res["late_stamp"] = {"calls": late_total, "of": ncalls * world}
         if rehearse:
             res["rehearsal"] = {"shards": rehearse, "note": f"shard 0 of {rehearse} on a 1-rank RCCL "
                                 "communicator; value = this shard's points/s, not a node figure"}

@@ -97,6 +97,12 @@ def lib():
     return L
 
 
+# late call-end stamps (tsdbhip_timing.late_stamp) over every context closed
+# in this process, and the calls they came from: the test suite's summary
+# reports them (tests/conftest.py)
+STAMP_TOTALS = {"late_stamp": 0, "calls": 0}
+
+
 class Context:
     """One tsdbhip_ctx: a GPU (or, with `devices`, one shard per listed GPU of
     this process, a device may repeat), its pool of per-call streams and HBM
@@ -156,6 +162,12 @@ class Context:
 
     def close(self):
         if self._h:
+            try:
+                t, n = self.timing_totals()
+                STAMP_TOTALS["late_stamp"] += int(t.late_stamp)
+                STAMP_TOTALS["calls"] += n
+            except Exception:  # (bookkeeping only)
+                pass
             self._lib.tsdbhip_close(self._h)
             self._h = C.c_void_p()
 

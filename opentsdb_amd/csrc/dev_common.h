@@ -80,6 +80,17 @@ DEVI uint32_t wave_incl_scan_u32_dpp(uint32_t x) {
   x += dpp_u32<0x143, 0xc>(x);
   return x;
 }
+// the wave's maximum of non-negative x (DPP max scan; lanes outside a step's
+// source keep 0, the identity), uniform
+DEVI uint32_t wave_max_u32_dpp(uint32_t x) {
+  x = max(x, dpp_u32<0x111, 0xf>(x));
+  x = max(x, dpp_u32<0x112, 0xf>(x));
+  x = max(x, dpp_u32<0x114, 0xf>(x));
+  x = max(x, dpp_u32<0x118, 0xf>(x));
+  x = max(x, dpp_u32<0x142, 0xa>(x));
+  x = max(x, dpp_u32<0x143, 0xc>(x));
+  return __builtin_amdgcn_readlane(x, 63);
+}
 template <int CTRL, int ROWMASK>
 DEVI uint64_t dpp_u64(uint64_t x) {
   const uint32_t lo = dpp_u32<CTRL, ROWMASK>((uint32_t)x);

@@ -789,6 +789,9 @@ DEVI int cq_row_lds(const CompactArgs& a, uint64_t r, const RowHdr& h, const Row
       *ncells_out = ncells;
       return -1;
     }
+#ifdef CR_ABL
+    if (CR_ABL & 2) st = CQ_ERROR; else
+#endif
     st = cq_complex_lds<SORT>(L, p, nk, nvalid - nmulti, ncells, keys, pay, runs, lane, &oql, &ovl);
     reached = CQ_REACHED_COMPLEX;
   } else if (!any_fix && !any_junk) {
@@ -876,9 +879,7 @@ DEVI void cq_dup_core(const CompactArgs& a, uint64_t r, uint64_t nk, uint64_t qs
     qcar += readlane_u32(qi, 63);
     vcar += readlane_u32(vi, 63);
     const bool multi = act && ql != 2 && ql != 0 && (ql & 1) == 0;
-    uint32_t mx = multi ? ql : 0u;
-#pragma unroll
-    for (int m = 1; m < WAVE; m <<= 1) mx = max(mx, (uint32_t)__shfl_xor((int)mx, m));
+    const uint32_t mx = wave_max_u32_dpp(multi ? ql : 0u);
     if (mx > lbest) {  // first KV of this chunk at the new maximum
       const int fl = __ffsll((long long)ballot(multi && ql == mx)) - 1;
       lbest = mx;
@@ -1095,6 +1096,12 @@ DEVI void cq_unstage_wave(uint8_t* dst, const uint8_t* lds, uint32_t i0, uint64_
 #ifndef CW_SORT
 #define CW_SORT 128u    // cells of an in-wave complexCompact
 #endif
+#ifndef CR_WPE
+#define CR_WPE 0        // (build knob) waves per SIMD the register allocation aims at, 0: the compiler's choice
+#endif
+#ifndef CR_ABL
+#define CR_ABL 0        // (ablation builds only, wrong results: 1 no write/delete decision, 2 no complexCompact)
+#endif
 static_assert(CW_SORT % WAVE == 0 && (CW_SORT & (CW_SORT - 1)) == 0, "in-wave sort size");
 struct __attribute__((aligned(16))) CrLds {
   uint8_t qlen[2 * CR_KCAP + 32];
@@ -1105,60 +1112,25 @@ struct __attribute__((aligned(16))) CrLds {
   uint32_t keys[CW_SORT], pay[CW_SORT], runs[CQ_RUNS_SLOTS];
 };
 
-// A row's staging: its four segments' 16-B chunks in one flat index space
-// (KV qualifier lengths, KV value lengths, qualifier bytes, value bytes);
-// chunks lane and lane + 64 are loaded into registers while the wave still
-// works on its previous row, and written to LDS once that row is done.
-struct CrGeom {
-  uintptr_t sk, sv, sq, sx;  // the segments' first bytes
-  uint32_t hk, hv, hq, hx;   // their 16-B phases
-  uint32_t n1, n2, n3, n4;   // segment ends, in chunks
-};
-DEVI CrGeom cr_geom(const CompactArgs& a, const RowHdr& h) {
-  CrGeom S;
-  S.sk = (uintptr_t)(a.kv_qual_len + h.kb);
-  S.sv = (uintptr_t)(a.kv_val_len + h.kb);
-  S.sq = (uintptr_t)(a.qual + h.qs);
-  S.sx = (uintptr_t)(a.val + h.vs);
-  S.hk = (uint32_t)(S.sk & 15u); S.hv = (uint32_t)(S.sv & 15u); S.hq = (uint32_t)(S.sq & 15u); S.hx = (uint32_t)(S.sx & 15u);
-  const uint32_t nk = (uint32_t)h.nk;
-  S.n1 = nk ? (S.hk + 2 * nk + 15) / 16 : 0u;
-  S.n2 = S.n1 + (nk ? (S.hv + 2 * nk + 15) / 16 : 0u);
-  S.n3 = S.n2 + (h.qe > h.qs ? (uint32_t)((S.hq + (h.qe - h.qs) + 15) / 16) : 0u);
-  S.n4 = S.n3 + (h.ve > h.vs ? (uint32_t)((S.hx + (h.ve - h.vs) + 15) / 16) : 0u);
-  return S;
+// the headers of up to 10 rows, six words a row (lanes 6 m .. 6 m + 5:
+// row_kv_start, row_qual_off, row_val_off at r and r + 1), in one round trip
+DEVI uint64_t cr_hdr_load(const CompactArgs& a, const uint32_t* list, uint32_t i0, uint32_t step, uint32_t n,
+                          int lane) {
+  const uint32_t m = (uint32_t)lane / 6, f = (uint32_t)lane % 6, i = i0 + step * m;
+  if (m >= 10 || i >= n) return 0ull;
+  const uint32_t r = list[i];
+  const uint64_t* p = f < 2 ? a.row_kv_start : f < 4 ? a.row_qual_off : a.row_val_off;
+  return p[r + (f & 1)];
 }
-DEVI const uint4* cr_src(const CrGeom& S, uint32_t c) {
-  return c < S.n1   ? (const uint4*)(S.sk - S.hk) + c
-         : c < S.n2 ? (const uint4*)(S.sv - S.hv) + (c - S.n1)
-         : c < S.n3 ? (const uint4*)(S.sq - S.hq) + (c - S.n2)
-                    : (const uint4*)(S.sx - S.hx) + (c - S.n3);
-}
-DEVI uint4* cr_dst(CrLds& L, const CrGeom& S, uint32_t c) {
-  return c < S.n1   ? (uint4*)L.qlen + c
-         : c < S.n2 ? (uint4*)L.vlen + (c - S.n1)
-         : c < S.n3 ? (uint4*)L.qin + (c - S.n2)
-                    : (uint4*)L.vin + (c - S.n3);
-}
-DEVI bool cr_fits(const RowHdr& h) {
-  return h.ok && h.nk <= CR_KCAP && h.qe - h.qs <= CR_QCAP && h.ve - h.vs <= CR_VCAP;
-}
-// the row's header words, a lane each (lanes 0-5: row_kv_start, row_qual_off,
-// row_val_off at r and r + 1), loaded ahead as vector loads (vmcnt, not the
-// lgkmcnt every LDS wait drains)
-DEVI uint64_t cr_hdr_load(const CompactArgs& a, uint32_t r, int lane) {
-  const uint64_t* p = lane < 2 ? a.row_kv_start : lane < 4 ? a.row_qual_off : a.row_val_off;
-  return lane < 6 ? p[r + (lane & 1)] : 0ull;
-}
-// (cq_row's header from the six words)
-DEVI RowHdr cr_hdr(const CompactArgs& a, uint64_t v, uint64_t r, uint64_t Q0, uint64_t V0) {
+// (cq_row's header from row m's six words)
+DEVI RowHdr cr_hdr(const CompactArgs& a, uint64_t v, uint32_t m, uint64_t r, uint64_t Q0, uint64_t V0) {
   RowHdr h;
-  h.kb = readlane_u64(v, 0);
-  const uint64_t ke = readlane_u64(v, 1);
-  h.qs = readlane_u64(v, 2);
-  h.qe = readlane_u64(v, 3);
-  h.vs = readlane_u64(v, 4);
-  h.ve = readlane_u64(v, 5);
+  h.kb = readlane_u64(v, 6 * m);
+  const uint64_t ke = readlane_u64(v, 6 * m + 1);
+  h.qs = readlane_u64(v, 6 * m + 2);
+  h.qe = readlane_u64(v, 6 * m + 3);
+  h.vs = readlane_u64(v, 6 * m + 4);
+  h.ve = readlane_u64(v, 6 * m + 5);
   h.ok = h.kb <= ke && ke <= a.n_kvs && h.qs <= h.qe && h.qe <= a.qual_nbytes && h.vs <= h.ve &&
          h.ve <= a.val_nbytes && h.qs >= Q0 && h.vs >= V0 && (h.ve - h.vs) < (1ull << 32);
   h.nk = h.ok ? ke - h.kb : 0;
@@ -1168,15 +1140,49 @@ DEVI RowHdr cr_hdr(const CompactArgs& a, uint64_t v, uint64_t r, uint64_t Q0, ui
   return h;
 }
 
-// One row, staged in L: cq_row_lds, the write/delete decision, the output.
-DEVI void cr_row(const CompactArgs& a, CrLds& L, const RowHdr& h, const CrGeom& S, uint64_t r, uint32_t* n_cx,
-                 int lane) {
+DEVI void cr_row(const CompactArgs& a, CrLds& L, const RowHdr& h, uint64_t r, uint32_t* n_cx, int lane) {
+  if (lane == 0) {
+    a.out_qoff[r] = h.oqo;
+    a.out_voff[r] = h.ovo;
+  }
+  if (!h.ok || h.nk > CR_KCAP || h.qe - h.qs > CR_QCAP || h.ve - h.vs > CR_VCAP) {
+    cq_row_global(a, r, lane);
+    return;
+  }
+  // ---- staging: the four segments' 16-B chunks in one flat loop (every
+  // load of the row in flight together) ----
+  const uintptr_t sk = (uintptr_t)(a.kv_qual_len + h.kb), sv = (uintptr_t)(a.kv_val_len + h.kb);
+  const uintptr_t sq = (uintptr_t)(a.qual + h.qs), sx = (uintptr_t)(a.val + h.vs);
+  const uint32_t hk = (uint32_t)(sk & 15u), hv = (uint32_t)(sv & 15u), hq = (uint32_t)(sq & 15u), hx = (uint32_t)(sx & 15u);
+  const uint32_t nk = (uint32_t)h.nk;
+  const uint32_t n1 = nk ? (hk + 2 * nk + 15) / 16 : 0u, n2 = n1 + (nk ? (hv + 2 * nk + 15) / 16 : 0u);
+  const uint32_t n3 = n2 + (h.qe > h.qs ? (uint32_t)((hq + (h.qe - h.qs) + 15) / 16) : 0u);
+  const uint32_t n4 = n3 + (h.ve > h.vs ? (uint32_t)((hx + (h.ve - h.vs) + 15) / 16) : 0u);
+  auto at = [&](uint32_t c, uint4*& d) {
+    if (c < n1) { d = (uint4*)L.qlen + c; return (const uint4*)(sk - hk) + c; }
+    if (c < n2) { d = (uint4*)L.vlen + (c - n1); return (const uint4*)(sv - hv) + (c - n1); }
+    if (c < n3) { d = (uint4*)L.qin + (c - n2); return (const uint4*)(sq - hq) + (c - n2); }
+    d = (uint4*)L.vin + (c - n3);
+    return (const uint4*)(sx - hx) + (c - n3);
+  };
+  for (uint32_t c = lane; c < n4; c += 2 * WAVE) {
+    const bool b = c + WAVE < n4;
+    uint4 *d0, *d1 = nullptr;
+    const uint4* g0 = at(c, d0);
+    const uint4* g1 = b ? at(c + WAVE, d1) : nullptr;
+    const uint4 v0 = *g0;
+    uint4 v1 = {};
+    if (b) v1 = *g1;
+    *d0 = v0;
+    if (b) *d1 = v1;
+  }
   RowLds p;
-  p.k0 = S.hk;
-  p.kv0 = S.hv;
-  p.qi = p.qo = S.hq;
-  p.vi = S.hx;
+  p.k0 = hk;
+  p.kv0 = hv;
+  p.qi = p.qo = hq;
+  p.vi = hx;
   p.vo = (uint32_t)((uintptr_t)(a.ov + h.ovo) & 15u);
+  wave_lds_sync();
   const RowBufs B{L.qlen, L.vlen, L.qin, L.vin, L.qin, L.vout, CR_QCAP + 14, CR_VCAP + 14};
   uint32_t oql = 0, ovl = 0, nc = 0;
   const int st = cq_row_lds<CW_SORT>(a, r, h, B, p, L.keys, L.pay, L.runs, lane, &oql, &ovl, &nc);
@@ -1190,7 +1196,7 @@ DEVI void cr_row(const CompactArgs& a, CrLds& L, const RowHdr& h, const CrGeom& 
   wave_lds_sync();
   if (st & CQ_REACHED_COMPLEX) {
     (*n_cx)++;
-    if ((st & 0xFF) == CQ_COMPLEX && a.out_write)
+    if ((st & 0xFF) == CQ_COMPLEX && a.out_write && !(CR_ABL & 1))
       cq_dup_core(
           a, r, h.nk, h.qs, h.vs, oql, ovl, L.qin + p.qo, L.vout + p.vo,
           [&](uint64_t k) { return lds_u16(L.qlen, p.k0 + 2 * (uint32_t)k); },
@@ -1198,11 +1204,9 @@ DEVI void cr_row(const CompactArgs& a, CrLds& L, const RowHdr& h, const CrGeom& 
   }
   cq_unstage_wave(a.oq, L.qin, p.qo, h.oqo, h.oqo + oql, lane);
   cq_unstage_wave(a.ov, L.vout, p.vo, h.ovo, h.ovo + ovl, lane);
+  wave_lds_sync();  // (the row's LDS consumed before the wave's next row is staged)
 }
 
-#ifndef CR_WPE
-#define CR_WPE 0  // (build knob) waves per SIMD the register allocation aims at, 0: the compiler's choice
-#endif
 __global__ void __launch_bounds__(256)
 #if CR_WPE
 __attribute__((amdgpu_waves_per_eu(CR_WPE, CR_WPE)))
@@ -1212,7 +1216,6 @@ k_compact_rows(CompactArgs a) {
   __shared__ uint32_t s_list[CR_RANGE], s_wn[4], s_cx;
   const int tid = threadIdx.x, lane = lane_id(), w = tid / WAVE;
   const uint64_t Q0 = a.row_qual_off[0], V0 = a.row_val_off[0];
-  CrLds& L = Ls[w];
   if (tid == 0) s_cx = 0;
   uint32_t n_cx = 0;
   for (uint64_t rb = (uint64_t)blockIdx.x * CR_RANGE; rb < a.n_rows; rb += (uint64_t)gridDim.x * CR_RANGE) {
@@ -1238,65 +1241,13 @@ k_compact_rows(CompactArgs a) {
     for (int u = 0; u < CR_U; u++)
       if (pend[u] != ~0u) s_list[woff + pend[u]] = (uint32_t)(rb + (uint64_t)w * (CR_RANGE / 4) + u * WAVE + lane);
     __syncthreads();
-    // ---- a wave a row, the next row's staging loads in flight meanwhile
-    // (its header loaded a row earlier) ----
-    uint32_t i = w;
-    if (i >= n) continue;
-    uint32_t r = uni32(s_list[i]);
-    uint64_t vh = cr_hdr_load(a, r, lane);  // (this row's header words)
-    uint4 x0 = {}, x1 = {};                 // (its first two staging chunks a lane)
-    {
-      const RowHdr h = cr_hdr(a, vh, r, Q0, V0);
-      if (cr_fits(h)) {
-        const CrGeom S = cr_geom(a, h);
-        if ((uint32_t)lane < S.n4) x0 = *cr_src(S, lane);
-        if ((uint32_t)lane + WAVE < S.n4) x1 = *cr_src(S, lane + WAVE);
+    // ---- a wave a row; its rows' headers loaded ten at a time ----
+    for (uint32_t i0 = w; i0 < n; i0 += 40) {
+      const uint64_t hv = cr_hdr_load(a, s_list, i0, 4, n, lane);
+      for (uint32_t m = 0; m < 10 && i0 + 4 * m < n; m++) {
+        const uint32_t r = uni32(s_list[i0 + 4 * m]);
+        cr_row(a, Ls[w], cr_hdr(a, hv, m, r, Q0, V0), r, &n_cx, lane);
       }
-    }
-    uint32_t rn = i + 4 < n ? uni32(s_list[i + 4]) : 0u;
-    uint64_t vn = i + 4 < n ? cr_hdr_load(a, rn, lane) : 0ull;
-    while (true) {
-      const RowHdr h = cr_hdr(a, vh, r, Q0, V0);
-      const bool fit = cr_fits(h);
-      if (lane == 0) {
-        a.out_qoff[r] = h.oqo;
-        a.out_voff[r] = h.ovo;
-      }
-      if (fit) {  // the staged chunks to LDS (rows over 2 KB: the rest now)
-        const CrGeom S = cr_geom(a, h);
-        if ((uint32_t)lane < S.n4) *cr_dst(L, S, lane) = x0;
-        if ((uint32_t)lane + WAVE < S.n4) *cr_dst(L, S, lane + WAVE) = x1;
-        for (uint32_t c = lane + 2 * WAVE; c < S.n4; c += WAVE) *cr_dst(L, S, c) = *cr_src(S, c);
-        wave_lds_sync();
-      }
-      // the next row's staging loads; the header of the one after it
-      const bool more = i + 4 < n;
-      uint4 y0 = {}, y1 = {};
-      uint32_t rnn = 0;
-      uint64_t vnn = 0;
-      if (more) {
-        const RowHdr hn = cr_hdr(a, vn, rn, Q0, V0);
-        if (cr_fits(hn)) {
-          const CrGeom Sn = cr_geom(a, hn);
-          if ((uint32_t)lane < Sn.n4) y0 = *cr_src(Sn, lane);
-          if ((uint32_t)lane + WAVE < Sn.n4) y1 = *cr_src(Sn, lane + WAVE);
-        }
-        if (i + 8 < n) {
-          rnn = uni32(s_list[i + 8]);
-          vnn = cr_hdr_load(a, rnn, lane);
-        }
-      }
-      if (fit) cr_row(a, L, h, cr_geom(a, h), r, &n_cx, lane);
-      else cq_row_global(a, r, lane);
-      if (!more) break;
-      wave_lds_sync();  // (the row's LDS consumed before the next one is written)
-      i += 4;
-      r = rn;
-      vh = vn;
-      x0 = y0;
-      x1 = y1;
-      rn = rnn;
-      vn = vnn;
     }
   }
   if (lane == 0 && n_cx) atomicAdd(&s_cx, n_cx);

@@ -18,3 +18,13 @@ def ctx():
     c = Context(0)
     yield c
     c.close()
+
+
+def pytest_terminal_summary(terminalreporter):
+    """late call-end stamps (tsdbhip_timing.late_stamp: the snapshot's stamp
+    seen only after spinning past the stream sync, the precursor of a stale
+    read) over every context the session closed"""
+    from opentsdb_amd import _lib
+    s = _lib.STAMP_TOTALS
+    if s["calls"]:
+        terminalreporter.write_line(f"tsdbhip late_stamp: {s['late_stamp']} of {s['calls']} calls")
