@@ -1910,6 +1910,9 @@ struct UgIn {
 // always is). A layout other than hourly rows only makes the device check
 // refuse the pieces, as before (45-min or 3-h buckets over hourly
 // 1-s rows).
+#ifndef UG_DEV_GP
+#define UG_DEV_GP 16u  // k_ug_dev: grid points (chains) a block
+#endif
 static uint32_t ug_e_pieces(uint32_t t0, uint32_t step, uint32_t n, uint32_t kk, uint32_t want) {
   if (want <= 1 || !step || !kk || n == 0) return 1;
   const uint64_t last = (uint64_t)t0 + (uint64_t)(n - 1) * step;
@@ -2219,11 +2222,12 @@ static int uniform_run(Slot* ctx, const UgIn& u, tsdbhip_sg_out* out, tsdbhip_ti
   } else if (u.dev) {  // integer dev: one sequential chain a grid point (k_ug_dev)
     ctx->hot_kernel = TSDBHIP_HOT_UG_DEV;
     EV_START(ctx, 8);
+    constexpr uint32_t GP = UG_DEV_GP;  // (grid points a block)
     if (lsp.w8)
-      LAUNCH_STOP(EV_STOP_K(ctx, 9), k_ug_dev<8>, dim3((unsigned)((T + WAVE - 1) / WAVE)), dim3(256), 0, st,
+      LAUNCH_STOP(EV_STOP_K(ctx, 9), (k_ug_dev<8, GP>), dim3((unsigned)((T + GP - 1) / GP)), dim3(256), 0, st,
                   u.da.val, u.uk_vo, u.da.qual, u.uk_qo, q0, &sm->ls_broken, n_kept, T, gridv, x0, step, fin);
     else
-      LAUNCH_STOP(EV_STOP_K(ctx, 9), k_ug_dev<4>, dim3((unsigned)((T + WAVE - 1) / WAVE)), dim3(256), 0, st,
+      LAUNCH_STOP(EV_STOP_K(ctx, 9), (k_ug_dev<4, GP>), dim3((unsigned)((T + GP - 1) / GP)), dim3(256), 0, st,
                   u.da.val, u.uk_vo, u.da.qual, u.uk_qo, q0, &sm->ls_broken, n_kept, T, gridv, x0, step, fin);
     EV_STOP_M(ctx, 9);
   } else if (!sharded) {
@@ -3876,31 +3880,34 @@ static int compact_rows(Slot* ctx, const tsdbhip_rows_desc* d, tsdbhip_rows_out*
     const bool dev = (d->flags & TSDBHIP_DESC_DEVICE) != 0;
     ctx->h2d_bytes = 0;
     ctx->reuse_inputs = false;
-    uint64_t ext[4];  // row_qual_off[0], [R], row_val_off[0], [R]
-    if (dev) {
-      uint64_t* h = (uint64_t*)ctx->host_small;
-      HIPCHK(hipMemcpyAsync(h + 0, d->row_qual_off, 8, hipMemcpyDeviceToHost, ctx->stream));
-      HIPCHK(hipMemcpyAsync(h + 1, d->row_qual_off + R, 8, hipMemcpyDeviceToHost, ctx->stream));
-      HIPCHK(hipMemcpyAsync(h + 2, d->row_val_off, 8, hipMemcpyDeviceToHost, ctx->stream));
-      HIPCHK(hipMemcpyAsync(h + 3, d->row_val_off + R, 8, hipMemcpyDeviceToHost, ctx->stream));
-      HIPCHK(hipStreamSynchronize(ctx->stream));
-      std::memcpy(ext, h, sizeof ext);
-    } else {
+    // the batch's extents row_qual_off[0], [R], row_val_off[0], [R]: read on
+    // the host for a host descriptor; for a device descriptor the kernels
+    // read them (k_compact_wave's first lane) and the call checks them with
+    // the counters at its end — no round trip before the first launch (every
+    // kernel keeps each row inside the buffers and capacities on its own)
+    uint64_t ext[4] = {0, 0, 0, 0};
+    auto check_ext = [&]() -> int {
+      if (ext[1] < ext[0] || ext[3] < ext[2] || ext[1] > d->qual_nbytes || ext[3] > d->val_nbytes) {
+        set_error(ctx, "tsdbhip_compact_rows: row offsets out of range");
+        return TSDBHIP_E_INVALID_ARG;
+      }
+      const uint64_t qx = ext[1] - ext[0], vx = ext[3] - ext[2];
+      if (out->qual_capacity < qx || out->val_capacity < vx + R) {
+        set_error(ctx, "tsdbhip_compact_rows: output needs %llu qualifier / %llu value bytes", (unsigned long long)qx,
+                  (unsigned long long)(vx + R));
+        return TSDBHIP_E_CAPACITY;
+      }
+      return TSDBHIP_OK;
+    };
+    if (!dev) {
       ext[0] = d->row_qual_off[0];
       ext[1] = d->row_qual_off[R];
       ext[2] = d->row_val_off[0];
       ext[3] = d->row_val_off[R];
+      if (const int rc = check_ext()) return rc;
     }
-    if (ext[1] < ext[0] || ext[3] < ext[2] || ext[1] > d->qual_nbytes || ext[3] > d->val_nbytes) {
-      set_error(ctx, "tsdbhip_compact_rows: row offsets out of range");
-      return TSDBHIP_E_INVALID_ARG;
-    }
-    const uint64_t qext = ext[1] - ext[0], vext = ext[3] - ext[2];
-    if (out->qual_capacity < qext || out->val_capacity < vext + R) {
-      set_error(ctx, "tsdbhip_compact_rows: output needs %llu qualifier / %llu value bytes",
-                (unsigned long long)qext, (unsigned long long)(vext + R));
-      return TSDBHIP_E_CAPACITY;
-    }
+    // (device descriptor: bounds for the scratch sizes until the extents are known)
+    const uint64_t qext = dev ? d->qual_nbytes : ext[1] - ext[0], vext = dev ? d->val_nbytes : ext[3] - ext[2];
     CompactArgs a = {};
     a.n_rows = R;
     a.n_kvs = d->n_kvs;
@@ -3942,7 +3949,8 @@ static int compact_rows(Slot* ctx, const tsdbhip_rows_desc* d, tsdbhip_rows_out*
         a.out_keep = scratch<int32_t>(ctx, "c_ok", R);
       }
     }
-    a.counters = scratch<uint32_t>(ctx, "c_cnt", 8, true);
+    a.counters = scratch<uint32_t>(ctx, "c_cnt", 16, true);
+    a.ext_out = dev ? (uint64_t*)(a.counters + 8) : nullptr;
     a.list_lds = scratch<uint32_t>(ctx, "c_llds", R);
     a.list_big = scratch<uint32_t>(ctx, "c_lbig", R);
     a.big_cells = scratch<uint64_t>(ctx, "c_cells", qext / 2 + R + 1);
@@ -3973,8 +3981,12 @@ static int compact_rows(Slot* ctx, const tsdbhip_rows_desc* d, tsdbhip_rows_out*
     if (a.out_write) LAUNCH(k_compact_dups, dim3(256), dim3(256), 0, ctx->stream, a);
     HIPCHK(hipGetLastError());
     EV_FINAL(ctx, 1);
-    uint32_t cnt[4];
+    uint32_t cnt[16];
     readback(ctx, cnt, a.counters, sizeof cnt);
+    if (dev) {
+      std::memcpy(ext, cnt + 8, sizeof ext);
+      if (const int rc = check_ext()) return rc;
+    }
     if (cnt[2]) {
       set_error(ctx, "tsdbhip_compact_rows: a row's KV lengths do not match its offsets");
       return TSDBHIP_E_INVALID_ARG;
@@ -4003,8 +4015,8 @@ static int compact_rows(Slot* ctx, const tsdbhip_rows_desc* d, tsdbhip_rows_out*
     t.reduce_ms = ev_ms(ctx, 3, 1);  // k_compact_complex + k_compact_dups
     t.h2d_bytes = ctx->h2d_bytes;
     ctx->timing = t;
-    out->qual_used = qext;
-    out->val_used = vext + R;
+    out->qual_used = ext[1] - ext[0];
+    out->val_used = ext[3] - ext[2] + R;
     out->n_complex = n_cx;
   } catch (Fail& f) {
     return f.code;

@@ -68,6 +68,7 @@ struct CompactArgs {
   uint32_t* list_lds;   // complex rows with <= CQ_LDS_CELLS cells
   uint32_t* list_big;   // the others
   uint64_t* big_cells;  // scratch: row r's cells at (row_qual_off[r]-row_qual_off[0])/2 + r
+  uint64_t* ext_out;    // optional: row_qual_off[0], [n_rows], row_val_off[0], [n_rows] for the host's checks
 };
 constexpr int CQ_REACHED_COMPLEX = 0x100;  // cq_row_lds: the row went through complexCompact
 
@@ -1558,6 +1559,12 @@ k_compact_wave(CompactArgs a) {
   if (r0 >= a.n_rows) return;
   const uint32_t nr = (uint32_t)min((uint64_t)CW_ROWS, a.n_rows - r0);
   const uint64_t Q0 = a.row_qual_off[0], V0 = a.row_val_off[0];
+  if (r0 == 0 && t == 0 && a.ext_out) {  // (the batch's extents, for the host's checks at the call's end)
+    a.ext_out[0] = Q0;
+    a.ext_out[1] = a.row_qual_off[a.n_rows];
+    a.ext_out[2] = V0;
+    a.ext_out[3] = a.row_val_off[a.n_rows];
+  }
   if (t <= nr) {
     L.kv[t] = a.row_kv_start[r0 + t];
     L.qo[t] = a.row_qual_off[r0 + t];

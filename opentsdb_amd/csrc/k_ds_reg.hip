@@ -97,6 +97,16 @@ DEVI void reg_flush(const DecodeArgs& a, const RegSpan& sp, const int64_t* BK, u
   wave_lds_sync();
 }
 
+// L_v's layout: lane l stages cells 8 l .. 8 l + 7 as four 16-B pairs, pair
+// p at slot (p + (l >> 1)) & 3 of the lane's 64 bytes, so the 8 lanes of a
+// ds_write_b128 group hit 8 distinct 16-B bank quads (the
+// unrotated 64-B lane stride cost 15.6 conflict cycles an LDS instruction on
+// C2); cell c sits at lv_ix(c).
+DEVI uint32_t lv_ix(uint32_t c) {
+  const uint32_t l = c >> 3;
+  return (l << 3) | (((((c >> 1) & 3u) + (l >> 1)) & 3u) << 1) | (c & 1u);
+}
+
 // The chunks of rows [ra, rb) of one span (two register sets, the next
 // chunk's loads in flight while one is processed, as ds_span); buckets that
 // close in these rows go to E. Returns true if the premise breaks. The
@@ -183,7 +193,7 @@ DEVI bool reg_piece(const DecodeArgs& a, const RegSpan& sp, uint64_t ra, uint64_
       ulonglong2 v2;
       v2.x = pvi[j] + xv;
       v2.y = pvi[j + 1] + xv;
-      *(ulonglong2*)&L_v[8 * lane + j] = v2;
+      *(ulonglong2*)&L_v[8 * lane + 2 * (((uint32_t)(j >> 1) + ((uint32_t)lane >> 1)) & 3u)] = v2;
     }
   };
   auto step = [&](const ChunkPos& p, const RawW<W>& cur) {
@@ -215,15 +225,15 @@ DEVI bool reg_piece(const DecodeArgs& a, const RegSpan& sp, uint64_t ra, uint64_
       const bool cont = sb < cs;  // began in an earlier chunk
       int64_t v;
       if (PREFIX) {
-        v = (int64_t)(L_v[lb] - (la > 0 ? L_v[la - 1] : 0ull));
+        v = (int64_t)(L_v[lv_ix(lb)] - (la > 0 ? L_v[lv_ix(la - 1)] : 0ull));
         if (cont) v = ladd(v, carry);
       } else if (FLT) {
-        double d = cont ? bitsd(carry) : bitsd((int64_t)L_v[la]);
-        for (uint32_t i = cont ? la : la + 1; act && i <= lb; i++) d = ds_dcombine<AGG>(d, bitsd((int64_t)L_v[i]));
+        double d = cont ? bitsd(carry) : bitsd((int64_t)L_v[lv_ix(la)]);
+        for (uint32_t i = cont ? la : la + 1; act && i <= lb; i++) d = ds_dcombine<AGG>(d, bitsd((int64_t)L_v[lv_ix(i)]));
         v = dbits(d);
       } else {
-        v = cont ? carry : (int64_t)L_v[la];
-        for (uint32_t i = cont ? la : la + 1; act && i <= lb; i++) v = ds_combine<AGG>(v, (int64_t)L_v[i]);
+        v = cont ? carry : (int64_t)L_v[lv_ix(la)];
+        for (uint32_t i = cont ? la : la + 1; act && i <= lb; i++) v = ds_combine<AGG>(v, (int64_t)L_v[lv_ix(i)]);
       }
       // closed buckets -> the bucket buffer (room for this pass's first)
       const uint32_t pc = min(nclose - min(nclose, jb), (uint32_t)WAVE);

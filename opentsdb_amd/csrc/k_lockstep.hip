@@ -256,69 +256,171 @@ __global__ void __launch_bounds__(256) k_lockstep(ReduceArgs r, LockstepArgs L) 
 // Welford over the spans in span order before the (long) truncation
 // (Aggregators.java:196-237) admits no merge of partial states, so each grid
 // point is one chain of n_kept dependent steps. A block holds the chains of
-// 64 grid points: wave 0 runs them (lane = grid point, wf_push with the true
-// division, bit-exact with k_reduce's span-ordered pass), waves 1-3 stream
-// the values into LDS ahead of it — span k's 64 values are 512 contiguous
-// bytes (cell g of every span sits at grid point g) — DEV_B spans a phase,
-// double-buffered, so the chain waits on LDS, not on HBM round trips (the
-// general pass kept 8 loads in flight a lane: 23.6 ms at 100k series). The
-// producers prove the proposal as they stream: every qualifier is compared
-// with (x0 + g step - base) << 4 | flags (as k_lockstep); a mismatch sets
-// `broken` and the call runs again on the proven path.
-constexpr uint32_t DEV_B = 96;  // spans a phase (32 loads in flight a producer lane)
-template <uint32_t W>
+// GP grid points, its four waves on four SIMDs:
+//   wave 0  the mean chains (lane = grid point): mean' = mean + (x - mean)/n,
+//           each step's (x - mean, mean') to LDS;
+//   wave 1  the M2 sums one phase behind: var += (x - mean) (x - mean'), in
+//           span order (the same roundings as wf_push, dev_common.h);
+//   waves 2-3  stream the values into LDS ahead of them — span k's GP values
+//           are W * GP contiguous bytes (cell g of every span sits at grid
+//           point g), 64 / GP spans a load instruction — DEV_B spans a phase,
+//           a software pipeline one phase deep (values of phase ph + 1 stored
+//           while those of ph + 2 and the row offsets of ph + 3 load), and
+//           convert them to double; they also prove the proposal as they
+//           stream: every qualifier is compared with (x0 + g step - base) << 4
+//           | flags (as k_lockstep); a mismatch sets `broken` and the call
+//           runs again on the proven path.
+// The chain's division (x - mean) / n is Markstein's correction of a product
+// with r = RN(1/n): q0 = RN(d r), e = d - n q0 (exact, one fma), q = RN(q0 +
+// e r) = RN(d / n) — the quotient of a double by an integer n never sits on a
+// rounding midpoint and stays normal here — bit-exact with the division; n
+// and r are uniform (n = span index + 1) and come from the producers. The mean
+// chain is then five dependent double operations a step on a SIMD of its own
+// (round 6: 95 -> 63 ms for C3's 1M series, 9.5 -> 6.3 ms for 100k, with GP =
+// 16: 225 blocks instead of 57, and the conversions off the chain).
+constexpr uint32_t DEV_B = 96;  // spans a phase
+#ifndef UG_DEV_ABL
+#define UG_DEV_ABL 0
+#endif
+template <uint32_t W, uint32_t GP>
 __global__ void __launch_bounds__(256) k_ug_dev(const uint8_t* val, const uint64_t* vo, const uint8_t* qual,
                                                const uint64_t* qo, uint32_t q0, uint32_t* broken, uint32_t n_kept,
                                                uint64_t T, uint32_t* grid, uint32_t x0, uint32_t step, FinalArgs f) {
-  __shared__ int64_t s_buf[2][DEV_B][WAVE];
+  static_assert(GP == 16 || GP == 32 || GP == 64, "grid points a block");
+  constexpr uint32_t SPL = WAVE / GP;  // spans a producer load instruction
+  constexpr uint32_t NP = 2;           // producer waves
+  static_assert(DEV_B % (NP * SPL) == 0, "a phase's spans split over the producers");
+  __shared__ double s_buf[3][DEV_B][GP];              // the values (three phases: producers, chain, M2 sums)
+  __shared__ double2 s_dm[2][DEV_B][GP];              // each step's (x - mean, mean')
+  __shared__ double s_rcp[2][DEV_B], s_dn[2][DEV_B];  // RN(1/n), n (n = span index + 1)
+  __shared__ double s_var[GP];
   const uint32_t w = __builtin_amdgcn_readfirstlane(threadIdx.x / WAVE);
   const int lane = lane_id();
-  const uint64_t g = (uint64_t)blockIdx.x * WAVE + lane;
-  const bool gv = g < T;
-  const uint64_t gc = gv ? g : T - 1;  // (loads stay inside the row)
+  const uint32_t gl = (uint32_t)lane % GP, si = (uint32_t)lane / GP;  // (producers: grid point, span of the load)
+  const uint32_t gchain = w < 2 ? (uint32_t)lane : gl;
+  const uint64_t g = (uint64_t)blockIdx.x * GP + gchain;
+  const bool gv = g < T && gchain < GP;
+  const uint64_t gc = g < T ? g : T - 1;  // (loads stay inside the row)
   const uint32_t nph = (n_kept + DEV_B - 1) / DEV_B;
   // this lane's qualifier under the proposal (big-endian as loaded)
   const uint32_t qe = (q0 + (uint32_t)gc * (step << 4)) & 0xFFFFu;
   const uint32_t qexp = ((qe & 0xFFu) << 8) | (qe >> 8);
   uint32_t bad = 0;
-  auto produce = [&](uint32_t ph, int b) {  // waves 1..3: spans ph * DEV_B + j, j = w - 1, w + 2, ...
-    constexpr uint32_t PER = DEV_B / 3;
-    int64_t v[PER];
-    uint32_t q[PER];
+  constexpr uint32_t PER = DEV_B / (NP * SPL);  // load instructions a producer a phase
+  int64_t v[PER];
+  uint32_t q[PER];
+  uint64_t ov[PER], oq[PER];  // row offsets of the spans of the phase whose values load next
+  auto slot = [&](uint32_t i) { return (w - 2) * SPL + NP * SPL * i + si; };  // span slot of the phase
+  auto load_offs = [&](uint32_t ph) {
 #pragma unroll
     for (uint32_t i = 0; i < PER; i++) {
-      const uint32_t k = min(ph * DEV_B + (w - 1) + 3 * i, n_kept - 1);
-      const uint8_t* p = val + vo[k] + (uint64_t)W * gc;
-      v[i] = W == 8 ? (int64_t)bswap64(*(const uint64_t*)p) : (int64_t)(int32_t)bswap32(*(const uint32_t*)p);
-      q[i] = *(const uint16_t*)(qual + qo[k] + 2 * gc);
+      const uint32_t k = min(ph * DEV_B + slot(i), n_kept - 1);
+      ov[i] = vo[k];
+      oq[i] = qo[k];
     }
+  };
+  auto load_vals = [&]() {
 #pragma unroll
     for (uint32_t i = 0; i < PER; i++) {
-      s_buf[b][(w - 1) + 3 * i][lane] = v[i];
+      const uint8_t* p = val + ov[i] + (uint64_t)W * gc;
+      v[i] = W == 8 ? (int64_t)bswap64(*(const uint64_t*)p) : (int64_t)(int32_t)bswap32(*(const uint32_t*)p);
+      q[i] = *(const uint16_t*)(qual + oq[i] + 2 * gc);
+    }
+  };
+  auto store = [&](uint32_t ph) {  // phase ph's values (in v, q), converted, and its counts
+    if (w == 2)
+      for (uint32_t j = (uint32_t)lane; j < DEV_B; j += WAVE) {
+        const double dn = (double)(ph * DEV_B + j + 1);
+        s_dn[ph & 1][j] = dn;
+        s_rcp[ph & 1][j] = 1.0 / dn;
+      }
+#pragma unroll
+    for (uint32_t i = 0; i < PER; i++) {
+      s_buf[ph % 3][slot(i)][gl] = (double)v[i];
       bad |= q[i] ^ qexp;
     }
   };
-  if (w > 0) produce(0, 0);
+  if (w >= 2) {
+    load_offs(0);
+    load_vals();
+    store(0);
+    if (nph > 1) {
+      load_offs(1);
+      load_vals();
+    }
+    if (nph > 2) load_offs(2);
+  }
   __syncthreads();
-  Welford st;
-  wf_init(st);
-  for (uint32_t ph = 0; ph < nph; ph++) {
-    const int b = ph & 1;
-    if (w > 0) {
-      if (ph + 1 < nph) produce(ph + 1, b ^ 1);
-    } else {
-      const uint32_t nk = min(DEV_B, n_kept - ph * DEV_B);
-      for (uint32_t j = 0; j < nk; j++) wf_push(st, (double)s_buf[b][j][lane]);
+  double mean = 0, var = 0;
+  for (uint32_t ph = 0; ph <= nph; ph++) {
+    if (w >= 2) {
+      if (ph + 1 < nph) store(ph + 1);
+      if (ph + 2 < nph) load_vals();
+      if (ph + 3 < nph) load_offs(ph + 3);
+    } else if (w == 0 && ph < nph && (uint32_t)lane < GP) {  // the mean chains
+      const uint32_t nk = min(DEV_B, n_kept - ph * DEV_B), b3 = ph % 3, b2 = ph & 1;
+      uint32_t j = 0;
+      if (ph == 0) {  // (wf_push's first value: mean = x)
+        mean = s_buf[0][0][lane];
+        j = 1;
+      }
+      // the LDS reads of the next 8 steps in flight during these 8
+      constexpr uint32_t U = 8;
+      double xa[U], ra[U], da[U];
+      auto fetch = [&](uint32_t j0, double* x, double* r, double* dn) {
+#pragma unroll
+        for (uint32_t u = 0; u < U; u++) {
+          const uint32_t jj = min(j0 + u, DEV_B - 1);
+          x[u] = s_buf[b3][jj][lane];
+          r[u] = s_rcp[b2][jj];
+          dn[u] = s_dn[b2][jj];
+        }
+      };
+      fetch(j, xa, ra, da);
+      for (; j < nk; j += U) {
+        double xb[U], rb[U], db[U];
+        fetch(j + U, xb, rb, db);
+#pragma unroll
+        for (uint32_t u = 0; u < U; u++) {
+          if (j + u >= nk) break;  // (uniform)
+          const double d = xa[u] - mean;
+          const double qa = d * ra[u];
+#if UG_DEV_ABL  // (ablation builds only, wrong results: the product without its correction)
+          const double nm = mean + qa;
+#else
+          const double e = __builtin_fma(-da[u], qa, d);
+          const double nm = mean + __builtin_fma(e, ra[u], qa);
+#endif
+          s_dm[b2][j + u][lane] = make_double2(d, nm);
+          mean = nm;
+        }
+#pragma unroll
+        for (uint32_t u = 0; u < U; u++) {
+          xa[u] = xb[u];
+          ra[u] = rb[u];
+          da[u] = db[u];
+        }
+      }
+    } else if (w == 1 && ph >= 1 && (uint32_t)lane < GP) {  // the M2 sums of the phase before
+      const uint32_t p = ph - 1, nk = min(DEV_B, n_kept - p * DEV_B), b3 = p % 3, b2 = p & 1;
+      for (uint32_t j = p == 0 ? 1u : 0u; j < nk; j++) {
+        const double2 dm = s_dm[b2][j][lane];
+        var += dm.x * (s_buf[b3][j][lane] - dm.y);
+      }
     }
     __syncthreads();
   }
-  if (w > 0 && ballot(bad != 0) && lane == 0) atomicOr(broken, 1u);
+  if (w == 1 && (uint32_t)lane < GP) s_var[lane] = var;
+  if (w >= 2 && ballot(bad != 0) && lane == 0) atomicOr(broken, 1u);
+  __syncthreads();
   if (w == 0 && gv) {
     grid[g] = x0 + (uint32_t)g * step;
     Acc a;
     acc_init(a);
     a.cnt = n_kept;
-    a.wi = st;
+    a.wi.n = n_kept;
+    a.wi.mean = mean;
+    a.wi.var = s_var[lane];
     finalize_one<4, MODE_INT, false>(f, g, a);
   }
 }

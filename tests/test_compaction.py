@@ -296,3 +296,74 @@ def test_gpu_compaction_bad_offsets(ctx):
     res, out = compaction.out_buffers(b)
     import ctypes as C
     assert ctx._lib.tsdbhip_compact_rows(ctx.handle, C.byref(d), C.byref(out)) == _abi.E_INVALID_ARG
+
+
+def _device_call(ctx, b, qcap=None, vcap=None):
+    """tsdbhip_compact_rows with a device descriptor (HBM-resident rows and
+    outputs, as bench.py's C5 line): the batch's extents are read by the
+    kernels and checked at the call's end. -> (return code, RowsResult)"""
+    import ctypes as C
+    import torch
+    dev = torch.device("cuda", 0)
+    keep = []
+
+    def up(a, ctype):
+        t = torch.from_numpy(np.ascontiguousarray(a).view(np.uint8)).to(dev)
+        keep.append(t)
+        return C.cast(C.c_void_p(t.data_ptr()), C.POINTER(ctype))
+    d = _abi.RowsDesc(flags=_abi.DESC_DEVICE, n_rows=b.n_rows, n_kvs=b.n_kvs,
+                      row_kv_start=up(b.row_kv_start, C.c_uint64), row_qual_off=up(b.row_qual_off, C.c_uint64),
+                      row_val_off=up(b.row_val_off, C.c_uint64), kv_qual_len=up(b.kv_qual_len, C.c_uint16),
+                      kv_val_len=up(b.kv_val_len, C.c_uint16), qual_bytes=up(b.qual_bytes, C.c_uint8),
+                      qual_nbytes=len(b.qual_bytes), val_bytes=up(b.val_bytes, C.c_uint8), val_nbytes=len(b.val_bytes))
+    R = b.n_rows
+    qcap = b.qual_extent + 64 if qcap is None else qcap
+    vcap = b.val_extent + R + 64 if vcap is None else vcap
+    o = {k: torch.zeros(max(n, 1), dtype=dt, device=dev) for k, n, dt in
+         [("st", R, torch.uint8), ("qo", R, torch.int64), ("ql", R, torch.int32), ("vo", R, torch.int64),
+          ("vl", R, torch.int32), ("q", qcap, torch.uint8), ("v", vcap, torch.uint8), ("w", R, torch.uint8),
+          ("k", R, torch.int32)]}
+    P = lambda t, ct: C.cast(C.c_void_p(t.data_ptr()), C.POINTER(ct))  # noqa: E731
+    out = _abi.RowsOut(qual_capacity=qcap, val_capacity=vcap, row_status=P(o["st"], C.c_uint8),
+                       row_qual_off=P(o["qo"], C.c_uint64), row_qual_len=P(o["ql"], C.c_uint32),
+                       row_val_off=P(o["vo"], C.c_uint64), row_val_len=P(o["vl"], C.c_uint32),
+                       qual_bytes=P(o["q"], C.c_uint8), val_bytes=P(o["v"], C.c_uint8),
+                       row_write=P(o["w"], C.c_uint8), row_keep_kv=P(o["k"], C.c_int32))
+    rc = ctx._lib.tsdbhip_compact_rows(ctx.handle, C.byref(d), C.byref(out))
+    torch.cuda.synchronize()
+    h = {k: v.cpu().numpy() for k, v in o.items()}
+    res = compaction.RowsResult(h["st"][:R], h["qo"][:R].view(np.uint64), h["ql"][:R].view(np.uint32),
+                                h["vo"][:R].view(np.uint64), h["vl"][:R].view(np.uint32), h["q"], h["v"],
+                                h["w"][:R], h["k"][:R], int(out.n_complex))
+    return rc, res, out
+
+
+@pytest.mark.gpu
+def test_gpu_compaction_device_desc(ctx):
+    """HBM-resident rows and outputs (the bench's C5 call): same bytes and
+    decisions as the oracle; qual_used / val_used from the kernels' extents"""
+    b = compaction.synth_rows(20000, seed=17, p_complex=0.3, p_conflict=0.02, p_junk=0.02)
+    rc, g, out = _device_call(ctx, b)
+    assert rc == _abi.OK
+    assert_same(g, oracle.compact_rows(b))
+    assert out.qual_used == b.qual_extent and out.val_used == b.val_extent + b.n_rows
+
+
+@pytest.mark.gpu
+def test_gpu_compaction_device_desc_errors(ctx):
+    """device descriptor: too small an output is E_CAPACITY, offsets past the
+    buffers E_INVALID_ARG — found at the call's end, as the host descriptor
+    finds them before it"""
+    b = compaction.synth_rows(3000, seed=19)
+    rc, _, _ = _device_call(ctx, b, qcap=b.qual_extent - 1)
+    assert rc == _abi.E_CAPACITY
+    rc, _, _ = _device_call(ctx, b, vcap=b.val_extent + b.n_rows - 1)
+    assert rc == _abi.E_CAPACITY
+    bad = compaction.RowBatch(b.row_kv_start.copy(), b.row_qual_off.copy(), b.row_val_off.copy(), b.kv_qual_len,
+                              b.kv_val_len, b.qual_bytes, b.val_bytes)
+    bad.row_qual_off[-1] = len(b.qual_bytes) + 16
+    rc, _, _ = _device_call(ctx, bad)
+    assert rc == _abi.E_INVALID_ARG
+    rc, g, _ = _device_call(ctx, b)  # (the context is fine afterwards)
+    assert rc == _abi.OK
+    assert_same(g, oracle.compact_rows(b))
