@@ -1935,6 +1935,292 @@ static uint32_t ug_e_pieces(uint32_t t0, uint32_t step, uint32_t n, uint32_t kk,
   return 1;
 }
 
+// the aligned group (k_ug_ds_reg; sharded: one collective group and
+// k_fap_finish_end); RC_UG_FALLBACK when the group did not stand
+static int ug_aligned_group(Slot* ctx, const UgIn& u, tsdbhip_sg_out* out, tsdbhip_timing& tm) {
+  const tsdbhip_sg_desc* d = u.d;
+  Xchg* X = u.X;
+  const bool sharded = X != nullptr;
+  Small* sm = u.sm;
+  hipStream_t st = ctx->stream;
+  const int agg = d->agg;
+  const uint32_t n = (uint32_t)u.k1, x0 = (uint32_t)(u.k1 >> 32);
+  const uint32_t n_kept = u.n_kept;
+  const uint32_t step = (uint32_t)(u.k2 >> 32);
+  Small h;
+  // ---- aligned group ----
+  const int32_t I = d->ds_interval;
+  // (a rank making no attempt may hold no key: step 0; speculative: the
+  // device's key)
+  const uint32_t kk = u.mine && !u.spec ? (uint32_t)(((int64_t)I + step - 1) / step) : 1u;
+  const uint32_t nb = u.mine && !u.spec ? (n + kk - 1) / kk : 0u;
+  const int fop = agg == TSDBHIP_AGG_MIN ? 1 : (agg == TSDBHIP_AGG_MAX ? 2 : 0);
+  uint32_t* gridv = scratch<uint32_t>(ctx, "grid", WAVE);
+  int64_t* o_pi = scratch<int64_t>(ctx, "fo_i", WAVE);
+  uint32_t* o_pc = scratch<uint32_t>(ctx, "fo_cnt", WAVE);
+  // the agreement header of the general path's optimistic finish, with the
+  // class key in the grid-geometry words: xh_grids_agree() holds iff every
+  // rank made the attempt on the same key
+  const uint64_t a1 = u.mine ? u.k1 : ~0ull, a2 = u.mine ? u.k2 : 0ull;
+  const XField fx[XH_N + 1] = {{&sm->err, 0, 0},  {&sm->gflags[0], 2, 0}, {&sm->gflags[1], 2, 0},
+                               {&sm->fstar, 1, 0}, {nullptr, 3, a1},       {nullptr, 4, a2},
+                               {nullptr, 3, 0},    {nullptr, 4, 0},        {nullptr, 3, 0},
+                               {nullptr, 4, 0},    {nullptr, 4, a1},       {nullptr, 3, a2},
+                               {&sm->fap_valid, 0, 0}};
+  XMove pack = {};
+  if (sharded) pack = xchg_desc(ctx, fx, XH_N + 1, (uint64_t*)sm->xh);
+  XMove unpack = pack;
+  unpack.out = 1;
+  map_out_reserve(ctx, OUT_HDR + 17 * WAVE);
+  const uint64_t end_seq = ++ctx->pub_seq;
+  FinalArgs fo;
+  std::memset(&fo, 0, sizeof fo);
+  fo.T = WAVE;
+  fo.n_chunks = 1;
+  fo.grid = gridv;
+  fo.out_ts = (int64_t*)(ctx->map_out_dev + OUT_HDR);
+  fo.out_bits = fo.out_ts + WAVE;
+  fo.out_isint = (uint8_t*)(fo.out_bits + WAVE);
+  fo.nan_t = &sm->nan_t;
+  Small* snap = (Small*)ctx->map_out_dev;
+  const Small* ini = small_init_dev(ctx);
+  if (!u.mine) {
+    LAUNCH(k_fap_neutral64, dim3(1), dim3(WAVE), 0, st, o_pi, o_pc, fop, sm, pack);
+  } else {
+    // k_ds_reg, a wave a span, in the aligned group's mode, with the tail
+    // in its last block (k_ug_ds_reg)
+    const uint32_t rblocks = (n_kept + 3) / 4;
+    SpanDsArgs gr = {};
+    gr.nseg = CK_NSEG;
+    gr.seg_cap = 4u * ((rblocks + CK_NSEG - 1) / CK_NSEG);
+    gr.list = scratch<uint32_t>(ctx, "cr_list", (uint64_t)gr.seg_cap * CK_NSEG);
+    gr.list_count = sm->seg2;
+    gr.rate = 0;
+    FapArgs fa = {};
+    fa.op = fop;
+    fa.key = sm->fap_key;
+    fa.broken = &sm->fap_broken;
+    fa.nrows = rblocks;
+    fa.ncopy = UG_NCOPY;
+    if (u.spec) {
+      fa.spec_n_kept = &sm->n_kept;
+      fa.spec_go = &sm->ug_go;
+    }
+    {  // the copies, neutral on entry (left neutral by every tail; a new allocation filled once)
+      static const char* names[3] = {"ug_copies0", "ug_copies1", "ug_copies2"};
+      fa.copies = scratch<unsigned long long>(ctx, names[fop], (uint64_t)UG_NCOPY * WAVE);
+      Buf& b = ctx->bufs[names[fop]];
+      Buf& seen = ctx->zeroed[names[fop]];
+      if (b.p != seen.p || b.n != seen.n) {
+        LAUNCH(k_fill_u64, dim3(UG_NCOPY), dim3(WAVE), 0, st, fa.copies, UG_NCOPY * WAVE,
+               (unsigned long long)(fop == 1 ? INT64_MAX : (fop == 2 ? INT64_MIN : 0)));
+        seen = b;
+      }
+    }
+    UgTail t = {};
+    t.sm = sm; t.op = fop; t.agg = agg; t.sharded = sharded ? 1 : 0;
+    t.n_kept = n_kept; t.t0 = x0; t.step = step; t.kk = kk; t.ncell = n; t.nb = nb;
+    t.grid = gridv; t.p_i = o_pi; t.p_cnt = o_pc; t.pack = pack; t.fo = fo; t.snap = snap; t.init = ini;
+    t.seq = end_seq;
+    t.spec = u.spec ? 1u : 0u;
+    t.interval = I;
+    auto reg = [&](auto aggc) {
+      constexpr int A = decltype(aggc)::value;
+      static const unsigned stat_lds = [] {
+        hipFuncAttributes at = {};
+        return hipFuncGetAttributes(&at, (const void*)k_ug_ds_reg<A, false>) == hipSuccess
+                   ? (unsigned)at.sharedSizeBytes
+                   : 21000u;
+      }();
+      const unsigned pad = stat_lds < 40960u ? 40960u - stat_lds : 0u;
+      EV_START(ctx, 8);
+      if (u.spec)
+        LAUNCH_STOP(EV_STOP_K(ctx, 9), (k_ug_ds_reg<A, true>), dim3(rblocks), dim3(256), pad, st, u.da, gr,
+                    u.row_ncells, u.row_val_len, fa, t);
+      else
+        LAUNCH_STOP(EV_STOP_K(ctx, 9), (k_ug_ds_reg<A, false>), dim3(rblocks), dim3(256), pad, st, u.da, gr,
+                    u.row_ncells, u.row_val_len, fa, t);
+      EV_STOP_M(ctx, 9);
+    };
+    switch (d->ds_agg) {
+      case 0: reg(std::integral_constant<int, 0>()); break;
+      case 1: reg(std::integral_constant<int, 1>()); break;
+      case 2: reg(std::integral_constant<int, 2>()); break;
+      default: reg(std::integral_constant<int, 3>()); break;
+    }
+    ctx->hot_kernel = TSDBHIP_HOT_UG_DS_REG;
+  }
+  if (sharded) {
+    // the agreement, the validity (MIN) and the 64-slot partials: one
+    // collective group; then the finish
+    const XExtra ex[2] = {{o_pi, WAVE, fop ? X_I64 : X_U64, fop == 1 ? X_MIN : (fop == 2 ? X_MAX : X_SUM)},
+                          {o_pc, WAVE, X_U32, X_SUM}};
+    xchg_group(ctx, X, pack, (uint64_t*)&sm->n_input, ex, 2);
+    auto fin = [&](auto aggc) {
+      constexpr int A = decltype(aggc)::value;
+      LAUNCH(k_fap_finish_end<A>, dim3(1), dim3(256), 0, st, sm, (const int64_t*)o_pi, (const uint32_t*)o_pc, fo,
+             (int32_t)1, unpack, snap, ini, (uint32_t*)nullptr, (const uint32_t*)gridv, (int64_t)0, end_seq);
+    };
+    if (agg == TSDBHIP_AGG_MIN) fin(std::integral_constant<int, 1>());
+    else if (agg == TSDBHIP_AGG_MAX) fin(std::integral_constant<int, 2>());
+    else if (agg == TSDBHIP_AGG_AVG) fin(std::integral_constant<int, 3>());
+    else fin(std::integral_constant<int, 0>());
+  }
+  EV_FINAL(ctx, 5);
+  HIPCHK(hipStreamSynchronize(st));
+  check_stamp(ctx, end_seq);
+  tm.late_stamp = ctx->timing_late;
+  std::memcpy(&h, ctx->map_out, sizeof h);
+  if (!h.fap_done) {
+    // the group did not stand (somewhere): the call state back to its
+    // initial values, the general path runs the call
+    const uint64_t seq2 = ++ctx->pub_seq;
+    LAUNCH(k_call_end, dim3(1), dim3(256), 0, st, sm, (Small*)ctx->map_out_dev, ini, (uint32_t*)nullptr,
+           (const uint32_t*)nullptr, (uint64_t)0, (int64_t)0, BadArgs{}, seq2, (const uint32_t*)nullptr);
+    HIPCHK(hipStreamSynchronize(st));
+    check_stamp(ctx, seq2);
+    ctx->sm_ready = true;
+    return RC_UG_FALLBACK;
+  }
+  ctx->sm_ready = true;
+  const uint64_t T = h.T;
+  out->n_input_points = h.n_input;
+  tm.n_grid = T;
+  tm.paths |= TSDBHIP_PATH_ALIGNED_GROUP;
+  if (sharded) {
+    tm.n_collectives = X->n_coll;
+    tm.x_bytes = X->x_bytes;
+  }
+  if (ctx->hot_kernel) tm.hot_ms = ev_ms(ctx, 8, 9);
+  tm.hot_kernel = ctx->hot_kernel;
+  tm.total_ms = ev_ms(ctx, 0, 5);
+  tm.n_emitted = T * h.n_kept;
+  ctx->timing = tm;
+  if (T > out->capacity && ctx->want_output) {
+    out->err_code = TSDBHIP_E_CAPACITY;
+    return TSDBHIP_E_CAPACITY;
+  }
+  if (ctx->want_output) {
+    const uint8_t* hb = ctx->map_out;
+    std::memcpy(out->ts, hb + OUT_HDR, T * 8);
+    std::memcpy(out->bits, hb + OUT_HDR + 8 * WAVE, T * 8);
+    std::memcpy(out->is_int, hb + OUT_HDR + 16 * WAVE, T);
+  }
+  out->n_out = T;
+  out->err_code = TSDBHIP_OK;
+  out->err_index = -1;
+  return TSDBHIP_OK;
+}
+
+// the E variant's launches: k_ds_reg in E mode, then k_ug_reduce
+static void ug_e_launch(Slot* ctx, const UgIn& u, uint64_t T, uint32_t e_kk, int mode, uint32_t* gridv,
+                        const FinalArgs& fin) {
+  const tsdbhip_sg_desc* d = u.d;
+  Small* sm = u.sm;
+  hipStream_t st = ctx->stream;
+  const int agg = d->agg;
+  const uint32_t n = (uint32_t)u.k1, x0 = (uint32_t)(u.k1 >> 32), step = (uint32_t)(u.k2 >> 32);
+  const uint32_t n_kept = u.n_kept;
+  // k_ds_reg in E mode (its block 0 writes G from the key, the spans their
+  // bucket values; an outsider sets the broken flag), then k_ug_reduce:
+  // every span's E is G itself (no bitmap, no grid ranks, no cursors)
+  ctx->hot_kernel = TSDBHIP_HOT_DS_CHUNKS;
+  const uint64_t rps = d->n_rows / std::max<uint32_t>(n_kept, 1);
+  const uint32_t wps_log2 = rps >= 12 ? 2 : (rps >= 6 ? 1 : 0);
+  // (waves a span, its rows in contiguous pieces: C2's 24 rows a span, 0.266
+  // ms a step with 3 pieces, 0.269 with 2, 0.281 with 4, 0.290 with 1,
+  // 0.310 with 8, 0.489 with 24 — same box)
+  uint32_t pieces = ug_e_pieces(x0, step, n, e_kk, (uint32_t)std::max<uint64_t>(1, rps / 8));
+  if (const char* e = getenv("TSDBHIP_UG_P")) pieces = (uint32_t)std::max(1, atoi(e));  // (A/B runs)
+  const uint32_t rblocks = (uint32_t)(((uint64_t)n_kept * pieces + 3) / 4);
+  SpanDsArgs gr = {};
+  gr.nseg = CK_NSEG;
+  FapArgs fa = {};
+  fa.op = -1;
+  fa.broken = &sm->ls_broken;
+  fa.ug_grid = gridv;
+  fa.ug_t0 = x0; fa.ug_step = step; fa.ug_kk = e_kk; fa.ug_n = n; fa.ug_pieces = pieces;
+  auto reg = [&](auto aggc) {
+    constexpr int A = decltype(aggc)::value;
+    static const unsigned stat_lds = [] {
+      hipFuncAttributes at = {};
+      return hipFuncGetAttributes(&at, (const void*)k_ds_reg<A>) == hipSuccess ? (unsigned)at.sharedSizeBytes
+                                                                               : 18960u;
+    }();
+    const unsigned pad = pieces == 1 ? (stat_lds < 40960u ? 40960u - stat_lds : 0u) : 0u;
+    EV_START(ctx, 8);
+    LAUNCH_STOP(EV_STOP_K(ctx, 9), (k_ds_reg<A>), dim3(rblocks), dim3(256), pad, st, u.da, gr, u.row_ncells,
+                u.row_val_len, wps_log2, fa);
+    EV_STOP_M(ctx, 9);
+  };
+  switch (d->ds_agg) {
+    case 0: reg(std::integral_constant<int, 0>()); break;
+    case 1: reg(std::integral_constant<int, 1>()); break;
+    case 2: reg(std::integral_constant<int, 2>()); break;
+    default: reg(std::integral_constant<int, 3>()); break;
+  }
+  // (integer dev: one span-ordered chunk, Aggregators.java:196-217; else
+  // chunks of 64 spans, merged in chunk order by the finalize)
+  const bool seq = agg == TSDBHIP_AGG_DEV && mode != MODE_DBL;
+  const uint32_t spc = seq ? std::max<uint32_t>(n_kept, 1) : 64u;
+  ReduceArgs re;
+  std::memset(&re, 0, sizeof re);
+  re.e_off = u.da.e_off; re.e_val = u.da.e_val; re.n_kept = n_kept; re.grid = gridv; re.T = T;
+  re.spans_per_chunk = spc;
+  re.n_chunks = (n_kept + spc - 1) / spc;
+  alloc_partials(ctx, re, "p_", (uint64_t)re.n_chunks * T, agg);
+  FinalArgs fe = fin;
+  fe.n_chunks = re.n_chunks;
+  dispatch_ug_reduce(ctx, agg, mode, re, fe);
+}
+
+// the sharded lockstep group: this rank's lockstep partials combined, the
+// exchange (exact integers: an allreduce a field; doubles: every rank's slot
+// gathered and merged in rank order), then the finalize
+static void ug_lockstep_sharded(Slot* ctx, const UgIn& u, uint64_t T, int mode, unsigned blocks, ReduceArgs& r,
+                                const LsPlan& lsp, const FinalArgs& f, const FinalArgs& fin) {
+  Xchg* X = u.X;
+  Small* sm = u.sm;
+  const int agg = u.d->agg;
+  const bool rate = u.d->rate != 0;
+  const uint32_t n_chunks = r.n_chunks;
+  const int nr = X->nranks, rk = X->rank;
+  dispatch_lockstep(ctx, agg, rate, blocks, r, lsp, f, false);
+  ReduceArgs src;
+  uint32_t n_src = 1;
+  if (mode == MODE_INT) {  // exact integer partials: one allreduce a field
+    ReduceArgs mine = r;
+    alloc_partials(ctx, mine, "m_", T, agg);
+    dispatch_combine(ctx, agg, mode, r, mine, T, n_chunks);
+    X->group_start(ctx);
+    for (const Fld& fl : partial_fields(mine, 0, agg, mode)) X->allreduce(ctx, fl.p, T, fl.t, fl.op);
+    X->allreduce(ctx, &sm->ls_broken, 1, X_U32, X_MAX);
+    X->allreduce(ctx, &sm->n_input, 1, X_U64, X_SUM);
+    X->group_end(ctx);
+    src = mine;
+  } else {  // doubles: every rank's slot gathered, merged in rank order
+    ReduceArgs all = r;
+    alloc_partials(ctx, all, "x_", (uint64_t)nr * T, agg);
+    ReduceArgs mine = all;
+    const uint64_t off = (uint64_t)rk * T;
+    mine.p_cnt += off; mine.p_flag += off; mine.p_i += off; mine.p_d += off; mine.p_dhas += off;
+    if (agg == TSDBHIP_AGG_DEV) { mine.p_wim += off; mine.p_wiv += off; mine.p_wdm += off; mine.p_wdv += off; }
+    dispatch_combine(ctx, agg, mode, r, mine, T, n_chunks);
+    const std::vector<Fld> fm = partial_fields(mine, 0, agg, mode), fa = partial_fields(all, 0, agg, mode);
+    X->group_start(ctx);
+    for (size_t i = 0; i < fm.size(); i++) X->allgather(ctx, fm[i].p, fa[i].p, T * fm[i].esz);
+    X->allreduce(ctx, &sm->ls_broken, 1, X_U32, X_MAX);
+    X->allreduce(ctx, &sm->n_input, 1, X_U64, X_SUM);
+    X->group_end(ctx);
+    src = all;
+    n_src = (uint32_t)nr;
+  }
+  FinalArgs ff = fin;
+  ff.n_chunks = n_src;
+  src.n_chunks = n_src;
+  dispatch_final(ctx, agg, mode, rate, src, ff);
+}
+
 static int uniform_run(Slot* ctx, const UgIn& u, tsdbhip_sg_out* out, tsdbhip_timing& tm) {
   const tsdbhip_sg_desc* d = u.d;
   Xchg* X = u.X;
@@ -1948,170 +2234,7 @@ static int uniform_run(Slot* ctx, const UgIn& u, tsdbhip_sg_out* out, tsdbhip_ti
   const uint32_t n_kept = u.n_kept;
   Small h;
   tm.paths |= TSDBHIP_PATH_UNIFORM;
-  if (!u.lockstep && !u.e) {
-    // ---- aligned group ----
-    const int32_t I = d->ds_interval;
-    // (a rank making no attempt may hold no key: step 0; speculative: the
-    // device's key)
-    const uint32_t kk = u.mine && !u.spec ? (uint32_t)(((int64_t)I + step - 1) / step) : 1u;
-    const uint32_t nb = u.mine && !u.spec ? (n + kk - 1) / kk : 0u;
-    const int fop = agg == TSDBHIP_AGG_MIN ? 1 : (agg == TSDBHIP_AGG_MAX ? 2 : 0);
-    uint32_t* gridv = scratch<uint32_t>(ctx, "grid", WAVE);
-    int64_t* o_pi = scratch<int64_t>(ctx, "fo_i", WAVE);
-    uint32_t* o_pc = scratch<uint32_t>(ctx, "fo_cnt", WAVE);
-    // the agreement header of the general path's optimistic finish, with the
-    // class key in the grid-geometry words: xh_grids_agree() holds iff every
-    // rank made the attempt on the same key
-    const uint64_t a1 = u.mine ? u.k1 : ~0ull, a2 = u.mine ? u.k2 : 0ull;
-    const XField fx[XH_N + 1] = {{&sm->err, 0, 0},  {&sm->gflags[0], 2, 0}, {&sm->gflags[1], 2, 0},
-                                 {&sm->fstar, 1, 0}, {nullptr, 3, a1},       {nullptr, 4, a2},
-                                 {nullptr, 3, 0},    {nullptr, 4, 0},        {nullptr, 3, 0},
-                                 {nullptr, 4, 0},    {nullptr, 4, a1},       {nullptr, 3, a2},
-                                 {&sm->fap_valid, 0, 0}};
-    XMove pack = {};
-    if (sharded) pack = xchg_desc(ctx, fx, XH_N + 1, (uint64_t*)sm->xh);
-    XMove unpack = pack;
-    unpack.out = 1;
-    map_out_reserve(ctx, OUT_HDR + 17 * WAVE);
-    const uint64_t end_seq = ++ctx->pub_seq;
-    FinalArgs fo;
-    std::memset(&fo, 0, sizeof fo);
-    fo.T = WAVE;
-    fo.n_chunks = 1;
-    fo.grid = gridv;
-    fo.out_ts = (int64_t*)(ctx->map_out_dev + OUT_HDR);
-    fo.out_bits = fo.out_ts + WAVE;
-    fo.out_isint = (uint8_t*)(fo.out_bits + WAVE);
-    fo.nan_t = &sm->nan_t;
-    Small* snap = (Small*)ctx->map_out_dev;
-    const Small* ini = small_init_dev(ctx);
-    if (!u.mine) {
-      LAUNCH(k_fap_neutral64, dim3(1), dim3(WAVE), 0, st, o_pi, o_pc, fop, sm, pack);
-    } else {
-      // k_ds_reg, a wave a span, in the aligned group's mode, with the tail
-      // in its last block (k_ug_ds_reg)
-      const uint32_t rblocks = (n_kept + 3) / 4;
-      SpanDsArgs gr = {};
-      gr.nseg = CK_NSEG;
-      gr.seg_cap = 4u * ((rblocks + CK_NSEG - 1) / CK_NSEG);
-      gr.list = scratch<uint32_t>(ctx, "cr_list", (uint64_t)gr.seg_cap * CK_NSEG);
-      gr.list_count = sm->seg2;
-      gr.rate = 0;
-      FapArgs fa = {};
-      fa.op = fop;
-      fa.key = sm->fap_key;
-      fa.broken = &sm->fap_broken;
-      fa.nrows = rblocks;
-      fa.ncopy = UG_NCOPY;
-      if (u.spec) {
-        fa.spec_n_kept = &sm->n_kept;
-        fa.spec_go = &sm->ug_go;
-      }
-      {  // the copies, neutral on entry (left neutral by every tail; a new allocation filled once)
-        static const char* names[3] = {"ug_copies0", "ug_copies1", "ug_copies2"};
-        fa.copies = scratch<unsigned long long>(ctx, names[fop], (uint64_t)UG_NCOPY * WAVE);
-        Buf& b = ctx->bufs[names[fop]];
-        Buf& seen = ctx->zeroed[names[fop]];
-        if (b.p != seen.p || b.n != seen.n) {
-          LAUNCH(k_fill_u64, dim3(UG_NCOPY), dim3(WAVE), 0, st, fa.copies, UG_NCOPY * WAVE,
-                 (unsigned long long)(fop == 1 ? INT64_MAX : (fop == 2 ? INT64_MIN : 0)));
-          seen = b;
-        }
-      }
-      UgTail t = {};
-      t.sm = sm; t.op = fop; t.agg = agg; t.sharded = sharded ? 1 : 0;
-      t.n_kept = n_kept; t.t0 = x0; t.step = step; t.kk = kk; t.ncell = n; t.nb = nb;
-      t.grid = gridv; t.p_i = o_pi; t.p_cnt = o_pc; t.pack = pack; t.fo = fo; t.snap = snap; t.init = ini;
-      t.seq = end_seq;
-      t.spec = u.spec ? 1u : 0u;
-      t.interval = I;
-      auto reg = [&](auto aggc) {
-        constexpr int A = decltype(aggc)::value;
-        static const unsigned stat_lds = [] {
-          hipFuncAttributes at = {};
-          return hipFuncGetAttributes(&at, (const void*)k_ug_ds_reg<A, false>) == hipSuccess
-                     ? (unsigned)at.sharedSizeBytes
-                     : 21000u;
-        }();
-        const unsigned pad = stat_lds < 40960u ? 40960u - stat_lds : 0u;
-        EV_START(ctx, 8);
-        if (u.spec)
-          LAUNCH_STOP(EV_STOP_K(ctx, 9), (k_ug_ds_reg<A, true>), dim3(rblocks), dim3(256), pad, st, u.da, gr,
-                      u.row_ncells, u.row_val_len, fa, t);
-        else
-          LAUNCH_STOP(EV_STOP_K(ctx, 9), (k_ug_ds_reg<A, false>), dim3(rblocks), dim3(256), pad, st, u.da, gr,
-                      u.row_ncells, u.row_val_len, fa, t);
-        EV_STOP_M(ctx, 9);
-      };
-      switch (d->ds_agg) {
-        case 0: reg(std::integral_constant<int, 0>()); break;
-        case 1: reg(std::integral_constant<int, 1>()); break;
-        case 2: reg(std::integral_constant<int, 2>()); break;
-        default: reg(std::integral_constant<int, 3>()); break;
-      }
-      ctx->hot_kernel = TSDBHIP_HOT_UG_DS_REG;
-    }
-    if (sharded) {
-      // the agreement, the validity (MIN) and the 64-slot partials: one
-      // collective group; then the finish
-      const XExtra ex[2] = {{o_pi, WAVE, fop ? X_I64 : X_U64, fop == 1 ? X_MIN : (fop == 2 ? X_MAX : X_SUM)},
-                            {o_pc, WAVE, X_U32, X_SUM}};
-      xchg_group(ctx, X, pack, (uint64_t*)&sm->n_input, ex, 2);
-      auto fin = [&](auto aggc) {
-        constexpr int A = decltype(aggc)::value;
-        LAUNCH(k_fap_finish_end<A>, dim3(1), dim3(256), 0, st, sm, (const int64_t*)o_pi, (const uint32_t*)o_pc, fo,
-               (int32_t)1, unpack, snap, ini, (uint32_t*)nullptr, (const uint32_t*)gridv, (int64_t)0, end_seq);
-      };
-      if (agg == TSDBHIP_AGG_MIN) fin(std::integral_constant<int, 1>());
-      else if (agg == TSDBHIP_AGG_MAX) fin(std::integral_constant<int, 2>());
-      else if (agg == TSDBHIP_AGG_AVG) fin(std::integral_constant<int, 3>());
-      else fin(std::integral_constant<int, 0>());
-    }
-    EV_FINAL(ctx, 5);
-    HIPCHK(hipStreamSynchronize(st));
-    check_stamp(ctx, end_seq);
-    tm.late_stamp = ctx->timing_late;
-    std::memcpy(&h, ctx->map_out, sizeof h);
-    if (!h.fap_done) {
-      // the group did not stand (somewhere): the call state back to its
-      // initial values, the general path runs the call
-      const uint64_t seq2 = ++ctx->pub_seq;
-      LAUNCH(k_call_end, dim3(1), dim3(256), 0, st, sm, (Small*)ctx->map_out_dev, ini, (uint32_t*)nullptr,
-             (const uint32_t*)nullptr, (uint64_t)0, (int64_t)0, BadArgs{}, seq2, (const uint32_t*)nullptr);
-      HIPCHK(hipStreamSynchronize(st));
-      check_stamp(ctx, seq2);
-      ctx->sm_ready = true;
-      return RC_UG_FALLBACK;
-    }
-    ctx->sm_ready = true;
-    const uint64_t T = h.T;
-    out->n_input_points = h.n_input;
-    tm.n_grid = T;
-    tm.paths |= TSDBHIP_PATH_ALIGNED_GROUP;
-    if (sharded) {
-      tm.n_collectives = X->n_coll;
-      tm.x_bytes = X->x_bytes;
-    }
-    if (ctx->hot_kernel) tm.hot_ms = ev_ms(ctx, 8, 9);
-    tm.hot_kernel = ctx->hot_kernel;
-    tm.total_ms = ev_ms(ctx, 0, 5);
-    tm.n_emitted = T * h.n_kept;
-    ctx->timing = tm;
-    if (T > out->capacity && ctx->want_output) {
-      out->err_code = TSDBHIP_E_CAPACITY;
-      return TSDBHIP_E_CAPACITY;
-    }
-    if (ctx->want_output) {
-      const uint8_t* hb = ctx->map_out;
-      std::memcpy(out->ts, hb + OUT_HDR, T * 8);
-      std::memcpy(out->bits, hb + OUT_HDR + 8 * WAVE, T * 8);
-      std::memcpy(out->is_int, hb + OUT_HDR + 16 * WAVE, T);
-    }
-    out->n_out = T;
-    out->err_code = TSDBHIP_OK;
-    out->err_index = -1;
-    return TSDBHIP_OK;
-  }
+  if (!u.lockstep && !u.e) return ug_aligned_group(ctx, u, out, tm);
 
   // ---- lockstep, E ----
   const uint32_t e_kk = u.e ? (uint32_t)(((int64_t)d->ds_interval + step - 1) / step) : 0u;
@@ -2168,57 +2291,7 @@ static int uniform_run(Slot* ctx, const UgIn& u, tsdbhip_sg_out* out, tsdbhip_ti
   FinalArgs f = fin;
   f.n_chunks = n_chunks;
   if (u.e) {
-    // k_ds_reg in E mode (its block 0 writes G from the key, the spans their
-    // bucket values; an outsider sets the broken flag), then k_ug_reduce:
-    // every span's E is G itself (no bitmap, no grid ranks, no cursors)
-    ctx->hot_kernel = TSDBHIP_HOT_DS_CHUNKS;
-    const uint64_t rps = d->n_rows / std::max<uint32_t>(n_kept, 1);
-    const uint32_t wps_log2 = rps >= 12 ? 2 : (rps >= 6 ? 1 : 0);
-    // (waves a span, its rows in contiguous pieces: C2's 24 rows a span, 0.266
-    // ms a step with 3 pieces, 0.269 with 2, 0.281 with 4, 0.290 with 1,
-    // 0.310 with 8, 0.489 with 24 — same box)
-    uint32_t pieces = ug_e_pieces(x0, step, n, e_kk, (uint32_t)std::max<uint64_t>(1, rps / 8));
-    if (const char* e = getenv("TSDBHIP_UG_P")) pieces = (uint32_t)std::max(1, atoi(e));  // (A/B runs)
-    const uint32_t rblocks = (uint32_t)(((uint64_t)n_kept * pieces + 3) / 4);
-    SpanDsArgs gr = {};
-    gr.nseg = CK_NSEG;
-    FapArgs fa = {};
-    fa.op = -1;
-    fa.broken = &sm->ls_broken;
-    fa.ug_grid = gridv;
-    fa.ug_t0 = x0; fa.ug_step = step; fa.ug_kk = e_kk; fa.ug_n = n; fa.ug_pieces = pieces;
-    auto reg = [&](auto aggc) {
-      constexpr int A = decltype(aggc)::value;
-      static const unsigned stat_lds = [] {
-        hipFuncAttributes at = {};
-        return hipFuncGetAttributes(&at, (const void*)k_ds_reg<A>) == hipSuccess ? (unsigned)at.sharedSizeBytes
-                                                                                 : 18960u;
-      }();
-      const unsigned pad = pieces == 1 ? (stat_lds < 40960u ? 40960u - stat_lds : 0u) : 0u;
-      EV_START(ctx, 8);
-      LAUNCH_STOP(EV_STOP_K(ctx, 9), (k_ds_reg<A>), dim3(rblocks), dim3(256), pad, st, u.da, gr, u.row_ncells,
-                  u.row_val_len, wps_log2, fa);
-      EV_STOP_M(ctx, 9);
-    };
-    switch (d->ds_agg) {
-      case 0: reg(std::integral_constant<int, 0>()); break;
-      case 1: reg(std::integral_constant<int, 1>()); break;
-      case 2: reg(std::integral_constant<int, 2>()); break;
-      default: reg(std::integral_constant<int, 3>()); break;
-    }
-    // (integer dev: one span-ordered chunk, Aggregators.java:196-217; else
-    // chunks of 64 spans, merged in chunk order by the finalize)
-    const bool seq = agg == TSDBHIP_AGG_DEV && mode != MODE_DBL;
-    const uint32_t spc = seq ? std::max<uint32_t>(n_kept, 1) : 64u;
-    ReduceArgs re;
-    std::memset(&re, 0, sizeof re);
-    re.e_off = u.da.e_off; re.e_val = u.da.e_val; re.n_kept = n_kept; re.grid = gridv; re.T = T;
-    re.spans_per_chunk = spc;
-    re.n_chunks = (n_kept + spc - 1) / spc;
-    alloc_partials(ctx, re, "p_", (uint64_t)re.n_chunks * T, agg);
-    FinalArgs fe = fin;
-    fe.n_chunks = re.n_chunks;
-    dispatch_ug_reduce(ctx, agg, mode, re, fe);
+    ug_e_launch(ctx, u, T, e_kk, mode, gridv, fin);
   } else if (u.dev) {  // integer dev: one sequential chain a grid point (k_ug_dev)
     ctx->hot_kernel = TSDBHIP_HOT_UG_DEV;
     EV_START(ctx, 8);
@@ -2233,41 +2306,7 @@ static int uniform_run(Slot* ctx, const UgIn& u, tsdbhip_sg_out* out, tsdbhip_ti
   } else if (!sharded) {
     dispatch_lockstep(ctx, agg, rate, blocks, r, lsp, f, true);
   } else {
-    const int nr = X->nranks, rk = X->rank;
-    dispatch_lockstep(ctx, agg, rate, blocks, r, lsp, f, false);
-    ReduceArgs src;
-    uint32_t n_src = 1;
-    if (mode == MODE_INT) {  // exact integer partials: one allreduce a field
-      ReduceArgs mine = r;
-      alloc_partials(ctx, mine, "m_", T, agg);
-      dispatch_combine(ctx, agg, mode, r, mine, T, n_chunks);
-      X->group_start(ctx);
-      for (const Fld& fl : partial_fields(mine, 0, agg, mode)) X->allreduce(ctx, fl.p, T, fl.t, fl.op);
-      X->allreduce(ctx, &sm->ls_broken, 1, X_U32, X_MAX);
-      X->allreduce(ctx, &sm->n_input, 1, X_U64, X_SUM);
-      X->group_end(ctx);
-      src = mine;
-    } else {  // doubles: every rank's slot gathered, merged in rank order
-      ReduceArgs all = r;
-      alloc_partials(ctx, all, "x_", (uint64_t)nr * T, agg);
-      ReduceArgs mine = all;
-      const uint64_t off = (uint64_t)rk * T;
-      mine.p_cnt += off; mine.p_flag += off; mine.p_i += off; mine.p_d += off; mine.p_dhas += off;
-      if (agg == TSDBHIP_AGG_DEV) { mine.p_wim += off; mine.p_wiv += off; mine.p_wdm += off; mine.p_wdv += off; }
-      dispatch_combine(ctx, agg, mode, r, mine, T, n_chunks);
-      const std::vector<Fld> fm = partial_fields(mine, 0, agg, mode), fa = partial_fields(all, 0, agg, mode);
-      X->group_start(ctx);
-      for (size_t i = 0; i < fm.size(); i++) X->allgather(ctx, fm[i].p, fa[i].p, T * fm[i].esz);
-      X->allreduce(ctx, &sm->ls_broken, 1, X_U32, X_MAX);
-      X->allreduce(ctx, &sm->n_input, 1, X_U64, X_SUM);
-      X->group_end(ctx);
-      src = all;
-      n_src = (uint32_t)nr;
-    }
-    FinalArgs ff = fin;
-    ff.n_chunks = n_src;
-    src.n_chunks = n_src;
-    dispatch_final(ctx, agg, mode, rate, src, ff);
+    ug_lockstep_sharded(ctx, u, T, mode, blocks, r, lsp, f, fin);
   }
   const uint64_t end_seq = ++ctx->pub_seq;
   LAUNCH(k_call_end, dim3(1), dim3(256), 0, st, sm, (Small*)ctx->map_out_dev, small_init_dev(ctx), (uint32_t*)nullptr,
@@ -2324,484 +2363,619 @@ static int uniform_run(Slot* ctx, const UgIn& u, tsdbhip_sg_out* out, tsdbhip_ti
 }
 
 // ------------------------------------------------------- the hot path ----
+// One call of the general path (and the entry of the uniform path), as the
+// stages the call runs in order, sharing the call's state as members:
+//   begin           flags, the inputs in HBM, the call state
+//   assemble        Span.addRow / RowSeq.addRow, the keep rule, the kept list
+//                   (and the uniform path's class keys)
+//   sync1           the first host round trip (the speculative sharded
+//                   aligned group instead, which ends the call)
+//   plan            the union grid's range, the aligned-group plan, E
+//   uniform_try     the uniform path when every kept span proposed one key
+//   decode          decode + downsampling (direct / lockstep proposals)
+//   grid            the union-grid bitmap and its ranks
+//   fap_finish      the optimistic aligned-group finish (ends the call if the
+//                   group stood)
+//   exchange_header the sharded agreement (sync 2), the global grid
+//   plan_reduce     the reduce mode and variant, G emitted, the output block
+//   reduce          the cross-span reduction, the exchange of the partials,
+//                   the finalize
+//   finish          the end of the call: the state snapshot, the outputs
 // ls_allow: the lockstep proposal may be tried (k_direct_opt / k_lockstep);
-// false for the rerun after k_lockstep found a qualifier off the proposal
+// false for the rerun after k_lockstep found a qualifier off the proposal.
 // ug_allow: the uniform path (uniform_run) may be taken; false for the rerun
-// after it found the group not uniform
-static int spangroup_run_once(Slot* ctx, const tsdbhip_sg_desc* d, tsdbhip_sg_out* out, bool ls_allow,
-                              bool ug_allow) {
-  const bool dev = (d->flags & TSDBHIP_DESC_DEVICE) != 0;
-  const bool exact = (d->flags & TSDBHIP_EXACT_ORDER) != 0;
-  // (a 1-rank communicator runs the same exchange code: tests use it)
-  Xchg* X = (d->flags & TSDBHIP_SHARDED) ? ctx->x : nullptr;
-  const bool sharded = X != nullptr;
-  if (X) {
-    X->n_coll = 0;
-    X->x_bytes = 0;
-  }
-  const uint32_t S = d->n_spans;
-  const uint64_t R = d->n_rows;
-  const bool rate = d->rate != 0;
-  const int agg = d->agg;
-  const int ds_agg = d->ds_agg;
-  const int32_t interval = d->ds_interval > 0 ? d->ds_interval : 0;
-  hipStream_t st = ctx->stream;
+// after it found the group not uniform (spangroup_run holds both edges).
+constexpr int RC_CONTINUE = INT32_MIN;  // (a stage that did not end the call)
+struct SgCall {
+  Slot* ctx;
+  const tsdbhip_sg_desc* d;
+  tsdbhip_sg_out* out;
+  bool ls_allow, ug_allow;
+  // begin
+  bool dev = false, exact = false, sharded = false, rate = false, check_clean = false, bm_clean = false;
+  bool tgd_clean = false, tgd_used = false, detail = false;
+  Xchg* X = nullptr;
+  uint32_t S = 0;
+  uint64_t R = 0;
+  int agg = 0, ds_agg = 0;
+  int32_t interval = 0;
+  hipStream_t st = nullptr;
   tsdbhip_timing tm = {};
-  ctx->timing_late = 0;
-  ctx->hot_kernel = TSDBHIP_HOT_NONE;
-  ctx->time_reduce = false;
-  out->n_out = 0;
-  out->n_input_points = 0;
-  out->err_code = 0;
-  out->err_index = -1;
-
-  // ---- inputs in HBM ----
-  const uint64_t* span_row_start = stage(ctx, "in_srs", d->span_row_start, (size_t)S + 1, dev);
-  const uint32_t* row_base = stage(ctx, "in_base", d->row_base, R, dev);
-  const uint32_t* row_ncells = stage(ctx, "in_ncells", d->row_ncells, R, dev);
-  const uint64_t* row_qual_off = stage(ctx, "in_qoff", d->row_qual_off, R, dev);
-  const uint64_t* row_val_off = stage(ctx, "in_voff", d->row_val_off, R, dev);
-  const uint32_t* row_val_len = stage(ctx, "in_vlen", d->row_val_len, R, dev);
-  const uint8_t* qual = stage(ctx, "in_qual", d->qual_bytes, d->qual_nbytes, dev, 16);
-  const uint8_t* val = stage(ctx, "in_val", d->val_bytes, d->val_nbytes, dev, 16);
-
-  Small* sm = scratch<Small>(ctx, "small", 1);
-  const bool check_clean = ctx->opt.check_clean;
-  if (check_clean && ctx->sm_ready) {  // (debug) the reset state must equal small_init()
-    Small cur, ini = small_init();
-    readback(ctx, &cur, sm, sizeof cur);
-    if (std::memcmp(&cur, &ini, sizeof cur) != 0) {
-      const uint8_t* a = (const uint8_t*)&cur; const uint8_t* b = (const uint8_t*)&ini;
-      size_t i = 0;
-      while (a[i] == b[i]) i++;
-      fprintf(stderr, "TSDBHIP_CHECK_CLEAN: call state not reset (first differing byte %zu)\n", i);
-    }
-  }
-  if (!ctx->sm_ready) {  // (a completed call leaves it reset: k_call_end)
-    const Small init = small_init();
-    std::memcpy(ctx->host_small, &init, sizeof init);
-    HIPCHK(hipMemcpyAsync(sm, ctx->host_small, sizeof init, hipMemcpyHostToDevice, st));
-  }
-  ctx->sm_ready = false;
-  const bool bm_clean = ctx->bitmap_clean;
-  ctx->bitmap_clean = false;
-  const bool tgd_clean = ctx->tgdone_clean;
-  ctx->tgdone_clean = false;
-  bool tgd_used = false;
-  const bool detail = ctx->opt.timing_detail;  // decode / grid event pairs
-  g_ev_pend = nullptr;
-  g_ev_pend_i = -1;
-  std::memset(ctx->ev_alias, 0xff, sizeof ctx->ev_alias);
-  EV_START(ctx, 0);
-
-  // ---- assemble ----
-  uint8_t* row_ok = scratch<uint8_t>(ctx, "row_ok", R);
-  uint32_t* row_cell0 = scratch<uint32_t>(ctx, "row_cell0", R);
-  uint32_t* sp_ncells = scratch<uint32_t>(ctx, "sp_ncells", S);
-  int64_t* sp_first = scratch<int64_t>(ctx, "sp_first", S);
-  int64_t* sp_last = scratch<int64_t>(ctx, "sp_last", S);
-  uint8_t* sp_kept = scratch<uint8_t>(ctx, "sp_kept", S);
-  uint64_t* sp_cap = scratch<uint64_t>(ctx, "sp_cap", S);
-  int64_t* sp_q1 = scratch<int64_t>(ctx, "sp_q1", S);
-  int32_t* sp_q1s = scratch<int32_t>(ctx, "sp_q1s", S);
-  int64_t* sp_q1rs = scratch<int64_t>(ctx, "sp_q1rs", 2ull * S);
-  int64_t* sp_ovf = scratch<int64_t>(ctx, "sp_ovf", S);
+  const uint64_t* span_row_start = nullptr;
+  const uint32_t* row_base = nullptr;
+  const uint32_t* row_ncells = nullptr;
+  const uint64_t* row_qual_off = nullptr;
+  const uint64_t* row_val_off = nullptr;
+  const uint32_t* row_val_len = nullptr;
+  const uint8_t* qual = nullptr;
+  const uint8_t* val = nullptr;
+  Small* sm = nullptr;
+  // assemble
+  uint8_t* row_ok = nullptr;
+  uint32_t* row_cell0 = nullptr;
+  uint32_t* sp_ncells = nullptr;
+  int64_t* sp_first = nullptr;
+  int64_t* sp_last = nullptr;
+  uint8_t* sp_kept = nullptr;
+  uint64_t* sp_cap = nullptr;
+  int64_t* sp_q1 = nullptr;
+  int32_t* sp_q1s = nullptr;
+  int64_t* sp_q1rs = nullptr;
+  int64_t* sp_ovf = nullptr;
   uint32_t* kept = nullptr;
   uint64_t* eoff = nullptr;
   bool pub1 = false;
   HostPub p1 = {};
-  // the uniform path's queries (uniform_run): lockstep (no downsampling, the
-  // conditions of the general path's lockstep try) or the aligned group
-  // (downsampled exact integer aggregation); the spans' class keys are
-  // proposed at assembly for them
-  const bool auto_dec = ctx->opt.decode == DEC_AUTO;
-  // (unsharded, lockstep "on": the group needs >= 2048 lockstep waves, and
-  // with C <= qual_nbytes / 2 cells in all and n in each of n_kept <= S
-  // spans, ceil(n / LS_TILE) * max(1, n_kept / 64) <= max(ceil(C / LS_TILE),
-  // C / (64 LS_TILE) + S / 64 + 1): a group under that bound cannot take it,
-  // and its assembly skips the key probe — C1's 100 spans: 7 us)
-  const uint64_t c_max = d->qual_nbytes / 2;
-  const bool ls_size_ok = sharded || ctx->opt.lockstep == 2 ||
-                          std::max<uint64_t>((c_max + LS_TILE - 1) / LS_TILE, c_max / (64 * LS_TILE) + S / 64 + 1) >= 2048;
-  const bool ug_ls_q = ug_allow && auto_dec && interval == 0 && ls_allow && ctx->opt.lockstep && !exact &&
-                       (agg != TSDBHIP_AGG_DEV || rate) && ls_size_ok;
-  const bool ug_fap_q = ug_allow && auto_dec && interval > 0 && !rate && ds_agg <= 3 && agg <= 3 && !exact &&
-                        ctx->opt.aligned_group && !ctx->opt.timing_detail;
-  // (integer dev without rate, unsharded: the sequential chains of k_ug_dev)
-  const bool ug_dev_q = ug_allow && auto_dec && interval == 0 && !exact && agg == TSDBHIP_AGG_DEV && !rate &&
-                        !sharded;
-  // (other downsampled queries, unsharded: k_ds_reg's E on the key's buckets)
-  const bool ug_e_q = ug_allow && auto_dec && interval > 0 && !rate && ds_agg <= 3 && !exact && !sharded &&
-                      !ctx->opt.timing_detail;
-  const bool ug_q = ug_ls_q || ug_fap_q || ug_dev_q || ug_e_q;
-  // sharded lockstep: the ranks agree on the key before the host's round trip
-  const bool ug_agree = ug_ls_q && sharded;
-  uint64_t* u_key1 = ug_q ? scratch<uint64_t>(ctx, "u_key1", S) : nullptr;
-  uint64_t* u_key2 = ug_q ? scratch<uint64_t>(ctx, "u_key2", S) : nullptr;
-  uint64_t* u_vo = ug_q ? scratch<uint64_t>(ctx, "u_vo", S) : nullptr;
-  uint64_t* u_qo = ug_q ? scratch<uint64_t>(ctx, "u_qo", S) : nullptr;
-  uint64_t* uk_vo = ug_q ? scratch<uint64_t>(ctx, "uk_vo", S) : nullptr;
-  uint64_t* uk_qo = ug_q ? scratch<uint64_t>(ctx, "uk_qo", S) : nullptr;
-  {
-    AssembleArgs a;
-    a.span_row_start = span_row_start; a.row_base = row_base; a.row_ncells = row_ncells;
-    a.row_qual_off = row_qual_off; a.row_val_len = row_val_len; a.qual = qual;
-    a.n_spans = S; a.start = d->start_time; a.end = d->end_time; a.interval = interval;
-    a.row_ok = row_ok; a.row_cell0 = row_cell0; a.sp_ncells = sp_ncells; a.sp_first = sp_first;
-    a.sp_last = sp_last; a.sp_kept = sp_kept; a.sp_cap = sp_cap; a.sp_q1 = sp_q1;
-    a.sp_q1_shift = sp_q1s; a.sp_q1_rs = sp_q1rs; a.sp_ovf_cell = sp_ovf; a.err = &sm->err;
-    a.span0 = sharded ? d->span0 : 0;
-    a.row_val_off = row_val_off;
-    a.u_key1 = u_key1; a.u_key2 = u_key2; a.u_vo = u_vo; a.u_qo = u_qo;
-    // kept list, E offsets, counts and bounds (unsharded groups of up to
-    // KC_MAX spans: the kernel hands the call state to the host itself)
-    kept = scratch<uint32_t>(ctx, "kept", S);
-    eoff = scratch<uint64_t>(ctx, "eoff", S);
-    pub1 = S && S <= KC_MAX && !ug_agree;
-    p1 = pub1 ? next_pub(ctx, sizeof(Small)) : HostPub{};
-    KeptArgs K;
-    K.kept = sp_kept; K.cap = sp_cap; K.ncells = sp_ncells; K.n = S; K.kept_list = kept; K.eoff_k = eoff;
-    K.n_input = &sm->n_input; K.sp_first = sp_first; K.sp_last = sp_last; K.bound = sm->bound;
-    K.n_kept_out = &sm->n_kept; K.e_total_out = &sm->e_total; K.pub = p1; K.pub_src = (const uint64_t*)sm;
-    K.u_key1 = u_key1; K.u_key2 = u_key2; K.u_vo = u_vo; K.u_qo = u_qo; K.uk_vo = uk_vo; K.uk_qo = uk_qo;
-    K.ukey = sm->ukey;
-    // (the speculative aligned group's verdict: every fap query, see below)
-    K.ug_go = ug_fap_q && sharded ? &sm->ug_go : nullptr;
-    K.err = &sm->err;
-    K.ug_interval = interval;
-    // one block: assembly + kept list in one launch, for groups with few rows
-    // (the block's 16 waves walk the deferred spans: a group of long spans of
-    // many rows, C4's, needs the wave-per-span kernel's whole grid)
-    if (S && S <= 1024 && R <= 8192) {
-      LAUNCH(k_assemble_small, dim3(1), dim3(1024), 0, st, a, K);
-    } else if (S > KC_MAX && R <= 2ull * S) {
-      // (nearly) single-row spans: assembly + tile sums in one launch, then
-      // the scatter (its last block publishes the call state)
-      const uint32_t na = (S + 255) / 256, nt = (S + 1023) / 1024;  // (assembly tiles of 256, scatter tiles of 1024)
-      KeptTile* ts = scratch<KeptTile>(ctx, "kept_tiles", na);
-      ulonglong2* tke = scratch<ulonglong2>(ctx, "kept_tiles_ke", na);
-      LAUNCH(k_assemble_tiles, dim3(na), dim3(256), 0, st, a, ts, tke);
-      pub1 = !ug_agree;
+  bool auto_dec = false, ug_ls_q = false, ug_fap_q = false, ug_dev_q = false, ug_e_q = false, ug_q = false;
+  bool ug_agree = false;
+  uint64_t *u_key1 = nullptr, *u_key2 = nullptr, *u_vo = nullptr, *u_qo = nullptr, *uk_vo = nullptr, *uk_qo = nullptr;
+  // sync1, plan
+  Small h;
+  bool poisoned = false;
+  uint32_t n_kept = 0;
+  uint64_t n_input_global = 0;
+  int64_t lo = 0, hi = -1;
+  bool empty_grid = true, used_bitmap_x = false;
+  uint64_t nwords = 0;
+  uint32_t* bitmap = nullptr;
+  FapPlan fap;
+  bool fap_off = false, fap_ran = false;
+  uint64_t e_total = 0;
+  uint32_t* e_ts = nullptr;
+  int64_t* e_val = nullptr;
+  uint8_t* e_flt = nullptr;
+  uint32_t* e_len = nullptr;
+  int64_t* e_bad = nullptr;
+  DecodeArgs da;
+  // decode, grid
+  bool chunk_marked = false, direct = false, ls_try = false;
+  uint64_t* d_qoff = nullptr;
+  DirectArgs dg = {};
+  const uint32_t* mark_list = nullptr;
+  const uint32_t* mark_count = nullptr;
+  bool fap_query = false, fap_opt = false;
+  uint64_t T = 0;
+  uint32_t* word_rank = nullptr;
+  uint32_t* gridv = nullptr;
+  GridArgs ga = {};
+  // exchange_header, plan_reduce
+  bool grids_agreed = true;
+  int mode = 0;
+  bool ls_use = false;
+  LsPlan lsp = {};
+  uint64_t fstar = 0;
+  bool fap_use = false;
+  BadArgs bad;
+  bool bad_at_end = false, seq = false, int_parts = false, sliced = false, small_out = false, out_direct = false;
+  uint64_t xs = 0, To = 0;
+  uint8_t* outblk = nullptr;
+  int64_t* o_ts = nullptr;
+  int64_t* o_bits = nullptr;
+  uint8_t* o_isint = nullptr;
+  FinalArgs fin_map;
+
+  SgCall(Slot* c, const tsdbhip_sg_desc* dd, tsdbhip_sg_out* o, bool ls, bool ug)
+      : ctx(c), d(dd), out(o), ls_allow(ls), ug_allow(ug) {}
+  int run() {
+    begin();
+    assemble();
+    int rc = sync1();
+    if (rc != RC_CONTINUE) return rc;
+    plan();
+    if ((rc = uniform_try()) != RC_CONTINUE) return rc;
+    decode();
+    grid();
+    if ((rc = fap_finish()) != RC_CONTINUE) return rc;
+    exchange_header();
+    plan_reduce();
+    reduce();
+    return finish();
+  }
+
+  void begin() {
+    dev = (d->flags & TSDBHIP_DESC_DEVICE) != 0;
+    exact = (d->flags & TSDBHIP_EXACT_ORDER) != 0;
+    // (a 1-rank communicator runs the same exchange code: tests use it)
+    X = (d->flags & TSDBHIP_SHARDED) ? ctx->x : nullptr;
+    sharded = X != nullptr;
+    if (X) {
+      X->n_coll = 0;
+      X->x_bytes = 0;
+    }
+    S = d->n_spans;
+    R = d->n_rows;
+    rate = d->rate != 0;
+    agg = d->agg;
+    ds_agg = d->ds_agg;
+    interval = d->ds_interval > 0 ? d->ds_interval : 0;
+    st = ctx->stream;
+    tm = {};
+    ctx->timing_late = 0;
+    ctx->hot_kernel = TSDBHIP_HOT_NONE;
+    ctx->time_reduce = false;
+    out->n_out = 0;
+    out->n_input_points = 0;
+    out->err_code = 0;
+    out->err_index = -1;
+
+    // ---- inputs in HBM ----
+    span_row_start = stage(ctx, "in_srs", d->span_row_start, (size_t)S + 1, dev);
+    row_base = stage(ctx, "in_base", d->row_base, R, dev);
+    row_ncells = stage(ctx, "in_ncells", d->row_ncells, R, dev);
+    row_qual_off = stage(ctx, "in_qoff", d->row_qual_off, R, dev);
+    row_val_off = stage(ctx, "in_voff", d->row_val_off, R, dev);
+    row_val_len = stage(ctx, "in_vlen", d->row_val_len, R, dev);
+    qual = stage(ctx, "in_qual", d->qual_bytes, d->qual_nbytes, dev, 16);
+    val = stage(ctx, "in_val", d->val_bytes, d->val_nbytes, dev, 16);
+
+    sm = scratch<Small>(ctx, "small", 1);
+    check_clean = ctx->opt.check_clean;
+    if (check_clean && ctx->sm_ready) {  // (debug) the reset state must equal small_init()
+      Small cur, ini = small_init();
+      readback(ctx, &cur, sm, sizeof cur);
+      if (std::memcmp(&cur, &ini, sizeof cur) != 0) {
+        const uint8_t* a = (const uint8_t*)&cur; const uint8_t* b = (const uint8_t*)&ini;
+        size_t i = 0;
+        while (a[i] == b[i]) i++;
+        fprintf(stderr, "TSDBHIP_CHECK_CLEAN: call state not reset (first differing byte %zu)\n", i);
+      }
+    }
+    if (!ctx->sm_ready) {  // (a completed call leaves it reset: k_call_end)
+      const Small init = small_init();
+      std::memcpy(ctx->host_small, &init, sizeof init);
+      HIPCHK(hipMemcpyAsync(sm, ctx->host_small, sizeof init, hipMemcpyHostToDevice, st));
+    }
+    ctx->sm_ready = false;
+    bm_clean = ctx->bitmap_clean;
+    ctx->bitmap_clean = false;
+    tgd_clean = ctx->tgdone_clean;
+    ctx->tgdone_clean = false;
+    tgd_used = false;
+    detail = ctx->opt.timing_detail;  // decode / grid event pairs
+    g_ev_pend = nullptr;
+    g_ev_pend_i = -1;
+    std::memset(ctx->ev_alias, 0xff, sizeof ctx->ev_alias);
+    EV_START(ctx, 0);
+  }
+
+  void assemble() {
+    // ---- assemble ----
+    row_ok = scratch<uint8_t>(ctx, "row_ok", R);
+    row_cell0 = scratch<uint32_t>(ctx, "row_cell0", R);
+    sp_ncells = scratch<uint32_t>(ctx, "sp_ncells", S);
+    sp_first = scratch<int64_t>(ctx, "sp_first", S);
+    sp_last = scratch<int64_t>(ctx, "sp_last", S);
+    sp_kept = scratch<uint8_t>(ctx, "sp_kept", S);
+    sp_cap = scratch<uint64_t>(ctx, "sp_cap", S);
+    sp_q1 = scratch<int64_t>(ctx, "sp_q1", S);
+    sp_q1s = scratch<int32_t>(ctx, "sp_q1s", S);
+    sp_q1rs = scratch<int64_t>(ctx, "sp_q1rs", 2ull * S);
+    sp_ovf = scratch<int64_t>(ctx, "sp_ovf", S);
+    kept = nullptr;
+    eoff = nullptr;
+    pub1 = false;
+    p1 = {};
+    // the uniform path's queries (uniform_run): lockstep (no downsampling, the
+    // conditions of the general path's lockstep try) or the aligned group
+    // (downsampled exact integer aggregation); the spans' class keys are
+    // proposed at assembly for them
+    auto_dec = ctx->opt.decode == DEC_AUTO;
+    // (unsharded, lockstep "on": the group needs >= 2048 lockstep waves, and
+    // with C <= qual_nbytes / 2 cells in all and n in each of n_kept <= S
+    // spans, ceil(n / LS_TILE) * max(1, n_kept / 64) <= max(ceil(C / LS_TILE),
+    // C / (64 LS_TILE) + S / 64 + 1): a group under that bound cannot take it,
+    // and its assembly skips the key probe — C1's 100 spans: 7 us)
+    const uint64_t c_max = d->qual_nbytes / 2;
+    const bool ls_size_ok = sharded || ctx->opt.lockstep == 2 ||
+                            std::max<uint64_t>((c_max + LS_TILE - 1) / LS_TILE, c_max / (64 * LS_TILE) + S / 64 + 1) >= 2048;
+    ug_ls_q = ug_allow && auto_dec && interval == 0 && ls_allow && ctx->opt.lockstep && !exact &&
+                         (agg != TSDBHIP_AGG_DEV || rate) && ls_size_ok;
+    ug_fap_q = ug_allow && auto_dec && interval > 0 && !rate && ds_agg <= 3 && agg <= 3 && !exact &&
+                          ctx->opt.aligned_group && !ctx->opt.timing_detail;
+    // (integer dev without rate, unsharded: the sequential chains of k_ug_dev)
+    ug_dev_q = ug_allow && auto_dec && interval == 0 && !exact && agg == TSDBHIP_AGG_DEV && !rate &&
+                          !sharded;
+    // (other downsampled queries, unsharded: k_ds_reg's E on the key's buckets)
+    ug_e_q = ug_allow && auto_dec && interval > 0 && !rate && ds_agg <= 3 && !exact && !sharded &&
+                        !ctx->opt.timing_detail;
+    ug_q = ug_ls_q || ug_fap_q || ug_dev_q || ug_e_q;
+    // sharded lockstep: the ranks agree on the key before the host's round trip
+    ug_agree = ug_ls_q && sharded;
+    u_key1 = ug_q ? scratch<uint64_t>(ctx, "u_key1", S) : nullptr;
+    u_key2 = ug_q ? scratch<uint64_t>(ctx, "u_key2", S) : nullptr;
+    u_vo = ug_q ? scratch<uint64_t>(ctx, "u_vo", S) : nullptr;
+    u_qo = ug_q ? scratch<uint64_t>(ctx, "u_qo", S) : nullptr;
+    uk_vo = ug_q ? scratch<uint64_t>(ctx, "uk_vo", S) : nullptr;
+    uk_qo = ug_q ? scratch<uint64_t>(ctx, "uk_qo", S) : nullptr;
+    {
+      AssembleArgs a;
+      a.span_row_start = span_row_start; a.row_base = row_base; a.row_ncells = row_ncells;
+      a.row_qual_off = row_qual_off; a.row_val_len = row_val_len; a.qual = qual;
+      a.n_spans = S; a.start = d->start_time; a.end = d->end_time; a.interval = interval;
+      a.row_ok = row_ok; a.row_cell0 = row_cell0; a.sp_ncells = sp_ncells; a.sp_first = sp_first;
+      a.sp_last = sp_last; a.sp_kept = sp_kept; a.sp_cap = sp_cap; a.sp_q1 = sp_q1;
+      a.sp_q1_shift = sp_q1s; a.sp_q1_rs = sp_q1rs; a.sp_ovf_cell = sp_ovf; a.err = &sm->err;
+      a.span0 = sharded ? d->span0 : 0;
+      a.row_val_off = row_val_off;
+      a.u_key1 = u_key1; a.u_key2 = u_key2; a.u_vo = u_vo; a.u_qo = u_qo;
+      // kept list, E offsets, counts and bounds (unsharded groups of up to
+      // KC_MAX spans: the kernel hands the call state to the host itself)
+      kept = scratch<uint32_t>(ctx, "kept", S);
+      eoff = scratch<uint64_t>(ctx, "eoff", S);
+      pub1 = S && S <= KC_MAX && !ug_agree;
       p1 = pub1 ? next_pub(ctx, sizeof(Small)) : HostPub{};
-      LAUNCH(k_kept_scatter_tiles, dim3(nt), dim3(256), 0, st, sp_kept, sp_cap, S, (const KeptTile*)ts,
-             (const ulonglong2*)tke, 4u, na, kept, eoff, &sm->n_input, sm->bound, &sm->n_kept, &sm->e_total, p1,
-             (const uint64_t*)sm, K);
-    } else if (S) {  // thread per span, then a wave per span for the ones it queued
-      uint32_t* alist = scratch<uint32_t>(ctx, "asm_list", S);
-      uint32_t* acount = &sm->cnt[0];
-      LAUNCH(k_assemble_fast, dim3(grid_for(S, 256)), dim3(256), 0, st, a, alist, acount);
-      LAUNCH(k_assemble, dim3(grid_for(S, 4, 4096)), dim3(256), 0, st, a, (const uint32_t*)alist,
-                         (const uint32_t*)acount);
-      if (S <= KC_MAX) {
-        LAUNCH(k_kept_compact, dim3(1), dim3(1024), 0, st, K);
-      } else {  // bigger groups: tile sums, then per-tile offsets + scatter
-        const uint32_t nt = (S + 1023) / 1024;
-        KeptTile* ts = scratch<KeptTile>(ctx, "kept_tiles", nt);
-        ulonglong2* tke = scratch<ulonglong2>(ctx, "kept_tiles_ke", nt);
-        LAUNCH(k_kept_tiles, dim3(nt), dim3(256), 0, st, sp_kept, sp_cap, sp_ncells, sp_first, sp_last, S, ts, tke,
-               (const uint64_t*)u_key1, (const uint64_t*)u_key2);
-        // (its last block publishes the call state)
+      KeptArgs K;
+      K.kept = sp_kept; K.cap = sp_cap; K.ncells = sp_ncells; K.n = S; K.kept_list = kept; K.eoff_k = eoff;
+      K.n_input = &sm->n_input; K.sp_first = sp_first; K.sp_last = sp_last; K.bound = sm->bound;
+      K.n_kept_out = &sm->n_kept; K.e_total_out = &sm->e_total; K.pub = p1; K.pub_src = (const uint64_t*)sm;
+      K.u_key1 = u_key1; K.u_key2 = u_key2; K.u_vo = u_vo; K.u_qo = u_qo; K.uk_vo = uk_vo; K.uk_qo = uk_qo;
+      K.ukey = sm->ukey;
+      // (the speculative aligned group's verdict: every fap query, see below)
+      K.ug_go = ug_fap_q && sharded ? &sm->ug_go : nullptr;
+      K.err = &sm->err;
+      K.ug_interval = interval;
+      // one block: assembly + kept list in one launch, for groups with few rows
+      // (the block's 16 waves walk the deferred spans: a group of long spans of
+      // many rows, C4's, needs the wave-per-span kernel's whole grid)
+      if (S && S <= 1024 && R <= 8192) {
+        LAUNCH(k_assemble_small, dim3(1), dim3(1024), 0, st, a, K);
+      } else if (S > KC_MAX && R <= 2ull * S) {
+        // (nearly) single-row spans: assembly + tile sums in one launch, then
+        // the scatter (its last block publishes the call state)
+        const uint32_t na = (S + 255) / 256, nt = (S + 1023) / 1024;  // (assembly tiles of 256, scatter tiles of 1024)
+        KeptTile* ts = scratch<KeptTile>(ctx, "kept_tiles", na);
+        ulonglong2* tke = scratch<ulonglong2>(ctx, "kept_tiles_ke", na);
+        LAUNCH(k_assemble_tiles, dim3(na), dim3(256), 0, st, a, ts, tke);
         pub1 = !ug_agree;
         p1 = pub1 ? next_pub(ctx, sizeof(Small)) : HostPub{};
         LAUNCH(k_kept_scatter_tiles, dim3(nt), dim3(256), 0, st, sp_kept, sp_cap, S, (const KeptTile*)ts,
-               (const ulonglong2*)tke, 1u, nt, kept, eoff, &sm->n_input, sm->bound, &sm->n_kept, &sm->e_total, p1,
+               (const ulonglong2*)tke, 4u, na, kept, eoff, &sm->n_input, sm->bound, &sm->n_kept, &sm->e_total, p1,
                (const uint64_t*)sm, K);
+      } else if (S) {  // thread per span, then a wave per span for the ones it queued
+        uint32_t* alist = scratch<uint32_t>(ctx, "asm_list", S);
+        uint32_t* acount = &sm->cnt[0];
+        LAUNCH(k_assemble_fast, dim3(grid_for(S, 256)), dim3(256), 0, st, a, alist, acount);
+        LAUNCH(k_assemble, dim3(grid_for(S, 4, 4096)), dim3(256), 0, st, a, (const uint32_t*)alist,
+                           (const uint32_t*)acount);
+        if (S <= KC_MAX) {
+          LAUNCH(k_kept_compact, dim3(1), dim3(1024), 0, st, K);
+        } else {  // bigger groups: tile sums, then per-tile offsets + scatter
+          const uint32_t nt = (S + 1023) / 1024;
+          KeptTile* ts = scratch<KeptTile>(ctx, "kept_tiles", nt);
+          ulonglong2* tke = scratch<ulonglong2>(ctx, "kept_tiles_ke", nt);
+          LAUNCH(k_kept_tiles, dim3(nt), dim3(256), 0, st, sp_kept, sp_cap, sp_ncells, sp_first, sp_last, S, ts, tke,
+                 (const uint64_t*)u_key1, (const uint64_t*)u_key2);
+          // (its last block publishes the call state)
+          pub1 = !ug_agree;
+          p1 = pub1 ? next_pub(ctx, sizeof(Small)) : HostPub{};
+          LAUNCH(k_kept_scatter_tiles, dim3(nt), dim3(256), 0, st, sp_kept, sp_cap, S, (const KeptTile*)ts,
+                 (const ulonglong2*)tke, 1u, nt, kept, eoff, &sm->n_input, sm->bound, &sm->n_kept, &sm->e_total, p1,
+                 (const uint64_t*)sm, K);
+        }
       }
     }
   }
-  // (sharded: no collective here. Each rank builds its grid on its own
-  // bounds; one collective after the local grids tells whether they agree,
-  // and only when they do not are the bitmaps remapped and exchanged.)
-  Small h;
-  if (ug_agree) {
-    // the uniform path's key agreement (sharded lockstep queries, every rank):
-    // the first error, the fewest kept spans and the keys' [min, max] over
-    // the ranks, one MIN allreduce into Small.xh[0..5]
-    const XField ag[6] = {{&sm->err, 5, 0},     {&sm->n_kept, 5, 0},  {&sm->ukey[0], 5, 0},
-                          {&sm->ukey[1], 6, 0}, {&sm->ukey[2], 5, 0}, {&sm->ukey[3], 6, 0}};
-    const XMove m = xchg_desc(ctx, ag, 6, (uint64_t*)sm->xh);
-    LAUNCH(k_xmove, dim3(1), dim3(64), 0, st, m);
-    X->group_start(ctx);
-    X->allreduce(ctx, m.buf, 6, X_U64, X_MIN);
-    X->group_end(ctx);
-  }
-  // the speculative aligned group (sharded downsampled integer sum / min /
-  // max / avg): k_ug_ds_reg launched now, over every span slot, its blocks
-  // reading the kept-list kernel's verdict (Small.ug_go) and the key from the
-  // call state; the one collective group and the finish follow — no host
-  // round trip before the call's end. Every rank, whatever its shard (the
-  // collectives are everyone's). It saves ~35 us of a 0.94 ms C3* 8-way
-  // shard step; unsharded, a launch that finds no group cost C2 ~10 us and
-  // C3*'s own gained nothing measurable (same-box A/Bs, round 5), so the
-  // unsharded aligned group waits for the round trip below.
-  if (ug_fap_q && sharded) {
-    DecodeArgs sa;
-    std::memset(&sa, 0, sizeof sa);
-    sa.span_row_start = span_row_start; sa.row_base = row_base; sa.row_qual_off = row_qual_off;
-    sa.row_val_off = row_val_off; sa.qual = qual; sa.val = val; sa.row_ok = row_ok; sa.row_cell0 = row_cell0;
-    sa.kept = kept; sa.n_kept = 0; sa.sp_ncells = sp_ncells; sa.sp_q1 = sp_q1; sa.sp_q1_shift = sp_q1s;
-    sa.sp_q1_rs = sp_q1rs; sa.row_ncells = row_ncells; sa.row_val_len = row_val_len; sa.sp_ovf_cell = sp_ovf;
-    sa.sp_cap = sp_cap; sa.e_off = eoff; sa.start = d->start_time; sa.end = d->end_time; sa.interval = interval;
-    sa.ds_agg = ds_agg; sa.rate = rate; sa.err = &sm->err; sa.gflags = sm->gflags; sa.range = sm->range;
-    sa.fstar = &sm->fstar; sa.span0 = d->span0; sa.sp_first = sp_first;
-    UgIn u = {};
-    u.d = d; u.X = X; u.sm = sm; u.da = sa; u.row_ncells = row_ncells; u.row_val_len = row_val_len;
-    u.n_kept = S; u.lockstep = false; u.mine = S > 0; u.spec = true;
-    const int rc = uniform_run(ctx, u, out, tm);
-    ctx->bitmap_clean = bm_clean;  // (no bitmap touched)
-    ctx->tgdone_clean = tgd_clean;
-    return rc;
-  }
-  if (!pub1) {  // (the state's last writer cannot publish it: a one-wave kernel does)
-    p1 = next_pub(ctx, sizeof(Small));
-    LAUNCH(k_publish, dim3(1), dim3(64), 0, st, p1, (const uint64_t*)sm);
-  }
-  wait_pub(ctx, p1, &h, sizeof h);  // sync 1
-  // a rank whose own scan failed still takes part in the agreement below (its
-  // peers wait there for it), with nothing kept; every rank throws after it
-  const bool poisoned = h.err != ERR_NONE;
-  if (poisoned && !sharded) throw Fail{err_code(h.err)};
-  const uint32_t n_kept = poisoned ? 0u : (uint32_t)h.n_kept;
-  out->n_input_points = h.n_input;
-  uint64_t n_input_global = h.n_input;
 
-  // ---- union-grid bitmap range: every E point lies in [first, last] of its
-  // span and in [start, ...]; G keeps those <= end (SURVEY.md §8a closed form).
-  // A kept span has first <= end and last >= start, so [lo, hi] is non-empty
-  // whenever some span (of this rank) is kept.
-  int64_t lo = std::max<int64_t>(d->start_time, h.bound[0] == ~0ull ? INT64_MAX : (int64_t)h.bound[0]);
-  int64_t hi = std::min<int64_t>(d->end_time, (int64_t)h.bound[1]);
-  if (h.bound[0] == ~0ull || poisoned) hi = -1;
-  bool empty_grid = lo > hi;
-  uint64_t nwords = empty_grid ? 0 : (uint64_t)(hi - lo + 1 + 31) / 32;
-  // (zero on entry without a memset: the last call's k_call_end cleared it)
-  uint32_t* bitmap = empty_grid ? nullptr : scratch_zero_kept<uint32_t>(ctx, "gbitmap", nwords, bm_clean);
-  bool used_bitmap_x = false;  // (sharded, grids not agreed: the global bitmap is "gbitmap_x")
-  if (check_clean && bitmap) {  // (debug) the bitmap must be zero on entry
-    unsigned long long* cnt = scratch<unsigned long long>(ctx, "chk_cnt", 1, true);
-    const uint64_t nall = ctx->bufs["gbitmap"].n / 4;
-    LAUNCH(k_count_nonzero, dim3(grid_for(nall, 256, 1024)), dim3(256), 0, st, bitmap, nall, cnt);
-    unsigned long long nz = 0;
-    readback(ctx, &nz, cnt, 8);
-    if (nz) fprintf(stderr, "TSDBHIP_CHECK_CLEAN: %llu non-zero bitmap words on entry (clean=%d, nwords=%llu)\n", nz,
-                    (int)bm_clean, (unsigned long long)nwords);
-  }
-
-  // ---- aligned-group reduction (k_ds_reg.hip FapArgs): tried when every
-  // kept span has the same first and last timestamp (Small.bound), the group
-  // downsamples, and the aggregation is exact integer (no rate, no dev) ----
-  FapPlan fap;
-  fap.a.op = -1;
-  const bool fap_off = !ctx->opt.aligned_group;
-  if (!fap_off && interval > 0 && !rate && ds_agg <= 3 && agg <= 3 && !(sharded && exact) && n_kept > 0 &&
-      h.bound[0] == h.bound[2] && h.bound[1] == h.bound[3] && h.bound[1] - h.bound[0] <= 62ull * (uint64_t)interval) {
-    // (at most 64 buckets a span: a partial row holds them)
-    fap.a.op = agg == TSDBHIP_AGG_MIN ? 1 : (agg == TSDBHIP_AGG_MAX ? 2 : 0);
-    fap.a.key = sm->fap_key;
-    fap.a.broken = &sm->fap_broken;
-  }
-  bool fap_ran = false;
-
-  // ---- decode (+ downsample) ----
-  const uint64_t e_total = h.e_total;
-  uint32_t* e_ts = scratch<uint32_t>(ctx, "e_ts", e_total);
-  int64_t* e_val = scratch<int64_t>(ctx, "e_val", e_total);
-  uint8_t* e_flt = scratch<uint8_t>(ctx, "e_flt", e_total);
-  uint32_t* e_len = scratch<uint32_t>(ctx, "e_len", n_kept);
-  int64_t* e_bad = scratch<int64_t>(ctx, "e_bad", n_kept);
-  DecodeArgs da;
-  da.span_row_start = span_row_start; da.row_base = row_base; da.row_qual_off = row_qual_off;
-  da.row_val_off = row_val_off; da.qual = qual; da.val = val; da.row_ok = row_ok; da.row_cell0 = row_cell0;
-  da.kept = kept; da.n_kept = n_kept; da.sp_ncells = sp_ncells; da.sp_q1 = sp_q1; da.sp_q1_shift = sp_q1s;
-  da.sp_q1_rs = sp_q1rs; da.row_ncells = row_ncells; da.row_val_len = row_val_len;
-  da.sp_ovf_cell = sp_ovf; da.sp_cap = sp_cap; da.e_off = eoff; da.e_ts = e_ts; da.e_val = e_val;
-  da.e_flt = e_flt; da.e_len = e_len; da.e_bad = e_bad; da.start = d->start_time; da.end = d->end_time;
-  da.interval = interval; da.ds_agg = ds_agg; da.rate = rate; da.err = &sm->err; da.gflags = sm->gflags;
-  da.range = sm->range; da.fstar = &sm->fstar; da.span0 = sharded ? d->span0 : 0; da.sp_first = sp_first;
-  // ---- the uniform path (uniform_run): every kept span proposed one class key
-  if (ug_q) {
-    UgIn u = {};
-    u.d = d; u.X = X; u.sm = sm; u.da = da; u.row_ncells = row_ncells; u.row_val_len = row_val_len;
-    u.uk_vo = uk_vo; u.uk_qo = uk_qo; u.n_kept = n_kept;
-    bool take = false;
-    const bool local_ok = !poisoned && n_kept > 0 && h.ukey[0] != ~0ull && h.ukey[0] == h.ukey[1] &&
-                          h.ukey[2] == h.ukey[3] && (uint32_t)h.ukey[0] >= 64;
-    // (k_lockstep and k_ug_dev read one row a span: k2 bit 16 clear)
-    const bool one_row = !(h.ukey[2] & 0x10000u);
-    if (ug_dev_q) {
-      u.lockstep = true;
-      u.dev = true;
-      u.k1 = h.ukey[0];
-      u.k2 = h.ukey[2];
-      take = local_ok && one_row && !(u.k2 & 8u);  // (integer cells)
-    } else if (ug_ls_q) {
-      u.lockstep = true;
-      if (sharded) {  // (from the agreed words alone: every rank takes the same branch)
-        const unsigned long long* x = h.xh;
-        take = x[0] == ERR_NONE && x[1] > 0 && x[2] != ~0ull && x[2] == ~x[3] && x[4] == ~x[5] &&
-               (uint32_t)x[2] >= 64 && !(x[4] & 0x10000u);
-        u.k1 = x[2];
-        u.k2 = x[4];
-      } else {
-        const uint32_t n = (uint32_t)h.ukey[0];
-        const uint64_t ls_waves = (n + LS_TILE - 1) / LS_TILE * std::max<uint64_t>(1, n_kept / 64);
-        take = local_ok && one_row && (ctx->opt.lockstep == 2 || ls_waves >= 2048);
-        u.k1 = h.ukey[0];
-        u.k2 = h.ukey[2];
-      }
-    } else {
-      u.lockstep = false;
-      u.k1 = h.ukey[0];
-      u.k2 = h.ukey[2];
-      const uint32_t step = (uint32_t)(u.k2 >> 32), n = (uint32_t)u.k1;
-      const uint64_t kk = step ? ((uint64_t)interval + step - 1) / step : 0;
-      const bool fits = local_ok && !(u.k2 & 8u) && kk && (n + kk - 1) / kk <= WAVE;
-      if (ug_fap_q && (sharded || fits)) {
-        // (sharded: every rank makes the attempt, the key and the validity
-        // agreed in its one collective group; unsharded: only a group that is one)
-        u.mine = fits;
-        take = true;
-      } else if (ug_e_q && local_ok && kk) {
-        u.e = true;
-        take = true;
-      }
+  int sync1() {
+    // (sharded: no collective here. Each rank builds its grid on its own
+    // bounds; one collective after the local grids tells whether they agree,
+    // and only when they do not are the bitmaps remapped and exchanged.)
+    if (ug_agree) {
+      // the uniform path's key agreement (sharded lockstep queries, every rank):
+      // the first error, the fewest kept spans and the keys' [min, max] over
+      // the ranks, one MIN allreduce into Small.xh[0..5]
+      const XField ag[6] = {{&sm->err, 5, 0},     {&sm->n_kept, 5, 0},  {&sm->ukey[0], 5, 0},
+                            {&sm->ukey[1], 6, 0}, {&sm->ukey[2], 5, 0}, {&sm->ukey[3], 6, 0}};
+      const XMove m = xchg_desc(ctx, ag, 6, (uint64_t*)sm->xh);
+      LAUNCH(k_xmove, dim3(1), dim3(64), 0, st, m);
+      X->group_start(ctx);
+      X->allreduce(ctx, m.buf, 6, X_U64, X_MIN);
+      X->group_end(ctx);
     }
-    if (take) {
+    // the speculative aligned group (sharded downsampled integer sum / min /
+    // max / avg): k_ug_ds_reg launched now, over every span slot, its blocks
+    // reading the kept-list kernel's verdict (Small.ug_go) and the key from the
+    // call state; the one collective group and the finish follow — no host
+    // round trip before the call's end. Every rank, whatever its shard (the
+    // collectives are everyone's). It saves ~35 us of a 0.94 ms C3* 8-way
+    // shard step; unsharded, a launch that finds no group cost C2 ~10 us and
+    // C3*'s own gained nothing measurable (same-box A/Bs, round 5), so the
+    // unsharded aligned group waits for the round trip below.
+    if (ug_fap_q && sharded) {
+      DecodeArgs sa;
+      std::memset(&sa, 0, sizeof sa);
+      sa.span_row_start = span_row_start; sa.row_base = row_base; sa.row_qual_off = row_qual_off;
+      sa.row_val_off = row_val_off; sa.qual = qual; sa.val = val; sa.row_ok = row_ok; sa.row_cell0 = row_cell0;
+      sa.kept = kept; sa.n_kept = 0; sa.sp_ncells = sp_ncells; sa.sp_q1 = sp_q1; sa.sp_q1_shift = sp_q1s;
+      sa.sp_q1_rs = sp_q1rs; sa.row_ncells = row_ncells; sa.row_val_len = row_val_len; sa.sp_ovf_cell = sp_ovf;
+      sa.sp_cap = sp_cap; sa.e_off = eoff; sa.start = d->start_time; sa.end = d->end_time; sa.interval = interval;
+      sa.ds_agg = ds_agg; sa.rate = rate; sa.err = &sm->err; sa.gflags = sm->gflags; sa.range = sm->range;
+      sa.fstar = &sm->fstar; sa.span0 = d->span0; sa.sp_first = sp_first;
+      UgIn u = {};
+      u.d = d; u.X = X; u.sm = sm; u.da = sa; u.row_ncells = row_ncells; u.row_val_len = row_val_len;
+      u.n_kept = S; u.lockstep = false; u.mine = S > 0; u.spec = true;
       const int rc = uniform_run(ctx, u, out, tm);
-      // (no bitmap was touched: it is as clean as scratch_zero_kept left it)
-      ctx->bitmap_clean = bm_clean || bitmap != nullptr;
+      ctx->bitmap_clean = bm_clean;  // (no bitmap touched)
       ctx->tgdone_clean = tgd_clean;
       return rc;
     }
+    if (!pub1) {  // (the state's last writer cannot publish it: a one-wave kernel does)
+      p1 = next_pub(ctx, sizeof(Small));
+      LAUNCH(k_publish, dim3(1), dim3(64), 0, st, p1, (const uint64_t*)sm);
+    }
+    wait_pub(ctx, p1, &h, sizeof h);  // sync 1
+    // a rank whose own scan failed still takes part in the agreement below (its
+    // peers wait there for it), with nothing kept; every rank throws after it
+    poisoned = h.err != ERR_NONE;
+    if (poisoned && !sharded) throw Fail{err_code(h.err)};
+    n_kept = poisoned ? 0u : (uint32_t)h.n_kept;
+    out->n_input_points = h.n_input;
+    n_input_global = h.n_input;
+    return RC_CONTINUE;
   }
-  if (detail) HIPCHK(hipEventRecord(ctx->ev[1], st));
-  bool chunk_marked = false;     // k_ds_spans marked G for the spans it took
-  bool direct = false;           // k_direct_scan took the no-downsampling path
-  bool ls_try = false;           // k_direct_opt made the lockstep proposal
-  uint64_t* d_qoff = nullptr;    // (its per-span qualifier offsets)
-  DirectArgs dg = {};
-  const uint32_t* mark_list = nullptr, *mark_count = nullptr;
-  if (n_kept) {
-    const unsigned blocks = grid_for(n_kept, 4, 65536);
-    // wide rows (the reference's hourly compacted rows) take the streaming
-    // kernels; rows of a few cells (sparse series) the general one. With
-    // downsampling, regular-cadence integer spans go chunk-parallel first.
-    const int force = ctx->opt.decode;
-    bool fast = R > 0 && h.n_input / R >= 64;
-    bool chunks = fast;
-    direct = fast && interval == 0 && bitmap != nullptr;
-    if (force == DEC_GENERAL) fast = chunks = direct = false;
-    if (force == DEC_FAST) { fast = true; chunks = direct = false; }
-    if (force == DEC_CHUNKS) { fast = chunks = true; direct = false; }
-    // "spans": the chain-proved downsampler alone (k_ds_spans, no k_ds_reg first)
-    const bool use_reg = force != DEC_SPANS;
-    if (!use_reg) { fast = chunks = true; direct = false; }
-    if (force == DEC_DIRECT) { fast = chunks = true; direct = interval == 0 && bitmap != nullptr; }
-    da.fb_list = scratch<uint32_t>(ctx, "fb_list", n_kept);
-    da.fb_count = &sm->cnt[1];
-    da.use_fb = 0;
-    da.span_list = nullptr;
-    da.span_count = nullptr;
-    DecodeArgs ga = da;  // spans the streaming kernels hand to the general ones
-    ga.use_fb = 1;
-    ctx->hot_kernel = fast ? TSDBHIP_HOT_DECODE_FAST : TSDBHIP_HOT_DECODE_GEN;
-    if (!direct) EV_START(ctx, 8);
-    if (!fast) {
-      // (spans of many short rows, C4: a block per span decodes its rows in
-      // parallel; else a wave per span walks them)
-      if (interval == 0 && R >= 64ull * n_kept) LAUNCH(k_decode_rows, dim3(n_kept), dim3(DR_THREADS), 0, st, da);
-      else if (interval == 0) LAUNCH(k_decode_nods, dim3(blocks), dim3(256), 0, st, da);
-      else launch_agg<LaunchGeneralDs>(ds_agg, ctx, blocks, da);
-      HIPCHK(hipEventRecord(ctx->ev[9], st));
-    } else if (interval == 0) {
-      DecodeArgs fa = da;
-      if (direct) {
-        // regular-cadence spans on consecutive grid ranks skip E (k_direct.hip)
-        dg.info = scratch<uint32_t>(ctx, "d_info", n_kept);
-        dg.n = scratch<uint32_t>(ctx, "d_n", n_kept);
-        dg.x0 = scratch<uint32_t>(ctx, "d_x0", n_kept);
-        dg.step = scratch<uint32_t>(ctx, "d_step", n_kept);
-        dg.voff = scratch<uint64_t>(ctx, "d_voff", n_kept);
-        dg.c0 = scratch<uint32_t>(ctx, "d_c0", n_kept);
-        dg.r0 = scratch<uint64_t>(ctx, "d_r0", n_kept);
-        dg.ga = scratch<uint32_t>(ctx, "d_ga", n_kept);
-        dg.row_cpre = scratch<uint32_t>(ctx, "row_cpre", R);
-        dg.list = scratch<uint32_t>(ctx, "d_list", n_kept);
-        dg.list_count = &sm->cnt[2];
-        dg.bitmap = bitmap;
-        dg.lo = lo;
-        dg.hi = hi;
-        dg.rate = rate;
-        ctx->hot_kernel = TSDBHIP_HOT_REDUCE_DIRECT;  // timed around k_reduce
-        // (spans per wave: 32 for big groups; fewer below ~64k spans, so a
-        // small group still spreads over ~2048 waves instead of a handful)
-        dg.batch = std::max<uint32_t>(1, std::min<uint32_t>(DIRB, n_kept / 2048));
-        // the lockstep proposal (k_lockstep.hip), where the reduce is not the
-        // span-ordered pass (EXACT_ORDER, integer dev): three qualifiers a
-        // span now, every other one proven by k_lockstep as it reduces
-        // Unsharded, only when k_lockstep gets >= 2048 waves (LS_TILE grid
-        // points x >= 64 spans each, the points per span estimated from the
-        // input): C1's 100 spans made 8 waves (38 us) where k_reduce takes
-        // 11 us. (Sharded: every rank alike, whatever its shard.)
-        const uint64_t ls_waves = (h.n_input / n_kept + LS_TILE - 1) / LS_TILE * std::max<uint64_t>(1, n_kept / 64);
-        ls_try = ls_allow && ctx->opt.lockstep && !exact && (agg != TSDBHIP_AGG_DEV || rate) &&
-                 (ctx->opt.lockstep == 2 || sharded || ls_waves >= 2048);
-        if (ls_try) {
-          d_qoff = scratch<uint64_t>(ctx, "d_qoff", n_kept);
-          dg.ls_key = sm->ls_key;
-          dg.ls_other = &sm->cnt[5];
-          LAUNCH(k_direct_opt, dim3(grid_for(n_kept, 256)), dim3(256), 0, st, da, dg, row_ncells,
-                             row_val_len, d_qoff, sm->ls_key, &sm->cnt[5]);
+
+  void plan() {
+    // ---- union-grid bitmap range: every E point lies in [first, last] of its
+    // span and in [start, ...]; G keeps those <= end (SURVEY.md §8a closed form).
+    // A kept span has first <= end and last >= start, so [lo, hi] is non-empty
+    // whenever some span (of this rank) is kept.
+    lo = std::max<int64_t>(d->start_time, h.bound[0] == ~0ull ? INT64_MAX : (int64_t)h.bound[0]);
+    hi = std::min<int64_t>(d->end_time, (int64_t)h.bound[1]);
+    if (h.bound[0] == ~0ull || poisoned) hi = -1;
+    empty_grid = lo > hi;
+    nwords = empty_grid ? 0 : (uint64_t)(hi - lo + 1 + 31) / 32;
+    // (zero on entry without a memset: the last call's k_call_end cleared it)
+    bitmap = empty_grid ? nullptr : scratch_zero_kept<uint32_t>(ctx, "gbitmap", nwords, bm_clean);
+    used_bitmap_x = false;  // (sharded, grids not agreed: the global bitmap is "gbitmap_x")
+    if (check_clean && bitmap) {  // (debug) the bitmap must be zero on entry
+      unsigned long long* cnt = scratch<unsigned long long>(ctx, "chk_cnt", 1, true);
+      const uint64_t nall = ctx->bufs["gbitmap"].n / 4;
+      LAUNCH(k_count_nonzero, dim3(grid_for(nall, 256, 1024)), dim3(256), 0, st, bitmap, nall, cnt);
+      unsigned long long nz = 0;
+      readback(ctx, &nz, cnt, 8);
+      if (nz) fprintf(stderr, "TSDBHIP_CHECK_CLEAN: %llu non-zero bitmap words on entry (clean=%d, nwords=%llu)\n", nz,
+                      (int)bm_clean, (unsigned long long)nwords);
+    }
+
+    // ---- aligned-group reduction (k_ds_reg.hip FapArgs): tried when every
+    // kept span has the same first and last timestamp (Small.bound), the group
+    // downsamples, and the aggregation is exact integer (no rate, no dev) ----
+    fap.a.op = -1;
+    fap_off = !ctx->opt.aligned_group;
+    if (!fap_off && interval > 0 && !rate && ds_agg <= 3 && agg <= 3 && !(sharded && exact) && n_kept > 0 &&
+        h.bound[0] == h.bound[2] && h.bound[1] == h.bound[3] && h.bound[1] - h.bound[0] <= 62ull * (uint64_t)interval) {
+      // (at most 64 buckets a span: a partial row holds them)
+      fap.a.op = agg == TSDBHIP_AGG_MIN ? 1 : (agg == TSDBHIP_AGG_MAX ? 2 : 0);
+      fap.a.key = sm->fap_key;
+      fap.a.broken = &sm->fap_broken;
+    }
+    fap_ran = false;
+
+    // ---- decode (+ downsample) ----
+    e_total = h.e_total;
+    e_ts = scratch<uint32_t>(ctx, "e_ts", e_total);
+    e_val = scratch<int64_t>(ctx, "e_val", e_total);
+    e_flt = scratch<uint8_t>(ctx, "e_flt", e_total);
+    e_len = scratch<uint32_t>(ctx, "e_len", n_kept);
+    e_bad = scratch<int64_t>(ctx, "e_bad", n_kept);
+    da.span_row_start = span_row_start; da.row_base = row_base; da.row_qual_off = row_qual_off;
+    da.row_val_off = row_val_off; da.qual = qual; da.val = val; da.row_ok = row_ok; da.row_cell0 = row_cell0;
+    da.kept = kept; da.n_kept = n_kept; da.sp_ncells = sp_ncells; da.sp_q1 = sp_q1; da.sp_q1_shift = sp_q1s;
+    da.sp_q1_rs = sp_q1rs; da.row_ncells = row_ncells; da.row_val_len = row_val_len;
+    da.sp_ovf_cell = sp_ovf; da.sp_cap = sp_cap; da.e_off = eoff; da.e_ts = e_ts; da.e_val = e_val;
+    da.e_flt = e_flt; da.e_len = e_len; da.e_bad = e_bad; da.start = d->start_time; da.end = d->end_time;
+    da.interval = interval; da.ds_agg = ds_agg; da.rate = rate; da.err = &sm->err; da.gflags = sm->gflags;
+    da.range = sm->range; da.fstar = &sm->fstar; da.span0 = sharded ? d->span0 : 0; da.sp_first = sp_first;
+  }
+
+  int uniform_try() {
+    // ---- the uniform path (uniform_run): every kept span proposed one class key
+    if (ug_q) {
+      UgIn u = {};
+      u.d = d; u.X = X; u.sm = sm; u.da = da; u.row_ncells = row_ncells; u.row_val_len = row_val_len;
+      u.uk_vo = uk_vo; u.uk_qo = uk_qo; u.n_kept = n_kept;
+      bool take = false;
+      const bool local_ok = !poisoned && n_kept > 0 && h.ukey[0] != ~0ull && h.ukey[0] == h.ukey[1] &&
+                            h.ukey[2] == h.ukey[3] && (uint32_t)h.ukey[0] >= 64;
+      // (k_lockstep and k_ug_dev read one row a span: k2 bit 16 clear)
+      const bool one_row = !(h.ukey[2] & 0x10000u);
+      if (ug_dev_q) {
+        u.lockstep = true;
+        u.dev = true;
+        u.k1 = h.ukey[0];
+        u.k2 = h.ukey[2];
+        take = local_ok && one_row && !(u.k2 & 8u);  // (integer cells)
+      } else if (ug_ls_q) {
+        u.lockstep = true;
+        if (sharded) {  // (from the agreed words alone: every rank takes the same branch)
+          const unsigned long long* x = h.xh;
+          take = x[0] == ERR_NONE && x[1] > 0 && x[2] != ~0ull && x[2] == ~x[3] && x[4] == ~x[5] &&
+                 (uint32_t)x[2] >= 64 && !(x[4] & 0x10000u);
+          u.k1 = x[2];
+          u.k2 = x[4];
+        } else {
+          const uint32_t n = (uint32_t)h.ukey[0];
+          const uint64_t ls_waves = (n + LS_TILE - 1) / LS_TILE * std::max<uint64_t>(1, n_kept / 64);
+          take = local_ok && one_row && (ctx->opt.lockstep == 2 || ls_waves >= 2048);
+          u.k1 = h.ukey[0];
+          u.k2 = h.ukey[2];
         }
-        LAUNCH(k_direct_scan, dim3(grid_for(n_kept, 4 * dg.batch, 1u << 20)), dim3(256), 0, st, da, dg,
-                           row_ncells, row_val_len);
-        fa.span_list = dg.list;
-        fa.span_count = dg.list_count;
-        mark_list = dg.list;
-        mark_count = dg.list_count;
-      }
-      if (fa.span_list) {  // (the direct scan's leftovers: general code inline)
-        LAUNCH((k_decode_fast<0, false, true>), dim3(std::min(blocks, 1024u)), dim3(256), 0, st, fa,
-                           row_ncells, row_val_len);
       } else {
-        LAUNCH((k_decode_fast<0, false>), dim3(blocks), dim3(256), 0, st, fa, row_ncells, row_val_len);
+        u.lockstep = false;
+        u.k1 = h.ukey[0];
+        u.k2 = h.ukey[2];
+        const uint32_t step = (uint32_t)(u.k2 >> 32), n = (uint32_t)u.k1;
+        const uint64_t kk = step ? ((uint64_t)interval + step - 1) / step : 0;
+        const bool fits = local_ok && !(u.k2 & 8u) && kk && (n + kk - 1) / kk <= WAVE;
+        if (ug_fap_q && (sharded || fits)) {
+          // (sharded: every rank makes the attempt, the key and the validity
+          // agreed in its one collective group; unsharded: only a group that is one)
+          u.mine = fits;
+          take = true;
+        } else if (ug_e_q && local_ok && kk) {
+          u.e = true;
+          take = true;
+        }
+      }
+      if (take) {
+        const int rc = uniform_run(ctx, u, out, tm);
+        // (no bitmap was touched: it is as clean as scratch_zero_kept left it)
+        ctx->bitmap_clean = bm_clean || bitmap != nullptr;
+        ctx->tgdone_clean = tgd_clean;
+        return rc;
+      }
+    }
+    return RC_CONTINUE;
+  }
+
+  void decode() {
+    if (detail) HIPCHK(hipEventRecord(ctx->ev[1], st));
+    chunk_marked = false;     // k_ds_spans marked G for the spans it took
+    direct = false;           // k_direct_scan took the no-downsampling path
+    ls_try = false;           // k_direct_opt made the lockstep proposal
+    d_qoff = nullptr;    // (its per-span qualifier offsets)
+    dg = {};
+    mark_list = nullptr;
+    mark_count = nullptr;
+    if (n_kept) {
+      const unsigned blocks = grid_for(n_kept, 4, 65536);
+      // wide rows (the reference's hourly compacted rows) take the streaming
+      // kernels; rows of a few cells (sparse series) the general one. With
+      // downsampling, regular-cadence integer spans go chunk-parallel first.
+      const int force = ctx->opt.decode;
+      bool fast = R > 0 && h.n_input / R >= 64;
+      bool chunks = fast;
+      direct = fast && interval == 0 && bitmap != nullptr;
+      if (force == DEC_GENERAL) fast = chunks = direct = false;
+      if (force == DEC_FAST) { fast = true; chunks = direct = false; }
+      if (force == DEC_CHUNKS) { fast = chunks = true; direct = false; }
+      // "spans": the chain-proved downsampler alone (k_ds_spans, no k_ds_reg first)
+      const bool use_reg = force != DEC_SPANS;
+      if (!use_reg) { fast = chunks = true; direct = false; }
+      if (force == DEC_DIRECT) { fast = chunks = true; direct = interval == 0 && bitmap != nullptr; }
+      da.fb_list = scratch<uint32_t>(ctx, "fb_list", n_kept);
+      da.fb_count = &sm->cnt[1];
+      da.use_fb = 0;
+      da.span_list = nullptr;
+      da.span_count = nullptr;
+      DecodeArgs ga = da;  // spans the streaming kernels hand to the general ones
+      ga.use_fb = 1;
+      ctx->hot_kernel = fast ? TSDBHIP_HOT_DECODE_FAST : TSDBHIP_HOT_DECODE_GEN;
+      if (!direct) EV_START(ctx, 8);
+      if (!fast) {
+        // (spans of many short rows, C4: a block per span decodes its rows in
+        // parallel; else a wave per span walks them)
+        if (interval == 0 && R >= 64ull * n_kept) LAUNCH(k_decode_rows, dim3(n_kept), dim3(DR_THREADS), 0, st, da);
+        else if (interval == 0) LAUNCH(k_decode_nods, dim3(blocks), dim3(256), 0, st, da);
+        else launch_agg<LaunchGeneralDs>(ds_agg, ctx, blocks, da);
         HIPCHK(hipEventRecord(ctx->ev[9], st));
-        LAUNCH(k_decode_nods, dim3(std::min(blocks, 1024u)), dim3(256), 0, st, ga);
-      }
-    } else {
-      DecodeArgs fa = da;
-      if (chunks && ds_agg != 4) {
-        SpanDsArgs g = {};
-        g.bitmap = bitmap;
-        g.lo = lo;
-        g.hi = hi;
-        g.rate = rate;
-        if (!bitmap) fap.a.op = -1;
-        launch_agg<LaunchChunks>(ds_agg, ctx, da, fa, row_ncells, row_val_len, g, R, use_reg, &sm->cnt[3], sm->seg,
-                                 sm->seg2, &fap);
-        fap_ran = fap.a.op >= 0;
-        chunk_marked = bitmap != nullptr && fa.span_list != nullptr;
-      }
-      if (chunk_marked) {
-        mark_list = fa.span_list;
-        mark_count = fa.span_count;
-      }
-      if (fa.span_list) {  // (grid-stride over the spans left by k_ds_spans: usually few; general inline)
-        launch_agg<LaunchFastDsInl>(ds_agg, ctx, std::min(blocks, 1024u), fa, row_ncells, row_val_len);
+      } else if (interval == 0) {
+        DecodeArgs fa = da;
+        if (direct) {
+          // regular-cadence spans on consecutive grid ranks skip E (k_direct.hip)
+          dg.info = scratch<uint32_t>(ctx, "d_info", n_kept);
+          dg.n = scratch<uint32_t>(ctx, "d_n", n_kept);
+          dg.x0 = scratch<uint32_t>(ctx, "d_x0", n_kept);
+          dg.step = scratch<uint32_t>(ctx, "d_step", n_kept);
+          dg.voff = scratch<uint64_t>(ctx, "d_voff", n_kept);
+          dg.c0 = scratch<uint32_t>(ctx, "d_c0", n_kept);
+          dg.r0 = scratch<uint64_t>(ctx, "d_r0", n_kept);
+          dg.ga = scratch<uint32_t>(ctx, "d_ga", n_kept);
+          dg.row_cpre = scratch<uint32_t>(ctx, "row_cpre", R);
+          dg.list = scratch<uint32_t>(ctx, "d_list", n_kept);
+          dg.list_count = &sm->cnt[2];
+          dg.bitmap = bitmap;
+          dg.lo = lo;
+          dg.hi = hi;
+          dg.rate = rate;
+          ctx->hot_kernel = TSDBHIP_HOT_REDUCE_DIRECT;  // timed around k_reduce
+          // (spans per wave: 32 for big groups; fewer below ~64k spans, so a
+          // small group still spreads over ~2048 waves instead of a handful)
+          dg.batch = std::max<uint32_t>(1, std::min<uint32_t>(DIRB, n_kept / 2048));
+          // the lockstep proposal (k_lockstep.hip), where the reduce is not the
+          // span-ordered pass (EXACT_ORDER, integer dev): three qualifiers a
+          // span now, every other one proven by k_lockstep as it reduces
+          // Unsharded, only when k_lockstep gets >= 2048 waves (LS_TILE grid
+          // points x >= 64 spans each, the points per span estimated from the
+          // input): C1's 100 spans made 8 waves (38 us) where k_reduce takes
+          // 11 us. (Sharded: every rank alike, whatever its shard.)
+          const uint64_t ls_waves = (h.n_input / n_kept + LS_TILE - 1) / LS_TILE * std::max<uint64_t>(1, n_kept / 64);
+          ls_try = ls_allow && ctx->opt.lockstep && !exact && (agg != TSDBHIP_AGG_DEV || rate) &&
+                   (ctx->opt.lockstep == 2 || sharded || ls_waves >= 2048);
+          if (ls_try) {
+            d_qoff = scratch<uint64_t>(ctx, "d_qoff", n_kept);
+            dg.ls_key = sm->ls_key;
+            dg.ls_other = &sm->cnt[5];
+            LAUNCH(k_direct_opt, dim3(grid_for(n_kept, 256)), dim3(256), 0, st, da, dg, row_ncells,
+                               row_val_len, d_qoff, sm->ls_key, &sm->cnt[5]);
+          }
+          LAUNCH(k_direct_scan, dim3(grid_for(n_kept, 4 * dg.batch, 1u << 20)), dim3(256), 0, st, da, dg,
+                             row_ncells, row_val_len);
+          fa.span_list = dg.list;
+          fa.span_count = dg.list_count;
+          mark_list = dg.list;
+          mark_count = dg.list_count;
+        }
+        if (fa.span_list) {  // (the direct scan's leftovers: general code inline)
+          LAUNCH((k_decode_fast<0, false, true>), dim3(std::min(blocks, 1024u)), dim3(256), 0, st, fa,
+                             row_ncells, row_val_len);
+        } else {
+          LAUNCH((k_decode_fast<0, false>), dim3(blocks), dim3(256), 0, st, fa, row_ncells, row_val_len);
+          HIPCHK(hipEventRecord(ctx->ev[9], st));
+          LAUNCH(k_decode_nods, dim3(std::min(blocks, 1024u)), dim3(256), 0, st, ga);
+        }
       } else {
-        launch_agg<LaunchFastDs>(ds_agg, ctx, blocks, fa, row_ncells, row_val_len);
-        if (ctx->hot_kernel == TSDBHIP_HOT_DECODE_FAST) HIPCHK(hipEventRecord(ctx->ev[9], st));
-        launch_agg<LaunchGeneralDs>(ds_agg, ctx, std::min(blocks, 1024u), ga);
+        DecodeArgs fa = da;
+        if (chunks && ds_agg != 4) {
+          SpanDsArgs g = {};
+          g.bitmap = bitmap;
+          g.lo = lo;
+          g.hi = hi;
+          g.rate = rate;
+          if (!bitmap) fap.a.op = -1;
+          launch_agg<LaunchChunks>(ds_agg, ctx, da, fa, row_ncells, row_val_len, g, R, use_reg, &sm->cnt[3], sm->seg,
+                                   sm->seg2, &fap);
+          fap_ran = fap.a.op >= 0;
+          chunk_marked = bitmap != nullptr && fa.span_list != nullptr;
+        }
+        if (chunk_marked) {
+          mark_list = fa.span_list;
+          mark_count = fa.span_count;
+        }
+        if (fa.span_list) {  // (grid-stride over the spans left by k_ds_spans: usually few; general inline)
+          launch_agg<LaunchFastDsInl>(ds_agg, ctx, std::min(blocks, 1024u), fa, row_ncells, row_val_len);
+        } else {
+          launch_agg<LaunchFastDs>(ds_agg, ctx, blocks, fa, row_ncells, row_val_len);
+          if (ctx->hot_kernel == TSDBHIP_HOT_DECODE_FAST) HIPCHK(hipEventRecord(ctx->ev[9], st));
+          launch_agg<LaunchGeneralDs>(ds_agg, ctx, std::min(blocks, 1024u), ga);
+        }
       }
     }
   }
-  if (detail) HIPCHK(hipEventRecord(ctx->ev[2], st));
-  // (k_span_summary's work, empty spans and F*, is done by k_grid_mark below:
-  // a kept span implies a non-empty grid range)
-  // (no readback here: the flags, F*, errors and input count come back with
-  // |G| below. A decode error leaves every e_len <= its capacity, so the grid
-  // kernels stay inside E before the error is thrown.)
-  auto after_sync2 = [&]() {
+
+  // (after sync 2: a scan / SpanGroup.add error throws; sharded, the agreed
+  // input count)
+  void after_sync2() {
     if (h.err != ERR_NONE) {
       // (a scan / SpanGroup.add error: no SpanGroup, aggregatedSize() never
       // reached; a sharded rank may have set its local count at sync 1)
@@ -2812,30 +2986,11 @@ static int spangroup_run_once(Slot* ctx, const tsdbhip_sg_desc* d, tsdbhip_sg_ou
       n_input_global = h.n_input;
       out->n_input_points = n_input_global;
     }
-  };
+  }
 
-  // the optimistic aligned-group finish (below): unsharded, when this group
-  // was tried as one; sharded, for every query that allows the attempt (all
-  // ranks must issue the same collectives)
-  const bool fap_query = interval > 0 && !rate && ds_agg <= 3 && agg <= 3 && !exact && !fap_off;
-  const bool fap_opt = !detail && (sharded ? fap_query : (fap_ran && !empty_grid));
-  // ---- union grid ----
-  uint64_t T = 0;
-  uint32_t* word_rank = nullptr;
-  uint32_t* gridv = nullptr;
-  if (detail) HIPCHK(hipEventRecord(ctx->ev[3], st));
-  GridArgs ga = {};
-  ga.e_off = eoff; ga.e_len = e_len; ga.e_ts = e_ts; ga.n_kept = n_kept; ga.rate = rate; ga.total = &sm->T;
-  ga.e_flt = e_flt; ga.err = &sm->err; ga.fstar = &sm->fstar;
-  ga.list = mark_list;  // spans k_ds_spans / the direct scan did not mark (null: all)
-  ga.list_count = mark_count;
-  // the direct path's verify appends to the direct / fallback lists again:
-  // k_grid_popc zeroes their counters (cnt[1], cnt[2])
-  ga.zero2 = direct && n_kept ? &sm->cnt[1] : nullptr;
-  ga.pub_src = (const uint64_t*)sm;
   // word ranks (block-local) and block sums of the bitmap (lo, nwords); the
   // single-block kernel that finishes T publishes the call state when `pub`
-  auto grid_ranks = [&](bool pub, bool hash) {
+  void grid_ranks(bool pub, bool hash) {
     word_rank = scratch<uint32_t>(ctx, "word_rank", nwords);
     const uint64_t nb = (nwords + 1023) / 1024;
     ga.lo = lo; ga.hi = hi; ga.bitmap = bitmap; ga.nwords = nwords; ga.word_rank = word_rank;
@@ -2847,660 +3002,715 @@ static int spangroup_run_once(Slot* ctx, const tsdbhip_sg_desc* d, tsdbhip_sg_ou
     ga.pub = pub ? next_pub(ctx, sizeof(Small)) : HostPub{};
     LAUNCH(k_grid_popc, dim3((unsigned)nb), dim3(256), 0, st, ga);
     if (nb > 1) LAUNCH(k_grid_scan_blocks, dim3(1), dim3(256), 0, st, ga, (uint32_t)nb);
-  };
-  if (!empty_grid) {
-    ga.lo = lo; ga.hi = hi; ga.bitmap = bitmap; ga.nwords = nwords;
-    // (a bitmap of many slices marked by few spans each, C4: sliced through
-    // LDS; else an atomic a point)
-    const uint32_t n_sl = (uint32_t)((nwords + GM_WORDS - 1) >> GM_SHIFT);
-    if (n_kept && n_sl >= 8 && (uint64_t)(n_sl + 1) * n_kept <= (64ull << 20)) {
-      uint32_t* B = scratch<uint32_t>(ctx, "gm_bounds", (uint64_t)(n_sl + 1) * n_kept);
-      LAUNCH(k_grid_bounds, dim3(mark_list ? std::min(grid_for(n_kept, 4, 65536), 1024u) : grid_for(n_kept, 4, 65536)),
-                         dim3(256), 0, st, ga, B, n_sl);
-      LAUNCH(k_grid_mark_slices, dim3(n_sl), dim3(256), 0, st, ga, (const uint32_t*)B, n_sl);
-    } else if (n_kept) {
-      LAUNCH(k_grid_mark, dim3(mark_list ? std::min(grid_for(n_kept, 4, 65536), 1024u) : grid_for(n_kept, 4, 65536)),
-                         dim3(256), 0, st, ga);
-    }
-    grid_ranks(!sharded && !fap_opt, sharded);
   }
-  // ---- the optimistic aligned-group finish: when the group is tried as an
-  // aligned group (sharded: every rank does this for a query that allows it,
-  // so that all issue the same collectives), the rest of the call is enqueued
-  // without the second host round trip: G emitted, the block partials reduced
-  // to 64 slots (sharded: exchanged in the agreement's collective group), and
-  // k_fap_finish writes the results iff the group stood (everywhere); the
-  // host then waits once. If it did not stand, the state after the grid (and
-  // the agreement) is intact and the usual path continues from it. ----
-  if (fap_opt) {
-    uint32_t* gridv_o = nullptr;
+
+  void grid() {
+    if (detail) HIPCHK(hipEventRecord(ctx->ev[2], st));
+    // (k_span_summary's work, empty spans and F*, is done by k_grid_mark below:
+    // a kept span implies a non-empty grid range)
+    // (no readback here: the flags, F*, errors and input count come back with
+    // |G| below. A decode error leaves every e_len <= its capacity, so the grid
+    // kernels stay inside E before the error is thrown.)
+
+
+    // the optimistic aligned-group finish (below): unsharded, when this group
+    // was tried as one; sharded, for every query that allows the attempt (all
+    // ranks must issue the same collectives)
+    fap_query = interval > 0 && !rate && ds_agg <= 3 && agg <= 3 && !exact && !fap_off;
+    fap_opt = !detail && (sharded ? fap_query : (fap_ran && !empty_grid));
+    // ---- union grid ----
+    T = 0;
+    word_rank = nullptr;
+    gridv = nullptr;
+    if (detail) HIPCHK(hipEventRecord(ctx->ev[3], st));
+    ga = {};
+    ga.e_off = eoff; ga.e_len = e_len; ga.e_ts = e_ts; ga.n_kept = n_kept; ga.rate = rate; ga.total = &sm->T;
+    ga.e_flt = e_flt; ga.err = &sm->err; ga.fstar = &sm->fstar;
+    ga.list = mark_list;  // spans k_ds_spans / the direct scan did not mark (null: all)
+    ga.list_count = mark_count;
+    // the direct path's verify appends to the direct / fallback lists again:
+    // k_grid_popc zeroes their counters (cnt[1], cnt[2])
+    ga.zero2 = direct && n_kept ? &sm->cnt[1] : nullptr;
+    ga.pub_src = (const uint64_t*)sm;
+
     if (!empty_grid) {
-      gridv_o = scratch<uint32_t>(ctx, "grid", nwords * 32);  // (>= |G|)
-      ga.grid = gridv_o;
-      if (!ga.emit1) {  // (a single-block k_grid_popc emitted it)
-        uint32_t* word_rank_f = scratch<uint32_t>(ctx, "word_rank_f", nwords);
-        const uint32_t eb = grid_for(nwords, 256);
-        LAUNCH(k_emit_verify, dim3(eb), dim3(256), 0, st, ga, word_rank_f, dg, 0u, eb);
+      ga.lo = lo; ga.hi = hi; ga.bitmap = bitmap; ga.nwords = nwords;
+      // (a bitmap of many slices marked by few spans each, C4: sliced through
+      // LDS; else an atomic a point)
+      const uint32_t n_sl = (uint32_t)((nwords + GM_WORDS - 1) >> GM_SHIFT);
+      if (n_kept && n_sl >= 8 && (uint64_t)(n_sl + 1) * n_kept <= (64ull << 20)) {
+        uint32_t* B = scratch<uint32_t>(ctx, "gm_bounds", (uint64_t)(n_sl + 1) * n_kept);
+        LAUNCH(k_grid_bounds, dim3(mark_list ? std::min(grid_for(n_kept, 4, 65536), 1024u) : grid_for(n_kept, 4, 65536)),
+                           dim3(256), 0, st, ga, B, n_sl);
+        LAUNCH(k_grid_mark_slices, dim3(n_sl), dim3(256), 0, st, ga, (const uint32_t*)B, n_sl);
+      } else if (n_kept) {
+        LAUNCH(k_grid_mark, dim3(mark_list ? std::min(grid_for(n_kept, 4, 65536), 1024u) : grid_for(n_kept, 4, 65536)),
+                           dim3(256), 0, st, ga);
       }
-    }
-    EV_START(ctx, 4);
-    const int fop = agg == TSDBHIP_AGG_MIN ? 1 : (agg == TSDBHIP_AGG_MAX ? 2 : 0);
-    int64_t* o_pi = scratch<int64_t>(ctx, "fo_i", WAVE);
-    uint32_t* o_pc = scratch<uint32_t>(ctx, "fo_cnt", WAVE);
-    const bool mine = fap_ran && !empty_grid;
-    // (sharded: the agreement header packed by the partial kernel and unpacked
-    // by the finish, no pack / unpack launches of their own)
-    const uint64_t elo = empty_grid ? ~0ull : (uint64_t)lo, ehi = empty_grid ? 0ull : (uint64_t)hi;
-    if (sharded && empty_grid) HIPCHK(hipMemsetAsync(sm->ghash, 0, sizeof sm->ghash, st));
-    const XField fx[XH_N + 1] = {{&sm->err, 0, 0},      {&sm->gflags[0], 2, 0}, {&sm->gflags[1], 2, 0},
-                                 {&sm->fstar, 1, 0},    {nullptr, 3, elo},      {nullptr, 4, ehi},
-                                 {&sm->ghash[0], 5, 0}, {&sm->ghash[0], 6, 0},  {&sm->ghash[1], 5, 0},
-                                 {&sm->ghash[1], 6, 0}, {nullptr, 4, elo},      {nullptr, 3, ehi},
-                                 {&sm->fap_valid, 0, 0}};
-    XMove pack = {};
-    if (sharded) pack = xchg_desc(ctx, fx, XH_N + 1, (uint64_t*)sm->xh);
-    XMove unpack = pack;
-    unpack.out = 1;
-    if (mine) {
-      const uint32_t nrows = fap.a.nrows;
-      const unsigned g1 = std::max(1u, std::min(256u, nrows / 128));
-      int64_t* tmp = scratch<int64_t>(ctx, "fap_tmp", (uint64_t)g1 * WAVE);
-      auto go = [&](auto opc) {
-        constexpr int OP = decltype(opc)::value;
-        // (two launches: a last-block-done fusion of the two measured slower,
-        // 20.3 us against 4.6 + 9.3, its 244 blocks' counter atomics contended)
-        LAUNCH((k_fap_rows<OP>), dim3(g1), dim3(1024), 0, st, (const int64_t*)fap.a.part, nrows, tmp);
-        LAUNCH((k_fap_final64v<OP>), dim3(1), dim3(1024), 0, st, (const int64_t*)tmp, g1, n_kept, o_pi, o_pc, sm,
-               pack);
-      };
-      if (fop == 1) go(std::integral_constant<int, 1>());
-      else if (fop == 2) go(std::integral_constant<int, 2>());
-      else go(std::integral_constant<int, 0>());
-    } else {
-      LAUNCH(k_fap_neutral64, dim3(1), dim3(WAVE), 0, st, o_pi, o_pc, fop, sm, pack);
-    }
-    if (sharded) {  // the agreement, the validity (MIN) and the 64-slot partials: one collective group
-      const XExtra ex[2] = {{o_pi, WAVE, fop ? X_I64 : X_U64, fop == 1 ? X_MIN : (fop == 2 ? X_MAX : X_SUM)},
-                            {o_pc, WAVE, X_U32, X_SUM}};
-      xchg_group(ctx, X, pack, (uint64_t*)&sm->n_input, ex, 2);
-    }
-    map_out_reserve(ctx, OUT_HDR + 17 * WAVE);
-    const uint64_t end_seq = ++ctx->pub_seq;
-    FinalArgs fo;
-    std::memset(&fo, 0, sizeof fo);
-    fo.T = WAVE;
-    fo.n_chunks = 1;
-    fo.grid = gridv_o;
-    fo.out_ts = (int64_t*)(ctx->map_out_dev + OUT_HDR);
-    fo.out_bits = fo.out_ts + WAVE;
-    fo.out_isint = (uint8_t*)(fo.out_bits + WAVE);
-    fo.nan_t = &sm->nan_t;
-    {  // (an empty local grid: never valid; launched anyway, every rank alike)
-      // the finish and the end of the call in one single-block launch
-      const XMove um = sharded ? unpack : XMove{};
-      Small* snap = (Small*)ctx->map_out_dev;
-      const Small* ini = small_init_dev(ctx);
-      const uint64_t seq = end_seq;
-      if (agg == TSDBHIP_AGG_MIN)
-        LAUNCH(k_fap_finish_end<1>, dim3(1), dim3(256), 0, st, sm, (const int64_t*)o_pi, (const uint32_t*)o_pc, fo, (int32_t)sharded, um, snap, ini, bitmap, (const uint32_t*)gridv_o, lo, seq);
-      else if (agg == TSDBHIP_AGG_MAX)
-        LAUNCH(k_fap_finish_end<2>, dim3(1), dim3(256), 0, st, sm, (const int64_t*)o_pi, (const uint32_t*)o_pc, fo, (int32_t)sharded, um, snap, ini, bitmap, (const uint32_t*)gridv_o, lo, seq);
-      else if (agg == TSDBHIP_AGG_AVG)
-        LAUNCH(k_fap_finish_end<3>, dim3(1), dim3(256), 0, st, sm, (const int64_t*)o_pi, (const uint32_t*)o_pc, fo, (int32_t)sharded, um, snap, ini, bitmap, (const uint32_t*)gridv_o, lo, seq);
-      else
-        LAUNCH(k_fap_finish_end<0>, dim3(1), dim3(256), 0, st, sm, (const int64_t*)o_pi, (const uint32_t*)o_pc, fo, (int32_t)sharded, um, snap, ini, bitmap, (const uint32_t*)gridv_o, lo, seq);
-    }
-    EV_FINAL(ctx, 5);
-    HIPCHK(hipStreamSynchronize(st));
-    check_stamp(ctx, end_seq);
-    tm.late_stamp = ctx->timing_late;
-    std::memcpy(&h, ctx->map_out, sizeof h);
-    if (h.fap_done) {  // the call is over (state reset, bitmap clear)
-      ctx->sm_ready = true;
-      ctx->bitmap_clean = true;
-      T = h.T;
-      out->n_input_points = h.n_input;
-      tm.n_grid = T;
-      tm.paths |= TSDBHIP_PATH_ALIGNED_GROUP;
-      if (sharded) {
-        tm.n_collectives = X->n_coll;
-        tm.x_bytes = X->x_bytes;
-      }
-      if (ctx->hot_kernel) tm.hot_ms = ev_ms(ctx, 8, 9);
-      tm.hot_kernel = ctx->hot_kernel;
-      tm.reduce_ms = ev_ms(ctx, 4, 5);
-      tm.total_ms = ev_ms(ctx, 0, 5);
-      tm.n_emitted = e_total;
-      ctx->timing = tm;
-      if (T > out->capacity && ctx->want_output) {
-        out->err_code = TSDBHIP_E_CAPACITY;
-        return TSDBHIP_E_CAPACITY;
-      }
-      if (ctx->want_output) {
-        const uint8_t* hb = ctx->map_out;
-        std::memcpy(out->ts, hb + OUT_HDR, T * 8);
-        std::memcpy(out->bits, hb + OUT_HDR + 8 * WAVE, T * 8);
-        std::memcpy(out->is_int, hb + OUT_HDR + 16 * WAVE, T);
-      }
-      out->n_out = T;
-      out->err_code = TSDBHIP_OK;
-      out->err_index = -1;
-      return TSDBHIP_OK;
+      grid_ranks(!sharded && !fap_opt, sharded);
     }
   }
-  bool grids_agreed = true;  // (sharded: every rank's local grid is the global one)
-  if (sharded) {
-    // One collective: the error, the int / float flags and F* (agreed in
-    // place), the input count (sum), and each rank's grid geometry and bitmap
-    // hashes as MIN / MAX pairs. Equal geometry and hashes on every rank: the
-    // local grid is the global one (aligned series, C3 / C3*), nothing else is
-    // exchanged before the partials. Otherwise the bitmaps are remapped onto
-    // the global [lo, hi] and OR-ed over the ranks (allgather) below.
-    // (an empty local grid: hashes 0, never a non-empty grid's, so the ranks
-    // agree only when every grid is empty)
-    const uint64_t elo = empty_grid ? ~0ull : (uint64_t)lo, ehi = empty_grid ? 0ull : (uint64_t)hi;
-    if (empty_grid) HIPCHK(hipMemsetAsync(sm->ghash, 0, sizeof sm->ghash, st));
-    const XField fx[XH_N] = {{&sm->err, 0, 0}, {&sm->gflags[0], 2, 0}, {&sm->gflags[1], 2, 0}, {&sm->fstar, 1, 0},
-                             {nullptr, 3, elo}, {nullptr, 4, ehi}, {&sm->ghash[0], 5, 0}, {&sm->ghash[0], 6, 0},
-                             {&sm->ghash[1], 5, 0}, {&sm->ghash[1], 6, 0}, {nullptr, 4, elo}, {nullptr, 3, ehi}};
-    if (!fap_opt) {  // (an optimistic call ran the agreement already; h holds it)
-      xchg_minmax(ctx, X, fx, XH_N, (uint64_t*)&sm->n_input, (uint64_t*)sm->xh);
-      const HostPub p2 = next_pub(ctx, sizeof(Small));
-      LAUNCH(k_publish, dim3(1), dim3(64), 0, st, p2, (const uint64_t*)sm);
-      wait_pub(ctx, p2, &h, sizeof h);  // sync 2: agreed error / flags / count, the grids' geometry and hashes
-    }
-    after_sync2();
-    const int64_t glo = (int64_t)h.xh[XH_LO], ghi = (int64_t)~h.xh[XH_HI];
-    const bool all_empty = h.xh[XH_LO] == ~0ull;
-    // (from the agreed words only: every rank takes the same branch)
-    const bool agreed = all_empty || xh_grids_agree(h.xh);
-    grids_agreed = agreed;
-    if (!agreed) {
-      // the global geometry: this rank's bitmap shifted onto [glo, ghi] (a
-      // separate buffer; the local one is cleared), then OR-ed over the ranks
-      const uint64_t gw = (uint64_t)(ghi - glo + 1 + 31) / 32;
-      const bool clean_x = ctx->bitmapx_clean;
-      ctx->bitmapx_clean = false;
-      uint32_t* gbm = scratch_zero_kept<uint32_t>(ctx, "gbitmap_x", gw, clean_x);
+
+  int fap_finish() {
+    // ---- the optimistic aligned-group finish: when the group is tried as an
+    // aligned group (sharded: every rank does this for a query that allows it,
+    // so that all issue the same collectives), the rest of the call is enqueued
+    // without the second host round trip: G emitted, the block partials reduced
+    // to 64 slots (sharded: exchanged in the agreement's collective group), and
+    // k_fap_finish writes the results iff the group stood (everywhere); the
+    // host then waits once. If it did not stand, the state after the grid (and
+    // the agreement) is intact and the usual path continues from it. ----
+    if (fap_opt) {
+      uint32_t* gridv_o = nullptr;
       if (!empty_grid) {
-        LAUNCH(k_bitmap_remap, dim3(grid_for(gw, 256)), dim3(256), 0, st, (const uint32_t*)bitmap, nwords,
-                           lo, gbm, gw, glo);
-        HIPCHK(hipMemsetAsync(bitmap, 0, nwords * 4, st));
-      }
-      bitmap = gbm;
-      lo = glo;
-      hi = ghi;
-      nwords = gw;
-      empty_grid = false;
-      used_bitmap_x = true;
-      uint32_t* all = scratch<uint32_t>(ctx, "bitmap_all", nwords * X->nranks);
-      X->allgather(ctx, bitmap, all, nwords * 4);
-      LAUNCH(k_bitmap_or, dim3(grid_for(nwords, 256)), dim3(256), 0, st, all, (uint32_t)X->nranks,
-                         nwords, bitmap);
-      grid_ranks(true, false);
-      wait_pub(ctx, ga.pub, &h, sizeof h);  // sync 3: |G| of the global grid
-    }
-    dg.lo = lo;
-    dg.hi = hi;
-  } else if (!empty_grid) {
-    if (!fap_opt) wait_pub(ctx, ga.pub, &h, sizeof h);  // sync 2: |G|, flags, F*, errors
-    after_sync2();
-  } else {
-    readback(ctx, &h, sm, sizeof h);  // sync 2 (no grid)
-    after_sync2();
-  }
-  // lockstep: every kept span proposed the one class key, and the grid is
-  // its pattern (sharded: no other rank put a point elsewhere). A rank whose
-  // proposal stood but whose grid is wider cannot use it: the call is marked
-  // broken and runs again on the proven path (every rank, after the exchange)
-  // The reduce mode is the agreed one (sharded: every rank's flags); a rank
-  // whose lockstep proposal would reduce in another mode (an int shard next
-  // to a float shard on one cadence: MODE_INT where the group is MODE_DUAL,
-  // so the double partials would go unwritten) cannot use it either
-  const bool anyf = h.gflags[0] != 0, anyi = h.gflags[1] != 0;
-  const int mode = rate ? MODE_DBL : (!anyf ? MODE_INT : (!anyi ? MODE_DBL : MODE_DUAL));
-  bool ls_use = false;
-  LsPlan lsp = {};
-  if (ls_try && h.cnt[5] == 0 && h.ls_key[0] != ~0ull && h.ls_key[0] == h.ls_key[1] && h.ls_key[2] == h.ls_key[3]) {
-    const uint32_t ln = (uint32_t)h.ls_key[0];
-    const bool ls_flt = (h.ls_key[2] & 8u) != 0;
-    const int ls_mode = (rate || ls_flt) ? MODE_DBL : MODE_INT;
-    if (h.T == (uint64_t)(rate ? ln - 1 : ln) && ls_mode == mode) {
-      ls_use = true;
-      lsp.a.d_voff = dg.voff;
-      lsp.a.d_qoff = d_qoff;
-      lsp.a.val = val;
-      lsp.a.qual = qual;
-      lsp.a.n = ln;
-      lsp.a.q0 = (uint32_t)(h.ls_key[2] & 0xFFFFu);
-      lsp.a.step = (uint32_t)(h.ls_key[2] >> 32);
-      lsp.a.broken = &sm->ls_broken;
-      lsp.w8 = ((lsp.a.q0 & 7u) == 7u);
-      lsp.flt = (lsp.a.q0 & 8u) != 0;
-      tm.paths |= TSDBHIP_PATH_LOCKSTEP;
-    } else {
-      HIPCHK(hipMemsetD32Async((hipDeviceptr_t)&sm->ls_broken, 1, 1, st));
-    }
-  }
-  if (!empty_grid) {
-    T = h.T;
-    gridv = scratch<uint32_t>(ctx, "grid", T);
-    ga.grid = gridv;
-    // G emitted with the final word ranks (word_rank_f); in the same launch
-    // the direct candidates whose points are not consecutive grid ranks go
-    // to the E path (their grid points are already marked; types, F* and
-    // errors already counted)
-    uint32_t* word_rank_f = scratch<uint32_t>(ctx, "word_rank_f", nwords);
-    const bool verify = direct && n_kept && !ls_use;  // (lockstep: every span's points are G itself)
-    dg.word_rank = word_rank;  // (block-local ranks + ga.block_sum)
-    dg.bitmap = bitmap;
-    const uint32_t eb = grid_for(nwords, 256);
-    LAUNCH(k_emit_verify, dim3(eb + (verify ? grid_for(n_kept, 256) : 0)), dim3(256), 0, st, ga,
-                       word_rank_f, dg, verify ? n_kept : 0u, eb);
-    word_rank = word_rank_f;
-    dg.word_rank = word_rank_f;
-    if (verify) {
-      DecodeArgs fa = da;
-      fa.span_list = dg.list;
-      fa.span_count = dg.list_count;
-      LAUNCH((k_decode_fast<0, false, true>), dim3(std::min(grid_for(n_kept, 4, 65536), 1024u)), dim3(256),
-                         0, st, fa, row_ncells, row_val_len);
-    }
-  }
-  const uint64_t fstar = h.fstar;
-  // the aligned-group partials stand for the reduce iff every kept span was in
-  // the one class (no span outside it, one key) and G is the class's bucket
-  // sequence (sharded: the local grid is the global one); else the members'
-  // E is written now by a rerun of k_ds_reg
-  const bool fap_use = fap_ran && !h.fap_broken && h.fap_key[0] == h.fap_key[1] && h.fap_key[2] == h.fap_key[3] &&
-                       !anyf && T > 0 && T <= WAVE && grids_agreed;
-  if (fap_ran && !fap_use) launch_agg<LaunchRegRerun>(ds_agg, ctx, da, fap, row_ncells, row_val_len);
-  tm.paths |= fap_use ? TSDBHIP_PATH_ALIGNED_GROUP : (fap_ran ? TSDBHIP_PATH_ALIGNED_RERUN : 0u);
-  EV_START(ctx, 4);
-  tm.n_grid = T;
-  // lazy error index for illegal cells (every span's E and e_bad are final
-  // here; sharded: a rank of the global grid, reduced with the exchange)
-  BadArgs bad;
-  bad.e_bad = e_bad; bad.e_off = eoff; bad.e_ts = e_ts; bad.n_kept = n_kept; bad.rate = (int32_t)rate; bad.hi = hi;
-  bad.lo = lo; bad.bitmap = bitmap; bad.word_rank = word_rank; bad.T = T;
-  // (small unsharded calls: computed by k_call_end instead, one launch fewer)
-  // (k_call_end then runs as one block: its bitmap clearing must follow the
-  // error index's grid ranks)
-  const bool bad_at_end = !sharded && n_kept <= 4096 && T <= 65536;
-  // (an aligned group holds no E span, hence no bad cell)
-  // (an aligned or lockstep group holds no E span, hence no bad cell)
-  if (ls_use) bad.n_kept = 0;
-  if (n_kept && !bad_at_end && !fap_use && !ls_use)
-    LAUNCH(k_bad_index, dim3(grid_for(n_kept, 256)), dim3(256), 0, st, bad, &sm->bad_at);
-
-  // ---- the reduce's shape: the span-ordered pass (integer dev before the
-  // (long) truncation, Aggregators.java:196-217, or EXACT_ORDER), exact
-  // integer partials, or order-dependent doubles; sharded doubles over a long
-  // grid exchange rank-owned slices of G (below) ----
-  const bool seq = exact || (agg == TSDBHIP_AGG_DEV && mode != MODE_DBL);
-  const bool int_parts = mode == MODE_INT && agg != TSDBHIP_AGG_DEV;
-  // (per rank (N-1)/N (esz + 17) B a point against (N-1) esz: a gain from 3
-  // ranks on; at 2 it is even, and the slices cost a second collective)
-  const bool sliced = sharded && T > 0 && !seq && !int_parts && X->nranks >= 3 && T >= XSLICE_MIN_T;
-  const uint64_t xs = sliced ? (T + X->nranks - 1) / X->nranks : 0;  // slice length (the last one shorter)
-  // ---- output block: [Small snapshot | ts T | bits T | is_int T], written
-  // by the kernels straight into mapped pinned host memory when small (a
-  // sliced exchange gathers the results in device memory: T padded to whole
-  // slices) ----
-  const uint64_t To = sliced ? xs * X->nranks : T;
-  const bool small_out = To * 17 <= (256u << 10) && ctx->want_output && !sliced;
-  map_out_reserve(ctx, OUT_HDR + (small_out ? 17 * To : 0));
-  uint8_t* outblk = small_out ? ctx->map_out_dev : scratch<uint8_t>(ctx, "outblk", OUT_HDR + 17 * To);
-  int64_t* o_ts = (int64_t*)(outblk + OUT_HDR);
-  int64_t* o_bits = o_ts + To;
-  uint8_t* o_isint = (uint8_t*)(o_bits + To);
-  // a long unsharded result into registered (mapped) caller buffers: the
-  // reduce finalizes each tile group into them as soon as its last chunk is
-  // done, so the results cross PCIe while the reduce still runs (no D2H copy
-  // after it; C4: 178 MB)
-  FinalArgs fin_map;
-  std::memset(&fin_map, 0, sizeof fin_map);
-  if (!sharded && !small_out && ctx->want_output && T >= 65536 && out->capacity >= T) {
-    fin_map.out_ts = (int64_t*)mapped_dev_ptr(out->ts, T * 8);
-    fin_map.out_bits = (int64_t*)mapped_dev_ptr(out->bits, T * 8);
-    fin_map.out_isint = (uint8_t*)mapped_dev_ptr(out->is_int, T);
-    if (!fin_map.out_ts || !fin_map.out_bits || !fin_map.out_isint) fin_map.out_ts = nullptr;
-  }
-  bool out_direct = false;  // the results are already in the caller's buffers
-
-  // ---- reduce ----
-  if (T > 0) {
-    ctx->time_reduce = direct;
-    // (integer dev is reduced in one span-ordered pass, and, sharded, in rank
-    // order: the reference's sequential Welford before the (long)
-    // truncation admits no merge of partial states; EXACT_ORDER does the
-    // same for every aggregator)
-    FinalArgs fin;
-    std::memset(&fin, 0, sizeof fin);
-    fin.T = T; fin.n_chunks = 1; fin.grid = gridv; fin.fstar = fstar; fin.rate = rate;
-    fin.out_ts = o_ts;
-    fin.out_isint = o_isint;
-    fin.out_bits = o_bits;
-    fin.nan_t = &sm->nan_t;
-    auto partials = [&](ReduceArgs& r, const char* pre, uint64_t np) { alloc_partials(ctx, r, pre, np, agg); };
-    auto fields = [&](const ReduceArgs& r, uint64_t off) { return partial_fields(r, off, agg, mode); };
-    // one reduce launch over this rank's kept spans; `init`: the per-t state
-    // to continue from (one chunk)
-    auto run_reduce = [&](bool one_chunk, bool finalize, const ReduceArgs* init) {
-      // span state in LDS while 4 waves' regions fit 40 KB (4 blocks a CU)
-      const uint32_t spc_cap = (uint32_t)(RED_LDS_BLOCK / 4 / red_lds_span_bytes(rate));
-      const ReduceGeom rg = reduce_geom(T, n_kept, one_chunk || init, 16384, 2048, spc_cap);
-      const uint32_t spc = rg.spc, n_chunks = rg.n_chunks, tpw = rg.tpw, ntg = rg.ntg;
-      const uint64_t n_waves = rg.n_waves;
-      ReduceArgs r;
-      std::memset(&r, 0, sizeof r);
-      r.e_off = eoff; r.e_len = e_len; r.e_ts = e_ts; r.e_val = e_val; r.e_flt = e_flt; r.n_kept = n_kept;
-      r.grid = gridv; r.T = T; r.bitmap = bitmap; r.word_rank = word_rank; r.lo = lo;
-      r.spans_per_chunk = spc; r.n_chunks = n_chunks; r.tiles_per_wave = tpw; r.n_tile_groups = ntg;
-      r.d_info = direct ? dg.info : nullptr;
-      r.d_n = dg.n; r.d_ga = dg.ga; r.d_voff = dg.voff; r.d_x0 = dg.x0; r.d_step = dg.step; r.d_c0 = dg.c0;
-      r.d_r0 = dg.r0; r.span_row_start = span_row_start; r.kept = kept; r.row_cpre = dg.row_cpre;
-      r.row_ncells = row_ncells; r.row_val_off = row_val_off; r.val = val;
-      r.chunk_e = nullptr;
-      r.fstar = fstar;
-      r.exact = exact ? 1 : 0;
-      r.lds_state = 4 * red_lds_stride(spc, rate) <= RED_LDS_BLOCK ? 1u : 0u;
-      if (init) {
-        r.i_cnt = init->p_cnt; r.i_flag = init->p_flag; r.i_i = init->p_i; r.i_d = init->p_d;
-        r.i_dhas = init->p_dhas; r.i_wim = init->p_wim; r.i_wiv = init->p_wiv; r.i_wdm = init->p_wdm;
-        r.i_wdv = init->p_wdv;
-      }
-      // (small reductions: the general instantiation takes every chunk, direct
-      // spans included; no flags, one launch)
-      if (direct && n_waves > 4096) {
-        uint32_t* ce = scratch<uint32_t>(ctx, "chunk_e", n_chunks);
-        LAUNCH(k_chunk_flags_w, dim3(grid_for(n_chunks, 4)), dim3(256), 0, st, dg.info, n_kept, spc,
-                           n_chunks, ce);
-        r.chunk_e = ce;
-      }
-      // the in-kernel finalize into the mapped result (unsharded, one pass,
-      // no direct spans, few chunks: the last chunk-wave merges them)
-      if (finalize && !init && !one_chunk && !direct && fin_map.out_ts && n_chunks > 1 && n_chunks < 64) {
-        r.tg_done = scratch_zero_kept<uint32_t>(ctx, "tg_done", ntg, tgd_clean);
-        tgd_used = true;
-        r.fin = fin;
-        r.fin.n_chunks = n_chunks;
-        r.fin.out_ts = fin_map.out_ts;
-        r.fin.out_bits = fin_map.out_bits;
-        r.fin.out_isint = fin_map.out_isint;
-        out_direct = true;
-        finalize = false;
-      }
-      r.ptr = scratch<uint32_t>(ctx, "cursor", n_waves * spc);
-      r.st_x = scratch<uint2>(ctx, "st_x", n_waves * spc);
-      r.st_y = scratch<longlong2>(ctx, "st_y", n_waves * spc);
-      r.st_rv = scratch<double>(ctx, "st_rv", n_waves * spc);
-      r.st_f = scratch<uint32_t>(ctx, "st_f", n_waves * spc);
-      partials(r, "p_", (uint64_t)n_chunks * T);
-      FinalArgs f = fin;
-      f.n_chunks = n_chunks;
-      const unsigned blocks = (unsigned)((n_waves + 3) / 4);
-      dispatch_reduce(ctx, agg, mode, rate, blocks, r, f, n_chunks >= 64, finalize);
-      return r;
-    };
-    // the lockstep group: tiles of LS_TILE grid points x chunks of spans
-    auto ls_reduce = [&](bool finalize) {
-      const uint32_t n_tiles = (uint32_t)((T + LS_TILE - 1) / LS_TILE);
-      uint64_t want = std::max<uint64_t>(1, 16384 / n_tiles);
-      want = std::min<uint64_t>(want, std::max<uint32_t>(1, n_kept / LS_MIN_SPC));
-      const uint32_t spc = (uint32_t)((n_kept + want - 1) / want);
-      const uint32_t n_chunks = (n_kept + spc - 1) / spc;
-      const uint32_t n_cg = (n_chunks + LS_GROUP - 1) / LS_GROUP;  // (a block's chunks merged in LDS)
-      ReduceArgs r;
-      std::memset(&r, 0, sizeof r);
-      r.T = T;
-      r.n_chunks = n_cg;
-      r.n_kept = n_kept;
-      partials(r, "p_", (uint64_t)n_cg * T);
-      LsPlan p = lsp;
-      p.a.spc = spc;
-      p.a.n_tiles = n_tiles;
-      p.a.n_chunks = n_chunks;
-      FinalArgs f = fin;
-      f.n_chunks = n_cg;
-      ctx->hot_kernel = TSDBHIP_HOT_LOCKSTEP;
-      dispatch_lockstep(ctx, agg, rate, n_tiles * n_cg, r, p, f, finalize);
-      return r;
-    };
-    // the aligned group: its block partials reduced into the 1-chunk layout
-    auto fap_reduce = [&](bool finalize) {
-      ReduceArgs r;
-      std::memset(&r, 0, sizeof r);
-      r.T = T;
-      r.n_chunks = 1;
-      r.n_kept = n_kept;
-      partials(r, "p_", T);
-      const uint32_t nrows = fap.a.nrows;
-      // (16-wave blocks, >= 128 rows each, at most 256 of them)
-      const unsigned g1 = std::max(1u, std::min(256u, nrows / 128));
-      int64_t* tmp = scratch<int64_t>(ctx, "fap_tmp", (uint64_t)g1 * WAVE);
-      FinalArgs f = fin;
-      f.n_chunks = 1;
-      auto go = [&](auto opc) {
-        constexpr int OP = decltype(opc)::value;
-        LAUNCH((k_fap_rows<OP>), dim3(g1), dim3(1024), 0, st, (const int64_t*)fap.a.part, nrows, tmp);
-        if (!finalize) {
-          LAUNCH((k_fap_final<OP>), dim3(1), dim3(1024), 0, st, (const int64_t*)tmp, g1, T, n_kept, r.p_i,
-                             r.p_cnt, r.p_flag);
-          return;
+        gridv_o = scratch<uint32_t>(ctx, "grid", nwords * 32);  // (>= |G|)
+        ga.grid = gridv_o;
+        if (!ga.emit1) {  // (a single-block k_grid_popc emitted it)
+          uint32_t* word_rank_f = scratch<uint32_t>(ctx, "word_rank_f", nwords);
+          const uint32_t eb = grid_for(nwords, 256);
+          LAUNCH(k_emit_verify, dim3(eb), dim3(256), 0, st, ga, word_rank_f, dg, 0u, eb);
         }
-        // (the cross-series aggregator: OP 0 is sum or avg)
-        if (OP == 1) LAUNCH((k_fap_final_out<OP, 1>), dim3(1), dim3(1024), 0, st, (const int64_t*)tmp, g1, n_kept, f);
-        else if (OP == 2) LAUNCH((k_fap_final_out<OP, 2>), dim3(1), dim3(1024), 0, st, (const int64_t*)tmp, g1, n_kept, f);
-        else if (agg == TSDBHIP_AGG_AVG) LAUNCH((k_fap_final_out<0, 3>), dim3(1), dim3(1024), 0, st, (const int64_t*)tmp, g1, n_kept, f);
-        else LAUNCH((k_fap_final_out<0, 0>), dim3(1), dim3(1024), 0, st, (const int64_t*)tmp, g1, n_kept, f);
-      };
-      if (fap.a.op == 1) go(std::integral_constant<int, 1>());
-      else if (fap.a.op == 2) go(std::integral_constant<int, 2>());
-      else go(std::integral_constant<int, 0>());
-      return r;
-    };
-    if (!sharded) {
-      if (fap_use) fap_reduce(true);
-      else if (ls_use) ls_reduce(true);
-      else run_reduce(seq, true, nullptr);
+      }
+      EV_START(ctx, 4);
+      const int fop = agg == TSDBHIP_AGG_MIN ? 1 : (agg == TSDBHIP_AGG_MAX ? 2 : 0);
+      int64_t* o_pi = scratch<int64_t>(ctx, "fo_i", WAVE);
+      uint32_t* o_pc = scratch<uint32_t>(ctx, "fo_cnt", WAVE);
+      const bool mine = fap_ran && !empty_grid;
+      // (sharded: the agreement header packed by the partial kernel and unpacked
+      // by the finish, no pack / unpack launches of their own)
+      const uint64_t elo = empty_grid ? ~0ull : (uint64_t)lo, ehi = empty_grid ? 0ull : (uint64_t)hi;
+      if (sharded && empty_grid) HIPCHK(hipMemsetAsync(sm->ghash, 0, sizeof sm->ghash, st));
+      const XField fx[XH_N + 1] = {{&sm->err, 0, 0},      {&sm->gflags[0], 2, 0}, {&sm->gflags[1], 2, 0},
+                                   {&sm->fstar, 1, 0},    {nullptr, 3, elo},      {nullptr, 4, ehi},
+                                   {&sm->ghash[0], 5, 0}, {&sm->ghash[0], 6, 0},  {&sm->ghash[1], 5, 0},
+                                   {&sm->ghash[1], 6, 0}, {nullptr, 4, elo},      {nullptr, 3, ehi},
+                                   {&sm->fap_valid, 0, 0}};
+      XMove pack = {};
+      if (sharded) pack = xchg_desc(ctx, fx, XH_N + 1, (uint64_t*)sm->xh);
+      XMove unpack = pack;
+      unpack.out = 1;
+      if (mine) {
+        const uint32_t nrows = fap.a.nrows;
+        const unsigned g1 = std::max(1u, std::min(256u, nrows / 128));
+        int64_t* tmp = scratch<int64_t>(ctx, "fap_tmp", (uint64_t)g1 * WAVE);
+        auto go = [&](auto opc) {
+          constexpr int OP = decltype(opc)::value;
+          // (two launches: a last-block-done fusion of the two measured slower,
+          // 20.3 us against 4.6 + 9.3, its 244 blocks' counter atomics contended)
+          LAUNCH((k_fap_rows<OP>), dim3(g1), dim3(1024), 0, st, (const int64_t*)fap.a.part, nrows, tmp);
+          LAUNCH((k_fap_final64v<OP>), dim3(1), dim3(1024), 0, st, (const int64_t*)tmp, g1, n_kept, o_pi, o_pc, sm,
+                 pack);
+        };
+        if (fop == 1) go(std::integral_constant<int, 1>());
+        else if (fop == 2) go(std::integral_constant<int, 2>());
+        else go(std::integral_constant<int, 0>());
+      } else {
+        LAUNCH(k_fap_neutral64, dim3(1), dim3(WAVE), 0, st, o_pi, o_pc, fop, sm, pack);
+      }
+      if (sharded) {  // the agreement, the validity (MIN) and the 64-slot partials: one collective group
+        const XExtra ex[2] = {{o_pi, WAVE, fop ? X_I64 : X_U64, fop == 1 ? X_MIN : (fop == 2 ? X_MAX : X_SUM)},
+                              {o_pc, WAVE, X_U32, X_SUM}};
+        xchg_group(ctx, X, pack, (uint64_t*)&sm->n_input, ex, 2);
+      }
+      map_out_reserve(ctx, OUT_HDR + 17 * WAVE);
+      const uint64_t end_seq = ++ctx->pub_seq;
+      FinalArgs fo;
+      std::memset(&fo, 0, sizeof fo);
+      fo.T = WAVE;
+      fo.n_chunks = 1;
+      fo.grid = gridv_o;
+      fo.out_ts = (int64_t*)(ctx->map_out_dev + OUT_HDR);
+      fo.out_bits = fo.out_ts + WAVE;
+      fo.out_isint = (uint8_t*)(fo.out_bits + WAVE);
+      fo.nan_t = &sm->nan_t;
+      {  // (an empty local grid: never valid; launched anyway, every rank alike)
+        // the finish and the end of the call in one single-block launch
+        const XMove um = sharded ? unpack : XMove{};
+        Small* snap = (Small*)ctx->map_out_dev;
+        const Small* ini = small_init_dev(ctx);
+        const uint64_t seq = end_seq;
+        if (agg == TSDBHIP_AGG_MIN)
+          LAUNCH(k_fap_finish_end<1>, dim3(1), dim3(256), 0, st, sm, (const int64_t*)o_pi, (const uint32_t*)o_pc, fo, (int32_t)sharded, um, snap, ini, bitmap, (const uint32_t*)gridv_o, lo, seq);
+        else if (agg == TSDBHIP_AGG_MAX)
+          LAUNCH(k_fap_finish_end<2>, dim3(1), dim3(256), 0, st, sm, (const int64_t*)o_pi, (const uint32_t*)o_pc, fo, (int32_t)sharded, um, snap, ini, bitmap, (const uint32_t*)gridv_o, lo, seq);
+        else if (agg == TSDBHIP_AGG_AVG)
+          LAUNCH(k_fap_finish_end<3>, dim3(1), dim3(256), 0, st, sm, (const int64_t*)o_pi, (const uint32_t*)o_pc, fo, (int32_t)sharded, um, snap, ini, bitmap, (const uint32_t*)gridv_o, lo, seq);
+        else
+          LAUNCH(k_fap_finish_end<0>, dim3(1), dim3(256), 0, st, sm, (const int64_t*)o_pi, (const uint32_t*)o_pc, fo, (int32_t)sharded, um, snap, ini, bitmap, (const uint32_t*)gridv_o, lo, seq);
+      }
+      EV_FINAL(ctx, 5);
+      HIPCHK(hipStreamSynchronize(st));
+      check_stamp(ctx, end_seq);
+      tm.late_stamp = ctx->timing_late;
+      std::memcpy(&h, ctx->map_out, sizeof h);
+      if (h.fap_done) {  // the call is over (state reset, bitmap clear)
+        ctx->sm_ready = true;
+        ctx->bitmap_clean = true;
+        T = h.T;
+        out->n_input_points = h.n_input;
+        tm.n_grid = T;
+        tm.paths |= TSDBHIP_PATH_ALIGNED_GROUP;
+        if (sharded) {
+          tm.n_collectives = X->n_coll;
+          tm.x_bytes = X->x_bytes;
+        }
+        if (ctx->hot_kernel) tm.hot_ms = ev_ms(ctx, 8, 9);
+        tm.hot_kernel = ctx->hot_kernel;
+        tm.reduce_ms = ev_ms(ctx, 4, 5);
+        tm.total_ms = ev_ms(ctx, 0, 5);
+        tm.n_emitted = e_total;
+        ctx->timing = tm;
+        if (T > out->capacity && ctx->want_output) {
+          out->err_code = TSDBHIP_E_CAPACITY;
+          return TSDBHIP_E_CAPACITY;
+        }
+        if (ctx->want_output) {
+          const uint8_t* hb = ctx->map_out;
+          std::memcpy(out->ts, hb + OUT_HDR, T * 8);
+          std::memcpy(out->bits, hb + OUT_HDR + 8 * WAVE, T * 8);
+          std::memcpy(out->is_int, hb + OUT_HDR + 16 * WAVE, T);
+        }
+        out->n_out = T;
+        out->err_code = TSDBHIP_OK;
+        out->err_index = -1;
+        return TSDBHIP_OK;
+      }
+    }
+    return RC_CONTINUE;
+  }
+
+  void exchange_header() {
+    grids_agreed = true;  // (sharded: every rank's local grid is the global one)
+    if (sharded) {
+      // One collective: the error, the int / float flags and F* (agreed in
+      // place), the input count (sum), and each rank's grid geometry and bitmap
+      // hashes as MIN / MAX pairs. Equal geometry and hashes on every rank: the
+      // local grid is the global one (aligned series, C3 / C3*), nothing else is
+      // exchanged before the partials. Otherwise the bitmaps are remapped onto
+      // the global [lo, hi] and OR-ed over the ranks (allgather) below.
+      // (an empty local grid: hashes 0, never a non-empty grid's, so the ranks
+      // agree only when every grid is empty)
+      const uint64_t elo = empty_grid ? ~0ull : (uint64_t)lo, ehi = empty_grid ? 0ull : (uint64_t)hi;
+      if (empty_grid) HIPCHK(hipMemsetAsync(sm->ghash, 0, sizeof sm->ghash, st));
+      const XField fx[XH_N] = {{&sm->err, 0, 0}, {&sm->gflags[0], 2, 0}, {&sm->gflags[1], 2, 0}, {&sm->fstar, 1, 0},
+                               {nullptr, 3, elo}, {nullptr, 4, ehi}, {&sm->ghash[0], 5, 0}, {&sm->ghash[0], 6, 0},
+                               {&sm->ghash[1], 5, 0}, {&sm->ghash[1], 6, 0}, {nullptr, 4, elo}, {nullptr, 3, ehi}};
+      if (!fap_opt) {  // (an optimistic call ran the agreement already; h holds it)
+        xchg_minmax(ctx, X, fx, XH_N, (uint64_t*)&sm->n_input, (uint64_t*)sm->xh);
+        const HostPub p2 = next_pub(ctx, sizeof(Small));
+        LAUNCH(k_publish, dim3(1), dim3(64), 0, st, p2, (const uint64_t*)sm);
+        wait_pub(ctx, p2, &h, sizeof h);  // sync 2: agreed error / flags / count, the grids' geometry and hashes
+      }
+      after_sync2();
+      const int64_t glo = (int64_t)h.xh[XH_LO], ghi = (int64_t)~h.xh[XH_HI];
+      const bool all_empty = h.xh[XH_LO] == ~0ull;
+      // (from the agreed words only: every rank takes the same branch)
+      const bool agreed = all_empty || xh_grids_agree(h.xh);
+      grids_agreed = agreed;
+      if (!agreed) {
+        // the global geometry: this rank's bitmap shifted onto [glo, ghi] (a
+        // separate buffer; the local one is cleared), then OR-ed over the ranks
+        const uint64_t gw = (uint64_t)(ghi - glo + 1 + 31) / 32;
+        const bool clean_x = ctx->bitmapx_clean;
+        ctx->bitmapx_clean = false;
+        uint32_t* gbm = scratch_zero_kept<uint32_t>(ctx, "gbitmap_x", gw, clean_x);
+        if (!empty_grid) {
+          LAUNCH(k_bitmap_remap, dim3(grid_for(gw, 256)), dim3(256), 0, st, (const uint32_t*)bitmap, nwords,
+                             lo, gbm, gw, glo);
+          HIPCHK(hipMemsetAsync(bitmap, 0, nwords * 4, st));
+        }
+        bitmap = gbm;
+        lo = glo;
+        hi = ghi;
+        nwords = gw;
+        empty_grid = false;
+        used_bitmap_x = true;
+        uint32_t* all = scratch<uint32_t>(ctx, "bitmap_all", nwords * X->nranks);
+        X->allgather(ctx, bitmap, all, nwords * 4);
+        LAUNCH(k_bitmap_or, dim3(grid_for(nwords, 256)), dim3(256), 0, st, all, (uint32_t)X->nranks,
+                           nwords, bitmap);
+        grid_ranks(true, false);
+        wait_pub(ctx, ga.pub, &h, sizeof h);  // sync 3: |G| of the global grid
+      }
+      dg.lo = lo;
+      dg.hi = hi;
+    } else if (!empty_grid) {
+      if (!fap_opt) wait_pub(ctx, ga.pub, &h, sizeof h);  // sync 2: |G|, flags, F*, errors
+      after_sync2();
     } else {
-      const int nr = X->nranks, rk = X->rank;
-      ReduceArgs src;  // per-t partials the finalize merges ([n_src][T])
-      uint32_t n_src = 1;
-      if (seq) {
-        // span order across ranks: rank 0 reduces its spans in one chunk;
-        // rank r continues from rank r-1's per-t state, which reaches it by
-        // broadcast; the last broadcast gives every rank the final state
-        ReduceArgs S;
-        std::memset(&S, 0, sizeof S);
-        partials(S, "s_", T);
-        if (detail) HIPCHK(hipEventRecord(ctx->ev[6], st));
-        for (int step = 0; step < nr; step++) {
-          ReduceArgs P = S;  // (non-roots: the send side of the broadcast is unused)
-          if (rk == step) P = run_reduce(true, false, step ? &S : nullptr);
-          const std::vector<Fld> fp = fields(P, 0), fs = fields(S, 0);
-          X->group_start(ctx);
-          for (size_t i = 0; i < fp.size(); i++) X->broadcast(ctx, fp[i].p, fs[i].p, T * fp[i].esz, step);
-          if (step == 0) {
+      readback(ctx, &h, sm, sizeof h);  // sync 2 (no grid)
+      after_sync2();
+    }
+  }
+
+  void plan_reduce() {
+    // lockstep: every kept span proposed the one class key, and the grid is
+    // its pattern (sharded: no other rank put a point elsewhere). A rank whose
+    // proposal stood but whose grid is wider cannot use it: the call is marked
+    // broken and runs again on the proven path (every rank, after the exchange)
+    // The reduce mode is the agreed one (sharded: every rank's flags); a rank
+    // whose lockstep proposal would reduce in another mode (an int shard next
+    // to a float shard on one cadence: MODE_INT where the group is MODE_DUAL,
+    // so the double partials would go unwritten) cannot use it either
+    const bool anyf = h.gflags[0] != 0, anyi = h.gflags[1] != 0;
+    mode = rate ? MODE_DBL : (!anyf ? MODE_INT : (!anyi ? MODE_DBL : MODE_DUAL));
+    ls_use = false;
+    lsp = {};
+    if (ls_try && h.cnt[5] == 0 && h.ls_key[0] != ~0ull && h.ls_key[0] == h.ls_key[1] && h.ls_key[2] == h.ls_key[3]) {
+      const uint32_t ln = (uint32_t)h.ls_key[0];
+      const bool ls_flt = (h.ls_key[2] & 8u) != 0;
+      const int ls_mode = (rate || ls_flt) ? MODE_DBL : MODE_INT;
+      if (h.T == (uint64_t)(rate ? ln - 1 : ln) && ls_mode == mode) {
+        ls_use = true;
+        lsp.a.d_voff = dg.voff;
+        lsp.a.d_qoff = d_qoff;
+        lsp.a.val = val;
+        lsp.a.qual = qual;
+        lsp.a.n = ln;
+        lsp.a.q0 = (uint32_t)(h.ls_key[2] & 0xFFFFu);
+        lsp.a.step = (uint32_t)(h.ls_key[2] >> 32);
+        lsp.a.broken = &sm->ls_broken;
+        lsp.w8 = ((lsp.a.q0 & 7u) == 7u);
+        lsp.flt = (lsp.a.q0 & 8u) != 0;
+        tm.paths |= TSDBHIP_PATH_LOCKSTEP;
+      } else {
+        HIPCHK(hipMemsetD32Async((hipDeviceptr_t)&sm->ls_broken, 1, 1, st));
+      }
+    }
+    if (!empty_grid) {
+      T = h.T;
+      gridv = scratch<uint32_t>(ctx, "grid", T);
+      ga.grid = gridv;
+      // G emitted with the final word ranks (word_rank_f); in the same launch
+      // the direct candidates whose points are not consecutive grid ranks go
+      // to the E path (their grid points are already marked; types, F* and
+      // errors already counted)
+      uint32_t* word_rank_f = scratch<uint32_t>(ctx, "word_rank_f", nwords);
+      const bool verify = direct && n_kept && !ls_use;  // (lockstep: every span's points are G itself)
+      dg.word_rank = word_rank;  // (block-local ranks + ga.block_sum)
+      dg.bitmap = bitmap;
+      const uint32_t eb = grid_for(nwords, 256);
+      LAUNCH(k_emit_verify, dim3(eb + (verify ? grid_for(n_kept, 256) : 0)), dim3(256), 0, st, ga,
+                         word_rank_f, dg, verify ? n_kept : 0u, eb);
+      word_rank = word_rank_f;
+      dg.word_rank = word_rank_f;
+      if (verify) {
+        DecodeArgs fa = da;
+        fa.span_list = dg.list;
+        fa.span_count = dg.list_count;
+        LAUNCH((k_decode_fast<0, false, true>), dim3(std::min(grid_for(n_kept, 4, 65536), 1024u)), dim3(256),
+                           0, st, fa, row_ncells, row_val_len);
+      }
+    }
+    fstar = h.fstar;
+    // the aligned-group partials stand for the reduce iff every kept span was in
+    // the one class (no span outside it, one key) and G is the class's bucket
+    // sequence (sharded: the local grid is the global one); else the members'
+    // E is written now by a rerun of k_ds_reg
+    fap_use = fap_ran && !h.fap_broken && h.fap_key[0] == h.fap_key[1] && h.fap_key[2] == h.fap_key[3] &&
+                         !anyf && T > 0 && T <= WAVE && grids_agreed;
+    if (fap_ran && !fap_use) launch_agg<LaunchRegRerun>(ds_agg, ctx, da, fap, row_ncells, row_val_len);
+    tm.paths |= fap_use ? TSDBHIP_PATH_ALIGNED_GROUP : (fap_ran ? TSDBHIP_PATH_ALIGNED_RERUN : 0u);
+    EV_START(ctx, 4);
+    tm.n_grid = T;
+    // lazy error index for illegal cells (every span's E and e_bad are final
+    // here; sharded: a rank of the global grid, reduced with the exchange)
+    bad.e_bad = e_bad; bad.e_off = eoff; bad.e_ts = e_ts; bad.n_kept = n_kept; bad.rate = (int32_t)rate; bad.hi = hi;
+    bad.lo = lo; bad.bitmap = bitmap; bad.word_rank = word_rank; bad.T = T;
+    // (small unsharded calls: computed by k_call_end instead, one launch fewer)
+    // (k_call_end then runs as one block: its bitmap clearing must follow the
+    // error index's grid ranks)
+    bad_at_end = !sharded && n_kept <= 4096 && T <= 65536;
+    // (an aligned group holds no E span, hence no bad cell)
+    // (an aligned or lockstep group holds no E span, hence no bad cell)
+    if (ls_use) bad.n_kept = 0;
+    if (n_kept && !bad_at_end && !fap_use && !ls_use)
+      LAUNCH(k_bad_index, dim3(grid_for(n_kept, 256)), dim3(256), 0, st, bad, &sm->bad_at);
+
+    // ---- the reduce's shape: the span-ordered pass (integer dev before the
+    // (long) truncation, Aggregators.java:196-217, or EXACT_ORDER), exact
+    // integer partials, or order-dependent doubles; sharded doubles over a long
+    // grid exchange rank-owned slices of G (below) ----
+    seq = exact || (agg == TSDBHIP_AGG_DEV && mode != MODE_DBL);
+    int_parts = mode == MODE_INT && agg != TSDBHIP_AGG_DEV;
+    // (per rank (N-1)/N (esz + 17) B a point against (N-1) esz: a gain from 3
+    // ranks on; at 2 it is even, and the slices cost a second collective)
+    sliced = sharded && T > 0 && !seq && !int_parts && X->nranks >= 3 && T >= XSLICE_MIN_T;
+    xs = sliced ? (T + X->nranks - 1) / X->nranks : 0;  // slice length (the last one shorter)
+    // ---- output block: [Small snapshot | ts T | bits T | is_int T], written
+    // by the kernels straight into mapped pinned host memory when small (a
+    // sliced exchange gathers the results in device memory: T padded to whole
+    // slices) ----
+    To = sliced ? xs * X->nranks : T;
+    small_out = To * 17 <= (256u << 10) && ctx->want_output && !sliced;
+    map_out_reserve(ctx, OUT_HDR + (small_out ? 17 * To : 0));
+    outblk = small_out ? ctx->map_out_dev : scratch<uint8_t>(ctx, "outblk", OUT_HDR + 17 * To);
+    o_ts = (int64_t*)(outblk + OUT_HDR);
+    o_bits = o_ts + To;
+    o_isint = (uint8_t*)(o_bits + To);
+    // a long unsharded result into registered (mapped) caller buffers: the
+    // reduce finalizes each tile group into them as soon as its last chunk is
+    // done, so the results cross PCIe while the reduce still runs (no D2H copy
+    // after it; C4: 178 MB)
+    std::memset(&fin_map, 0, sizeof fin_map);
+    if (!sharded && !small_out && ctx->want_output && T >= 65536 && out->capacity >= T) {
+      fin_map.out_ts = (int64_t*)mapped_dev_ptr(out->ts, T * 8);
+      fin_map.out_bits = (int64_t*)mapped_dev_ptr(out->bits, T * 8);
+      fin_map.out_isint = (uint8_t*)mapped_dev_ptr(out->is_int, T);
+      if (!fin_map.out_ts || !fin_map.out_bits || !fin_map.out_isint) fin_map.out_ts = nullptr;
+    }
+    out_direct = false;  // the results are already in the caller's buffers
+  }
+
+  void partials(ReduceArgs& r, const char* pre, uint64_t np) { alloc_partials(ctx, r, pre, np, agg); }
+  std::vector<Fld> fields(const ReduceArgs& r, uint64_t off) { return partial_fields(r, off, agg, mode); }
+
+  // one reduce launch over this rank's kept spans; `init`: the per-t state
+  // to continue from (one chunk)
+  ReduceArgs run_reduce(bool one_chunk, bool finalize, const ReduceArgs* init, const FinalArgs& fin) {
+    // span state in LDS while 4 waves' regions fit 40 KB (4 blocks a CU)
+    const uint32_t spc_cap = (uint32_t)(RED_LDS_BLOCK / 4 / red_lds_span_bytes(rate));
+    const ReduceGeom rg = reduce_geom(T, n_kept, one_chunk || init, 16384, 2048, spc_cap);
+    const uint32_t spc = rg.spc, n_chunks = rg.n_chunks, tpw = rg.tpw, ntg = rg.ntg;
+    const uint64_t n_waves = rg.n_waves;
+    ReduceArgs r;
+    std::memset(&r, 0, sizeof r);
+    r.e_off = eoff; r.e_len = e_len; r.e_ts = e_ts; r.e_val = e_val; r.e_flt = e_flt; r.n_kept = n_kept;
+    r.grid = gridv; r.T = T; r.bitmap = bitmap; r.word_rank = word_rank; r.lo = lo;
+    r.spans_per_chunk = spc; r.n_chunks = n_chunks; r.tiles_per_wave = tpw; r.n_tile_groups = ntg;
+    r.d_info = direct ? dg.info : nullptr;
+    r.d_n = dg.n; r.d_ga = dg.ga; r.d_voff = dg.voff; r.d_x0 = dg.x0; r.d_step = dg.step; r.d_c0 = dg.c0;
+    r.d_r0 = dg.r0; r.span_row_start = span_row_start; r.kept = kept; r.row_cpre = dg.row_cpre;
+    r.row_ncells = row_ncells; r.row_val_off = row_val_off; r.val = val;
+    r.chunk_e = nullptr;
+    r.fstar = fstar;
+    r.exact = exact ? 1 : 0;
+    r.lds_state = 4 * red_lds_stride(spc, rate) <= RED_LDS_BLOCK ? 1u : 0u;
+    if (init) {
+      r.i_cnt = init->p_cnt; r.i_flag = init->p_flag; r.i_i = init->p_i; r.i_d = init->p_d;
+      r.i_dhas = init->p_dhas; r.i_wim = init->p_wim; r.i_wiv = init->p_wiv; r.i_wdm = init->p_wdm;
+      r.i_wdv = init->p_wdv;
+    }
+    // (small reductions: the general instantiation takes every chunk, direct
+    // spans included; no flags, one launch)
+    if (direct && n_waves > 4096) {
+      uint32_t* ce = scratch<uint32_t>(ctx, "chunk_e", n_chunks);
+      LAUNCH(k_chunk_flags_w, dim3(grid_for(n_chunks, 4)), dim3(256), 0, st, dg.info, n_kept, spc,
+                         n_chunks, ce);
+      r.chunk_e = ce;
+    }
+    // the in-kernel finalize into the mapped result (unsharded, one pass,
+    // no direct spans, few chunks: the last chunk-wave merges them)
+    if (finalize && !init && !one_chunk && !direct && fin_map.out_ts && n_chunks > 1 && n_chunks < 64) {
+      r.tg_done = scratch_zero_kept<uint32_t>(ctx, "tg_done", ntg, tgd_clean);
+      tgd_used = true;
+      r.fin = fin;
+      r.fin.n_chunks = n_chunks;
+      r.fin.out_ts = fin_map.out_ts;
+      r.fin.out_bits = fin_map.out_bits;
+      r.fin.out_isint = fin_map.out_isint;
+      out_direct = true;
+      finalize = false;
+    }
+    r.ptr = scratch<uint32_t>(ctx, "cursor", n_waves * spc);
+    r.st_x = scratch<uint2>(ctx, "st_x", n_waves * spc);
+    r.st_y = scratch<longlong2>(ctx, "st_y", n_waves * spc);
+    r.st_rv = scratch<double>(ctx, "st_rv", n_waves * spc);
+    r.st_f = scratch<uint32_t>(ctx, "st_f", n_waves * spc);
+    partials(r, "p_", (uint64_t)n_chunks * T);
+    FinalArgs f = fin;
+    f.n_chunks = n_chunks;
+    const unsigned blocks = (unsigned)((n_waves + 3) / 4);
+    dispatch_reduce(ctx, agg, mode, rate, blocks, r, f, n_chunks >= 64, finalize);
+    return r;
+  }
+
+  // the lockstep group: tiles of LS_TILE grid points x chunks of spans
+  ReduceArgs ls_reduce(bool finalize, const FinalArgs& fin) {
+    const uint32_t n_tiles = (uint32_t)((T + LS_TILE - 1) / LS_TILE);
+    uint64_t want = std::max<uint64_t>(1, 16384 / n_tiles);
+    want = std::min<uint64_t>(want, std::max<uint32_t>(1, n_kept / LS_MIN_SPC));
+    const uint32_t spc = (uint32_t)((n_kept + want - 1) / want);
+    const uint32_t n_chunks = (n_kept + spc - 1) / spc;
+    const uint32_t n_cg = (n_chunks + LS_GROUP - 1) / LS_GROUP;  // (a block's chunks merged in LDS)
+    ReduceArgs r;
+    std::memset(&r, 0, sizeof r);
+    r.T = T;
+    r.n_chunks = n_cg;
+    r.n_kept = n_kept;
+    partials(r, "p_", (uint64_t)n_cg * T);
+    LsPlan p = lsp;
+    p.a.spc = spc;
+    p.a.n_tiles = n_tiles;
+    p.a.n_chunks = n_chunks;
+    FinalArgs f = fin;
+    f.n_chunks = n_cg;
+    ctx->hot_kernel = TSDBHIP_HOT_LOCKSTEP;
+    dispatch_lockstep(ctx, agg, rate, n_tiles * n_cg, r, p, f, finalize);
+    return r;
+  }
+
+  // the aligned group: its block partials reduced into the 1-chunk layout
+  ReduceArgs fap_reduce(bool finalize, const FinalArgs& fin) {
+    ReduceArgs r;
+    std::memset(&r, 0, sizeof r);
+    r.T = T;
+    r.n_chunks = 1;
+    r.n_kept = n_kept;
+    partials(r, "p_", T);
+    const uint32_t nrows = fap.a.nrows;
+    // (16-wave blocks, >= 128 rows each, at most 256 of them)
+    const unsigned g1 = std::max(1u, std::min(256u, nrows / 128));
+    int64_t* tmp = scratch<int64_t>(ctx, "fap_tmp", (uint64_t)g1 * WAVE);
+    FinalArgs f = fin;
+    f.n_chunks = 1;
+    auto go = [&](auto opc) {
+      constexpr int OP = decltype(opc)::value;
+      LAUNCH((k_fap_rows<OP>), dim3(g1), dim3(1024), 0, st, (const int64_t*)fap.a.part, nrows, tmp);
+      if (!finalize) {
+        LAUNCH((k_fap_final<OP>), dim3(1), dim3(1024), 0, st, (const int64_t*)tmp, g1, T, n_kept, r.p_i,
+                           r.p_cnt, r.p_flag);
+        return;
+      }
+      // (the cross-series aggregator: OP 0 is sum or avg)
+      if (OP == 1) LAUNCH((k_fap_final_out<OP, 1>), dim3(1), dim3(1024), 0, st, (const int64_t*)tmp, g1, n_kept, f);
+      else if (OP == 2) LAUNCH((k_fap_final_out<OP, 2>), dim3(1), dim3(1024), 0, st, (const int64_t*)tmp, g1, n_kept, f);
+      else if (agg == TSDBHIP_AGG_AVG) LAUNCH((k_fap_final_out<0, 3>), dim3(1), dim3(1024), 0, st, (const int64_t*)tmp, g1, n_kept, f);
+      else LAUNCH((k_fap_final_out<0, 0>), dim3(1), dim3(1024), 0, st, (const int64_t*)tmp, g1, n_kept, f);
+    };
+    if (fap.a.op == 1) go(std::integral_constant<int, 1>());
+    else if (fap.a.op == 2) go(std::integral_constant<int, 2>());
+    else go(std::integral_constant<int, 0>());
+    return r;
+  }
+
+  void reduce() {
+    // ---- reduce ----
+    if (T > 0) {
+      ctx->time_reduce = direct;
+      // (integer dev is reduced in one span-ordered pass, and, sharded, in rank
+      // order: the reference's sequential Welford before the (long)
+      // truncation admits no merge of partial states; EXACT_ORDER does the
+      // same for every aggregator)
+      FinalArgs fin;
+      std::memset(&fin, 0, sizeof fin);
+      fin.T = T; fin.n_chunks = 1; fin.grid = gridv; fin.fstar = fstar; fin.rate = rate;
+      fin.out_ts = o_ts;
+      fin.out_isint = o_isint;
+      fin.out_bits = o_bits;
+      fin.nan_t = &sm->nan_t;
+      if (!sharded) {
+        if (fap_use) fap_reduce(true, fin);
+        else if (ls_use) ls_reduce(true, fin);
+        else run_reduce(seq, true, nullptr, fin);
+      } else {
+        const int nr = X->nranks, rk = X->rank;
+        ReduceArgs src;  // per-t partials the finalize merges ([n_src][T])
+        uint32_t n_src = 1;
+        if (seq) {
+          // span order across ranks: rank 0 reduces its spans in one chunk;
+          // rank r continues from rank r-1's per-t state, which reaches it by
+          // broadcast; the last broadcast gives every rank the final state
+          ReduceArgs S;
+          std::memset(&S, 0, sizeof S);
+          partials(S, "s_", T);
+          if (detail) HIPCHK(hipEventRecord(ctx->ev[6], st));
+          for (int step = 0; step < nr; step++) {
+            ReduceArgs P = S;  // (non-roots: the send side of the broadcast is unused)
+            if (rk == step) P = run_reduce(true, false, step ? &S : nullptr, fin);
+            const std::vector<Fld> fp = fields(P, 0), fs = fields(S, 0);
+            X->group_start(ctx);
+            for (size_t i = 0; i < fp.size(); i++) X->broadcast(ctx, fp[i].p, fs[i].p, T * fp[i].esz, step);
+            if (step == 0) {
+              X->allreduce(ctx, &sm->bad_at, 1, X_U64, X_MIN);
+              X->allreduce(ctx, &sm->ls_broken, 1, X_U32, X_MAX);
+            }
+            X->group_end(ctx);
+          }
+          if (detail) HIPCHK(hipEventRecord(ctx->ev[7], st));
+          src = S;
+        } else {
+          // this rank's chunks combined in order into one slot per t
+          ReduceArgs loc = fap_use ? fap_reduce(false, fin) : ls_use ? ls_reduce(false, fin) : run_reduce(false, false, nullptr, fin);
+          if (int_parts) {
+            // exact integer partials: one allreduce per field (wrapping u64
+            // sum, i64 min / max, count sum), no ordering needed
+            ReduceArgs mine = loc;
+            if (!fap_use) {  // (the aligned group's partials are one slot per t already, every count > 0)
+              partials(mine, "m_", T);
+              dispatch_combine(ctx, agg, mode, loc, mine, T, loc.n_chunks);
+              if (agg == TSDBHIP_AGG_MIN || agg == TSDBHIP_AGG_MAX)
+                LAUNCH(k_neutral_minmax, dim3(grid_for(T, 256)), dim3(256), 0, st, mine.p_cnt, mine.p_i, T,
+                                   agg == TSDBHIP_AGG_MIN ? INT64_MAX : INT64_MIN);
+            }
+            if (detail) HIPCHK(hipEventRecord(ctx->ev[6], st));
+            X->group_start(ctx);
+            for (const Fld& f : fields(mine, 0)) X->allreduce(ctx, f.p, T, f.t, f.op);
             X->allreduce(ctx, &sm->bad_at, 1, X_U64, X_MIN);
             X->allreduce(ctx, &sm->ls_broken, 1, X_U32, X_MAX);
-          }
-          X->group_end(ctx);
-        }
-        if (detail) HIPCHK(hipEventRecord(ctx->ev[7], st));
-        src = S;
-      } else {
-        // this rank's chunks combined in order into one slot per t
-        ReduceArgs loc = fap_use ? fap_reduce(false) : ls_use ? ls_reduce(false) : run_reduce(false, false, nullptr);
-        if (int_parts) {
-          // exact integer partials: one allreduce per field (wrapping u64
-          // sum, i64 min / max, count sum), no ordering needed
-          ReduceArgs mine = loc;
-          if (!fap_use) {  // (the aligned group's partials are one slot per t already, every count > 0)
-            partials(mine, "m_", T);
+            X->group_end(ctx);
+            if (detail) HIPCHK(hipEventRecord(ctx->ev[7], st));
+            src = mine;
+          } else if (sliced) {
+            // doubles over a long grid (C4): rank q owns slice q of G (xs
+            // points). Each rank's combined partials of slice q reach rank q
+            // (alltoall), which merges them in rank order (chunk-then-rank, as
+            // unsharded; SpanGroup.java:647-667) and finalizes its slice; the
+            // slices' results are then gathered. Per rank (N-1)/N of the
+            // partials plus the results, instead of N-1 times the partials.
+            ReduceArgs mine = loc, recv = loc;
+            partials(mine, "m_", xs * nr);  // [T] used
+            partials(recv, "x_", xs * nr);  // [rank q][xs]: rank q's partials of this rank's slice
             dispatch_combine(ctx, agg, mode, loc, mine, T, loc.n_chunks);
-            if (agg == TSDBHIP_AGG_MIN || agg == TSDBHIP_AGG_MAX)
-              LAUNCH(k_neutral_minmax, dim3(grid_for(T, 256)), dim3(256), 0, st, mine.p_cnt, mine.p_i, T,
-                                 agg == TSDBHIP_AGG_MIN ? INT64_MAX : INT64_MIN);
+            if (detail) HIPCHK(hipEventRecord(ctx->ev[6], st));
+            const std::vector<Fld> fm = fields(mine, 0), fr = fields(recv, 0);
+            X->group_start(ctx);
+            for (size_t i = 0; i < fm.size(); i++) X->alltoall(ctx, fm[i].p, fr[i].p, xs * fm[i].esz);
+            X->allreduce(ctx, &sm->bad_at, 1, X_U64, X_MIN);
+            X->allreduce(ctx, &sm->ls_broken, 1, X_U32, X_MAX);
+            X->group_end(ctx);
+            const uint64_t g0 = (uint64_t)rk * xs, ns = g0 < T ? std::min<uint64_t>(xs, T - g0) : 0;
+            FinalArgs f = fin;
+            f.T = ns;
+            f.stride = xs;
+            f.n_chunks = (uint32_t)nr;
+            f.g_base = g0;
+            f.grid = gridv + g0;
+            f.out_ts = o_ts + g0;
+            f.out_bits = o_bits + g0;
+            f.out_isint = o_isint + g0;
+            recv.n_chunks = (uint32_t)nr;
+            if (ns) dispatch_final(ctx, agg, mode, rate, recv, f);
+            X->group_start(ctx);
+            X->allgather(ctx, o_ts + g0, o_ts, xs * 8);
+            X->allgather(ctx, o_bits + g0, o_bits, xs * 8);
+            X->allgather(ctx, o_isint + g0, o_isint, xs);
+            X->allreduce(ctx, &sm->nan_t, 1, X_U64, X_MIN);
+            X->group_end(ctx);
+            if (detail) HIPCHK(hipEventRecord(ctx->ev[7], st));
+          } else {
+            // doubles (sums / Welford states depend on the order): every
+            // rank's slot gathered, merged in rank order on every rank
+            ReduceArgs all = loc;
+            partials(all, "x_", (uint64_t)nr * T);
+            ReduceArgs mine = all;
+            const uint64_t off = (uint64_t)rk * T;
+            mine.p_cnt += off; mine.p_flag += off; mine.p_i += off; mine.p_d += off; mine.p_dhas += off;
+            if (agg == TSDBHIP_AGG_DEV) { mine.p_wim += off; mine.p_wiv += off; mine.p_wdm += off; mine.p_wdv += off; }
+            dispatch_combine(ctx, agg, mode, loc, mine, T, loc.n_chunks);
+            if (detail) HIPCHK(hipEventRecord(ctx->ev[6], st));
+            const std::vector<Fld> fm = fields(mine, 0), fa = fields(all, 0);
+            X->group_start(ctx);
+            for (size_t i = 0; i < fm.size(); i++) X->allgather(ctx, fm[i].p, fa[i].p, T * fm[i].esz);
+            X->allreduce(ctx, &sm->bad_at, 1, X_U64, X_MIN);
+            X->allreduce(ctx, &sm->ls_broken, 1, X_U32, X_MAX);
+            X->group_end(ctx);
+            if (detail) HIPCHK(hipEventRecord(ctx->ev[7], st));
+            src = all;
+            n_src = (uint32_t)nr;
           }
-          if (detail) HIPCHK(hipEventRecord(ctx->ev[6], st));
-          X->group_start(ctx);
-          for (const Fld& f : fields(mine, 0)) X->allreduce(ctx, f.p, T, f.t, f.op);
-          X->allreduce(ctx, &sm->bad_at, 1, X_U64, X_MIN);
-          X->allreduce(ctx, &sm->ls_broken, 1, X_U32, X_MAX);
-          X->group_end(ctx);
-          if (detail) HIPCHK(hipEventRecord(ctx->ev[7], st));
-          src = mine;
-        } else if (sliced) {
-          // doubles over a long grid (C4): rank q owns slice q of G (xs
-          // points). Each rank's combined partials of slice q reach rank q
-          // (alltoall), which merges them in rank order (chunk-then-rank, as
-          // unsharded; SpanGroup.java:647-667) and finalizes its slice; the
-          // slices' results are then gathered. Per rank (N-1)/N of the
-          // partials plus the results, instead of N-1 times the partials.
-          ReduceArgs mine = loc, recv = loc;
-          partials(mine, "m_", xs * nr);  // [T] used
-          partials(recv, "x_", xs * nr);  // [rank q][xs]: rank q's partials of this rank's slice
-          dispatch_combine(ctx, agg, mode, loc, mine, T, loc.n_chunks);
-          if (detail) HIPCHK(hipEventRecord(ctx->ev[6], st));
-          const std::vector<Fld> fm = fields(mine, 0), fr = fields(recv, 0);
-          X->group_start(ctx);
-          for (size_t i = 0; i < fm.size(); i++) X->alltoall(ctx, fm[i].p, fr[i].p, xs * fm[i].esz);
-          X->allreduce(ctx, &sm->bad_at, 1, X_U64, X_MIN);
-          X->allreduce(ctx, &sm->ls_broken, 1, X_U32, X_MAX);
-          X->group_end(ctx);
-          const uint64_t g0 = (uint64_t)rk * xs, ns = g0 < T ? std::min<uint64_t>(xs, T - g0) : 0;
+        }
+        if (!sliced) {
           FinalArgs f = fin;
-          f.T = ns;
-          f.stride = xs;
-          f.n_chunks = (uint32_t)nr;
-          f.g_base = g0;
-          f.grid = gridv + g0;
-          f.out_ts = o_ts + g0;
-          f.out_bits = o_bits + g0;
-          f.out_isint = o_isint + g0;
-          recv.n_chunks = (uint32_t)nr;
-          if (ns) dispatch_final(ctx, agg, mode, rate, recv, f);
-          X->group_start(ctx);
-          X->allgather(ctx, o_ts + g0, o_ts, xs * 8);
-          X->allgather(ctx, o_bits + g0, o_bits, xs * 8);
-          X->allgather(ctx, o_isint + g0, o_isint, xs);
-          X->allreduce(ctx, &sm->nan_t, 1, X_U64, X_MIN);
-          X->group_end(ctx);
-          if (detail) HIPCHK(hipEventRecord(ctx->ev[7], st));
-        } else {
-          // doubles (sums / Welford states depend on the order): every
-          // rank's slot gathered, merged in rank order on every rank
-          ReduceArgs all = loc;
-          partials(all, "x_", (uint64_t)nr * T);
-          ReduceArgs mine = all;
-          const uint64_t off = (uint64_t)rk * T;
-          mine.p_cnt += off; mine.p_flag += off; mine.p_i += off; mine.p_d += off; mine.p_dhas += off;
-          if (agg == TSDBHIP_AGG_DEV) { mine.p_wim += off; mine.p_wiv += off; mine.p_wdm += off; mine.p_wdv += off; }
-          dispatch_combine(ctx, agg, mode, loc, mine, T, loc.n_chunks);
-          if (detail) HIPCHK(hipEventRecord(ctx->ev[6], st));
-          const std::vector<Fld> fm = fields(mine, 0), fa = fields(all, 0);
-          X->group_start(ctx);
-          for (size_t i = 0; i < fm.size(); i++) X->allgather(ctx, fm[i].p, fa[i].p, T * fm[i].esz);
-          X->allreduce(ctx, &sm->bad_at, 1, X_U64, X_MIN);
-          X->allreduce(ctx, &sm->ls_broken, 1, X_U32, X_MAX);
-          X->group_end(ctx);
-          if (detail) HIPCHK(hipEventRecord(ctx->ev[7], st));
-          src = all;
-          n_src = (uint32_t)nr;
+          f.n_chunks = n_src;
+          src.n_chunks = n_src;
+          dispatch_final(ctx, agg, mode, rate, src, f);
         }
       }
-      if (!sliced) {
-        FinalArgs f = fin;
-        f.n_chunks = n_src;
-        src.n_chunks = n_src;
-        dispatch_final(ctx, agg, mode, rate, src, f);
-      }
+    } else if (sharded) {
+      X->group_start(ctx);
+      X->allreduce(ctx, &sm->bad_at, 1, X_U64, X_MIN);
+      X->allreduce(ctx, &sm->ls_broken, 1, X_U32, X_MAX);
+      X->group_end(ctx);
     }
-  } else if (sharded) {
-    X->group_start(ctx);
-    X->allreduce(ctx, &sm->bad_at, 1, X_U64, X_MIN);
-    X->allreduce(ctx, &sm->ls_broken, 1, X_U32, X_MAX);
-    X->group_end(ctx);
   }
-  // ---- end of call: snapshot + reset of the call state, bitmap cleared ----
-  const uint64_t end_seq = ++ctx->pub_seq;
-  LAUNCH(k_call_end, dim3(bad_at_end ? 1u : grid_for(T, 256, 1024)), dim3(256), 0, st, sm,
-              (Small*)ctx->map_out_dev, small_init_dev(ctx), bitmap, (const uint32_t*)gridv, T, lo, bad_at_end ? bad : BadArgs{},
-              end_seq, (const uint32_t*)nullptr);
-  EV_FINAL(ctx, 5);
-  HIPCHK(hipStreamSynchronize(st));  // (the header and small results are already in host memory)
-  check_stamp(ctx, end_seq);
-  tm.late_stamp = ctx->timing_late;
-  const uint8_t* hb = ctx->map_out;
-  std::memcpy(&h, hb, sizeof h);
-  ctx->sm_ready = true;
-  ctx->bitmap_clean = true;
-  if (used_bitmap_x) ctx->bitmapx_clean = true;
-  if (tgd_used) ctx->tgdone_clean = true;  // (every counter reset by its group's last wave)
-  // the proposal did not hold: discard, run again. Sharded, from the agreed
-  // flag alone (MAX over the ranks): whether a rank tried depends on its own
-  // shard (empty, short rows), and every rank must issue the rerun's
-  // collectives. Unsharded the flag is only ever set by a try.
-  if (h.ls_broken) {
-    ctx->timing = tm;
-    return RC_REDO;
-  }
-  if (sharded) {
-    tm.exchange_ms = T > 0 && detail ? ev_ms(ctx, 6, 7) : 0.f;  // (timing_detail only)
-    tm.n_collectives = X->n_coll;
-    tm.x_bytes = X->x_bytes;
-  }
-  if (detail) {
-    tm.decode_ms = ev_ms(ctx, 1, 2);
-    tm.grid_ms = ev_ms(ctx, 3, 4);
-  }
-  if (ctx->hot_kernel) tm.hot_ms = ev_ms(ctx, 8, 9);
-  tm.hot_kernel = ctx->hot_kernel;
-  tm.reduce_ms = ev_ms(ctx, 4, 5);
-  tm.total_ms = ev_ms(ctx, 0, 5);
-  tm.n_emitted = e_total;
-  ctx->timing = tm;
 
-  // ---- outputs ----
-  uint64_t n_ok = T;
-  int code = TSDBHIP_OK;
-  int64_t err_at = -1;
-  if (h.bad_at != ~0ull) {
-    err_at = (int64_t)(h.bad_at >> 4);
-    code = (h.bad_at & 15) == BAD_OOB ? TSDBHIP_E_OUT_OF_BOUNDS : TSDBHIP_E_ILLEGAL_DATA;
+  int finish() {
+    // ---- end of call: snapshot + reset of the call state, bitmap cleared ----
+    const uint64_t end_seq = ++ctx->pub_seq;
+    LAUNCH(k_call_end, dim3(bad_at_end ? 1u : grid_for(T, 256, 1024)), dim3(256), 0, st, sm,
+                (Small*)ctx->map_out_dev, small_init_dev(ctx), bitmap, (const uint32_t*)gridv, T, lo, bad_at_end ? bad : BadArgs{},
+                end_seq, (const uint32_t*)nullptr);
+    EV_FINAL(ctx, 5);
+    HIPCHK(hipStreamSynchronize(st));  // (the header and small results are already in host memory)
+    check_stamp(ctx, end_seq);
+    tm.late_stamp = ctx->timing_late;
+    const uint8_t* hb = ctx->map_out;
+    std::memcpy(&h, hb, sizeof h);
+    ctx->sm_ready = true;
+    ctx->bitmap_clean = true;
+    if (used_bitmap_x) ctx->bitmapx_clean = true;
+    if (tgd_used) ctx->tgdone_clean = true;  // (every counter reset by its group's last wave)
+    // the proposal did not hold: discard, run again. Sharded, from the agreed
+    // flag alone (MAX over the ranks): whether a rank tried depends on its own
+    // shard (empty, short rows), and every rank must issue the rerun's
+    // collectives. Unsharded the flag is only ever set by a try.
+    if (h.ls_broken) {
+      ctx->timing = tm;
+      return RC_REDO;
+    }
+    if (sharded) {
+      tm.exchange_ms = T > 0 && detail ? ev_ms(ctx, 6, 7) : 0.f;  // (timing_detail only)
+      tm.n_collectives = X->n_coll;
+      tm.x_bytes = X->x_bytes;
+    }
+    if (detail) {
+      tm.decode_ms = ev_ms(ctx, 1, 2);
+      tm.grid_ms = ev_ms(ctx, 3, 4);
+    }
+    if (ctx->hot_kernel) tm.hot_ms = ev_ms(ctx, 8, 9);
+    tm.hot_kernel = ctx->hot_kernel;
+    tm.reduce_ms = ev_ms(ctx, 4, 5);
+    tm.total_ms = ev_ms(ctx, 0, 5);
+    tm.n_emitted = e_total;
+    ctx->timing = tm;
+
+    // ---- outputs ----
+    uint64_t n_ok = T;
+    int code = TSDBHIP_OK;
+    int64_t err_at = -1;
+    if (h.bad_at != ~0ull) {
+      err_at = (int64_t)(h.bad_at >> 4);
+      code = (h.bad_at & 15) == BAD_OOB ? TSDBHIP_E_OUT_OF_BOUNDS : TSDBHIP_E_ILLEGAL_DATA;
+    }
+    if (h.nan_t != ~0ull && (err_at < 0 || (int64_t)h.nan_t < err_at)) {
+      err_at = (int64_t)h.nan_t;
+      code = TSDBHIP_E_NAN_INF;
+    }
+    if (err_at >= 0) n_ok = (uint64_t)err_at;
+    if (n_ok > out->capacity && ctx->want_output) {
+      out->err_code = TSDBHIP_E_CAPACITY;
+      return TSDBHIP_E_CAPACITY;
+    }
+    if (!ctx->want_output || out_direct) {
+      // (a non-zero rank of an in-process sharded call: rank 0 returns the
+      // output; or the reduce wrote it into the mapped caller buffers)
+    } else if (n_ok && small_out) {  // (already in the pinned staging with the header)
+      std::memcpy(out->ts, hb + OUT_HDR, n_ok * 8);
+      std::memcpy(out->bits, hb + OUT_HDR + 8 * To, n_ok * 8);
+      std::memcpy(out->is_int, hb + OUT_HDR + 16 * To, n_ok);
+    } else if (n_ok) {
+      HIPCHK(hipMemcpyAsync(out->ts, o_ts, n_ok * 8, hipMemcpyDeviceToHost, st));
+      HIPCHK(hipMemcpyAsync(out->is_int, o_isint, n_ok, hipMemcpyDeviceToHost, st));
+      HIPCHK(hipMemcpyAsync(out->bits, o_bits, n_ok * 8, hipMemcpyDeviceToHost, st));
+      HIPCHK(hipStreamSynchronize(st));
+    }
+    out->n_out = n_ok;
+    out->err_code = code;
+    out->err_index = err_at;
+    // algorithmic bytes: reference row bytes + T x 17 B
+    tm.alg_bytes = 0;
+    ctx->timing = tm;
+    return code;
   }
-  if (h.nan_t != ~0ull && (err_at < 0 || (int64_t)h.nan_t < err_at)) {
-    err_at = (int64_t)h.nan_t;
-    code = TSDBHIP_E_NAN_INF;
-  }
-  if (err_at >= 0) n_ok = (uint64_t)err_at;
-  if (n_ok > out->capacity && ctx->want_output) {
-    out->err_code = TSDBHIP_E_CAPACITY;
-    return TSDBHIP_E_CAPACITY;
-  }
-  if (!ctx->want_output || out_direct) {
-    // (a non-zero rank of an in-process sharded call: rank 0 returns the
-    // output; or the reduce wrote it into the mapped caller buffers)
-  } else if (n_ok && small_out) {  // (already in the pinned staging with the header)
-    std::memcpy(out->ts, hb + OUT_HDR, n_ok * 8);
-    std::memcpy(out->bits, hb + OUT_HDR + 8 * To, n_ok * 8);
-    std::memcpy(out->is_int, hb + OUT_HDR + 16 * To, n_ok);
-  } else if (n_ok) {
-    HIPCHK(hipMemcpyAsync(out->ts, o_ts, n_ok * 8, hipMemcpyDeviceToHost, st));
-    HIPCHK(hipMemcpyAsync(out->is_int, o_isint, n_ok, hipMemcpyDeviceToHost, st));
-    HIPCHK(hipMemcpyAsync(out->bits, o_bits, n_ok * 8, hipMemcpyDeviceToHost, st));
-    HIPCHK(hipStreamSynchronize(st));
-  }
-  out->n_out = n_ok;
-  out->err_code = code;
-  out->err_index = err_at;
-  // algorithmic bytes: reference row bytes + T x 17 B
-  tm.alg_bytes = 0;
-  ctx->timing = tm;
-  return code;
+};
+
+static int spangroup_run_once(Slot* ctx, const tsdbhip_sg_desc* d, tsdbhip_sg_out* out, bool ls_allow,
+                              bool ug_allow) {
+  SgCall c(ctx, d, out, ls_allow, ug_allow);
+  return c.run();
 }
+
 
 // The call, and its rerun on the proven path when k_lockstep found a
 // qualifier off the lockstep proposal (every rank of a sharded call agrees
