@@ -3712,11 +3712,31 @@ static int spangroup_run_once(Slot* ctx, const tsdbhip_sg_desc* d, tsdbhip_sg_ou
 }
 
 
-// The call, and its rerun on the proven path when k_lockstep found a
-// qualifier off the lockstep proposal (every rank of a sharded call agrees
-// on that, so all of them rerun)
-// (a rerun stages nothing again: the host-resident inputs the first attempt
-// copied are still in HBM — ADVICE r5)
+// The call's attempts and their rerun edges, in one place. An attempt is
+// spangroup_run_once with the proposals it may try; an attempt that returns
+// a rerun code hands the call to the attempt its edge names (every rank of a
+// sharded call returns the same code: the verdicts are agreed):
+//   FULL     --RC_UG_FALLBACK--> NO_UNIFORM  the aligned group / E did not stand
+//                                            (test_uniform.py: *_fallback*)
+//   FULL     --RC_REDO---------> PROVEN      the uniform lockstep's proposal did
+//                                            not hold (test_uniform.py:67)
+//   NO_UNIFORM --RC_REDO-------> PROVEN      the general path's lockstep proposal
+//                                            did not hold (test_lockstep.py)
+// PROVEN tries no proposal and so ends the call. A rerun stages nothing
+// again: the host-resident inputs the first attempt copied are still in HBM
+// (ADVICE r5).
+enum SgAttempt { SG_FULL, SG_NO_UNIFORM, SG_PROVEN, SG_DONE };
+struct SgEdge {
+  SgAttempt from;
+  int rc;
+  SgAttempt to;
+  uint32_t path;  // (tsdbhip_timing.paths)
+};
+static const SgEdge kSgEdges[] = {
+    {SG_FULL, RC_UG_FALLBACK, SG_NO_UNIFORM, TSDBHIP_PATH_UNIFORM_FALLBACK},
+    {SG_FULL, RC_REDO, SG_PROVEN, TSDBHIP_PATH_DIRECT_REDO},
+    {SG_NO_UNIFORM, RC_REDO, SG_PROVEN, TSDBHIP_PATH_DIRECT_REDO},
+};
 static int spangroup_run(Slot* ctx, const tsdbhip_sg_desc* d, tsdbhip_sg_out* out) {
   struct Reuse {  // (reset on every exit, exceptions included)
     Slot* c;
@@ -3724,17 +3744,22 @@ static int spangroup_run(Slot* ctx, const tsdbhip_sg_desc* d, tsdbhip_sg_out* ou
   } reuse{ctx};
   ctx->h2d_bytes = 0;
   ctx->reuse_inputs = false;
-  int rc = spangroup_run_once(ctx, d, out, true, true);
   uint32_t paths = 0;
-  if (rc == RC_UG_FALLBACK) {  // (the uniform path's aligned group did not stand)
-    paths |= TSDBHIP_PATH_UNIFORM_FALLBACK;
+  int rc = 0;
+  for (SgAttempt a = SG_FULL; a != SG_DONE;) {
+    rc = spangroup_run_once(ctx, d, out, a != SG_PROVEN, a == SG_FULL);
+    SgAttempt next = SG_DONE;
+    for (const SgEdge& e : kSgEdges)
+      if (e.from == a && e.rc == rc) {
+        next = e.to;
+        paths |= e.path;
+      }
+    if (next == SG_DONE && (rc == RC_REDO || rc == RC_UG_FALLBACK)) {  // (an attempt that may not rerun)
+      set_error(ctx, "spangroup_run: rerun code %d with no edge from attempt %d", rc, (int)a);
+      throw Fail{TSDBHIP_E_HIP};
+    }
     ctx->reuse_inputs = true;
-    rc = spangroup_run_once(ctx, d, out, true, false);
-  }
-  if (rc == RC_REDO) {
-    paths |= TSDBHIP_PATH_DIRECT_REDO;
-    ctx->reuse_inputs = true;
-    rc = spangroup_run_once(ctx, d, out, false, false);
+    a = next;
   }
   ctx->timing.paths |= paths;
   ctx->timing.h2d_bytes = ctx->h2d_bytes;
