@@ -2,22 +2,22 @@
 // (reference: src/core/CompactionQueue.java:243-743), the secondary path.
 //
 // Launches over a batch of rows (tsdbhip_rows_desc), in this order:
-//   k_compact_wave     the main kernel (round 6, see its comment below): one
+//   k_compact_wave     the plain rows (round 6, see its comment below): one
 //                      wave per run of CW_ROWS consecutive rows, staged in the
 //                      wave's own LDS with 16-B loads; the plain-row test flat
-//                      over the run's KVs, every other row (single KVs, junk,
-//                      errors, complexCompact of <= CW_SORT cells, the
-//                      write/delete decision) finished by the same wave from
-//                      the same LDS copy; the run's output written back with
-//                      16-B stores. Wave-level LDS syncs only: no block
-//                      barrier, so the CU's resident waves overlap each
-//                      other's staging, tests and stores. Rows it cannot hold
-//                      go to a pending list.
-//   k_compact_rows     the pending rows, 16 per block: bigger LDS tiles, a
-//                      wave per row (cq_row_lds), cq_row_global for rows over
-//                      that budget too;
+//                      over the run's KVs; plain rows' results and the run's
+//                      qualifier / value output written back with 16-B
+//                      stores; every other row left CQ_PENDING. Wave-level LDS
+//                      syncs only: no block barrier, so the CU's resident
+//                      waves overlap each other's staging, tests and stores;
+//   k_compact_rows     the CQ_PENDING rows, gathered per range of CR_RANGE rows,
+//                      a wave per row: staged into the wave's LDS, the whole
+//                      compact() of the row (single KVs, junk, errors,
+//                      complexCompact of <= CW_SORT cells) and its write/delete
+//                      decision from that copy; rows over its budget through
+//                      cq_row_global, bigger complex rows listed for
 //   k_compact_complex  one 256-thread block per complex row of more than
-//                      CT_SORT cells: breakDownValues (:690-743) into a cell
+//                      CW_SORT cells: breakDownValues (:690-743) into a cell
 //                      table (LDS, or global scratch for rows over
 //                      LDS_CELLS cells), then the stable sort + duplicate
 //                      check of complexCompact (:600-679) as a 4096-slot
@@ -26,8 +26,8 @@
 //                      must equal it byte for byte (same q[1], same value) or
 //                      the row is an IllegalDataException. Emission walks the
 //                      slots in delta order, which is the sorted order;
-//   k_compact_dups     the write/delete decision of the pending rows that
-//                      ended COMPLEX.
+//   k_compact_dups     the write/delete decision of the rows k_compact_complex
+//                      (or cq_row_global) finished COMPLEX.
 // Output placement needs no scan: row r writes at its input qualifier offset
 // and at its input value offset + r (include/tsdbhip.h). Byte work, HBM-bound;
 // no MFMA.
@@ -454,27 +454,9 @@ __global__ void __launch_bounds__(256) k_compact_complex(CompactArgs a) {
 // single KV, the in-order delta check of the trivial pre-pass :286-333,
 // legacy floats) and compacted by one wave from LDS copies of its KV lengths,
 // qualifier and value bytes, complex rows of <= SORT cells included
-// (k_compact_wave: the wave's piece; k_compact_rows: a 16-row tile).
+// (k_compact_rows: a wave per pending row).
 // ===========================================================================
-constexpr int CT_ROWS = 16;    // k_compact_rows: rows per tile
-constexpr int CT_QB = 4096;    // qualifier bytes per tile
-constexpr int CT_VB = 7168;    // value bytes per tile (with CT_KB: k_compact_rows fits 4 blocks per CU)
-constexpr int CT_KB = 1280;    // KVs per tile
-constexpr int CT_SORT = 256;   // cells of an in-wave complexCompact in k_compact_rows
 constexpr int CQ_RUNS_SLOTS = 12;
-
-struct __attribute__((aligned(16))) TileLds {
-  uint8_t qin[CT_QB + 32];
-  uint8_t vin[CT_VB + 32];
-  uint8_t qout[CT_QB + 32];
-  uint8_t vout[CT_VB + 32 + CT_ROWS];
-  uint8_t qlen[2 * CT_KB + 32];
-  uint8_t vlen[2 * CT_KB + 32];
-  uint32_t keys[4][CT_SORT];
-  uint32_t pay[4][CT_SORT];
-  uint32_t runs[4][CQ_RUNS_SLOTS];
-  uint32_t n_complex;  // rows of this block that reached complexCompact in-wave
-};
 
 DEVI uint32_t lds_q16(const uint8_t* p, uint32_t i) { return ((uint32_t)p[i] << 8) | p[i + 1]; }
 DEVI uint32_t lds_u16(const uint8_t* p, uint32_t i) { return (uint32_t)p[i] | ((uint32_t)p[i + 1] << 8); }

@@ -312,6 +312,7 @@ __global__ void __launch_bounds__(256) k_ug_dev(const uint8_t* val, const uint64
   uint64_t ov[PER], oq[PER];  // row offsets of the spans of the phase whose values load next
   auto slot = [&](uint32_t i) { return (w - 2) * SPL + NP * SPL * i + si; };  // span slot of the phase
   auto load_offs = [&](uint32_t ph) {
+    if (UG_DEV_ABL == 2) return;
 #pragma unroll
     for (uint32_t i = 0; i < PER; i++) {
       const uint32_t k = min(ph * DEV_B + slot(i), n_kept - 1);
@@ -320,6 +321,10 @@ __global__ void __launch_bounds__(256) k_ug_dev(const uint8_t* val, const uint64
     }
   };
   auto load_vals = [&]() {
+    if (UG_DEV_ABL == 2) {
+      for (uint32_t i = 0; i < PER; i++) { v[i] = (int64_t)i; q[i] = qexp; }
+      return;
+    }
 #pragma unroll
     for (uint32_t i = 0; i < PER; i++) {
       const uint8_t* p = val + ov[i] + (uint64_t)W * gc;
@@ -385,8 +390,11 @@ __global__ void __launch_bounds__(256) k_ug_dev(const uint8_t* val, const uint64
           if (j + u >= nk) break;  // (uniform)
           const double d = xa[u] - mean;
           const double qa = d * ra[u];
-#if UG_DEV_ABL  // (ablation builds only, wrong results: the product without its correction)
+#if UG_DEV_ABL == 1  // (ablation builds only, wrong results: 1 the product without its correction,
+                    // 2 no loads, 3 a one-add chain)
           const double nm = mean + qa;
+#elif UG_DEV_ABL == 3
+          const double nm = mean + xa[u];
 #else
           const double e = __builtin_fma(-da[u], qa, d);
           const double nm = mean + __builtin_fma(e, ra[u], qa);

@@ -70,7 +70,7 @@ def summary(root, tag):
         if h is not None and m is not None and h + m > 0:
             d["l2_hit_rate"] = h / (h + m)
         if c.get("SQ_WAVES") and wc and t:
-            d["avg_resident_waves"] = wc / (t * 1e-3 * 2.4e9) / 4  # (SQ_WAVE_CYCLES counts per 4 cycles on gfx9)
+            d["avg_resident_waves"] = 4 * wc / (t * 1e-3 * 2.4e9)  # (SQ_WAVE_CYCLES counts quad-cycles on gfx9: x4)
         e["derived"] = d
     return out
 
