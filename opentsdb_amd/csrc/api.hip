@@ -2297,10 +2297,10 @@ static int uniform_run(Slot* ctx, const UgIn& u, tsdbhip_sg_out* out, tsdbhip_ti
     EV_START(ctx, 8);
     constexpr uint32_t GP = UG_DEV_GP;  // (grid points a block)
     if (lsp.w8)
-      LAUNCH_STOP(EV_STOP_K(ctx, 9), (k_ug_dev<8, GP>), dim3((unsigned)((T + GP - 1) / GP)), dim3(256), 0, st,
+      LAUNCH_STOP(EV_STOP_K(ctx, 9), (k_ug_dev<8, GP>), dim3((unsigned)((T + GP - 1) / GP)), dim3(64 * (2 + UG_DEV_NP)), 0, st,
                   u.da.val, u.uk_vo, u.da.qual, u.uk_qo, q0, &sm->ls_broken, n_kept, T, gridv, x0, step, fin);
     else
-      LAUNCH_STOP(EV_STOP_K(ctx, 9), (k_ug_dev<4, GP>), dim3((unsigned)((T + GP - 1) / GP)), dim3(256), 0, st,
+      LAUNCH_STOP(EV_STOP_K(ctx, 9), (k_ug_dev<4, GP>), dim3((unsigned)((T + GP - 1) / GP)), dim3(64 * (2 + UG_DEV_NP)), 0, st,
                   u.da.val, u.uk_vo, u.da.qual, u.uk_qo, q0, &sm->ls_broken, n_kept, T, gridv, x0, step, fin);
     EV_STOP_M(ctx, 9);
   } else if (!sharded) {

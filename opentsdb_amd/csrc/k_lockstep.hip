@@ -264,9 +264,10 @@ __global__ void __launch_bounds__(256) k_lockstep(ReduceArgs r, LockstepArgs L) 
 //   waves 2-3  stream the values into LDS ahead of them — span k's GP values
 //           are W * GP contiguous bytes (cell g of every span sits at grid
 //           point g), 64 / GP spans a load instruction — DEV_B spans a phase,
-//           a software pipeline one phase deep (values of phase ph + 1 stored
-//           while those of ph + 2 and the row offsets of ph + 3 load), and
-//           convert them to double; they also prove the proposal as they
+//           a software pipeline over two register sets (values of phase
+//           ph + 1 stored while those of ph + 3 and the row offsets of ph + 5
+//           load: two phases of latency for each level), and convert them
+//           to double; they also prove the proposal as they
 //           stream: every qualifier is compared with (x0 + g step - base) << 4
 //           | flags (as k_lockstep); a mismatch sets `broken` and the call
 //           runs again on the proven path.
@@ -276,19 +277,30 @@ __global__ void __launch_bounds__(256) k_lockstep(ReduceArgs r, LockstepArgs L) 
 // rounding midpoint and stays normal here — bit-exact with the division; n
 // and r are uniform (n = span index + 1) and come from the producers. The mean
 // chain is then five dependent double operations a step on a SIMD of its own
-// (round 6: 95 -> 63 ms for C3's 1M series, 9.5 -> 6.3 ms for 100k, with GP =
-// 16: 225 blocks instead of 57, and the conversions off the chain).
-constexpr uint32_t DEV_B = 96;  // spans a phase
+// (round 6: 95 -> 56.7 ms for C3's 1M series, 9.5 -> 5.7 ms for 100k, with
+// GP = 16: 225 blocks instead of 57, and the conversions off the chain; then
+// 64-span phases 44.8 ms and the two-set producer pipeline 41.3 ms. Without
+// the mean chain the kernel takes 32 ms: the chain is the limiter now.)
+#ifndef UG_DEV_B
+#define UG_DEV_B 64u  // (C3 1M series: 16 / 32 / 48 / 64 / 80 / 96 / 128 spans 73.7 / 55.2 / 48.4 / 44.8 / 57.0 / 56.7 / 57.7 ms)
+#endif
+#ifndef UG_DEV_U
+#define UG_DEV_U 8u  // chain steps whose LDS reads are in flight together
+#endif
+#ifndef UG_DEV_NP
+#define UG_DEV_NP 2u  // producer waves (the block: 2 + UG_DEV_NP waves)
+#endif
+constexpr uint32_t DEV_B = UG_DEV_B;  // spans a phase
 #ifndef UG_DEV_ABL
 #define UG_DEV_ABL 0
 #endif
 template <uint32_t W, uint32_t GP>
-__global__ void __launch_bounds__(256) k_ug_dev(const uint8_t* val, const uint64_t* vo, const uint8_t* qual,
+__global__ void __launch_bounds__(64 * (2 + UG_DEV_NP)) k_ug_dev(const uint8_t* val, const uint64_t* vo, const uint8_t* qual,
                                                const uint64_t* qo, uint32_t q0, uint32_t* broken, uint32_t n_kept,
                                                uint64_t T, uint32_t* grid, uint32_t x0, uint32_t step, FinalArgs f) {
   static_assert(GP == 16 || GP == 32 || GP == 64, "grid points a block");
   constexpr uint32_t SPL = WAVE / GP;  // spans a producer load instruction
-  constexpr uint32_t NP = 2;           // producer waves
+  constexpr uint32_t NP = UG_DEV_NP;   // producer waves
   static_assert(DEV_B % (NP * SPL) == 0, "a phase's spans split over the producers");
   __shared__ double s_buf[3][DEV_B][GP];              // the values (three phases: producers, chain, M2 sums)
   __shared__ double2 s_dm[2][DEV_B][GP];              // each step's (x - mean, mean')
@@ -307,32 +319,38 @@ __global__ void __launch_bounds__(256) k_ug_dev(const uint8_t* val, const uint64
   const uint32_t qexp = ((qe & 0xFFu) << 8) | (qe >> 8);
   uint32_t bad = 0;
   constexpr uint32_t PER = DEV_B / (NP * SPL);  // load instructions a producer a phase
-  int64_t v[PER];
-  uint32_t q[PER];
-  uint64_t ov[PER], oq[PER];  // row offsets of the spans of the phase whose values load next
+  // a producer's register set: the values of phase p and the row offsets of
+  // phase p + 2 (two sets: values two phases ahead of their store, offsets two
+  // phases ahead of their values)
+  struct DevSet {
+    int64_t v[PER];
+    uint32_t q[PER];
+    uint64_t ov[PER], oq[PER];
+  };
+  DevSet sa, sb;
   auto slot = [&](uint32_t i) { return (w - 2) * SPL + NP * SPL * i + si; };  // span slot of the phase
-  auto load_offs = [&](uint32_t ph) {
+  auto load_offs = [&](DevSet& S, uint32_t ph) {  // (spans past the last: the last one's, never stored)
     if (UG_DEV_ABL == 2) return;
 #pragma unroll
     for (uint32_t i = 0; i < PER; i++) {
       const uint32_t k = min(ph * DEV_B + slot(i), n_kept - 1);
-      ov[i] = vo[k];
-      oq[i] = qo[k];
+      S.ov[i] = vo[k];
+      S.oq[i] = qo[k];
     }
   };
-  auto load_vals = [&]() {
+  auto load_vals = [&](DevSet& S) {
     if (UG_DEV_ABL == 2) {
-      for (uint32_t i = 0; i < PER; i++) { v[i] = (int64_t)i; q[i] = qexp; }
+      for (uint32_t i = 0; i < PER; i++) { S.v[i] = (int64_t)i; S.q[i] = qexp; }
       return;
     }
 #pragma unroll
     for (uint32_t i = 0; i < PER; i++) {
-      const uint8_t* p = val + ov[i] + (uint64_t)W * gc;
-      v[i] = W == 8 ? (int64_t)bswap64(*(const uint64_t*)p) : (int64_t)(int32_t)bswap32(*(const uint32_t*)p);
-      q[i] = *(const uint16_t*)(qual + oq[i] + 2 * gc);
+      const uint8_t* p = val + S.ov[i] + (uint64_t)W * gc;
+      S.v[i] = W == 8 ? (int64_t)bswap64(*(const uint64_t*)p) : (int64_t)(int32_t)bswap32(*(const uint32_t*)p);
+      S.q[i] = *(const uint16_t*)(qual + S.oq[i] + 2 * gc);
     }
   };
-  auto store = [&](uint32_t ph) {  // phase ph's values (in v, q), converted, and its counts
+  auto store = [&](uint32_t ph, const DevSet& S) {  // phase ph's values, converted, and its counts
     if (w == 2)
       for (uint32_t j = (uint32_t)lane; j < DEV_B; j += WAVE) {
         const double dn = (double)(ph * DEV_B + j + 1);
@@ -341,36 +359,40 @@ __global__ void __launch_bounds__(256) k_ug_dev(const uint8_t* val, const uint64
       }
 #pragma unroll
     for (uint32_t i = 0; i < PER; i++) {
-      s_buf[ph % 3][slot(i)][gl] = (double)v[i];
-      bad |= q[i] ^ qexp;
+      s_buf[ph % 3][slot(i)][gl] = (double)S.v[i];
+      if (ph * DEV_B + slot(i) < n_kept) bad |= S.q[i] ^ qexp;
     }
   };
-  if (w >= 2) {
-    load_offs(0);
-    load_vals();
-    store(0);
-    if (nph > 1) {
-      load_offs(1);
-      load_vals();
-    }
-    if (nph > 2) load_offs(2);
+  if (w >= 2) {  // phase 0 stored; sa: values of 1, offsets of 3; sb: values of 2, offsets of 4
+    load_offs(sa, 0);
+    load_vals(sa);
+    store(0, sa);
+    load_offs(sa, 1);
+    load_offs(sb, 2);
+    load_vals(sa);
+    load_vals(sb);
+    load_offs(sa, 3);
+    load_offs(sb, 4);
   }
   __syncthreads();
   double mean = 0, var = 0;
-  for (uint32_t ph = 0; ph <= nph; ph++) {
+  // one phase: the producers store phase ph + 1 from `cur` and refill it
+  // (values of ph + 3, offsets of ph + 5); wave 0 runs the chains over phase
+  // ph, wave 1 the M2 sums over ph - 1
+  auto phase = [&](uint32_t ph, DevSet& cur) {
     if (w >= 2) {
-      if (ph + 1 < nph) store(ph + 1);
-      if (ph + 2 < nph) load_vals();
-      if (ph + 3 < nph) load_offs(ph + 3);
-    } else if (w == 0 && ph < nph && (uint32_t)lane < GP) {  // the mean chains
+      if (ph + 1 < nph) store(ph + 1, cur);
+      if (ph + 3 < nph) load_vals(cur);
+      if (ph + 5 < nph) load_offs(cur, ph + 5);
+    } else if (w == 0 && ph < nph && (uint32_t)lane < GP && UG_DEV_ABL != 5) {  // the mean chains
       const uint32_t nk = min(DEV_B, n_kept - ph * DEV_B), b3 = ph % 3, b2 = ph & 1;
       uint32_t j = 0;
       if (ph == 0) {  // (wf_push's first value: mean = x)
         mean = s_buf[0][0][lane];
         j = 1;
       }
-      // the LDS reads of the next 8 steps in flight during these 8
-      constexpr uint32_t U = 8;
+      // the LDS reads of the next U steps in flight during these U
+      constexpr uint32_t U = UG_DEV_U;
       double xa[U], ra[U], da[U];
       auto fetch = [&](uint32_t j0, double* x, double* r, double* dn) {
 #pragma unroll
@@ -391,7 +413,7 @@ __global__ void __launch_bounds__(256) k_ug_dev(const uint8_t* val, const uint64
           const double d = xa[u] - mean;
           const double qa = d * ra[u];
 #if UG_DEV_ABL == 1  // (ablation builds only, wrong results: 1 the product without its correction,
-                    // 2 no loads, 3 a one-add chain)
+                    // 2 no loads, 3 a one-add chain, 4 no M2 sums, 5 no mean chain)
           const double nm = mean + qa;
 #elif UG_DEV_ABL == 3
           const double nm = mean + xa[u];
@@ -409,7 +431,7 @@ __global__ void __launch_bounds__(256) k_ug_dev(const uint8_t* val, const uint64
           da[u] = db[u];
         }
       }
-    } else if (w == 1 && ph >= 1 && (uint32_t)lane < GP) {  // the M2 sums of the phase before
+    } else if (w == 1 && ph >= 1 && (uint32_t)lane < GP && UG_DEV_ABL != 4) {  // the M2 sums of the phase before
       const uint32_t p = ph - 1, nk = min(DEV_B, n_kept - p * DEV_B), b3 = p % 3, b2 = p & 1;
       for (uint32_t j = p == 0 ? 1u : 0u; j < nk; j++) {
         const double2 dm = s_dm[b2][j][lane];
@@ -417,6 +439,10 @@ __global__ void __launch_bounds__(256) k_ug_dev(const uint8_t* val, const uint64
       }
     }
     __syncthreads();
+  };
+  for (uint32_t ph = 0; ph <= nph; ph += 2) {
+    phase(ph, sa);
+    if (ph + 1 <= nph) phase(ph + 1, sb);
   }
   if (w == 1 && (uint32_t)lane < GP) s_var[lane] = var;
   if (w >= 2 && ballot(bad != 0) && lane == 0) atomicOr(broken, 1u);

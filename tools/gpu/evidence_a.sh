@@ -4,7 +4,7 @@
 # same command, the 2/4/8-way shard rehearsals (C3*, and C3 rate sum 8-way)
 # with the 8-way C3* step trace. Output under gpurun_out/$R/ (R: round tag).
 set -o pipefail
-R=${R:-r05}
+R=${R:-r06}
 O=gpurun_out/$R; mkdir -p $O
 timeout -k 10 900 python -u -m pytest tests -q -x --tb=short -rf --timeout 600 --timeout-method thread -m gpu --durations=15 \
   > $O/pytest_gpu.log 2>&1; rc=$?; tail -3 $O/pytest_gpu.log; [ $rc -eq 0 ] || exit $rc
