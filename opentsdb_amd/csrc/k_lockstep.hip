@@ -279,16 +279,20 @@ __global__ void __launch_bounds__(256) k_lockstep(ReduceArgs r, LockstepArgs L) 
 // chain is then five dependent double operations a step on a SIMD of its own
 // (round 6: 95 -> 56.7 ms for C3's 1M series, 9.5 -> 5.7 ms for 100k, with
 // GP = 16: 225 blocks instead of 57, and the conversions off the chain; then
-// 64-span phases 44.8 ms and the two-set producer pipeline 41.3 ms. Without
-// the mean chain the kernel takes 32 ms: the chain is the limiter now.)
+// 64-span phases 44.8 ms, the two-set producer pipeline 41.3 ms, the chain's
+// LDS reads a group ahead (scheduling barrier) 39.8 ms, four producer waves
+// 39.2 ms. Without the mean chain the kernel takes 30 ms.)
 #ifndef UG_DEV_B
 #define UG_DEV_B 64u  // (C3 1M series: 16 / 32 / 48 / 64 / 80 / 96 / 128 spans 73.7 / 55.2 / 48.4 / 44.8 / 57.0 / 56.7 / 57.7 ms)
 #endif
 #ifndef UG_DEV_U
 #define UG_DEV_U 8u  // chain steps whose LDS reads are in flight together
 #endif
+#ifndef UG_DEV_DEPTH
+#define UG_DEV_DEPTH 2u  // producer register sets (phases of load latency)
+#endif
 #ifndef UG_DEV_NP
-#define UG_DEV_NP 2u  // producer waves (the block: 2 + UG_DEV_NP waves)
+#define UG_DEV_NP 4u  // producer waves (the block: 2 + UG_DEV_NP waves; C3 1M series 2 / 4: 39.8 / 39.2 ms)
 #endif
 constexpr uint32_t DEV_B = UG_DEV_B;  // spans a phase
 #ifndef UG_DEV_ABL
@@ -304,7 +308,7 @@ __global__ void __launch_bounds__(64 * (2 + UG_DEV_NP)) k_ug_dev(const uint8_t* 
   static_assert(DEV_B % (NP * SPL) == 0, "a phase's spans split over the producers");
   __shared__ double s_buf[3][DEV_B][GP];              // the values (three phases: producers, chain, M2 sums)
   __shared__ double2 s_dm[2][DEV_B][GP];              // each step's (x - mean, mean')
-  __shared__ double s_rcp[2][DEV_B], s_dn[2][DEV_B];  // RN(1/n), n (n = span index + 1)
+  __shared__ double s_rcp[2][DEV_B];                  // RN(1/n) (n = span index + 1)
   __shared__ double s_var[GP];
   const uint32_t w = __builtin_amdgcn_readfirstlane(threadIdx.x / WAVE);
   const int lane = lane_id();
@@ -327,7 +331,9 @@ __global__ void __launch_bounds__(64 * (2 + UG_DEV_NP)) k_ug_dev(const uint8_t* 
     uint32_t q[PER];
     uint64_t ov[PER], oq[PER];
   };
-  DevSet sa, sb;
+  constexpr uint32_t D = UG_DEV_DEPTH;  // register sets: values D phases ahead of their store
+  static_assert(D == 2 || D == 3, "pipeline depth");
+  DevSet sa, sb, sc;
   auto slot = [&](uint32_t i) { return (w - 2) * SPL + NP * SPL * i + si; };  // span slot of the phase
   auto load_offs = [&](DevSet& S, uint32_t ph) {  // (spans past the last: the last one's, never stored)
     if (UG_DEV_ABL == 2) return;
@@ -354,7 +360,6 @@ __global__ void __launch_bounds__(64 * (2 + UG_DEV_NP)) k_ug_dev(const uint8_t* 
     if (w == 2)
       for (uint32_t j = (uint32_t)lane; j < DEV_B; j += WAVE) {
         const double dn = (double)(ph * DEV_B + j + 1);
-        s_dn[ph & 1][j] = dn;
         s_rcp[ph & 1][j] = 1.0 / dn;
       }
 #pragma unroll
@@ -363,73 +368,82 @@ __global__ void __launch_bounds__(64 * (2 + UG_DEV_NP)) k_ug_dev(const uint8_t* 
       if (ph * DEV_B + slot(i) < n_kept) bad |= S.q[i] ^ qexp;
     }
   };
-  if (w >= 2) {  // phase 0 stored; sa: values of 1, offsets of 3; sb: values of 2, offsets of 4
+  if (w >= 2) {  // phase 0 stored; set i (of D): values of phase 1 + i, offsets of 1 + i + D
     load_offs(sa, 0);
     load_vals(sa);
     store(0, sa);
     load_offs(sa, 1);
     load_offs(sb, 2);
+    if (D == 3) load_offs(sc, 3);
     load_vals(sa);
     load_vals(sb);
-    load_offs(sa, 3);
-    load_offs(sb, 4);
+    if (D == 3) load_vals(sc);
+    load_offs(sa, 1 + D);
+    load_offs(sb, 2 + D);
+    if (D == 3) load_offs(sc, 3 + D);
   }
   __syncthreads();
   double mean = 0, var = 0;
   // one phase: the producers store phase ph + 1 from `cur` and refill it
-  // (values of ph + 3, offsets of ph + 5); wave 0 runs the chains over phase
-  // ph, wave 1 the M2 sums over ph - 1
+  // (values of ph + 1 + D, offsets of ph + 1 + 2 D); wave 0 runs the chains
+  // over phase ph, wave 1 the M2 sums over ph - 1
   auto phase = [&](uint32_t ph, DevSet& cur) {
     if (w >= 2) {
       if (ph + 1 < nph) store(ph + 1, cur);
-      if (ph + 3 < nph) load_vals(cur);
-      if (ph + 5 < nph) load_offs(cur, ph + 5);
+      if (ph + 1 + D < nph) load_vals(cur);
+      if (ph + 1 + 2 * D < nph) load_offs(cur, ph + 1 + 2 * D);
     } else if (w == 0 && ph < nph && (uint32_t)lane < GP && UG_DEV_ABL != 5) {  // the mean chains
+      // (span 0 takes the same step from mean = 0 with n = 1: d = x, q = x
+      // exactly, mean' = x — wf_push's first value — so no step is special)
       const uint32_t nk = min(DEV_B, n_kept - ph * DEV_B), b3 = ph % 3, b2 = ph & 1;
-      uint32_t j = 0;
-      if (ph == 0) {  // (wf_push's first value: mean = x)
-        mean = s_buf[0][0][lane];
-        j = 1;
-      }
-      // the LDS reads of the next U steps in flight during these U
-      constexpr uint32_t U = UG_DEV_U;
-      double xa[U], ra[U], da[U];
-      auto fetch = [&](uint32_t j0, double* x, double* r, double* dn) {
-#pragma unroll
-        for (uint32_t u = 0; u < U; u++) {
-          const uint32_t jj = min(j0 + u, DEV_B - 1);
-          x[u] = s_buf[b3][jj][lane];
-          r[u] = s_rcp[b2][jj];
-          dn[u] = s_dn[b2][jj];
-        }
-      };
-      fetch(j, xa, ra, da);
-      for (; j < nk; j += U) {
-        double xb[U], rb[U], db[U];
-        fetch(j + U, xb, rb, db);
-#pragma unroll
-        for (uint32_t u = 0; u < U; u++) {
-          if (j + u >= nk) break;  // (uniform)
-          const double d = xa[u] - mean;
-          const double qa = d * ra[u];
+      const uint32_t base = ph * DEV_B + 1;  // n of the phase's first span
+      auto chain_step = [&](uint32_t j, double x, double r) {
+        const double dn = (double)(base + j);  // (exact: n < 2^32)
+        const double d = x - mean;
+        const double qa = d * r;
 #if UG_DEV_ABL == 1  // (ablation builds only, wrong results: 1 the product without its correction,
                     // 2 no loads, 3 a one-add chain, 4 no M2 sums, 5 no mean chain)
-          const double nm = mean + qa;
+        const double nm = mean + qa;
 #elif UG_DEV_ABL == 3
-          const double nm = mean + xa[u];
+        const double nm = mean + x;
 #else
-          const double e = __builtin_fma(-da[u], qa, d);
-          const double nm = mean + __builtin_fma(e, ra[u], qa);
+        const double e = __builtin_fma(-dn, qa, d);
+        const double nm = mean + __builtin_fma(e, r, qa);
 #endif
-          s_dm[b2][j + u][lane] = make_double2(d, nm);
-          mean = nm;
-        }
+        s_dm[b2][j][lane] = make_double2(d, nm);
+        mean = nm;
+      };
+      constexpr uint32_t U = UG_DEV_U;
+      static_assert(DEV_B % U == 0, "chain groups");
+      if (nk == DEV_B) {
+        // a full phase, straight-line: the next U steps' LDS reads issued
+        // before this group's chain (the scheduling barrier keeps them there;
+        // without it the compiler sank each read next to its use, an LDS
+        // latency on every step of the chain)
+        double xa[U], ra[U];
+        auto fetch = [&](uint32_t j0, double* x, double* r) {
 #pragma unroll
-        for (uint32_t u = 0; u < U; u++) {
-          xa[u] = xb[u];
-          ra[u] = rb[u];
-          da[u] = db[u];
+          for (uint32_t u = 0; u < U; u++) {
+            x[u] = s_buf[b3][j0 + u][lane];
+            r[u] = s_rcp[b2][j0 + u];
+          }
+        };
+        fetch(0, xa, ra);
+        for (uint32_t j = 0; j < DEV_B; j += U) {
+          double xb[U], rb[U];
+          fetch(j + U < DEV_B ? j + U : j, xb, rb);  // (the last group re-reads itself)
+          __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+          for (uint32_t u = 0; u < U; u++) chain_step(j + u, xa[u], ra[u]);
+          __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+          for (uint32_t u = 0; u < U; u++) {
+            xa[u] = xb[u];
+            ra[u] = rb[u];
+          }
         }
+      } else {  // the last, partial phase
+        for (uint32_t j = 0; j < nk; j++) chain_step(j, s_buf[b3][j][lane], s_rcp[b2][j]);
       }
     } else if (w == 1 && ph >= 1 && (uint32_t)lane < GP && UG_DEV_ABL != 4) {  // the M2 sums of the phase before
       const uint32_t p = ph - 1, nk = min(DEV_B, n_kept - p * DEV_B), b3 = p % 3, b2 = p & 1;
@@ -440,9 +454,10 @@ __global__ void __launch_bounds__(64 * (2 + UG_DEV_NP)) k_ug_dev(const uint8_t* 
     }
     __syncthreads();
   };
-  for (uint32_t ph = 0; ph <= nph; ph += 2) {
+  for (uint32_t ph = 0; ph <= nph; ph += D) {
     phase(ph, sa);
     if (ph + 1 <= nph) phase(ph + 1, sb);
+    if (D == 3 && ph + 2 <= nph) phase(ph + 2, sc);
   }
   if (w == 1 && (uint32_t)lane < GP) s_var[lane] = var;
   if (w >= 2 && ballot(bad != 0) && lane == 0) atomicOr(broken, 1u);
