@@ -86,6 +86,8 @@ extern "C" {
 #define TSDBHIP_HOT_LOCKSTEP    6 /* k_lockstep: one pass over qualifiers + values of a lockstep group */
 #define TSDBHIP_HOT_UG_DS_REG   7 /* k_ug_ds_reg: the uniform aligned group in one launch */
 #define TSDBHIP_HOT_UG_DEV      8 /* k_ug_dev: integer dev chains of a uniform group */
+#define TSDBHIP_HOT_DS_E        9 /* k_ds_reg in the uniform E variant: the spans' bucket values
+                                     on the key's buckets (k_ug_reduce runs after it) */
 #define TSDBHIP_HOT_COMPACT     4 /* k_compact_wave: every row's classification and compaction
                                      in one pass (tsdbhip_compact_rows)      */
 

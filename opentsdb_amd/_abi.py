@@ -95,7 +95,7 @@ class SgOut(C.Structure):
 
 HOT_NONE, HOT_DS_CHUNKS, HOT_DECODE_FAST, HOT_DECODE_GEN = 0, 1, 2, 3
 HOT_NAMES = {1: "k_ds_reg+k_ds_spans", 2: "k_decode_fast", 3: "k_decode_general", 4: "k_compact_wave",
-             5: "k_reduce", 6: "k_lockstep", 7: "k_ug_ds_reg", 8: "k_ug_dev"}
+             5: "k_reduce", 6: "k_lockstep", 7: "k_ug_ds_reg", 8: "k_ug_dev", 9: "k_ds_reg"}
 
 
 class Timing(C.Structure):

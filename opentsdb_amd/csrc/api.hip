@@ -2124,7 +2124,7 @@ static void ug_e_launch(Slot* ctx, const UgIn& u, uint64_t T, uint32_t e_kk, int
   // k_ds_reg in E mode (its block 0 writes G from the key, the spans their
   // bucket values; an outsider sets the broken flag), then k_ug_reduce:
   // every span's E is G itself (no bitmap, no grid ranks, no cursors)
-  ctx->hot_kernel = TSDBHIP_HOT_DS_CHUNKS;
+  ctx->hot_kernel = TSDBHIP_HOT_DS_E;
   const uint64_t rps = d->n_rows / std::max<uint32_t>(n_kept, 1);
   const uint32_t wps_log2 = rps >= 12 ? 2 : (rps >= 6 ? 1 : 0);
   // (waves a span, its rows in contiguous pieces: C2's 24 rows a span, 0.266

@@ -289,7 +289,7 @@ __global__ void __launch_bounds__(256) k_lockstep(ReduceArgs r, LockstepArgs L) 
 #define UG_DEV_U 8u  // chain steps whose LDS reads are in flight together
 #endif
 #ifndef UG_DEV_DEPTH
-#define UG_DEV_DEPTH 2u  // producer register sets (phases of load latency)
+#define UG_DEV_DEPTH 3u  // producer register sets (phases of load latency; 2 / 3: 39.2 / 35.0 ms)
 #endif
 #ifndef UG_DEV_NP
 #define UG_DEV_NP 4u  // producer waves (the block: 2 + UG_DEV_NP waves; C3 1M series 2 / 4: 39.8 / 39.2 ms)
@@ -332,8 +332,8 @@ __global__ void __launch_bounds__(64 * (2 + UG_DEV_NP)) k_ug_dev(const uint8_t* 
     uint64_t ov[PER], oq[PER];
   };
   constexpr uint32_t D = UG_DEV_DEPTH;  // register sets: values D phases ahead of their store
-  static_assert(D == 2 || D == 3, "pipeline depth");
-  DevSet sa, sb, sc;
+  static_assert(D >= 2 && D <= 4, "pipeline depth");
+  DevSet sa, sb, sc, sd;
   auto slot = [&](uint32_t i) { return (w - 2) * SPL + NP * SPL * i + si; };  // span slot of the phase
   auto load_offs = [&](DevSet& S, uint32_t ph) {  // (spans past the last: the last one's, never stored)
     if (UG_DEV_ABL == 2) return;
@@ -374,13 +374,16 @@ __global__ void __launch_bounds__(64 * (2 + UG_DEV_NP)) k_ug_dev(const uint8_t* 
     store(0, sa);
     load_offs(sa, 1);
     load_offs(sb, 2);
-    if (D == 3) load_offs(sc, 3);
+    if (D >= 3) load_offs(sc, 3);
+    if (D >= 4) load_offs(sd, 4);
     load_vals(sa);
     load_vals(sb);
-    if (D == 3) load_vals(sc);
+    if (D >= 3) load_vals(sc);
+    if (D >= 4) load_vals(sd);
     load_offs(sa, 1 + D);
     load_offs(sb, 2 + D);
-    if (D == 3) load_offs(sc, 3 + D);
+    if (D >= 3) load_offs(sc, 3 + D);
+    if (D >= 4) load_offs(sd, 4 + D);
   }
   __syncthreads();
   double mean = 0, var = 0;
@@ -457,7 +460,8 @@ __global__ void __launch_bounds__(64 * (2 + UG_DEV_NP)) k_ug_dev(const uint8_t* 
   for (uint32_t ph = 0; ph <= nph; ph += D) {
     phase(ph, sa);
     if (ph + 1 <= nph) phase(ph + 1, sb);
-    if (D == 3 && ph + 2 <= nph) phase(ph + 2, sc);
+    if (D >= 3 && ph + 2 <= nph) phase(ph + 2, sc);
+    if (D >= 4 && ph + 3 <= nph) phase(ph + 3, sd);
   }
   if (w == 1 && (uint32_t)lane < GP) s_var[lane] = var;
   if (w >= 2 && ballot(bad != 0) && lane == 0) atomicOr(broken, 1u);

@@ -7,7 +7,8 @@ import sys
 ORDER = [("c1", "C1"), ("c2", "C2"), ("c3", "C3 sum (no rate)"), ("c3r_sum", "C3 rate sum"),
          ("c3r_max", "C3 rate max"), ("c3r_dev", "C3 rate dev"), ("c3s", "C3* (headline)"),
          ("c3s_gb100", "C3* GROUP BY 100"), ("c3s_gb10k", "C3* GROUP BY 10k"), ("c3_gb100", "C3 GROUP BY 100"),
-         ("c4", "C4"), ("c4i", "C4-int"), ("c5", "C5"), ("c3_dev_100k", "C3 shape, 100k series, integer dev")]
+         ("c4", "C4"), ("c4i", "C4-int"), ("c5", "C5"), ("c3_dev", "C3 shape, 1M series, integer dev"),
+         ("c3_dev_100k", "C3 shape, 100k series, integer dev")]
 PAR = "bit-exact ints; doubles 1e-9 / bit-exact with EXACT_ORDER"
 d = sys.argv[1]
 print("| config | GPUs | value | ms/step | achieved (dominant kernel) | % of 8 TB/s | CPU value | CPU threads | parity |")
