@@ -597,12 +597,29 @@ extern "C" int tsdbhip_ranks(tsdbhip_ctx* ctx) {
 
 // The registered host ranges [p, p + n): the in-kernel finalize writes a long
 // result through a mapped pointer only into a range that holds all of it
-// (mapped_dev_ptr).
+// (mapped_dev_ptr). A HIP registration is process-wide, so contexts share it:
+// each entry counts its tsdbhip_host_register calls, and the range is
+// unregistered from HIP (and dropped here) only by the last unregister
+// (ADVICE r5).
+struct RegEntry {
+  size_t n;
+  uint32_t refs;
+};
 static std::mutex g_reg_mu;
-static std::map<uintptr_t, size_t> g_reg;
+static std::map<uintptr_t, RegEntry> g_reg;
 
 extern "C" int tsdbhip_host_register(tsdbhip_ctx* ctx, void* p, size_t n) {
   if (!ctx || !p || !n) return TSDBHIP_E_INVALID_ARG;
+  std::lock_guard<std::mutex> lk(g_reg_mu);
+  auto it = g_reg.find((uintptr_t)p);
+  if (it != g_reg.end()) {  // (registered by this library already: the same range, shared)
+    if (it->second.n != n) {
+      set_error(ctx, "host_register: %p is registered with %zu bytes, not %zu", p, it->second.n, n);
+      return TSDBHIP_E_INVALID_ARG;
+    }
+    it->second.refs++;
+    return TSDBHIP_OK;
+  }
   try {
     HIPCHK(hipSetDevice(ctx->device));
     // (portable: pinned for every device of a multi-device context)
@@ -611,21 +628,25 @@ extern "C" int tsdbhip_host_register(tsdbhip_ctx* ctx, void* p, size_t n) {
   } catch (Fail& f) {
     return f.code;
   }
-  std::lock_guard<std::mutex> lk(g_reg_mu);
-  g_reg[(uintptr_t)p] = n;
+  g_reg[(uintptr_t)p] = RegEntry{n, 1};
   return TSDBHIP_OK;
 }
 
 extern "C" int tsdbhip_host_unregister(tsdbhip_ctx* ctx, void* p) {
   if (!ctx || !p) return TSDBHIP_E_INVALID_ARG;
+  std::lock_guard<std::mutex> lk(g_reg_mu);
+  auto it = g_reg.find((uintptr_t)p);
+  if (it != g_reg.end() && it->second.refs > 1) {
+    it->second.refs--;
+    return TSDBHIP_OK;
+  }
   try {
     HIPCHK(hipSetDevice(ctx->device));
     HIPCHK(hipHostUnregister(p));
   } catch (Fail& f) {
     return f.code;
   }
-  std::lock_guard<std::mutex> lk(g_reg_mu);
-  g_reg.erase((uintptr_t)p);
+  if (it != g_reg.end()) g_reg.erase(it);
   return TSDBHIP_OK;
 }
 
@@ -1798,7 +1819,7 @@ static void* mapped_dev_ptr(void* h, size_t bytes) {
     auto it = g_reg.upper_bound((uintptr_t)h);
     if (it == g_reg.begin()) return nullptr;
     --it;
-    if ((uintptr_t)h + bytes > it->first + it->second) return nullptr;
+    if ((uintptr_t)h + bytes > it->first + it->second.n) return nullptr;
   }
   void* d = nullptr;
   if (hipHostGetDevicePointer(&d, h, 0) != hipSuccess) {
