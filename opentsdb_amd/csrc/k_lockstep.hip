@@ -291,6 +291,9 @@ __global__ void __launch_bounds__(256) k_lockstep(ReduceArgs r, LockstepArgs L) 
 #ifndef UG_DEV_DEPTH
 #define UG_DEV_DEPTH 3u  // producer register sets (phases of load latency; 2 / 3: 39.2 / 35.0 ms)
 #endif
+#ifndef UG_DEV_AHEAD
+#define UG_DEV_AHEAD 1u  // phases the producers store ahead of the chain
+#endif
 #ifndef UG_DEV_NP
 #define UG_DEV_NP 4u  // producer waves (the block: 2 + UG_DEV_NP waves; C3 1M series 2 / 4: 39.8 / 39.2 ms)
 #endif
@@ -306,9 +309,12 @@ __global__ void __launch_bounds__(64 * (2 + UG_DEV_NP)) k_ug_dev(const uint8_t* 
   constexpr uint32_t SPL = WAVE / GP;  // spans a producer load instruction
   constexpr uint32_t NP = UG_DEV_NP;   // producer waves
   static_assert(DEV_B % (NP * SPL) == 0, "a phase's spans split over the producers");
-  __shared__ double s_buf[3][DEV_B][GP];              // the values (three phases: producers, chain, M2 sums)
+  constexpr uint32_t AH = UG_DEV_AHEAD;  // phases the producers store ahead of the chain
+  static_assert(AH == 1 || AH == 2, "store lead");
+  constexpr uint32_t RB = AH + 2;        // the value ring: stored, (stored earlier,) chain, M2 sums
+  __shared__ double s_buf[RB][DEV_B][GP];
   __shared__ double2 s_dm[2][DEV_B][GP];              // each step's (x - mean, mean')
-  __shared__ double s_rcp[2][DEV_B];                  // RN(1/n) (n = span index + 1)
+  __shared__ double s_rcp[RB][DEV_B];                 // RN(1/n) (n = span index + 1)
   __shared__ double s_var[GP];
   const uint32_t w = __builtin_amdgcn_readfirstlane(threadIdx.x / WAVE);
   const int lane = lane_id();
@@ -360,11 +366,11 @@ __global__ void __launch_bounds__(64 * (2 + UG_DEV_NP)) k_ug_dev(const uint8_t* 
     if (w == 2)
       for (uint32_t j = (uint32_t)lane; j < DEV_B; j += WAVE) {
         const double dn = (double)(ph * DEV_B + j + 1);
-        s_rcp[ph & 1][j] = 1.0 / dn;
+        s_rcp[ph % RB][j] = 1.0 / dn;
       }
 #pragma unroll
     for (uint32_t i = 0; i < PER; i++) {
-      s_buf[ph % 3][slot(i)][gl] = (double)S.v[i];
+      s_buf[ph % RB][slot(i)][gl] = (double)S.v[i];
       if (ph * DEV_B + slot(i) < n_kept) bad |= S.q[i] ^ qexp;
     }
   };
@@ -372,18 +378,23 @@ __global__ void __launch_bounds__(64 * (2 + UG_DEV_NP)) k_ug_dev(const uint8_t* 
     load_offs(sa, 0);
     load_vals(sa);
     store(0, sa);
-    load_offs(sa, 1);
-    load_offs(sb, 2);
-    if (D >= 3) load_offs(sc, 3);
-    if (D >= 4) load_offs(sd, 4);
+    if (AH == 2) {
+      load_offs(sa, 1);
+      load_vals(sa);
+      store(1, sa);
+    }
+    load_offs(sa, AH);
+    load_offs(sb, AH + 1);
+    if (D >= 3) load_offs(sc, AH + 2);
+    if (D >= 4) load_offs(sd, AH + 3);
     load_vals(sa);
     load_vals(sb);
     if (D >= 3) load_vals(sc);
     if (D >= 4) load_vals(sd);
-    load_offs(sa, 1 + D);
-    load_offs(sb, 2 + D);
-    if (D >= 3) load_offs(sc, 3 + D);
-    if (D >= 4) load_offs(sd, 4 + D);
+    load_offs(sa, AH + D);
+    load_offs(sb, AH + 1 + D);
+    if (D >= 3) load_offs(sc, AH + 2 + D);
+    if (D >= 4) load_offs(sd, AH + 3 + D);
   }
   __syncthreads();
   double mean = 0, var = 0;
@@ -392,13 +403,13 @@ __global__ void __launch_bounds__(64 * (2 + UG_DEV_NP)) k_ug_dev(const uint8_t* 
   // over phase ph, wave 1 the M2 sums over ph - 1
   auto phase = [&](uint32_t ph, DevSet& cur) {
     if (w >= 2) {
-      if (ph + 1 < nph) store(ph + 1, cur);
-      if (ph + 1 + D < nph) load_vals(cur);
-      if (ph + 1 + 2 * D < nph) load_offs(cur, ph + 1 + 2 * D);
+      if (ph + AH < nph) store(ph + AH, cur);
+      if (ph + AH + D < nph) load_vals(cur);
+      if (ph + AH + 2 * D < nph) load_offs(cur, ph + AH + 2 * D);
     } else if (w == 0 && ph < nph && (uint32_t)lane < GP && UG_DEV_ABL != 5) {  // the mean chains
       // (span 0 takes the same step from mean = 0 with n = 1: d = x, q = x
       // exactly, mean' = x — wf_push's first value — so no step is special)
-      const uint32_t nk = min(DEV_B, n_kept - ph * DEV_B), b3 = ph % 3, b2 = ph & 1;
+      const uint32_t nk = min(DEV_B, n_kept - ph * DEV_B), b3 = ph % RB, b2 = ph & 1;
       const uint32_t base = ph * DEV_B + 1;  // n of the phase's first span
       auto chain_step = [&](uint32_t j, double x, double r) {
         const double dn = (double)(base + j);  // (exact: n < 2^32)
@@ -428,7 +439,7 @@ __global__ void __launch_bounds__(64 * (2 + UG_DEV_NP)) k_ug_dev(const uint8_t* 
 #pragma unroll
           for (uint32_t u = 0; u < U; u++) {
             x[u] = s_buf[b3][j0 + u][lane];
-            r[u] = s_rcp[b2][j0 + u];
+            r[u] = s_rcp[b3][j0 + u];
           }
         };
         fetch(0, xa, ra);
@@ -446,10 +457,10 @@ __global__ void __launch_bounds__(64 * (2 + UG_DEV_NP)) k_ug_dev(const uint8_t* 
           }
         }
       } else {  // the last, partial phase
-        for (uint32_t j = 0; j < nk; j++) chain_step(j, s_buf[b3][j][lane], s_rcp[b2][j]);
+        for (uint32_t j = 0; j < nk; j++) chain_step(j, s_buf[b3][j][lane], s_rcp[b3][j]);
       }
     } else if (w == 1 && ph >= 1 && (uint32_t)lane < GP && UG_DEV_ABL != 4) {  // the M2 sums of the phase before
-      const uint32_t p = ph - 1, nk = min(DEV_B, n_kept - p * DEV_B), b3 = p % 3, b2 = p & 1;
+      const uint32_t p = ph - 1, nk = min(DEV_B, n_kept - p * DEV_B), b3 = p % RB, b2 = p & 1;
       for (uint32_t j = p == 0 ? 1u : 0u; j < nk; j++) {
         const double2 dm = s_dm[b2][j][lane];
         var += dm.x * (s_buf[b3][j][lane] - dm.y);
