@@ -1080,7 +1080,7 @@ DEVI void cq_unstage_wave(uint8_t* dst, const uint8_t* lds, uint32_t i0, uint64_
 #define CW_SORT 128u    // cells of an in-wave complexCompact
 #endif
 #ifndef CR_WPE
-#define CR_WPE 0        // (build knob) waves per SIMD the register allocation aims at, 0: the compiler's choice
+#define CR_WPE 5        // waves per SIMD the register allocation aims at (the compiler's 119 VGPRs; 5: -0.02 ms, 6: none)
 #endif
 #ifndef CR_ABL
 #define CR_ABL 0        // (ablation builds only, wrong results: 1 no write/delete decision, 2 no complexCompact)
@@ -1282,10 +1282,10 @@ k_compact_rows(CompactArgs a) {
 #define CW_VCAP 1536u  // value bytes per piece
 #endif
 #ifndef CW_WAVES
-#define CW_WAVES 4u    // waves a block
+#define CW_WAVES 2u    // waves a block (C5 call, same box: 1 / 2 / 4 / 8 waves 0.794 / 0.798 / 0.845 / 0.925 ms: a block frees its slot only when its last wave ends)
 #endif
 #ifndef CW_WPE
-#define CW_WPE 0       // (build knob) waves per SIMD the register allocation aims at, 0: the compiler's choice
+#define CW_WPE 7       // waves per SIMD the register allocation aims at (C5 call, same box: the compiler's 80 VGPRs 0.898 ms, 7: 0.856, 8: 0.956)
 #endif
 #ifndef CW_ABL
 #define CW_ABL 0       // (ablation builds only, wrong results: 2 no value output, 4 no plain test)
