@@ -4228,8 +4228,8 @@ static int compact_rows(Slot* ctx, const tsdbhip_rows_desc* d, tsdbhip_rows_out*
     LAUNCH_STOP(det ? EV_STOP_K(ctx, 9) : nullptr, k_compact_wave, dim3(grid_for(R, CW_ROWS * CW_WAVES, 1u << 30)),
                 dim3(WAVE * CW_WAVES), 0, st, a);
     if (det) EV_STOP_M(ctx, 9);
-    LAUNCH_STOP(det ? EV_STOP_K(ctx, 3) : nullptr, k_compact_rows, dim3(grid_for(R, CR_RANGE, 1u << 14)), dim3(256),
-                0, st, a);
+    LAUNCH_STOP(det ? EV_STOP_K(ctx, 3) : nullptr, k_compact_rows, dim3(grid_for(R, CR_RANGE, 1u << 14)),
+                dim3(WAVE * CR_WAVES), 0, st, a);
     if (det) EV_STOP_M(ctx, 3);
     HIPCHK(hipGetLastError());
     LAUNCH(k_compact_complex<true>, dim3(1024), dim3(256), 0, ctx->stream, a);

@@ -1067,6 +1067,9 @@ DEVI void cq_unstage_wave(uint8_t* dst, const uint8_t* lds, uint32_t i0, uint64_
 #ifndef CR_RANGE
 #define CR_RANGE 256u   // rows scanned for CQ_PENDING per block iteration
 #endif
+#ifndef CR_WAVES
+#define CR_WAVES 4u     // waves a block (C5 call: 4 waves / 256 rows 0.802 ms, 2 / 128 0.805, 1 / 64 0.807, 2 / 256 0.856, 1 / 128 0.848)
+#endif
 #ifndef CR_KCAP
 #define CR_KCAP 256u    // a row in LDS: KVs
 #endif
@@ -1190,13 +1193,15 @@ DEVI void cr_row(const CompactArgs& a, CrLds& L, const RowHdr& h, uint64_t r, ui
   wave_lds_sync();  // (the row's LDS consumed before the wave's next row is staged)
 }
 
-__global__ void __launch_bounds__(256)
+__global__ void __launch_bounds__(WAVE * CR_WAVES)
 #if CR_WPE
 __attribute__((amdgpu_waves_per_eu(CR_WPE, CR_WPE)))
 #endif
 k_compact_rows(CompactArgs a) {
-  __shared__ CrLds Ls[4];
-  __shared__ uint32_t s_list[CR_RANGE], s_wn[4], s_cx;
+  constexpr uint32_t NW = CR_WAVES;
+  static_assert(CR_RANGE % NW == 0 && CR_RANGE / NW >= 1, "rows kernel range");
+  __shared__ CrLds Ls[NW];
+  __shared__ uint32_t s_list[CR_RANGE], s_wn[NW], s_cx;
   const int tid = threadIdx.x, lane = lane_id(), w = tid / WAVE;
   const uint64_t Q0 = a.row_qual_off[0], V0 = a.row_val_off[0];
   if (tid == 0) s_cx = 0;
@@ -1204,13 +1209,14 @@ k_compact_rows(CompactArgs a) {
   for (uint64_t rb = (uint64_t)blockIdx.x * CR_RANGE; rb < a.n_rows; rb += (uint64_t)gridDim.x * CR_RANGE) {
     // ---- the range's CQ_PENDING rows, in row order, into s_list ----
     __syncthreads();  // (the previous range's list consumed)
-    constexpr int CR_U = CR_RANGE >= 256 ? (int)(CR_RANGE / 256) : 1;
+    constexpr uint32_t QR = CR_RANGE / NW;  // a wave's share of the range
+    constexpr int CR_U = (int)((QR + WAVE - 1) / WAVE);
     uint32_t pend[CR_U], wpos = 0;
 #pragma unroll
     for (int u = 0; u < CR_U; u++) {
-      const uint32_t q = u * WAVE + lane;  // (wave w: a quarter of the range)
-      const uint64_t r = rb + (uint64_t)w * (CR_RANGE / 4) + q;
-      const bool pd = q < CR_RANGE / 4 && r < a.n_rows && a.status[r] == CQ_PENDING;
+      const uint32_t q = u * WAVE + lane;  // (wave w: its share of the range)
+      const uint64_t r = rb + (uint64_t)w * QR + q;
+      const bool pd = q < QR && r < a.n_rows && a.status[r] == CQ_PENDING;
       const uint64_t m = ballot(pd);
       pend[u] = pd ? wpos + (uint32_t)__popcll(m & lanemask_lt(lane)) : ~0u;
       wpos += (uint32_t)__popcll(m);
@@ -1219,16 +1225,17 @@ k_compact_rows(CompactArgs a) {
     __syncthreads();
     uint32_t woff = 0;
     for (int v = 0; v < w; v++) woff += s_wn[v];
-    const uint32_t n = s_wn[0] + s_wn[1] + s_wn[2] + s_wn[3];
+    uint32_t n = 0;
+    for (uint32_t v = 0; v < NW; v++) n += s_wn[v];
 #pragma unroll
     for (int u = 0; u < CR_U; u++)
-      if (pend[u] != ~0u) s_list[woff + pend[u]] = (uint32_t)(rb + (uint64_t)w * (CR_RANGE / 4) + u * WAVE + lane);
+      if (pend[u] != ~0u) s_list[woff + pend[u]] = (uint32_t)(rb + (uint64_t)w * QR + u * WAVE + lane);
     __syncthreads();
     // ---- a wave a row; its rows' headers loaded ten at a time ----
-    for (uint32_t i0 = w; i0 < n; i0 += 40) {
-      const uint64_t hv = cr_hdr_load(a, s_list, i0, 4, n, lane);
-      for (uint32_t m = 0; m < 10 && i0 + 4 * m < n; m++) {
-        const uint32_t r = uni32(s_list[i0 + 4 * m]);
+    for (uint32_t i0 = w; i0 < n; i0 += 10 * NW) {
+      const uint64_t hv = cr_hdr_load(a, s_list, i0, NW, n, lane);
+      for (uint32_t m = 0; m < 10 && i0 + NW * m < n; m++) {
+        const uint32_t r = uni32(s_list[i0 + NW * m]);
         cr_row(a, Ls[w], cr_hdr(a, hv, m, r, Q0, V0), r, &n_cx, lane);
       }
     }
