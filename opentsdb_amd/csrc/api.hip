@@ -1778,7 +1778,17 @@ DEVI void ug_fap_tail_spec(const FapArgs& fap, const UgTail& t) {
   small_snap(sm, t.snap, s_ok ? t.init : nullptr, t.seq);
 }
 template <int AGG, bool SPEC>
-__global__ void __launch_bounds__(256) k_ug_ds_reg(DecodeArgs a, SpanDsArgs g, const uint32_t* ncells,
+#ifndef UG_LDS_CAP
+#define UG_LDS_CAP 40960u  // (build knob) LDS a k_ug_ds_reg block claims: 40 KB = 4 blocks a CU
+#endif
+#ifndef UG_WPE
+#define UG_WPE 0  // (build knob) waves per SIMD the register allocation aims at, 0: the compiler's choice
+#endif
+__global__ void __launch_bounds__(256)
+#if UG_WPE
+__attribute__((amdgpu_waves_per_eu(UG_WPE, UG_WPE)))
+#endif
+k_ug_ds_reg(DecodeArgs a, SpanDsArgs g, const uint32_t* ncells,
                                                    const uint32_t* vlen, FapArgs fap, UgTail t) {
   extern __shared__ uint8_t s_pad[];
   if (threadIdx.x == 0 && a.n_kept == 0xFFFFFFFFu) s_pad[0] = 1;
@@ -2053,7 +2063,7 @@ static int ug_aligned_group(Slot* ctx, const UgIn& u, tsdbhip_sg_out* out, tsdbh
                    ? (unsigned)at.sharedSizeBytes
                    : 21000u;
       }();
-      const unsigned pad = stat_lds < 40960u ? 40960u - stat_lds : 0u;
+      const unsigned pad = stat_lds < UG_LDS_CAP ? UG_LDS_CAP - stat_lds : 0u;
       EV_START(ctx, 8);
       if (u.spec)
         LAUNCH_STOP(EV_STOP_K(ctx, 9), (k_ug_ds_reg<A, true>), dim3(rblocks), dim3(256), pad, st, u.da, gr,

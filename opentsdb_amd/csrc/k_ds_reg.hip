@@ -514,8 +514,16 @@ DEVI void ds_reg_body(const DecodeArgs& a, const SpanDsArgs& g, const uint32_t* 
   }
 }
 
+#ifndef DS_WPE
+#define DS_WPE 7  // waves per SIMD the register allocation aims at (C2, same box: the compiler's 83 VGPRs
+                  // 0.165 ms, 7: 0.150, 8: 0.161)
+#endif
 template <int AGG>
-__global__ void __launch_bounds__(256) k_ds_reg(DecodeArgs a, SpanDsArgs g, const uint32_t* ncells,
+__global__ void __launch_bounds__(256)
+#if DS_WPE
+__attribute__((amdgpu_waves_per_eu(DS_WPE, DS_WPE)))
+#endif
+k_ds_reg(DecodeArgs a, SpanDsArgs g, const uint32_t* ncells,
                                                 const uint32_t* vlen, uint32_t wps_log2, FapArgs fap) {
   // (dynamic LDS: padding that caps the resident blocks per CU, see LaunchChunks)
   extern __shared__ uint8_t s_pad[];
