@@ -256,32 +256,34 @@ __global__ void __launch_bounds__(256) k_lockstep(ReduceArgs r, LockstepArgs L) 
 // Welford over the spans in span order before the (long) truncation
 // (Aggregators.java:196-237) admits no merge of partial states, so each grid
 // point is one chain of n_kept dependent steps. A block holds the chains of
-// GP grid points, its four waves on four SIMDs:
+// GP grid points, 2 + UG_DEV_NP waves:
 //   wave 0  the mean chains (lane = grid point): mean' = mean + (x - mean)/n,
 //           each step's (x - mean, mean') to LDS;
 //   wave 1  the M2 sums one phase behind: var += (x - mean) (x - mean'), in
 //           span order (the same roundings as wf_push, dev_common.h);
-//   waves 2-3  stream the values into LDS ahead of them — span k's GP values
+//   waves 2+  stream the values into LDS ahead of them — span k's GP values
 //           are W * GP contiguous bytes (cell g of every span sits at grid
 //           point g), 64 / GP spans a load instruction — DEV_B spans a phase,
-//           a software pipeline over two register sets (values of phase
-//           ph + 1 stored while those of ph + 3 and the row offsets of ph + 5
-//           load: two phases of latency for each level), and convert them
-//           to double; they also prove the proposal as they
+//           a software pipeline over UG_DEV_DEPTH = 3 register sets (values
+//           of phase ph + 1 stored while those of ph + 4 and the row offsets
+//           of ph + 7 load: three phases of latency for each level), and
+//           convert them to double; they also prove the proposal as they
 //           stream: every qualifier is compared with (x0 + g step - base) << 4
 //           | flags (as k_lockstep); a mismatch sets `broken` and the call
 //           runs again on the proven path.
 // The chain's division (x - mean) / n is Markstein's correction of a product
 // with r = RN(1/n): q0 = RN(d r), e = d - n q0 (exact, one fma), q = RN(q0 +
 // e r) = RN(d / n) — the quotient of a double by an integer n never sits on a
-// rounding midpoint and stays normal here — bit-exact with the division; n
-// and r are uniform (n = span index + 1) and come from the producers. The mean
+// rounding midpoint and stays normal here — bit-exact with the division; r
+// comes from the producers through LDS, n is converted by the chain wave
+// (span 0 takes the same step from mean 0 with n = 1). The mean
 // chain is then five dependent double operations a step on a SIMD of its own
 // (round 6: 95 -> 56.7 ms for C3's 1M series, 9.5 -> 5.7 ms for 100k, with
 // GP = 16: 225 blocks instead of 57, and the conversions off the chain; then
 // 64-span phases 44.8 ms, the two-set producer pipeline 41.3 ms, the chain's
 // LDS reads a group ahead (scheduling barrier) 39.8 ms, four producer waves
-// 39.2 ms. Without the mean chain the kernel takes 30 ms.)
+// 39.2 ms, three register sets 35.0 ms. Without the mean chain the kernel
+// takes 25 ms.)
 #ifndef UG_DEV_B
 #define UG_DEV_B 64u  // (C3 1M series: 16 / 32 / 48 / 64 / 80 / 96 / 128 spans 73.7 / 55.2 / 48.4 / 44.8 / 57.0 / 56.7 / 57.7 ms)
 #endif
